@@ -1,0 +1,287 @@
+/*
+ * lincheck.h -- C ABI of the MI355X linearizability checker (liblincheck.so).
+ *
+ * Drop-in for the check phase of the Jepsen etcd demo:
+ *
+ *   (independent/checker
+ *     (checker/compose
+ *       {:linear (checker/linearizable {:model (model/cas-register)
+ *                                       :algorithm :linear}) ...}))
+ *
+ * at /root/reference/src/jepsen/etcdemo.clj:115-119.  The reference path is
+ * jepsen.independent/checker -> jepsen.checker/linearizable ->
+ * knossos.linear/analysis (knossos 0.3.7, jepsen.etcdemo.iml:58), all Clojure.
+ * Nothing in the reference is native, so every entry point below replaces a
+ * Clojure function; each cites the reference call site it stands behind.
+ *
+ * Layers:
+ *   lc_synth_*   synthetic cas-register histories with the demo's shape
+ *                (etcdemo.clj:67-69, :83-105, :120-125).          [test input]
+ *   lc_edn_*     Jepsen history.edn reader/writer (store/ layout,
+ *                .gitignore:13; SURVEY F-1).                        [ingest]
+ *   lc_pack      jepsen.independent/subhistory + knossos.history complete /
+ *                without-failures + knossos.model.memo, producing packed
+ *                per-key event streams (rows A1-A5).                 [host]
+ *   lc_check_*   knossos.linear/analysis on the GPU (rows A6, A7) and the
+ *                per-key verdict records jepsen.checker/linearizable and
+ *                independent/checker turn into result maps (A8, A9). [device]
+ *
+ * Conventions: the caller owns every array it passes in or out.  The library
+ * copies inputs to the device and never keeps caller pointers after a call
+ * returns.  Every function returns 0 on success and a negative LC_E_* code on
+ * failure; lc_last_error() (thread-local) describes the last failure.  The
+ * library never calls exit() or abort().  One lc_ctx serialises its own calls
+ * with an internal mutex; distinct contexts may run concurrently.
+ */
+#ifndef LINCHECK_H
+#define LINCHECK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LC_ABI_VERSION 1
+
+/* ---- error codes --------------------------------------------------------- */
+#define LC_OK            0
+#define LC_E_INVALID    -1  /* bad argument / malformed history               */
+#define LC_E_NOMEM      -2  /* host or device allocation failed               */
+#define LC_E_DEVICE     -3  /* HIP runtime error / no usable gfx950 device    */
+#define LC_E_PARSE      -4  /* EDN syntax error                               */
+#define LC_E_UNSUPPORTED -5 /* op the cas-register model cannot step          */
+#define LC_E_IO         -6  /* file could not be read / written               */
+
+/* ---- history vocabulary (etcdemo.clj:67-69, :83-105) --------------------- */
+/* :type of an op map */
+#define LC_INVOKE 0
+#define LC_OK_T   1
+#define LC_FAIL   2
+#define LC_INFO   3
+/* :f of an op map */
+#define LC_F_READ  0
+#define LC_F_WRITE 1
+#define LC_F_CAS   2
+#define LC_F_OTHER 3   /* nemesis :start/:stop and anything else */
+
+#define LC_NIL        INT64_MIN  /* a nil value                                */
+#define LC_NO_KEY     INT64_MIN  /* :value is not an independent tuple [k v]   */
+#define LC_NO_PROCESS INT64_MIN  /* :process is not an integer (:nemesis)      */
+
+/*
+ * A raw Jepsen history as struct-of-arrays, one row per op map, in history
+ * order.  This is what the Clojure side marshals a `history` vector into
+ * (INTEGRATION.md), what lc_edn_read produces and what lc_synth emits.
+ *   key   the k of an independent tuple [k v] (jepsen.independent/tuple,
+ *         etcdemo.clj:90,120) or LC_NO_KEY;
+ *   v0/v1 the unwrapped v: read/write -> v0 (v1 = LC_NIL); cas [old new] ->
+ *         v0 = old, v1 = new; LC_NIL for nil;
+ *   index the op's :index, or -1 when the map has none.
+ */
+typedef struct lc_history {
+    int64_t        n;
+    const uint8_t *type;     /* LC_INVOKE / LC_OK_T / LC_FAIL / LC_INFO */
+    const uint8_t *f;        /* LC_F_*                                   */
+    const int64_t *process;  /* or LC_NO_PROCESS                         */
+    const int64_t *key;      /* or LC_NO_KEY                             */
+    const int64_t *v0;
+    const int64_t *v1;
+    const int64_t *index;    /* may be NULL: rows are then their own index */
+} lc_history;
+
+/* ---- packed per-key event streams (rows A3-A5) ---------------------------- */
+/*
+ * Event word (u32), one per surviving client event of a key sub-history:
+ *   bit 31      0 = :invoke, 1 = :ok completion
+ *   bits 30..24 slot: the op's position in the key's pending window
+ *               (lowest free slot at invoke, freed at :ok; crashed ops keep
+ *               theirs forever)
+ *   bits 23..0  invoke: transition id (index into trans[] after adding
+ *               trans_off[key]); ok: 0
+ * Failed ops (:fail) are gone (knossos.history/without-failures); :info
+ * completions produce no event (the op stays callable forever).
+ */
+#define LC_EV_OK_BIT     0x80000000u
+#define LC_EV_SLOT(e)    (((e) >> 24) & 0x7Fu)
+#define LC_EV_TRANS(e)   ((e) & 0x00FFFFFFu)
+
+/*
+ * Transition descriptor (u32) = one interned cas-register op
+ * (knossos.model/cas-register step, knossos.model.memo):
+ *   bits 1..0   LC_T_READ_ANY (read of nil: legal in every state, no change)
+ *               LC_T_READ  (legal iff state == a, no change)
+ *               LC_T_WRITE (state := b)
+ *               LC_T_CAS   (legal iff state == a, then state := b)
+ *   bits 16..2  a (state id; LC_STATE_NONE = a value no op can produce)
+ *   bits 31..17 b (state id)
+ * State 0 is nil, the register's initial value ((model/cas-register) at
+ * etcdemo.clj:117).
+ */
+#define LC_T_READ_ANY 0u
+#define LC_T_READ     1u
+#define LC_T_WRITE    2u
+#define LC_T_CAS      3u
+#define LC_STATE_NONE 0x7FFFu
+#define LC_DESC(f, a, b) ((uint32_t)(f) | ((uint32_t)(a) << 2) | ((uint32_t)(b) << 17))
+
+/* Limits of the packed form.  A key beyond them is reported :unknown with
+ * cause LC_CAUSE_WINDOW / LC_CAUSE_STATES (identically in oracle/). */
+#define LC_NARROW_MAX_SLOTS  56   /* u64 config: 8-bit state | 56 slot bits   */
+#define LC_NARROW_MAX_STATES 255
+#define LC_WIDE_MAX_SLOTS    112  /* 2 x u64 config                          */
+#define LC_WIDE_MAX_STATES   32767
+
+/* A packed batch: caller-visible view of lc_pack output or caller-built. */
+typedef struct lc_batch {
+    int64_t         n_keys;
+    const uint64_t *ev_off;     /* [n_keys + 1] offsets into events          */
+    const uint32_t *events;     /* [ev_off[n_keys]]                           */
+    const uint32_t *trans;      /* transition descriptors                     */
+    int64_t         n_trans;
+    const uint32_t *trans_off;  /* [n_keys] per-key base into trans, or NULL  */
+    const uint8_t  *key_width;  /* [n_keys] max slots used (1 + max slot), or NULL */
+    const uint16_t *key_states; /* [n_keys] state ids used, or NULL           */
+    uint32_t        init_state; /* state id of the initial value (0 = nil)    */
+} lc_batch;
+
+typedef struct lc_pack_opts {
+    int32_t reserved;  /* must be 0 */
+} lc_pack_opts;
+
+typedef struct lc_packed lc_packed;  /* library-owned */
+
+/* jepsen.independent/checker's split (history-keys + subhistory, per
+ * etcdemo.clj:115) followed by knossos.history/complete + without-failures
+ * and model memoisation, for the cas-register model.  Keys appear in order
+ * of first appearance.  Non-tuple ops (nemesis) belong to every key's
+ * sub-history and, being :info, are no-ops for the search. */
+int  lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed **out);
+void lc_packed_free(lc_packed *p);
+/* Borrowed view of the packed arrays (valid until lc_packed_free). */
+int  lc_packed_view(const lc_packed *p, lc_batch *out);
+/* Independent key of packed key i. */
+int64_t lc_packed_key(const lc_packed *p, int64_t i);
+/* History row (0-based position in the lc_history) of event j of key i. */
+int64_t lc_packed_event_row(const lc_packed *p, int64_t i, int64_t j);
+/* Number of history rows in key i's sub-history (incl. nemesis rows) and the
+ * rows themselves (out may be NULL to query the count). */
+int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows);
+/* Register value of state id s of key i (state 0 = nil -> *is_nil = 1). */
+int lc_packed_state_value(const lc_packed *p, int64_t i, uint32_t s, int64_t *value, int *is_nil);
+
+/* ---- device checking (rows A6-A9) ------------------------------------------ */
+#define LC_ALGO_LINEAR 0   /* :algorithm :linear (etcdemo.clj:118) */
+
+typedef struct lc_opts {
+    int32_t  device;        /* HIP device ordinal                               */
+    int32_t  algorithm;     /* LC_ALGO_LINEAR                                   */
+    uint64_t max_configs;   /* search budget B (0 = default 1<<20): a key whose
+                               config set or JIT closure exceeds B configs is
+                               :unknown (LC_CAUSE_BUDGET); replaces
+                               knossos.search's heap-dependent abort (row A7)   */
+    int32_t  max_final;     /* configs kept per invalid key (<= 16, default 10,
+                               the truncation of jepsen.checker/linearizable)   */
+    int32_t  lds_configs;   /* per-wave LDS frontier capacity (0 = default)     */
+    int32_t  deep_slots;    /* concurrently searched HBM-tier keys (0 = auto)    */
+    int32_t  reserved[6];
+} lc_opts;
+
+/* :valid? per key */
+#define LC_VALID    1
+#define LC_INVALID  0
+#define LC_UNKNOWN -1
+
+/* why a key ended */
+#define LC_CAUSE_NONE    0  /* valid                                         */
+#define LC_CAUSE_NONLIN  1  /* invalid: config set empty at fail_event       */
+#define LC_CAUSE_BUDGET  2  /* unknown: > max_configs configs                 */
+#define LC_CAUSE_WINDOW  3  /* unknown: > LC_WIDE_MAX_SLOTS ops pending       */
+#define LC_CAUSE_STATES  4  /* unknown: > LC_WIDE_MAX_STATES register values  */
+#define LC_CAUSE_ERROR   5  /* unknown: device-side fault detected            */
+
+typedef struct lc_result {
+    int8_t   *valid;         /* [n_keys] LC_VALID / LC_INVALID / LC_UNKNOWN         */
+    int32_t  *fail_event;    /* [n_keys] event ordinal (within the key's stream) of
+                                the :ok that could not be linearized, else -1       */
+    uint8_t  *cause;         /* [n_keys] LC_CAUSE_*                                  */
+    uint32_t *peak_configs;  /* [n_keys] max config-set size seen (may be NULL)      */
+    uint64_t *final_configs; /* [n_keys * max_final * 2] (may be NULL): for invalid
+                                keys, up to max_final configs of the last non-empty
+                                set, as {state, slot mask lo} / {slot mask hi}      */
+    uint32_t *n_final;       /* [n_keys] configs written to final_configs (may be NULL) */
+} lc_result;
+
+typedef struct lc_stats {
+    double   kernel_ms;       /* device time of the search kernels (HIP events) */
+    double   total_ms;        /* wall time of the call                          */
+    uint64_t probes;          /* successor-config insert attempts (all tiers)   */
+    uint64_t lds_keys;        /* keys finished in the LDS tier                  */
+    uint64_t deep_keys;       /* keys (re)searched in the HBM tier              */
+    uint64_t events;          /* events processed                               */
+} lc_stats;
+
+typedef struct lc_ctx lc_ctx;
+typedef struct lc_dev_batch lc_dev_batch;
+
+int         lc_abi_version(void);
+const char *lc_last_error(void);
+int         lc_device_count(void);
+
+int  lc_create(const lc_opts *opts, lc_ctx **out);
+void lc_destroy(lc_ctx *ctx);
+
+/* One call per batch: H2D, search, D2H into caller-owned result arrays. */
+int  lc_check_batch(lc_ctx *ctx, const lc_batch *b, lc_result *r, lc_stats *s);
+
+/* Device-resident batches: upload once, check many times (the bench's step). */
+int  lc_upload(lc_ctx *ctx, const lc_batch *b, lc_dev_batch **out);
+void lc_dev_batch_free(lc_dev_batch *db);
+/* Search an uploaded batch.  If dev_result != 0 the result arrays in r are
+ * DEVICE pointers (e.g. torch tensors for an RCCL all-gather) and nothing is
+ * copied back; otherwise they are host arrays. */
+int  lc_check_device(lc_ctx *ctx, const lc_dev_batch *db, lc_result *r,
+                     int dev_result, lc_stats *s);
+
+/* ---- synthetic histories ------------------------------ */
+typedef struct lc_synth_opts {
+    int64_t  n_keys;
+    int64_t  ops_per_key;    /* client invocations per key (gen/limit, :125)     */
+    int32_t  concurrency;    /* client threads per key (concurrent-generator 10) */
+    int32_t  n_values;       /* values 0..n_values-1 (rand-int 5, :68-69)         */
+    double   info_rate;      /* fraction of write/cas that complete :info         */
+    double   info_effect_p;  /* probability a crashed op took effect              */
+    double   anomaly_rate;   /* fraction of keys given one stale read / lost cas  */
+    double   mean_think;     /* mean think time between a thread's ops            */
+    double   mean_latency;   /* mean op latency                                   */
+    int32_t  interleave;     /* 1: one time-ordered Jepsen history (keys in
+                                sequence per thread group, tuples, :index);
+                                0: key-major blocks                               */
+    double   nemesis_period; /* > 0 and interleave: nemesis :info :start/:stop
+                                every period (etcdemo.clj:138-143)                */
+    uint64_t seed;
+    int64_t  key_base;       /* first key id (shards of a larger key space)       */
+} lc_synth_opts;
+
+typedef struct lc_hist lc_hist;      /* library-owned history storage */
+int  lc_synth_generate(const lc_synth_opts *o, lc_hist **out);
+int  lc_hist_view(const lc_hist *h, lc_history *out);  /* borrowed view */
+/* Keys the generator corrupted (anomaly_rate), ascending; out may be NULL to
+ * query the count. */
+int64_t lc_hist_anomalous_keys(const lc_hist *h, int64_t *out_keys);
+void lc_hist_free(lc_hist *h);
+
+/* ---- history.edn (Jepsen store format) ------------------------------------- */
+/* Parse a Jepsen history.edn (one op map per line, or one vector of maps)
+ * into an owned history.  Supports the op maps this workload produces:
+ * :type :f :process :value (nil, ints, [k v] tuples, [old new]) :index :time
+ * :error; other keys are skipped. */
+int  lc_edn_read(const char *path, lc_hist **out);
+int  lc_edn_parse(const char *text, int64_t len, lc_hist **out);
+int  lc_edn_write(const char *path, const lc_history *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LINCHECK_H */

@@ -1,0 +1,376 @@
+// device_api.hip -- host orchestration of the device search (C ABI: lc_create,
+// lc_upload, lc_check_device, lc_check_batch; include/lincheck.h).
+//
+// This is the native side of the drop-in at etcdemo.clj:115-119: one call
+// checks every key of a batch (independent/checker's per-key pmap becomes a
+// work list walked by persistent kernels).  Inputs are validated on the host
+// before any launch, so a malformed batch can never drive a kernel out of
+// bounds.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+#include "device_search.hpp"
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            return lc::fail(LC_E_DEVICE, "%s failed: %s", #expr, hipGetErrorString(_e));  \
+    } while (0)
+
+namespace {
+
+template <class T>
+hipError_t dalloc(T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc((void **)p, n * sizeof(T));
+}
+
+template <class T>
+void dfree(T *&p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+}  // namespace
+
+struct lc_dev_batch {
+    int device = 0;
+    int64_t n_keys = 0;
+    uint64_t n_events = 0;
+    int64_t n_trans = 0;
+    uint32_t init_state = 0;
+    bool has_trans_off = false;
+    uint64_t *ev_off = nullptr;
+    uint32_t *events = nullptr;
+    uint32_t *trans = nullptr;
+    uint32_t *trans_off = nullptr;
+    uint8_t *key_width = nullptr;
+    uint16_t *key_states = nullptr;
+    int32_t *order = nullptr;  // LPT: keys by event count, descending
+    size_t input_bytes = 0;    // bytes the search reads per pass (events + offsets + tables)
+    ~lc_dev_batch() {
+        dfree(ev_off); dfree(events); dfree(trans); dfree(trans_off);
+        dfree(key_width); dfree(key_states); dfree(order);
+    }
+};
+
+struct lc_ctx {
+    lc_opts o{};
+    int device = 0;
+    int cu_count = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::mutex mu;
+    // scratch, grown on demand
+    int64_t cap_keys = 0;
+    int32_t *lists = nullptr;      // 3 x cap_keys: spill1, spill2, wide
+    int32_t *counters = nullptr;   // 16 ints: n_spill1, n_spill2, n_wide, tickets[4]
+    unsigned long long *acc = nullptr;  // probes, events, keys_done
+    int8_t *valid = nullptr;
+    int32_t *fail_event = nullptr;
+    uint8_t *cause = nullptr;
+    uint32_t *peak = nullptr;
+    uint64_t *final_cfg = nullptr;
+    uint32_t *n_final = nullptr;
+    ~lc_ctx() {
+        dfree(lists); dfree(counters); dfree(acc); dfree(valid); dfree(fail_event);
+        dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+static int ensure_capacity(lc_ctx *c, int64_t n_keys) {
+    if (n_keys <= c->cap_keys) return LC_OK;
+    int64_t cap = std::max<int64_t>(n_keys, 1024);
+    dfree(c->lists); dfree(c->valid); dfree(c->fail_event); dfree(c->cause);
+    dfree(c->peak); dfree(c->final_cfg); dfree(c->n_final);
+    HIPCHK(dalloc(&c->lists, (size_t)cap * 3));
+    HIPCHK(dalloc(&c->valid, (size_t)cap));
+    HIPCHK(dalloc(&c->fail_event, (size_t)cap));
+    HIPCHK(dalloc(&c->cause, (size_t)cap));
+    HIPCHK(dalloc(&c->peak, (size_t)cap));
+    HIPCHK(dalloc(&c->final_cfg, (size_t)cap * (size_t)c->o.max_final * 2));
+    HIPCHK(dalloc(&c->n_final, (size_t)cap));
+    c->cap_keys = cap;
+    return LC_OK;
+}
+
+extern "C" int lc_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
+    if (!out) return lc::fail(LC_E_INVALID, "lc_create: null out");
+    lc_opts o{};
+    if (opts) o = *opts;
+    if (o.algorithm != LC_ALGO_LINEAR) return lc::fail(LC_E_INVALID, "lc_create: only :algorithm :linear is supported");
+    if (o.max_configs == 0) o.max_configs = 1ull << 20;
+    if (o.max_configs > (1ull << 31)) return lc::fail(LC_E_INVALID, "lc_create: max_configs above 2^31");
+    if (o.max_final <= 0) o.max_final = 10;
+    if (o.max_final > 16) return lc::fail(LC_E_INVALID, "lc_create: max_final above 16");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return lc::fail(LC_E_DEVICE, "lc_create: no HIP device visible");
+    if (o.device < 0 || o.device >= ndev) return lc::fail(LC_E_DEVICE, "lc_create: device %d of %d", o.device, ndev);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, o.device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return lc::fail(LC_E_DEVICE, "lc_create: device %d is %s, this build targets gfx950", o.device, prop.gcnArchName);
+    lc_ctx *c = new (std::nothrow) lc_ctx();
+    if (!c) return lc::fail(LC_E_NOMEM, "lc_create: out of memory");
+    c->o = o;
+    c->device = o.device;
+    c->cu_count = prop.multiProcessorCount;
+    int rc = LC_OK;
+    auto init = [&]() -> int {
+        HIPCHK(hipSetDevice(o.device));
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreate(&c->e0));
+        HIPCHK(hipEventCreate(&c->e1));
+        HIPCHK(dalloc(&c->counters, 16));
+        HIPCHK(dalloc(&c->acc, 4));
+        return LC_OK;
+    };
+    rc = init();
+    if (rc) { delete c; return rc; }
+    *out = c;
+    return LC_OK;
+}
+
+extern "C" void lc_destroy(lc_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    delete c;
+}
+
+// Host validation of a packed batch: every index a kernel will follow is in
+// range, every :ok names a slot that is pending.
+static int validate_batch(const lc_batch *b) {
+    if (!b || b->n_keys < 0) return lc::fail(LC_E_INVALID, "batch: bad n_keys");
+    if (b->n_keys == 0) return LC_OK;
+    if (!b->ev_off || !b->trans || b->n_trans <= 0) return lc::fail(LC_E_INVALID, "batch: missing arrays");
+    if (b->ev_off[0] != 0) return lc::fail(LC_E_INVALID, "batch: ev_off[0] != 0");
+    for (int64_t k = 0; k < b->n_keys; ++k) {
+        if (b->ev_off[k + 1] < b->ev_off[k]) return lc::fail(LC_E_INVALID, "batch: ev_off not monotone at key %lld", (long long)k);
+        if (b->ev_off[k + 1] - b->ev_off[k] > 0x7FFFFFFFull) return lc::fail(LC_E_INVALID, "batch: key %lld has > 2^31 events", (long long)k);
+    }
+    if (b->ev_off[b->n_keys] && !b->events) return lc::fail(LC_E_INVALID, "batch: events missing");
+    if (b->init_state >= LC_STATE_NONE) return lc::fail(LC_E_INVALID, "batch: bad init_state");
+    const int64_t K = b->n_keys;
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<int> bad((size_t)nt, 0);
+    std::vector<int64_t> badkey((size_t)nt, -1);
+    auto work = [&](unsigned t) {
+        for (int64_t k = t; k < K && !bad[t]; k += nt) {
+            uint64_t tb = b->trans_off ? b->trans_off[k] : 0;
+            uint64_t pend[2] = {0, 0};
+            for (uint64_t j = b->ev_off[k]; j < b->ev_off[k + 1]; ++j) {
+                uint32_t ev = b->events[j];
+                uint32_t s = LC_EV_SLOT(ev);
+                // slot 127 marks ops beyond the encodable window: the search
+                // stops (LC_CAUSE_WINDOW) before it could follow one.
+                if (ev & LC_EV_OK_BIT) {
+                    if (s == 127) continue;
+                    if (!((pend[s >> 6] >> (s & 63)) & 1)) { bad[t] = 1; badkey[t] = k; break; }
+                    pend[s >> 6] &= ~(1ull << (s & 63));
+                } else {
+                    if (tb + LC_EV_TRANS(ev) >= (uint64_t)b->n_trans) { bad[t] = 2; badkey[t] = k; break; }
+                    if (s == 127) continue;
+                    if ((pend[s >> 6] >> (s & 63)) & 1) { bad[t] = 3; badkey[t] = k; break; }
+                    pend[s >> 6] |= 1ull << (s & 63);
+                }
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    if (K >= 256)
+        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
+    else
+        nt = 1, bad.resize(1), badkey.resize(1);
+    work(0);
+    for (auto &th : pool) th.join();
+    for (size_t t = 0; t < bad.size(); ++t) {
+        static const char *why[] = {"", ":ok of a slot with no pending op", "transition id out of range",
+                                    ":invoke into an occupied slot"};
+        if (bad[t]) return lc::fail(LC_E_INVALID, "batch: key %lld: %s", (long long)badkey[t], why[bad[t]]);
+    }
+    for (int64_t i = 0; i < b->n_trans; ++i) {
+        uint32_t d = b->trans[i];
+        uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, bb = d >> 17;
+        if ((f == LC_T_WRITE || f == LC_T_CAS) && bb >= LC_STATE_NONE)
+            return lc::fail(LC_E_INVALID, "batch: transition %lld installs an invalid state", (long long)i);
+        (void)a;
+    }
+    return LC_OK;
+}
+
+extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
+    if (!c || !b || !out) return lc::fail(LC_E_INVALID, "lc_upload: null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = validate_batch(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    lc_dev_batch *d = new (std::nothrow) lc_dev_batch();
+    if (!d) return lc::fail(LC_E_NOMEM, "lc_upload: out of memory");
+    const int64_t K = b->n_keys;
+    d->device = c->device;
+    d->n_keys = K;
+    d->n_events = K ? b->ev_off[K] : 0;
+    d->n_trans = b->n_trans > 0 ? b->n_trans : 1;
+    d->init_state = b->init_state;
+    d->has_trans_off = b->trans_off != nullptr;
+    // LPT order: longest keys first
+    std::vector<int32_t> order((size_t)K);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+        return b->ev_off[x + 1] - b->ev_off[x] > b->ev_off[y + 1] - b->ev_off[y];
+    });
+    auto up = [&]() -> int {
+        HIPCHK(dalloc(&d->ev_off, (size_t)K + 1));
+        HIPCHK(dalloc(&d->events, (size_t)d->n_events));
+        HIPCHK(dalloc(&d->trans, (size_t)d->n_trans));
+        HIPCHK(dalloc(&d->order, (size_t)K));
+        if (K) {
+            HIPCHK(hipMemcpyAsync(d->ev_off, b->ev_off, ((size_t)K + 1) * 8, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(d->order, order.data(), (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
+        }
+        if (d->n_events)
+            HIPCHK(hipMemcpyAsync(d->events, b->events, (size_t)d->n_events * 4, hipMemcpyHostToDevice, c->stream));
+        if (b->n_trans > 0)
+            HIPCHK(hipMemcpyAsync(d->trans, b->trans, (size_t)b->n_trans * 4, hipMemcpyHostToDevice, c->stream));
+        if (b->trans_off && K) {
+            HIPCHK(dalloc(&d->trans_off, (size_t)K));
+            HIPCHK(hipMemcpyAsync(d->trans_off, b->trans_off, (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
+        }
+        if (b->key_width && K) {
+            HIPCHK(dalloc(&d->key_width, (size_t)K));
+            HIPCHK(hipMemcpyAsync(d->key_width, b->key_width, (size_t)K, hipMemcpyHostToDevice, c->stream));
+        }
+        if (b->key_states && K) {
+            HIPCHK(dalloc(&d->key_states, (size_t)K));
+            HIPCHK(hipMemcpyAsync(d->key_states, b->key_states, (size_t)K * 2, hipMemcpyHostToDevice, c->stream));
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return LC_OK;
+    };
+    rc = up();
+    if (rc) { delete d; return rc; }
+    d->input_bytes = (size_t)d->n_events * 4 + ((size_t)K + 1) * 8;
+    *out = d;
+    return LC_OK;
+}
+
+extern "C" void lc_dev_batch_free(lc_dev_batch *d) {
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    delete d;
+}
+
+extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, int dev_result, lc_stats *st) {
+    if (!c || !d || !r || !r->valid || !r->fail_event || !r->cause)
+        return lc::fail(LC_E_INVALID, "lc_check_device: null argument");
+    if (d->device != c->device) return lc::fail(LC_E_INVALID, "lc_check_device: batch lives on another device");
+    std::lock_guard<std::mutex> g(c->mu);
+    auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t K = d->n_keys;
+    if (K > 0x7FFFFFFF) return lc::fail(LC_E_INVALID, "lc_check_device: too many keys");
+    int rc = ensure_capacity(c, K);
+    if (rc) return rc;
+
+    lcd::Args a{};
+    a.ev_off = d->ev_off; a.events = d->events; a.trans = d->trans; a.trans_off = d->trans_off;
+    a.key_width = d->key_width; a.key_states = d->key_states;
+    a.init_state = d->init_state; a.budget = c->o.max_configs; a.max_final = c->o.max_final;
+    if (dev_result) {
+        a.valid = r->valid; a.fail_event = r->fail_event; a.cause = r->cause;
+        a.peak = r->peak_configs; a.final_cfg = r->final_configs; a.n_final = r->n_final;
+    } else {
+        a.valid = c->valid; a.fail_event = c->fail_event; a.cause = c->cause;
+        a.peak = c->peak; a.final_cfg = c->final_cfg; a.n_final = c->n_final;
+    }
+    a.probes = c->acc + 0; a.ev_count = c->acc + 1; a.keys_done = c->acc + 2;
+    int32_t *spill1 = c->lists, *spill2 = c->lists + c->cap_keys, *wide = c->lists + 2 * c->cap_keys;
+    int32_t *n_spill1 = c->counters + 0, *n_spill2 = c->counters + 1, *n_wide = c->counters + 2;
+
+    HIPCHK(hipMemsetAsync(c->counters, 0, 16 * sizeof(int32_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->acc, 0, 4 * sizeof(unsigned long long), c->stream));
+    if (a.n_final && K > 0) HIPCHK(hipMemsetAsync(a.n_final, 0, (size_t)K * 4, c->stream));
+    HIPCHK(hipEventRecord(c->e0, c->stream));
+    if (K > 0) {
+        // T1: every key, LPT order
+        lcd::Args a1 = a;
+        a1.order = d->order; a1.n_order = (int32_t)K; a1.n_in = nullptr; a1.ticket = c->counters + 4;
+        a1.spill = spill1; a1.n_spill = n_spill1; a1.wide = wide; a1.n_wide = n_wide;
+        int g1 = (int)std::min<int64_t>(K, (int64_t)c->cu_count * 7);
+        HIPCHK(lcd::launch_t1(a1, g1, c->stream));
+        // T2: keys that outgrew T1
+        lcd::Args a2 = a;
+        a2.order = spill1; a2.n_order = 0; a2.n_in = n_spill1; a2.ticket = c->counters + 5;
+        a2.spill = spill2; a2.n_spill = n_spill2; a2.wide = wide; a2.n_wide = n_wide;
+        HIPCHK(lcd::launch_t2(a2, c->cu_count, c->stream));
+        // T3 (HBM tier): keys beyond T2, keys needing wide configs
+        lcd::Args a3 = a;
+        a3.order = spill2; a3.n_in = n_spill2;
+        HIPCHK(lcd::launch_unhandled(a3, 64, c->stream));
+        a3.order = wide; a3.n_in = n_wide;
+        HIPCHK(lcd::launch_unhandled(a3, 64, c->stream));
+    }
+    HIPCHK(hipEventRecord(c->e1, c->stream));
+    unsigned long long acc[4] = {0, 0, 0, 0};
+    int32_t cnt[16];
+    HIPCHK(hipMemcpyAsync(acc, c->acc, sizeof acc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(cnt, c->counters, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    if (!dev_result && K > 0) {
+        HIPCHK(hipMemcpyAsync(r->valid, c->valid, (size_t)K, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(r->fail_event, c->fail_event, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(r->cause, c->cause, (size_t)K, hipMemcpyDeviceToHost, c->stream));
+        if (r->peak_configs)
+            HIPCHK(hipMemcpyAsync(r->peak_configs, c->peak, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+        if (r->final_configs)
+            HIPCHK(hipMemcpyAsync(r->final_configs, c->final_cfg, (size_t)K * c->o.max_final * 16,
+                                  hipMemcpyDeviceToHost, c->stream));
+        if (r->n_final)
+            HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    if (st) {
+        st->kernel_ms = ms;
+        st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        st->probes = acc[0];
+        st->events = acc[1];
+        st->lds_keys = acc[2];
+        st->deep_keys = (uint64_t)cnt[1] + (uint64_t)cnt[2];
+    }
+    return LC_OK;
+}
+
+extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_stats *st) {
+    auto t0 = std::chrono::steady_clock::now();
+    lc_dev_batch *d = nullptr;
+    int rc = lc_upload(c, b, &d);
+    if (rc) return rc;
+    rc = lc_check_device(c, d, r, 0, st);
+    lc_dev_batch_free(d);
+    if (st && rc == LC_OK)
+        st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}

@@ -1,0 +1,52 @@
+// Kernel argument block and launchers shared by device_search.hip and the
+// host orchestration in device_api.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace lcd {
+
+struct Args {
+    // packed batch (device pointers; include/lincheck.h lc_batch)
+    const uint64_t *ev_off;
+    const uint32_t *events;
+    const uint32_t *trans;
+    const uint32_t *trans_off;   // may be null
+    const uint8_t *key_width;    // may be null
+    const uint16_t *key_states;  // may be null
+    uint32_t init_state;
+    uint64_t budget;
+    int32_t max_final;
+    // work list of this launch: keys order[0 .. n) with n = n_in ? *n_in : n_order
+    const int32_t *order;
+    int32_t n_order;
+    const int32_t *n_in;
+    int32_t *ticket;         // zeroed before the launch
+    // per-key results (device pointers)
+    int8_t *valid;
+    int32_t *fail_event;
+    uint8_t *cause;
+    uint32_t *peak;          // may be null
+    uint64_t *final_cfg;     // may be null: [key][max_final][2]
+    uint32_t *n_final;       // may be null
+    // counters
+    unsigned long long *probes;
+    unsigned long long *ev_count;
+    unsigned long long *keys_done;
+    // output work lists
+    int32_t *spill;
+    int32_t *n_spill;
+    int32_t *wide;
+    int32_t *n_wide;
+};
+
+size_t lds_bytes_t1();
+size_t lds_bytes_t2();
+hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
+hipError_t launch_t2(const Args &a, int grid, hipStream_t s);
+hipError_t launch_unhandled(const Args &a, int grid, hipStream_t s);
+
+}  // namespace lcd

@@ -1,0 +1,422 @@
+// lc_pack: Jepsen history -> packed per-key event streams for the device search.
+//
+// Host-side restatement of the steps between the raw history and
+// knossos.linear's search loop:
+//
+//   A2 jepsen.independent/checker (etcdemo.clj:115): history-keys + subhistory.
+//      Ops whose :value is a tuple [k v] go to key k, unwrapped to v; ops with a
+//      non-tuple value (the nemesis :info :start/:stop of etcdemo.clj:138-143)
+//      belong to every key's sub-history.
+//   A3 knossos.history/complete + without-failures: an :invoke is paired with
+//      the next completion of the same :process.  :ok -> the invocation takes
+//      (or invocation-value completion-value) (a read learns what it read);
+//      :fail -> invocation and completion are dropped; :info, or no completion
+//      at all -> the op stays pending (callable) forever.  A second :invoke by a
+//      process with an op outstanding leaves the first pending forever (the
+//      pending index is overwritten, as complete's assoc! does).  A completion
+//      with no outstanding invocation is an error (complete asserts).
+//   A4/A5 knossos.model/cas-register + knossos.model.memo: every surviving op
+//      becomes a transition descriptor over interned register states (state 0
+//      = nil, the initial value of (model/cas-register), etcdemo.clj:117).
+//
+// The pending-window slot of each op (lowest free slot at invoke, released at
+// :ok) is assigned here too: it is config-independent, so every device config
+// can name linearized ops by slot bit.
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <unordered_map>
+
+#include "common.hpp"
+
+namespace {
+
+inline bool is_client_f(uint8_t f) { return f == LC_F_READ || f == LC_F_WRITE || f == LC_F_CAS; }
+
+// Small process -> outstanding-op map; linear scan while small, hash beyond.
+struct ProcMap {
+    std::vector<std::pair<int64_t, int32_t>> small;
+    std::unordered_map<int64_t, int32_t> big;
+    bool use_big = false;
+    int32_t *find(int64_t p) {
+        if (use_big) { auto it = big.find(p); return it == big.end() ? nullptr : &it->second; }
+        for (auto &e : small) if (e.first == p) return &e.second;
+        return nullptr;
+    }
+    void set(int64_t p, int32_t op) {
+        if (int32_t *x = find(p)) { *x = op; return; }
+        if (!use_big && small.size() >= 64) {
+            use_big = true;
+            for (auto &e : small) big.emplace(e.first, e.second);
+            small.clear();
+        }
+        if (use_big) big.emplace(p, op); else small.emplace_back(p, op);
+    }
+    void erase(int64_t p) {
+        if (use_big) { big.erase(p); return; }
+        for (size_t i = 0; i < small.size(); ++i)
+            if (small[i].first == p) { small[i] = small.back(); small.pop_back(); return; }
+    }
+};
+
+// One surviving client op of a key, before interning.
+struct KOp {
+    int64_t row_inv, row_ret;  // row_ret = -1: never returns
+    uint8_t f, fate;           // fate: 0 pending-forever, 1 ok, 2 failed
+    int64_t v0, v1;
+};
+
+struct KeyOut {
+    std::vector<uint32_t> ev;     // event words, trans field = local op index for now
+    std::vector<int64_t> ev_row;
+    std::vector<int32_t> ev_op;   // op index per invoke event (-1 for ok)
+    std::vector<KOp> ops;
+    int width = 0;
+    int err = 0;
+    std::string msg;
+};
+
+// Pairing + event emission for one key (rows in history order).
+void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, KeyOut &out) {
+    ProcMap pm;
+    out.ops.clear();
+    out.ops.reserve((size_t)nrows / 2 + 1);
+    std::vector<int32_t> row_op((size_t)nrows, -1);  // op created/completed at this row
+    for (int64_t i = 0; i < nrows; ++i) {
+        int64_t r = rows[i];
+        uint8_t t = h.type[r];
+        int64_t p = h.process[r];
+        if (t == LC_INVOKE) {
+            if (!is_client_f(h.f[r])) {
+                out.err = LC_E_UNSUPPORTED;
+                out.msg = "row " + std::to_string(r) + ": cas-register cannot step this :f";
+                return;
+            }
+            int32_t id = (int32_t)out.ops.size();
+            out.ops.push_back({r, -1, h.f[r], 0, h.v0[r], h.v1[r]});
+            pm.set(p, id);
+            row_op[(size_t)i] = id;
+        } else if (t == LC_OK_T || t == LC_FAIL) {
+            int32_t *pid = pm.find(p);
+            if (!pid) {
+                out.err = LC_E_INVALID;
+                out.msg = "row " + std::to_string(r) + ": process completed an operation without a prior invocation";
+                return;
+            }
+            KOp &op = out.ops[(size_t)*pid];
+            if (t == LC_OK_T) {
+                op.fate = 1;
+                op.row_ret = r;
+                // (or (:value invocation) (:value completion))
+                if (op.f == LC_F_CAS) {
+                    if (op.v0 == LC_NIL && op.v1 == LC_NIL) { op.v0 = h.v0[r]; op.v1 = h.v1[r]; }
+                } else if (op.v0 == LC_NIL) {
+                    op.v0 = h.v0[r];
+                }
+                row_op[(size_t)i] = *pid;
+            } else {
+                op.fate = 2;
+            }
+            pm.erase(p);
+        } else if (t == LC_INFO) {
+            if (pm.find(p)) pm.erase(p);  // crashed: pending forever
+        }
+    }
+    // Emit events in row order; assign window slots.
+    uint64_t freemask[2] = {~0ull, ~0ull};
+    std::vector<int8_t> slot_of(out.ops.size(), -1);
+    out.ev.reserve((size_t)nrows);
+    out.ev_row.reserve((size_t)nrows);
+    out.ev_op.reserve((size_t)nrows);
+    int maxslot = -1;
+    for (int64_t i = 0; i < nrows; ++i) {
+        int32_t id = row_op[(size_t)i];
+        if (id < 0) continue;
+        KOp &op = out.ops[(size_t)id];
+        if (op.fate == 2) continue;  // without-failures
+        int64_t r = rows[i];
+        if (h.type[r] == LC_INVOKE) {
+            int s;
+            if (freemask[0]) s = __builtin_ctzll(freemask[0]);
+            else if (freemask[1]) s = 64 + __builtin_ctzll(freemask[1]);
+            else s = 128;
+            if (s < 127) freemask[s >> 6] &= ~(1ull << (s & 63));
+            int enc = s < 127 ? s : 127;  // >= 127 cannot be encoded; the search stops earlier
+            slot_of[(size_t)id] = (int8_t)enc;
+            maxslot = std::max(maxslot, s);
+            out.ev.push_back(((uint32_t)enc << 24) | (uint32_t)id);
+            out.ev_op.push_back(id);
+        } else {
+            int s = slot_of[(size_t)id];
+            if (s < 127) freemask[s >> 6] |= 1ull << (s & 63);
+            out.ev.push_back(LC_EV_OK_BIT | ((uint32_t)s << 24));
+            out.ev_op.push_back(-1);
+        }
+        out.ev_row.push_back(r);
+    }
+    out.width = std::min(maxslot + 1, 255);
+}
+
+}  // namespace
+
+struct lc_packed {
+    std::vector<int64_t> keys;
+    std::vector<uint64_t> ev_off;
+    std::vector<uint32_t> events;
+    std::vector<int64_t> ev_row;
+    std::vector<uint32_t> trans;
+    std::vector<uint32_t> trans_off;  // empty = shared table
+    std::vector<uint8_t> key_width;
+    std::vector<uint16_t> key_states;
+    // sub-history rows: per-key rows + rows shared by every key
+    std::vector<uint64_t> krow_off;
+    std::vector<int64_t> krows;
+    std::vector<int64_t> shared_rows;
+    // state id -> register value: shared table, or per key (state_off[k] ..)
+    std::vector<int64_t> state_vals;  // index 0 unused (nil)
+    std::vector<uint64_t> state_off;  // empty = shared
+};
+
+extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed **out) {
+    if (!h || !out) return lc::fail(LC_E_INVALID, "lc_pack: null argument");
+    if (opts && opts->reserved != 0) return lc::fail(LC_E_INVALID, "lc_pack: opts.reserved must be 0");
+    if (h->n < 0 || (h->n > 0 && (!h->type || !h->f || !h->process || !h->key || !h->v0 || !h->v1)))
+        return lc::fail(LC_E_INVALID, "lc_pack: history arrays missing");
+    const int64_t n = h->n;
+    lc_packed *P = new (std::nothrow) lc_packed();
+    if (!P) return lc::fail(LC_E_NOMEM, "lc_pack: out of memory");
+    try {
+        // ---- A2: key discovery + bucketing (stable) ----
+        std::unordered_map<int64_t, int32_t> kidx;
+        std::vector<int32_t> row_key((size_t)n);
+        int64_t last_key = LC_NO_KEY;
+        int32_t last_idx = -1;
+        for (int64_t r = 0; r < n; ++r) {
+            if (h->type[r] > LC_INFO || h->f[r] > LC_F_OTHER) {
+                delete P;
+                return lc::fail(LC_E_INVALID, "lc_pack: row %lld has a bad :type/:f code", (long long)r);
+            }
+            int64_t k = h->key[r];
+            if (k == LC_NO_KEY) {
+                row_key[(size_t)r] = -1;
+                // Non-tuple ops are shared by every sub-history.  Only :info ops
+                // (the nemesis) are no-ops for the search; anything else would be
+                // stepped by the model with a non-register :f or value.
+                if (h->type[r] != LC_INFO) {
+                    delete P;
+                    return lc::fail(LC_E_UNSUPPORTED,
+                                    "lc_pack: row %lld: non-tuple op of :type other than :info", (long long)r);
+                }
+                P->shared_rows.push_back(r);
+                continue;
+            }
+            if (k != last_key || last_idx < 0) {
+                auto it = kidx.find(k);
+                if (it == kidx.end()) {
+                    it = kidx.emplace(k, (int32_t)P->keys.size()).first;
+                    P->keys.push_back(k);
+                }
+                last_key = k;
+                last_idx = it->second;
+            }
+            row_key[(size_t)r] = last_idx;
+        }
+        const int64_t K = (int64_t)P->keys.size();
+        P->krow_off.assign((size_t)K + 1, 0);
+        for (int64_t r = 0; r < n; ++r)
+            if (row_key[(size_t)r] >= 0) P->krow_off[(size_t)row_key[(size_t)r] + 1]++;
+        for (int64_t k = 0; k < K; ++k) P->krow_off[(size_t)k + 1] += P->krow_off[(size_t)k];
+        P->krows.resize((size_t)P->krow_off[(size_t)K]);
+        {
+            std::vector<uint64_t> cur(P->krow_off.begin(), P->krow_off.end() - 1);
+            for (int64_t r = 0; r < n; ++r)
+                if (row_key[(size_t)r] >= 0) P->krows[cur[(size_t)row_key[(size_t)r]]++] = r;
+        }
+        std::vector<int32_t>().swap(row_key);
+
+        // ---- A3: per-key pairing, fail-drop, slots (parallel over keys) ----
+        std::vector<KeyOut> ko((size_t)K);
+        unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        if (K < 64) nt = 1;
+        {
+            auto work = [&](unsigned t) {
+                for (int64_t k = t; k < K; k += nt)
+                    pack_key(*h, P->krows.data() + P->krow_off[(size_t)k],
+                             (int64_t)(P->krow_off[(size_t)k + 1] - P->krow_off[(size_t)k]), ko[(size_t)k]);
+            };
+            std::vector<std::thread> pool;
+            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
+            work(0);
+            for (auto &th : pool) th.join();
+        }
+        for (int64_t k = 0; k < K; ++k)
+            if (ko[(size_t)k].err) {
+                int code = ko[(size_t)k].err;
+                std::string msg = ko[(size_t)k].msg;
+                long long key = (long long)P->keys[(size_t)k];
+                delete P;
+                return lc::fail(code, "lc_pack: key %lld: %s", key, msg.c_str());
+            }
+
+        // ---- A4/A5: register states + transition descriptors ----
+        // A state is a value some surviving write / cas could install.
+        auto state_values = [&](const KeyOut &o, std::vector<int64_t> &vals) {
+            for (const KOp &op : o.ops) {
+                if (op.fate == 2) continue;
+                if (op.f == LC_F_WRITE && op.v0 != LC_NIL) vals.push_back(op.v0);
+                if (op.f == LC_F_CAS && op.v1 != LC_NIL) vals.push_back(op.v1);
+            }
+        };
+        std::unordered_map<int64_t, uint32_t> gstate;
+        bool shared = true;
+        for (int64_t k = 0; k < K && shared; ++k) {
+            std::vector<int64_t> vals;
+            state_values(ko[(size_t)k], vals);
+            for (int64_t v : vals) {
+                if (gstate.size() >= LC_NARROW_MAX_STATES - 1 && !gstate.count(v)) { shared = false; break; }
+                gstate.emplace(v, (uint32_t)gstate.size() + 1);
+            }
+        }
+        if (shared) {
+            P->state_vals.assign(gstate.size() + 1, LC_NIL);
+            for (auto &kv : gstate) P->state_vals[kv.second] = kv.first;
+        } else {
+            P->state_off.assign((size_t)K + 1, 0);
+        }
+        P->key_states.assign((size_t)K, 0);
+        P->key_width.assign((size_t)K, 0);
+        P->ev_off.assign((size_t)K + 1, 0);
+        for (int64_t k = 0; k < K; ++k) P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + ko[(size_t)k].ev.size();
+        P->events.resize((size_t)P->ev_off[(size_t)K]);
+        P->ev_row.resize((size_t)P->ev_off[(size_t)K]);
+
+        auto sid = [](const std::unordered_map<int64_t, uint32_t> &m, int64_t v) -> uint32_t {
+            if (v == LC_NIL) return 0;
+            auto it = m.find(v);
+            return it == m.end() ? LC_STATE_NONE : it->second;
+        };
+        auto make_desc = [&](const std::unordered_map<int64_t, uint32_t> &m, const KOp &op) -> uint32_t {
+            if (op.f == LC_F_READ)
+                return op.v0 == LC_NIL ? LC_DESC(LC_T_READ_ANY, 0, 0) : LC_DESC(LC_T_READ, sid(m, op.v0), 0);
+            if (op.f == LC_F_WRITE) return LC_DESC(LC_T_WRITE, 0, sid(m, op.v0));
+            return LC_DESC(LC_T_CAS, sid(m, op.v0), sid(m, op.v1));
+        };
+        std::unordered_map<uint32_t, uint32_t> gtrans;
+        if (!shared) P->trans_off.assign((size_t)K, 0);
+        for (int64_t k = 0; k < K; ++k) {
+            KeyOut &o = ko[(size_t)k];
+            std::unordered_map<int64_t, uint32_t> lstate;
+            std::unordered_map<uint32_t, uint32_t> ltrans;
+            const std::unordered_map<int64_t, uint32_t> *sm = &gstate;
+            std::unordered_map<uint32_t, uint32_t> *tm = &gtrans;
+            if (!shared) {
+                std::vector<int64_t> vals;
+                state_values(o, vals);
+                for (int64_t v : vals)
+                    if (lstate.size() < LC_STATE_NONE - 1) lstate.emplace(v, (uint32_t)lstate.size() + 1);
+                    else if (!lstate.count(v)) { lstate.emplace(v, LC_STATE_NONE); }
+                sm = &lstate;
+                tm = &ltrans;
+                P->state_off[(size_t)k] = P->state_vals.size();
+                size_t base_sv = P->state_vals.size();
+                P->state_vals.resize(base_sv + lstate.size() + 1, LC_NIL);
+                for (auto &kv : lstate)
+                    if (kv.second != LC_STATE_NONE) P->state_vals[base_sv + kv.second] = kv.first;
+                P->trans_off[(size_t)k] = (uint32_t)P->trans.size();
+                P->key_states[(size_t)k] = (uint16_t)std::min<size_t>(lstate.size() + 1, 65535);
+            } else {
+                std::vector<int64_t> vals;
+                state_values(o, vals);
+                std::sort(vals.begin(), vals.end());
+                P->key_states[(size_t)k] =
+                    (uint16_t)(std::unique(vals.begin(), vals.end()) - vals.begin() + 1);
+            }
+            uint64_t base = P->ev_off[(size_t)k];
+            for (size_t j = 0; j < o.ev.size(); ++j) {
+                uint32_t w = o.ev[j];
+                if (!(w & LC_EV_OK_BIT)) {
+                    uint32_t d = make_desc(*sm, o.ops[(size_t)o.ev_op[j]]);
+                    auto it = tm->find(d);
+                    uint32_t tid;
+                    if (it == tm->end()) {
+                        tid = (uint32_t)(P->trans.size() - (shared ? 0 : P->trans_off[(size_t)k]));
+                        tm->emplace(d, tid);
+                        P->trans.push_back(d);
+                    } else {
+                        tid = it->second;
+                    }
+                    if (tid > 0xFFFFFFu) {
+                        delete P;
+                        return lc::fail(LC_E_UNSUPPORTED, "lc_pack: more than 2^24 distinct operations");
+                    }
+                    w = (w & 0xFF000000u) | tid;
+                }
+                P->events[base + j] = w;
+                P->ev_row[base + j] = o.ev_row[j];
+            }
+            P->key_width[(size_t)k] = (uint8_t)o.width;
+            std::vector<uint32_t>().swap(o.ev);
+            std::vector<int64_t>().swap(o.ev_row);
+            std::vector<int32_t>().swap(o.ev_op);
+            std::vector<KOp>().swap(o.ops);
+        }
+        if (!shared) P->state_off[(size_t)K] = P->state_vals.size();
+        if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
+    } catch (const std::bad_alloc &) {
+        delete P;
+        return lc::fail(LC_E_NOMEM, "lc_pack: out of memory");
+    }
+    *out = P;
+    return LC_OK;
+}
+
+extern "C" void lc_packed_free(lc_packed *p) { delete p; }
+
+extern "C" int lc_packed_view(const lc_packed *p, lc_batch *b) {
+    if (!p || !b) return lc::fail(LC_E_INVALID, "lc_packed_view: null argument");
+    b->n_keys = (int64_t)p->keys.size();
+    b->ev_off = p->ev_off.data();
+    b->events = p->events.data();
+    b->trans = p->trans.data();
+    b->n_trans = (int64_t)p->trans.size();
+    b->trans_off = p->trans_off.empty() ? nullptr : p->trans_off.data();
+    b->key_width = p->key_width.data();
+    b->key_states = p->key_states.data();
+    b->init_state = 0;
+    return LC_OK;
+}
+
+extern "C" int64_t lc_packed_key(const lc_packed *p, int64_t i) {
+    if (!p || i < 0 || i >= (int64_t)p->keys.size()) return lc::fail(LC_E_INVALID, "lc_packed_key: bad index"), LC_NO_KEY;
+    return p->keys[(size_t)i];
+}
+
+extern "C" int64_t lc_packed_event_row(const lc_packed *p, int64_t i, int64_t j) {
+    if (!p || i < 0 || i >= (int64_t)p->keys.size()) return lc::fail(LC_E_INVALID, "lc_packed_event_row: bad key");
+    uint64_t b = p->ev_off[(size_t)i], e = p->ev_off[(size_t)i + 1];
+    if (j < 0 || (uint64_t)j >= e - b) return lc::fail(LC_E_INVALID, "lc_packed_event_row: bad event");
+    return p->ev_row[b + (uint64_t)j];
+}
+
+extern "C" int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows) {
+    if (!p || i < 0 || i >= (int64_t)p->keys.size()) return lc::fail(LC_E_INVALID, "lc_packed_subhistory: bad key");
+    const int64_t *a = p->krows.data() + p->krow_off[(size_t)i];
+    int64_t na = (int64_t)(p->krow_off[(size_t)i + 1] - p->krow_off[(size_t)i]);
+    const int64_t *s = p->shared_rows.data();
+    int64_t ns = (int64_t)p->shared_rows.size();
+    if (out_rows) std::merge(a, a + na, s, s + ns, out_rows);
+    return na + ns;
+}
+
+extern "C" int lc_packed_state_value(const lc_packed *p, int64_t i, uint32_t s, int64_t *value, int *is_nil) {
+    if (!p || !value || !is_nil || i < 0 || i >= (int64_t)p->keys.size())
+        return lc::fail(LC_E_INVALID, "lc_packed_state_value: bad argument");
+    if (s == 0) { *is_nil = 1; *value = LC_NIL; return LC_OK; }
+    uint64_t base = p->state_off.empty() ? 0 : p->state_off[(size_t)i];
+    uint64_t lim = p->state_off.empty() ? p->state_vals.size() : p->state_off[(size_t)i + 1];
+    if (base + s >= lim) return lc::fail(LC_E_INVALID, "lc_packed_state_value: state %u out of range", s);
+    *is_nil = 0;
+    *value = p->state_vals[base + s];
+    return LC_OK;
+}

@@ -1,0 +1,192 @@
+"""Jepsen histories <-> the struct-of-arrays lc_history of include/lincheck.h.
+
+An op is a dict with Jepsen's keys as strings: "type" (invoke/ok/fail/info),
+"f" (read/write/cas/...), "value", "process", optional "index", "time",
+"error".  Independent ops carry `independent.tuple(k, v)` values
+(etcdemo.clj:90, :120); cas values are [old new] lists (etcdemo.clj:69).
+
+`History` keeps the integer columns the C ABI consumes; this is the
+marshalling the Clojure side does before its JNA call.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .independent import Tuple, is_tuple
+
+TYPES = {"invoke": N.LC_INVOKE, "ok": N.LC_OK_T, "fail": N.LC_FAIL, "info": N.LC_INFO}
+TYPE_NAMES = {v: k for k, v in TYPES.items()}
+FS = {"read": N.LC_F_READ, "write": N.LC_F_WRITE, "cas": N.LC_F_CAS}
+F_NAMES = {v: k for k, v in FS.items()}
+NIL = N.LC_NIL
+
+
+def _int_or_nil(v, what: str) -> int:
+    if v is None:
+        return NIL
+    if isinstance(v, bool) or not isinstance(v, (int, np.integer)):
+        raise ValueError(f"{what}: only integer (or nil) register values are supported, got {v!r}")
+    v = int(v)
+    if v == NIL:
+        raise ValueError(f"{what}: {v} is reserved for nil")
+    return v
+
+
+class History:
+    """Columns of one history (numpy arrays, history order)."""
+
+    def __init__(self, type_, f, process, key, v0, v1, index, other_f=None):
+        self.type = np.ascontiguousarray(type_, dtype=np.uint8)
+        self.f = np.ascontiguousarray(f, dtype=np.uint8)
+        self.process = np.ascontiguousarray(process, dtype=np.int64)
+        self.key = np.ascontiguousarray(key, dtype=np.int64)
+        self.v0 = np.ascontiguousarray(v0, dtype=np.int64)
+        self.v1 = np.ascontiguousarray(v1, dtype=np.int64)
+        self.index = np.ascontiguousarray(index, dtype=np.int64)
+        self.other_f = other_f or {}   # row -> original :f name for LC_F_OTHER rows
+        self.anomalous_keys: List[int] = []
+
+    def __len__(self):
+        return int(self.type.shape[0])
+
+    # -- construction -------------------------------------------------------
+    @classmethod
+    def from_ops(cls, ops: Sequence[dict], default_key: Optional[int] = None) -> "History":
+        """Columns of a list of op maps.  default_key files non-tuple client ops
+        under that key (a single key's unwrapped sub-history, etcdemo.clj:117)."""
+        n = len(ops)
+        t = np.empty(n, np.uint8); f = np.empty(n, np.uint8)
+        p = np.empty(n, np.int64); k = np.empty(n, np.int64)
+        a = np.empty(n, np.int64); b = np.empty(n, np.int64); ix = np.empty(n, np.int64)
+        other = {}
+        for i, op in enumerate(ops):
+            try:
+                t[i] = TYPES[op["type"]]
+            except KeyError:
+                raise ValueError(f"op {i}: bad :type {op.get('type')!r}")
+            fn = op.get("f")
+            f[i] = FS.get(fn, N.LC_F_OTHER)
+            if f[i] == N.LC_F_OTHER:
+                other[i] = fn
+            proc = op.get("process")
+            p[i] = proc if isinstance(proc, (int, np.integer)) and not isinstance(proc, bool) else N.LC_NO_PROCESS
+            v = op.get("value")
+            if is_tuple(v):
+                k[i] = _int_or_nil(v[0], f"op {i} key")
+                v = v[1]
+            elif default_key is not None and f[i] != N.LC_F_OTHER:
+                k[i] = default_key
+            else:
+                k[i] = N.LC_NO_KEY
+            if f[i] == N.LC_F_CAS:
+                if v is None:
+                    a[i] = b[i] = NIL
+                else:
+                    if len(v) != 2:
+                        raise ValueError(f"op {i}: cas value must be [old new], got {v!r}")
+                    a[i] = _int_or_nil(v[0], f"op {i}"); b[i] = _int_or_nil(v[1], f"op {i}")
+            elif f[i] == N.LC_F_OTHER:
+                a[i] = b[i] = NIL
+            else:
+                a[i] = _int_or_nil(v, f"op {i}"); b[i] = NIL
+            idx = op.get("index")
+            ix[i] = idx if isinstance(idx, (int, np.integer)) else -1
+        return cls(t, f, p, k, a, b, ix, other)
+
+    @classmethod
+    def _from_owned(cls, handle) -> "History":
+        L = N.lib()
+        v = N.LcHistory()
+        N.check(L.lc_hist_view(handle, C.byref(v)))
+        n = v.n
+        h = cls(N.carray(v.type, n, np.uint8), N.carray(v.f, n, np.uint8),
+                N.carray(v.process, n, np.int64), N.carray(v.key, n, np.int64),
+                N.carray(v.v0, n, np.int64), N.carray(v.v1, n, np.int64),
+                N.carray(v.index, n, np.int64))
+        na = L.lc_hist_anomalous_keys(handle, None)
+        if na > 0:
+            buf = np.zeros(na, np.int64)
+            L.lc_hist_anomalous_keys(handle, N.ptr(buf, C.c_int64))
+            h.anomalous_keys = buf.tolist()
+        L.lc_hist_free(handle)
+        return h
+
+    # -- views --------------------------------------------------------------
+    def as_c(self) -> N.LcHistory:
+        h = N.LcHistory()
+        h.n = len(self)
+        h.type = N.ptr(self.type, C.c_uint8); h.f = N.ptr(self.f, C.c_uint8)
+        h.process = N.ptr(self.process, C.c_int64); h.key = N.ptr(self.key, C.c_int64)
+        h.v0 = N.ptr(self.v0, C.c_int64); h.v1 = N.ptr(self.v1, C.c_int64)
+        h.index = N.ptr(self.index, C.c_int64)
+        h._keep = self  # arrays stay alive with the struct
+        return h
+
+    def op(self, i: int) -> dict:
+        """Row i as a Jepsen op map (tuples re-wrapped)."""
+        i = int(i)
+        f = int(self.f[i])
+        fn = F_NAMES.get(f, self.other_f.get(i, "nemesis" if f == N.LC_F_OTHER else f))
+        nil = lambda x: None if x == NIL else int(x)
+        if f == N.LC_F_CAS:
+            val = [nil(self.v0[i]), nil(self.v1[i])]
+        elif f == N.LC_F_OTHER:
+            val = None
+        else:
+            val = nil(self.v0[i])
+        if self.key[i] != N.LC_NO_KEY:
+            val = Tuple(int(self.key[i]), val)
+        proc = int(self.process[i])
+        op = {"type": TYPE_NAMES[int(self.type[i])], "f": fn, "value": val,
+              "process": "nemesis" if proc == N.LC_NO_PROCESS else proc}
+        op["index"] = int(self.index[i]) if self.index[i] >= 0 else i
+        return op
+
+    def to_ops(self) -> List[dict]:
+        return [self.op(i) for i in range(len(self))]
+
+
+# ---- generator / EDN --------------------------------------------------------
+def synth(n_keys: int, ops_per_key: int, concurrency: int = 10, *, n_values: int = 5,
+          info_rate: float = 0.0, info_effect_p: float = 0.5, anomaly_rate: float = 0.0,
+          mean_think: float = 1.0, mean_latency: float = 1.0, interleave: bool = False,
+          nemesis_period: float = 0.0, seed: int = 1, key_base: int = 0) -> History:
+    """Synthetic cas-register history (lc_synth_generate)."""
+    o = N.LcSynthOpts(n_keys, ops_per_key, concurrency, n_values, info_rate, info_effect_p,
+                      anomaly_rate, mean_think, mean_latency, int(interleave), nemesis_period,
+                      seed, key_base)
+    handle = C.c_void_p()
+    N.check(N.lib().lc_synth_generate(C.byref(o), C.byref(handle)))
+    return History._from_owned(handle)
+
+
+CONFIGS = {
+    # SURVEY.md 8(d) D-2 / BASELINE.md
+    "C1": dict(n_keys=6, ops_per_key=100, concurrency=10, interleave=True, nemesis_period=5.0, seed=1),
+    "C2": dict(n_keys=1000, ops_per_key=1000, concurrency=10, seed=2),
+    "C3": dict(n_keys=100_000, ops_per_key=2000, concurrency=10, seed=3),
+    "C4": dict(n_keys=256, ops_per_key=5000, concurrency=30, info_rate=0.02, seed=4),
+    "C5": dict(n_keys=1000, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=5),
+}
+
+
+def read_edn(path: str) -> History:
+    handle = C.c_void_p()
+    N.check(N.lib().lc_edn_read(path.encode(), C.byref(handle)))
+    return History._from_owned(handle)
+
+
+def parse_edn(text: str) -> History:
+    raw = text.encode()
+    handle = C.c_void_p()
+    N.check(N.lib().lc_edn_parse(raw, len(raw), C.byref(handle)))
+    return History._from_owned(handle)
+
+
+def write_edn(path: str, h: History) -> None:
+    N.check(N.lib().lc_edn_write(path.encode(), C.byref(h.as_c())))

@@ -1,0 +1,51 @@
+"""ctypes loader for oracle/_build/liboracle.so -- TEST ORACLE (see linear_ref.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "_build", "liboracle.so")
+
+
+class OracleKeyResult(C.Structure):
+    _fields_ = [("valid", C.c_int8), ("cause", C.c_uint8), ("fail_event", C.c_int32),
+                ("peak", C.c_uint32), ("probes", C.c_uint64), ("n_events", C.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            raise ImportError(f"{SO} missing: run `make -C oracle`")
+        L = C.CDLL(SO)
+        L.oracle_check_history.restype = C.c_int64
+        L.oracle_check_history.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
+        _lib = L
+    return _lib
+
+
+def check_history(hist_c, budget: int = 1 << 20, threads: int = 1):
+    """Run the C restatement over an lc_history struct (lincheck.history.History.as_c()).
+
+    Returns (keys, structured numpy array of per-key results)."""
+    L = lib()
+    nk = L.oracle_check_history(C.byref(hist_c), budget, threads, None, None, 0)
+    if nk < 0:
+        raise RuntimeError(f"oracle_check_history failed: {nk}")
+    keys = np.zeros(max(nk, 1), np.int64)
+    res = (OracleKeyResult * max(nk, 1))()
+    rc = L.oracle_check_history(C.byref(hist_c), budget, threads, keys.ctypes.data, C.addressof(res), nk)
+    if rc < 0:
+        raise RuntimeError(f"oracle_check_history failed: {rc}")
+    arr = np.ctypeslib.as_array(res)[:nk].copy()
+    return keys[:nk], arr
