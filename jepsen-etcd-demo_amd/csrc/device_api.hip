@@ -83,9 +83,17 @@ struct lc_ctx {
     uint32_t *peak = nullptr;
     uint64_t *final_cfg = nullptr;
     uint32_t *n_final = nullptr;
+    // T3 (HBM tier) workspaces: narrow / wide configs
+    struct Ws {
+        char *base = nullptr;
+        size_t bytes = 0;
+        int slots = 0;
+        lcd::HbmWs w{};
+    } ws[2];
     ~lc_ctx() {
         dfree(lists); dfree(counters); dfree(acc); dfree(valid); dfree(fail_event);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
+        dfree(ws[0].base); dfree(ws[1].base);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -105,6 +113,50 @@ static int ensure_capacity(lc_ctx *c, int64_t n_keys) {
     HIPCHK(dalloc(&c->final_cfg, (size_t)cap * (size_t)c->o.max_final * 2));
     HIPCHK(dalloc(&c->n_final, (size_t)cap));
     c->cap_keys = cap;
+    return LC_OK;
+}
+
+// Lay out (and if needed allocate) a T3 workspace for `want` blocks.
+static int ensure_ws(lc_ctx *c, int wide, int want, int *slots_out) {
+    lc_ctx::Ws &W = c->ws[wide];
+    const size_t cfg = wide ? lcd::cfg_bytes_wide() : lcd::cfg_bytes_narrow();
+    const uint64_t cap = c->o.max_configs + (uint64_t)lcd::t3_block() + 64;
+    uint64_t H = 1;
+    while (H < 2 * cap) H <<= 1;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    lcd::HbmWs w{};
+    size_t off = 0;
+    w.off_S0 = off; off += al(cap * cfg);
+    w.off_S1 = off; off += al(cap * cfg);
+    w.off_I = off; off += al(cap * cfg);
+    w.off_hS = off; off += al(H * cfg);
+    w.off_hI = off; off += al(H * cfg);
+    w.off_pS0 = off; off += al(cap * 4);
+    w.off_pS1 = off; off += al(cap * 4);
+    w.off_pI = off; off += al(cap * 4);
+    w.slot_bytes = off;
+    w.cap = (uint32_t)cap;
+    w.hmask = (uint32_t)(H - 1);
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const int max_slots = c->o.deep_slots > 0 ? c->o.deep_slots : 2 * c->cu_count;
+    int slots = std::min(want, max_slots);
+    const size_t limit = (W.bytes ? W.bytes : 0) + free_b / 2;
+    while (slots > 1 && (size_t)slots * w.slot_bytes > limit) slots /= 2;
+    if ((size_t)slots * w.slot_bytes > limit)
+        return lc::fail(LC_E_NOMEM, "T3 workspace: one slot needs %zu bytes (budget %llu)", w.slot_bytes,
+                        (unsigned long long)c->o.max_configs);
+    if (!W.base || W.w.slot_bytes != w.slot_bytes || W.slots < slots) {
+        dfree(W.base);
+        W.bytes = 0; W.slots = 0;
+        HIPCHK(hipMalloc((void **)&W.base, (size_t)slots * w.slot_bytes));
+        HIPCHK(hipMemsetAsync(W.base, 0xFF, (size_t)slots * w.slot_bytes, c->stream));  // EMPTY tables
+        W.bytes = (size_t)slots * w.slot_bytes;
+        W.slots = slots;
+    }
+    w.base = W.base;
+    W.w = w;
+    *slots_out = std::min(slots, W.slots);
     return LC_OK;
 }
 
@@ -325,12 +377,29 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         a2.order = spill1; a2.n_order = 0; a2.n_in = n_spill1; a2.ticket = c->counters + 5;
         a2.spill = spill2; a2.n_spill = n_spill2; a2.wide = wide; a2.n_wide = n_wide;
         HIPCHK(lcd::launch_t2(a2, c->cu_count, c->stream));
-        // T3 (HBM tier): keys beyond T2, keys needing wide configs
+        // T3 (HBM tier): keys beyond T2, then keys needing wide configs.
+        // The work-list lengths size the workspace, so read them back first.
+        int32_t cnt3[3];
+        HIPCHK(hipMemcpyAsync(cnt3, c->counters, sizeof cnt3, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
         lcd::Args a3 = a;
-        a3.order = spill2; a3.n_in = n_spill2;
-        HIPCHK(lcd::launch_unhandled(a3, 64, c->stream));
-        a3.order = wide; a3.n_in = n_wide;
-        HIPCHK(lcd::launch_unhandled(a3, 64, c->stream));
+        a3.wide = wide; a3.n_wide = n_wide;
+        if (cnt3[1] > 0) {
+            int slots = 0;
+            rc = ensure_ws(c, 0, cnt3[1], &slots);
+            if (rc) return rc;
+            a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 6;
+            HIPCHK(lcd::launch_t3_narrow(a3, c->ws[0].w, slots, c->stream));
+            HIPCHK(hipMemcpyAsync(cnt3, c->counters, sizeof cnt3, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
+        if (cnt3[2] > 0) {
+            int slots = 0;
+            rc = ensure_ws(c, 1, cnt3[2], &slots);
+            if (rc) return rc;
+            a3.order = wide; a3.n_order = 0; a3.n_in = n_wide; a3.ticket = c->counters + 7;
+            HIPCHK(lcd::launch_t3_wide(a3, c->ws[1].w, slots, c->stream));
+        }
     }
     HIPCHK(hipEventRecord(c->e1, c->stream));
     unsigned long long acc[4] = {0, 0, 0, 0};

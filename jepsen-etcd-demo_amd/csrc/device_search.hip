@@ -18,7 +18,8 @@
 //   T1  one wavefront per key, S / S' / I and two open-addressed hash sets in
 //       LDS (~20 KB per wave, 8 waves per CU): the common case.
 //   T2  the same code with ~6x the LDS (1 wave per CU).
-//   T3  (HBM tier) keys beyond T2 or needing > 56 window slots.
+//   T3  (HBM tier, device_hbm.hip) keys beyond T2 or needing > 56 window
+//       slots / > 255 register states.
 //
 // Hash sets: open addressing, linear probing, 64-bit ds_cmpst (LDS) CAS on
 // EMPTY; the slot each new config landed in is remembered so the table is
@@ -31,82 +32,9 @@
 
 #include "../../include/lincheck.h"
 #include "device_search.hpp"
+#include "device_common.hpp"
 
 namespace lcd {
-
-constexpr uint64_t EMPTY = ~0ull;
-constexpr uint64_t LMASK = (1ull << 56) - 1;
-
-__device__ __forceinline__ uint32_t hash64(uint64_t c) {
-    c ^= c >> 29;
-    c *= 0xBF58476D1CE4E5B9ull;
-    return (uint32_t)(c >> 32) ^ (uint32_t)c;
-}
-
-// cas-register step on a descriptor (include/lincheck.h LC_T_*), branch-free:
-//   READ_ANY: legal, same state   READ: legal iff s == a, same state
-//   WRITE:    legal, state := b   CAS:  legal iff s == a, state := b
-__device__ __forceinline__ bool step(uint32_t s, uint32_t d, uint32_t &s2) {
-    uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
-    s2 = f >= LC_T_WRITE ? b : s;
-    return f == LC_T_READ_ANY || f == LC_T_WRITE || s == a;
-}
-
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-
-// Rank of this lane among the lanes whose flag is set (wave-synchronous).
-__device__ __forceinline__ uint32_t rank_of(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-// Insert key into an LDS hash set; returns true if it was not there.
-// pos receives the table slot holding key.
-__device__ __forceinline__ bool lds_insert(uint64_t *tab, uint32_t mask, uint64_t key, bool active,
-                                           uint32_t &pos) {
-    bool isnew = false;
-    uint32_t h = hash64(key) & mask;
-    bool done = !active;
-    while (!done) {
-        unsigned long long old = atomicCAS((unsigned long long *)&tab[h], (unsigned long long)EMPTY,
-                                           (unsigned long long)key);
-        if (old == EMPTY) { isnew = true; done = true; }
-        else if (old == key) { done = true; }
-        else { h = (h + 1) & mask; }
-    }
-    pos = h;
-    return isnew;
-}
-
-__device__ __forceinline__ void write_final(const Args &a, int32_t key, const uint64_t *S, uint32_t nS) {
-    if (!a.final_cfg) return;
-    uint32_t nf = nS < (uint32_t)a.max_final ? nS : (uint32_t)a.max_final;
-    for (uint32_t i = lane_id(); i < nf; i += 64) {
-        uint64_t c = S[i];
-        a.final_cfg[((size_t)key * a.max_final + i) * 2 + 0] = c & LMASK;
-        a.final_cfg[((size_t)key * a.max_final + i) * 2 + 1] = (c >> 56) << 48;
-    }
-    if (lane_id() == 0 && a.n_final) a.n_final[key] = nf;
-}
-
-__device__ __forceinline__ void push_list(int32_t *list, int32_t *count, int32_t key) {
-    if (lane_id() == 0) {
-        int32_t i = atomicAdd(count, 1);
-        list[i] = key;
-    }
-}
-
-__device__ __forceinline__ void finish_key(const Args &a, int32_t key, int verdict, int cause,
-                                           int32_t fev, uint32_t peak, uint64_t probes, uint64_t nev) {
-    if (lane_id() == 0) {
-        a.valid[key] = (int8_t)verdict;
-        a.cause[key] = (uint8_t)cause;
-        a.fail_event[key] = fev;
-        if (a.peak) a.peak[key] = peak;
-        atomicAdd(a.probes, (unsigned long long)probes);
-        atomicAdd(a.ev_count, (unsigned long long)nev);
-        atomicAdd(a.keys_done, 1ull);
-    }
-}
 
 // ---------------------------------------------------------------- LDS tiers
 template <int CAP_S, int CAP_I>
@@ -123,8 +51,6 @@ struct LdsTier {
     uint8_t slotlist[64];
 };
 
-// Outcome of searching one key in a tier.
-enum { K_DONE = 0, K_SPILL = 1, K_WIDE = 2 };
 
 template <int CAP_S, int CAP_I>
 __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> &t) {
@@ -248,7 +174,7 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
             if (overflow) {
                 if (verdict == LC_UNKNOWN) {
                     fev = (int32_t)(base + i - b);
-                    write_final(a, key, S, nS);
+                    write_final_narrow(a, key, S, nS);
                     finish_key(a, key, verdict, cause, fev, peak, probes, base + i - b);
                     return K_DONE;
                 }
@@ -276,13 +202,13 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
             nI_last = nI < CAP_I ? nI : CAP_I;
             if (nSn == 0) {
                 verdict = LC_INVALID; cause = LC_CAUSE_NONLIN; fev = (int32_t)(base + i - b);
-                write_final(a, key, S, nS);
+                write_final_narrow(a, key, S, nS);
                 finish_key(a, key, verdict, cause, fev, peak, probes, base + i + 1 - b);
                 return K_DONE;
             }
             if (nSn > a.budget) {
                 verdict = LC_UNKNOWN; cause = LC_CAUSE_BUDGET; fev = (int32_t)(base + i - b);
-                write_final(a, key, S, nS);
+                write_final_narrow(a, key, S, nS);
                 finish_key(a, key, verdict, cause, fev, peak, probes, base + i - b);
                 return K_DONE;
             }
@@ -296,17 +222,9 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
             pending &= ~pbit;
         }
     }
-    write_final(a, key, t.S[cur], nS);
+    write_final_narrow(a, key, t.S[cur], nS);
     finish_key(a, key, LC_VALID, LC_CAUSE_NONE, -1, peak, probes, e - b);
     return K_DONE;
-}
-
-// Next entry of this launch's work list (dynamic: one atomic ticket per key,
-// so long keys -- listed first by the host's LPT order -- do not serialise).
-__device__ __forceinline__ int32_t next_work(const Args &a) {
-    int32_t w = 0;
-    if (lane_id() == 0) w = atomicAdd(a.ticket, 1);
-    return __builtin_amdgcn_readfirstlane(w);
 }
 
 template <int CAP_S, int CAP_I>
@@ -335,26 +253,6 @@ hipError_t launch_t1(const Args &a, int grid, hipStream_t s) {
 }
 hipError_t launch_t2(const Args &a, int grid, hipStream_t s) {
     hipLaunchKernelGGL((k_search_lds<T2_S, T2_I>), dim3(grid), dim3(64), 0, s, a);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------- HBM tier
-// Placeholder until the HBM tier lands: keys that outgrow T2 or need wide
-// configs are reported :unknown with cause LC_CAUSE_ERROR (never silently).
-__global__ __launch_bounds__(64) void k_unhandled(Args a) {
-    const int32_t n = *a.n_in;
-    for (int32_t w = blockIdx.x * 64 + threadIdx.x; w < n; w += gridDim.x * 64) {
-        const int32_t key = a.order[w];
-        a.valid[key] = LC_UNKNOWN;
-        a.cause[key] = LC_CAUSE_ERROR;
-        a.fail_event[key] = -1;
-        if (a.peak) a.peak[key] = 0;
-        if (a.n_final) a.n_final[key] = 0;
-    }
-}
-
-hipError_t launch_unhandled(const Args &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_unhandled, dim3(grid), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

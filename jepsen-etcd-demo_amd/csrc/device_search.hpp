@@ -43,10 +43,23 @@ struct Args {
     int32_t *n_wide;
 };
 
+// Per-block HBM workspace of the T3 tier (one slot per resident block).
+struct HbmWs {
+    char *base;
+    size_t slot_bytes;
+    uint32_t cap;    // array capacity per set (budget + block + margin)
+    uint32_t hmask;  // hash slots - 1
+    size_t off_S0, off_S1, off_I, off_hS, off_hI, off_pS0, off_pS1, off_pI;
+};
+
 size_t lds_bytes_t1();
 size_t lds_bytes_t2();
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t2(const Args &a, int grid, hipStream_t s);
-hipError_t launch_unhandled(const Args &a, int grid, hipStream_t s);
+hipError_t launch_t3_narrow(const Args &a, const HbmWs &w, int grid, hipStream_t s);
+hipError_t launch_t3_wide(const Args &a, const HbmWs &w, int grid, hipStream_t s);
+int t3_block();
+size_t cfg_bytes_narrow();
+size_t cfg_bytes_wide();
 
 }  // namespace lcd

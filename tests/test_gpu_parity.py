@@ -41,3 +41,32 @@ def test_tight_budget_unknown(device):
 def test_high_concurrency_spills_to_t2(device):
     h = H.synth(n_keys=64, ops_per_key=600, concurrency=16, seed=17)
     _, res, _ = device_vs_oracle(h, device)
+
+
+def test_c4_shape_crashed_ops_wide(device):
+    """Crashed (:info) write/cas ops stay callable forever: frontier blow-up,
+    > 56 window slots (wide configs, HBM tier), budget -> :unknown."""
+    dev = Device(0, budget=1 << 14)
+    h = H.synth(n_keys=24, ops_per_key=2000, concurrency=30, info_rate=0.02, seed=4)
+    _, res, _ = device_vs_oracle(h, dev, budget=1 << 14)
+    assert (res.valid == -1).sum() > 0
+
+
+def test_many_register_values_wide(device):
+    """> 255 distinct register values in a key: per-key state tables, wide configs."""
+    h = H.synth(n_keys=32, ops_per_key=600, concurrency=8, n_values=5000, anomaly_rate=0.2, seed=21)
+    device_vs_oracle(h, device)
+
+
+def test_window_overflow(device):
+    """More than 112 ops pending at once -> :unknown (cause window), as the oracle."""
+    from lincheck.independent import Tuple
+    ops = []
+    for p in range(120):
+        ops.append({"type": "invoke", "f": "read", "value": Tuple(0, None), "process": p})
+    ops.append({"type": "ok", "f": "read", "value": Tuple(0, None), "process": 0})
+    ops.append({"type": "invoke", "f": "write", "value": Tuple(1, 3), "process": 500})
+    ops.append({"type": "ok", "f": "write", "value": Tuple(1, 3), "process": 500})
+    _, res, _ = device_vs_oracle(H.History.from_ops(ops), device)
+    assert list(res.valid) == [-1, 1]
+    assert list(res.cause) == [3, 0]
