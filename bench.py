@@ -1,0 +1,202 @@
+"""Benchmark: history ops linearizability-checked per second (BASELINE.json metric).
+
+One step = one pass of the device search (liblincheck.so, lc_check_device)
+over one batch of synthetic cas-register histories already resident in HBM,
+with the per-key verdict records left on the device and, for N > 1,
+all-gathered across ranks over RCCL (the one exchange step of the path,
+SURVEY.md 8(e)).
+
+Workload (N=1 = BASELINE.json configs[1], "C2"): 1,000 keys x 1,000 client
+ops, concurrency 10, cas-register over values 0..4 (etcdemo.clj:67-69),
+seed 2.  Weak scaling: rank r checks keys [r*1000, (r+1)*1000) of the same
+seeded key space, so per-GPU work is fixed as N grows.
+
+Also reported (one JSON line on rank 0):
+  roofline      the search kernels' algorithmic HBM bytes per launch over
+                their HIP-event time (DESIGN.md "Measurement"), MI355X
+                peak 8 TB/s; traffic from profiles/*pmc*.json if committed.
+  cpu_baseline  the C restatement of knossos.linear (oracle/linear_ref.c,
+                kind "port") on this host's cores, same workload (rank 0, N=1).
+"""
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "jepsen-etcd-demo_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    "C2": dict(keys=1000, ops=1000, concurrency=10, info_rate=0.0, anomaly_rate=0.0, seed=2,
+               desc="C2: 1,000 keys x 1,000 ops per GPU, concurrency 10, cas-register values 0..4, all linearizable"),
+    "C3": dict(keys=100_000, ops=2000, concurrency=10, info_rate=0.0, anomaly_rate=0.0, seed=3,
+               desc="C3 shard: 100,000 keys x 2,000 ops per GPU, concurrency 10"),
+    "C4": dict(keys=256, ops=5000, concurrency=30, info_rate=0.02, anomaly_rate=0.0, seed=4,
+               desc="C4: 256 keys x 5,000 ops, concurrency 30, 2% crashed write/cas"),
+    "C5": dict(keys=1000, ops=1000, concurrency=10, info_rate=0.0, anomaly_rate=0.05, seed=5,
+               desc="C5: C2 shape with stale reads / lost cas in 5% of keys"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--budget", type=int, default=1 << 20)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from lincheck import history as H
+    from lincheck import _native as N
+    from lincheck.checker import Device, Packed
+
+    cfg = CONFIGS[args.config]
+    K, ops = cfg["keys"], cfg["ops"]
+    t_gen = time.time()
+    hist = H.synth(n_keys=K, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
+                   anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"], key_base=rank * K)
+    packed = Packed(hist)
+    t_gen = time.time() - t_gen
+    dev = Device(local, budget=args.budget)
+    db = dev.upload(packed)
+
+    # device-resident result arrays (torch tensors) -> no D2H inside the step
+    tdev = torch.device("cuda", local)
+    valid = torch.empty(K, dtype=torch.int8, device=tdev)
+    fail_event = torch.empty(K, dtype=torch.int32, device=tdev)
+    cause = torch.empty(K, dtype=torch.uint8, device=tdev)
+    peak = torch.empty(K, dtype=torch.int32, device=tdev)
+    import ctypes as C
+    res = N.LcResult(C.cast(valid.data_ptr(), N.P(C.c_int8)), C.cast(fail_event.data_ptr(), N.P(C.c_int32)),
+                     C.cast(cause.data_ptr(), N.P(C.c_uint8)), C.cast(peak.data_ptr(), N.P(C.c_uint32)),
+                     None, None)
+    gathered = torch.empty(K * world, dtype=torch.int64, device=tdev) if world > 1 else None
+
+    from lincheck import parallel as P
+
+    def step():
+        st = db.check_into(res)
+        if world > 1:  # the path's one exchange step: verdict records over RCCL
+            dist.all_gather_into_tensor(gathered, P.pack_records(valid, cause, fail_event))
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms, probes, deep = [], 0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+        kernel_ms.append(st.kernel_ms)
+        probes = st.probes
+        deep = st.deep_keys
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # results of the last step (host copy, outside the timed region)
+    v_host = valid.cpu().numpy()
+    fe_host = fail_event.cpu().numpy()
+
+    if rank == 0:
+        n_ops_total = K * ops * world
+        value = n_ops_total * args.steps / elapsed
+        avg_kernel_ms = float(np.mean(kernel_ms))
+        n_events = int(packed.ev_off[-1])
+        # algorithmic HBM bytes per launch: event words + key offsets + LPT
+        # order read, verdict records written (Measurement)
+        alg_bytes = 4 * n_events + 8 * (K + 1) + 4 * K + (1 + 4 + 1 + 4) * K
+        achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        traffic = None
+        for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+            try:
+                d = json.load(open(fpath))
+                if d.get("workload") == args.config and d.get("bytes_per_launch"):
+                    traffic = d["bytes_per_launch"]
+            except (OSError, ValueError):
+                pass
+        cpu = None
+        parity = None
+        if world == 1 and not args.no_cpu:
+            import cref
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            tc = time.perf_counter()
+            keys, orc = cref.check_history(hist.as_c(), budget=args.budget, threads=threads)
+            tcpu = time.perf_counter() - tc
+            cpu = {"value": K * ops / tcpu, "unit": "ops/s", "cores": threads, "kind": "port",
+                   "sample": f"full {args.config} batch ({K} keys x {ops} ops), oracle/linear_ref.c, "
+                             f"{threads} threads, {tcpu:.2f} s"}
+            parity = bool(np.array_equal(orc["valid"], v_host) and np.array_equal(orc["fail_event"], fe_host))
+        line = {
+            "metric": "history ops linearizability-checked/sec (whole node)",
+            "value": value,
+            "unit": "ops/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": cfg["desc"], "keys_per_gpu": K, "ops_per_key": ops,
+                       "concurrency": cfg["concurrency"], "budget": args.budget,
+                       "parallelism": f"keys sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+            "cpu_baseline": cpu,
+            "kernel_ms": avg_kernel_ms,
+            "probes_per_s": probes / (avg_kernel_ms * 1e-3),
+            "deep_keys": deep,
+            "verdicts": {"valid": int((v_host == 1).sum()), "invalid": int((v_host == 0).sum()),
+                         "unknown": int((v_host == -1).sum())},
+            "parity_vs_oracle": parity,
+            "setup_s": round(t_gen, 2),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -50,6 +50,7 @@ struct lc_dev_batch {
     uint64_t n_events = 0;
     int64_t n_trans = 0;
     uint32_t init_state = 0;
+    uint32_t shared_states = 0;  // 1 + largest state id in a shared table
     bool has_trans_off = false;
     uint64_t *ev_off = nullptr;
     uint32_t *events = nullptr;
@@ -74,8 +75,8 @@ struct lc_ctx {
     std::mutex mu;
     // scratch, grown on demand
     int64_t cap_keys = 0;
-    int32_t *lists = nullptr;      // 3 x cap_keys: spill1, spill2, wide
-    int32_t *counters = nullptr;   // 16 ints: n_spill1, n_spill2, n_wide, tickets[4]
+    int32_t *lists = nullptr;      // 4 x cap_keys: spill0, spill1, spill2, wide
+    int32_t *counters = nullptr;   // 16 ints: n_spill0, n_spill1, n_spill2, n_wide, -, tickets[8..15]
     unsigned long long *acc = nullptr;  // probes, events, keys_done
     int8_t *valid = nullptr;
     int32_t *fail_event = nullptr;
@@ -105,7 +106,7 @@ static int ensure_capacity(lc_ctx *c, int64_t n_keys) {
     int64_t cap = std::max<int64_t>(n_keys, 1024);
     dfree(c->lists); dfree(c->valid); dfree(c->fail_event); dfree(c->cause);
     dfree(c->peak); dfree(c->final_cfg); dfree(c->n_final);
-    HIPCHK(dalloc(&c->lists, (size_t)cap * 3));
+    HIPCHK(dalloc(&c->lists, (size_t)cap * 4));
     HIPCHK(dalloc(&c->valid, (size_t)cap));
     HIPCHK(dalloc(&c->fail_event, (size_t)cap));
     HIPCHK(dalloc(&c->cause, (size_t)cap));
@@ -287,6 +288,15 @@ extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
     d->n_trans = b->n_trans > 0 ? b->n_trans : 1;
     d->init_state = b->init_state;
     d->has_trans_off = b->trans_off != nullptr;
+    {
+        uint32_t mx = b->init_state;
+        for (int64_t i = 0; i < b->n_trans; ++i) {
+            const uint32_t t = b->trans[i], f = t & 3u, a = (t >> 2) & 0x7FFFu, bb = t >> 17;
+            if ((f == LC_T_READ || f == LC_T_CAS) && a != LC_STATE_NONE) mx = std::max(mx, a);
+            if (f == LC_T_WRITE || f == LC_T_CAS) mx = std::max(mx, bb);
+        }
+        d->shared_states = mx + 1;
+    }
     // LPT order: longest keys first
     std::vector<int32_t> order((size_t)K);
     std::iota(order.begin(), order.end(), 0);
@@ -349,7 +359,8 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     lcd::Args a{};
     a.ev_off = d->ev_off; a.events = d->events; a.trans = d->trans; a.trans_off = d->trans_off;
     a.key_width = d->key_width; a.key_states = d->key_states;
-    a.init_state = d->init_state; a.budget = c->o.max_configs; a.max_final = c->o.max_final;
+    a.init_state = d->init_state; a.shared_states = d->shared_states;
+    a.budget = c->o.max_configs; a.max_final = c->o.max_final;
     if (dev_result) {
         a.valid = r->valid; a.fail_event = r->fail_event; a.cause = r->cause;
         a.peak = r->peak_configs; a.final_cfg = r->final_configs; a.n_final = r->n_final;
@@ -358,46 +369,54 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         a.peak = c->peak; a.final_cfg = c->final_cfg; a.n_final = c->n_final;
     }
     a.probes = c->acc + 0; a.ev_count = c->acc + 1; a.keys_done = c->acc + 2;
-    int32_t *spill1 = c->lists, *spill2 = c->lists + c->cap_keys, *wide = c->lists + 2 * c->cap_keys;
-    int32_t *n_spill1 = c->counters + 0, *n_spill2 = c->counters + 1, *n_wide = c->counters + 2;
+    int32_t *spill0 = c->lists, *spill1 = c->lists + c->cap_keys, *spill2 = c->lists + 2 * c->cap_keys;
+    int32_t *wide = c->lists + 3 * c->cap_keys;
+    int32_t *n_spill0 = c->counters + 0, *n_spill1 = c->counters + 1, *n_spill2 = c->counters + 2;
+    int32_t *n_wide = c->counters + 3;
 
     HIPCHK(hipMemsetAsync(c->counters, 0, 16 * sizeof(int32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->acc, 0, 4 * sizeof(unsigned long long), c->stream));
     if (a.n_final && K > 0) HIPCHK(hipMemsetAsync(a.n_final, 0, (size_t)K * 4, c->stream));
     HIPCHK(hipEventRecord(c->e0, c->stream));
     if (K > 0) {
-        // T1: every key, LPT order
+        // T0: every key, LPT order; keys outside the register lattice spill to T1
+        lcd::Args a0 = a;
+        a0.order = d->order; a0.n_order = (int32_t)K; a0.n_in = nullptr; a0.ticket = c->counters + 8;
+        a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
+        int g0 = (int)std::min<int64_t>(K, (int64_t)c->cu_count * 16);
+        HIPCHK(lcd::launch_t0(a0, g0, c->stream));
+        // T1: LDS hash sets
         lcd::Args a1 = a;
-        a1.order = d->order; a1.n_order = (int32_t)K; a1.n_in = nullptr; a1.ticket = c->counters + 4;
+        a1.order = spill0; a1.n_order = 0; a1.n_in = n_spill0; a1.ticket = c->counters + 9;
         a1.spill = spill1; a1.n_spill = n_spill1; a1.wide = wide; a1.n_wide = n_wide;
         int g1 = (int)std::min<int64_t>(K, (int64_t)c->cu_count * 7);
         HIPCHK(lcd::launch_t1(a1, g1, c->stream));
         // T2: keys that outgrew T1
         lcd::Args a2 = a;
-        a2.order = spill1; a2.n_order = 0; a2.n_in = n_spill1; a2.ticket = c->counters + 5;
+        a2.order = spill1; a2.n_order = 0; a2.n_in = n_spill1; a2.ticket = c->counters + 10;
         a2.spill = spill2; a2.n_spill = n_spill2; a2.wide = wide; a2.n_wide = n_wide;
         HIPCHK(lcd::launch_t2(a2, c->cu_count, c->stream));
         // T3 (HBM tier): keys beyond T2, then keys needing wide configs.
         // The work-list lengths size the workspace, so read them back first.
-        int32_t cnt3[3];
+        int32_t cnt3[4];
         HIPCHK(hipMemcpyAsync(cnt3, c->counters, sizeof cnt3, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         lcd::Args a3 = a;
         a3.wide = wide; a3.n_wide = n_wide;
-        if (cnt3[1] > 0) {
+        if (cnt3[2] > 0) {
             int slots = 0;
-            rc = ensure_ws(c, 0, cnt3[1], &slots);
+            rc = ensure_ws(c, 0, cnt3[2], &slots);
             if (rc) return rc;
-            a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 6;
+            a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 11;
             HIPCHK(lcd::launch_t3_narrow(a3, c->ws[0].w, slots, c->stream));
             HIPCHK(hipMemcpyAsync(cnt3, c->counters, sizeof cnt3, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
         }
-        if (cnt3[2] > 0) {
+        if (cnt3[3] > 0) {
             int slots = 0;
-            rc = ensure_ws(c, 1, cnt3[2], &slots);
+            rc = ensure_ws(c, 1, cnt3[3], &slots);
             if (rc) return rc;
-            a3.order = wide; a3.n_order = 0; a3.n_in = n_wide; a3.ticket = c->counters + 7;
+            a3.order = wide; a3.n_order = 0; a3.n_in = n_wide; a3.ticket = c->counters + 12;
             HIPCHK(lcd::launch_t3_wide(a3, c->ws[1].w, slots, c->stream));
         }
     }
@@ -427,7 +446,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         st->probes = acc[0];
         st->events = acc[1];
         st->lds_keys = acc[2];
-        st->deep_keys = (uint64_t)cnt[1] + (uint64_t)cnt[2];
+        st->deep_keys = (uint64_t)cnt[0];  // keys that left the register tier
     }
     return LC_OK;
 }

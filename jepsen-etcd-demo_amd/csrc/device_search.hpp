@@ -18,6 +18,7 @@ struct Args {
     const uint8_t *key_width;    // may be null
     const uint16_t *key_states;  // may be null
     uint32_t init_state;
+    uint32_t shared_states;      // state ids used by the shared table (trans_off == null)
     uint64_t budget;
     int32_t max_final;
     // work list of this launch: keys order[0 .. n) with n = n_in ? *n_in : n_order
@@ -54,6 +55,7 @@ struct HbmWs {
 
 size_t lds_bytes_t1();
 size_t lds_bytes_t2();
+hipError_t launch_t0(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t2(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t3_narrow(const Args &a, const HbmWs &w, int grid, hipStream_t s);

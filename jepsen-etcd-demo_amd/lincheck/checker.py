@@ -61,6 +61,8 @@ class Packed:
 
     def events(self, i: int) -> np.ndarray:
         b, e = int(self.ev_off[i]), int(self.ev_off[i + 1])
+        if e == b:
+            return np.zeros(0, np.uint32)
         return np.ctypeslib.as_array(self.view.events, shape=(int(self.ev_off[-1]) or 1,))[b:e].copy()
 
     def event_row(self, i: int, j: int) -> int:

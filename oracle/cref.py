@@ -47,5 +47,9 @@ def check_history(hist_c, budget: int = 1 << 20, threads: int = 1):
     rc = L.oracle_check_history(C.byref(hist_c), budget, threads, keys.ctypes.data, C.addressof(res), nk)
     if rc < 0:
         raise RuntimeError(f"oracle_check_history failed: {rc}")
-    arr = np.ctypeslib.as_array(res)[:nk].copy()
+    dt = np.dtype({"names": [f[0] for f in OracleKeyResult._fields_],
+                   "formats": [np.int8, np.uint8, np.int32, np.uint32, np.uint64, np.uint64],
+                   "offsets": [getattr(OracleKeyResult, f[0]).offset for f in OracleKeyResult._fields_],
+                   "itemsize": C.sizeof(OracleKeyResult)})
+    arr = np.frombuffer(res, dtype=dt, count=nk).copy()
     return keys[:nk], arr

@@ -1,0 +1,53 @@
+"""The C ABI library loads and exports every symbol include/lincheck.h
+declares; device entry points fail loudly (no CPU fallback) without a GPU."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from lincheck import _native as N
+
+HEADER = os.path.join(os.path.dirname(__file__), "..", "include", "lincheck.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lc_[a-z0-9_]+)\s*\(", src)) - {"lc_DESC"})
+
+
+def test_header_symbols_exported():
+    L = C.CDLL(N.LIB_PATH)
+    names = declared()
+    assert len(names) >= 20
+    for name in names:
+        assert hasattr(L, name), name
+    assert set(names) == set(N.SIGNATURES), set(names) ^ set(N.SIGNATURES)
+
+
+def test_abi_version():
+    assert N.lib().lc_abi_version() == N.LC_ABI_VERSION
+
+
+def test_struct_sizes_match_header():
+    # offsets the JNA / ctypes bindings rely on (x86-64 LP64)
+    assert C.sizeof(N.LcHistory) == 8 * 8
+    assert C.sizeof(N.LcBatch) == 8 * 9
+    assert C.sizeof(N.LcResult) == 8 * 6
+    assert C.sizeof(N.LcOpts) == 4 + 4 + 8 + 4 * 3 + 4 * 6 + 4
+
+
+@pytest.mark.skipif(N.lib().lc_device_count() > 0, reason="a GPU is visible")
+def test_device_calls_fail_loudly_without_gpu():
+    from lincheck.checker import Device
+    with pytest.raises(N.LincheckError, match="device"):
+        Device(0)
+
+
+def test_bad_options_rejected():
+    o = N.LcOpts()
+    o.algorithm = 7
+    h = C.c_void_p()
+    assert N.lib().lc_create(C.byref(o), C.byref(h)) == -1
+    assert b"algorithm" in N.lib().lc_last_error()

@@ -1,0 +1,115 @@
+"""Host side of the Checker mirror (jepsen.checker / jepsen.independent,
+etcdemo.clj:115-119, :165-167) without a GPU: result merging, check-safe,
+and the Knossos-shaped result maps built from per-key verdict records."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cref
+from lincheck import checker as ck
+from lincheck import history as H
+from lincheck import independent, model
+from lincheck.checker import KeyResults, Packed, _render_key
+from lincheck.independent import Tuple
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kat.json")
+
+
+def test_merge_valid():
+    assert ck.merge_valid([True, True]) is True
+    assert ck.merge_valid([True, "unknown"]) == "unknown"
+    assert ck.merge_valid(["unknown", False, True]) is False
+    assert ck.merge_valid([]) is True
+
+
+class Boom:
+    def check(self, test, history, opts):
+        raise RuntimeError("boom")
+
+
+class Const:
+    def __init__(self, v):
+        self.v = v
+
+    def check(self, test, history, opts):
+        return {"valid?": self.v, "n": len(history)}
+
+
+def test_check_safe_turns_exceptions_into_unknown():
+    r = ck.check_safe(Boom(), {}, [], {})
+    assert r["valid?"] == "unknown" and "boom" in r["error"]
+
+
+def test_compose():
+    r = ck.compose({"a": Const(True), "b": Boom()}).check({}, [], {})
+    assert r["valid?"] == "unknown" and r["a"]["valid?"] is True
+
+
+def test_independent_checker_generic_inner():
+    ops = [{"type": "invoke", "f": "read", "value": Tuple(k, None), "process": k} for k in range(3)]
+    ops.append({"type": "info", "f": "start", "value": None, "process": "nemesis"})
+    verdicts = {0: True, 1: False, 2: "unknown"}
+
+    class PerKey:
+        def check(self, test, history, opts):
+            k = opts["history-key"]
+            assert all((not independent.is_tuple(o["value"])) for o in history)
+            assert history[-1]["process"] == "nemesis"  # non-tuple ops stay in every sub-history
+            return {"valid?": verdicts[k]}
+
+    r = independent.checker(PerKey()).check({}, ops, {})
+    assert r["valid?"] is False
+    assert r["failures"] == [1]  # :unknown is truthy in Clojure, so not a failure
+    assert set(r["results"]) == {0, 1, 2}
+
+
+def test_linearizable_options():
+    with pytest.raises(ValueError):
+        ck.linearizable({})
+    with pytest.raises(NotImplementedError):
+        ck.linearizable({"model": model.cas_register(), "algorithm": "wgl"})
+    lin = ck.linearizable({"model": model.cas_register(), "algorithm": "linear"})
+    assert ck.batched_linearizable(lin) is lin
+    comp = ck.compose({"linear": lin, "timeline": ck.unbridled_optimism()})
+    assert ck.batched_linearizable(comp) is lin
+
+
+def test_model_messages():
+    r = model.cas_register()
+    assert r.step("write", 3).value == 3
+    assert r.step("cas", [3, 4]).msg == "can't CAS nil from 3 to 4"
+    assert r.step("write", 3).step("read", 1).msg == "can't read 1 from register 3"
+    assert r.step("write", 2).step("read", None).value == 2
+
+
+def kats():
+    cases = json.load(open(GOLDEN))
+    for c in cases:
+        for op in c["history"]:
+            v = op["value"]
+            if isinstance(v, dict) and "tuple" in v:
+                op["value"] = Tuple(*v["tuple"])
+    return cases
+
+
+@pytest.mark.parametrize("case", kats(), ids=lambda c: c["name"])
+def test_result_maps_from_verdict_records(case):
+    """Knossos-shaped maps (A8) from verdict records: :op / :previous-ok are
+    the original op maps (their :index), :configs render the model value."""
+    h = H.History.from_ops(case["history"])
+    pk = Packed(h)
+    keys, r = cref.check_history(h.as_c())
+    K = pk.n_keys
+    res = KeyResults(r["valid"], r["fail_event"], r["cause"], r["peak"],
+                     np.zeros((K, 10, 2), np.uint64), np.zeros(K, np.uint32), {})
+    for i, k in enumerate(pk.keys):
+        m = _render_key(pk, i, res, None)
+        exp = case["expect"][str(k)]
+        assert m["valid?"] == exp["valid?"]
+        assert m["analyzer"] == "linear"
+        if not exp["valid?"]:
+            assert m["op"]["index"] == exp["op"]
+            assert m["op"]["type"] == "ok"
+            assert m["previous-ok"]["index"] == exp["previous-ok"]

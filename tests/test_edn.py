@@ -1,0 +1,62 @@
+"""history.edn ingestion: round trips and Jepsen's
+line format with fields and values this workload never reads."""
+import numpy as np
+import pytest
+
+from lincheck import _native as N
+from lincheck import history as H
+from lincheck.checker import Packed
+
+JEPSEN_LINES = """\
+{:type :invoke, :f :write, :value [0 3], :process 0, :time 21304010, :index 0}
+{:type :info, :f :start, :value nil, :process :nemesis, :time 22000000, :index 1}
+{:type :info, :f :start, :value [:isolated {"n1" #{"n2" "n3"}, "n2" #{"n1"}}], :process :nemesis, :time 22000100, :index 2}
+{:type :ok, :f :write, :value [0 3], :process 0, :time 23000000, :index 3}
+{:type :invoke, :f :cas, :value [0 [3 1]], :process 1, :time 24000000, :index 4}
+{:type :info, :f :cas, :value [0 [3 1]], :process 1, :time 29000000, :error :timeout, :index 5}
+; a comment line
+{:type :invoke, :f :read, :value [0 nil], :process 0, :time 30000000, :index 6}
+{:type :ok, :f :read, :value [0 1], :process 0, :time 31000000, :index 7}
+{:type :invoke, :f :read, :value [1 nil], :process 11, :time 32000000, :index 8}
+{:type :fail, :f :read, :value [1 nil], :process 11, :time 33000000, :error [:not-found "Key not found"], :index 9}
+"""
+
+
+def test_parse_jepsen_lines():
+    h = H.parse_edn(JEPSEN_LINES)
+    assert len(h) == 10
+    assert list(h.type) == [0, 3, 3, 1, 0, 3, 0, 1, 0, 2]
+    assert list(h.key[[0, 3, 4, 6, 8]]) == [0, 0, 0, 0, 1]
+    assert h.key[1] == N.LC_NO_KEY and h.process[1] == N.LC_NO_PROCESS
+    assert (h.v0[4], h.v1[4]) == (3, 1)
+    assert h.v0[6] == N.LC_NIL and h.v0[7] == 1
+    assert list(h.index) == list(range(10))
+    pk = Packed(h)
+    assert pk.keys == [0, 1]
+
+
+def test_vector_form():
+    h = H.parse_edn("[" + JEPSEN_LINES.replace("\n; a comment line", "") + "]")
+    assert len(h) == 10
+
+
+@pytest.mark.parametrize("interleave", [True, False])
+def test_round_trip(tmp_path, interleave):
+    h = H.synth(n_keys=5, ops_per_key=60, concurrency=6, info_rate=0.05, interleave=interleave,
+                nemesis_period=2.0 if interleave else 0.0, seed=3)
+    path = str(tmp_path / "history.edn")
+    H.write_edn(path, h)
+    g = H.read_edn(path)
+    for col in ("type", "f", "process", "key", "v0", "v1", "index"):
+        np.testing.assert_array_equal(getattr(g, col), getattr(h, col), err_msg=col)
+
+
+@pytest.mark.parametrize("text", ["{:type :invoke", "{:type :wat}", "[{:type :ok} 3]", "{:f :read}"])
+def test_parse_errors(text):
+    with pytest.raises(N.LincheckError):
+        H.parse_edn(text)
+
+
+def test_missing_file():
+    with pytest.raises(N.LincheckError, match="io"):
+        H.read_edn("/nonexistent/history.edn")

@@ -1,0 +1,130 @@
+"""lc_pack (jepsen.independent split + knossos.history complete /
+without-failures + memoised cas-register transitions) against the oracle's
+own restatement of the same steps (oracle/linear_ref.py)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+import linear_ref as LR
+from histgen import random_history
+from lincheck import _native as N
+from lincheck import history as H
+from lincheck.checker import Packed
+from lincheck.independent import Tuple
+
+
+def decode(desc):
+    return desc & 3, (desc >> 2) & 0x7FFF, desc >> 17
+
+
+def check_packed_against_oracle(ops):
+    h = H.History.from_ops(ops)
+    pk = Packed(h)
+    assert pk.keys == LR.history_keys(ops)
+    view = pk.view
+    trans = np.ctypeslib.as_array(view.trans, shape=(view.n_trans,))
+    toff = None if not view.trans_off else np.ctypeslib.as_array(view.trans_off, shape=(pk.n_keys,))
+    width = np.ctypeslib.as_array(view.key_width, shape=(pk.n_keys,))
+    for i, k in enumerate(pk.keys):
+        sub = LR.subhistory(ops, k)
+        lops, events = LR.complete(sub)
+        # sub-history rows: tuple rows of k + shared (nemesis) rows, in order
+        nrows = N.lib().lc_packed_subhistory(pk.handle, i, None)
+        rows = np.zeros(max(nrows, 1), np.int64)
+        N.lib().lc_packed_subhistory(pk.handle, i, N.ptr(rows, C.c_int64))
+        rows = rows[:nrows]
+        assert len(rows) == len(sub)
+        ev = pk.events(i)
+        assert len(ev) == len(events)
+        free = list(range(128))
+        slot_of = {}
+        maxw = 0
+        for j, (kind, oid, pos) in enumerate(events):
+            w = int(ev[j])
+            assert pk.event_row(i, j) == rows[pos]
+            if kind == "invoke":
+                assert not w & N.LC_EV_OK_BIT
+                s = min(free); free.remove(s); slot_of[oid] = s
+                maxw = max(maxw, s + 1)
+                assert (w >> 24) & 0x7F == s
+                f, a, b = decode(int(trans[(0 if toff is None else toff[i]) + (w & 0xFFFFFF)]))
+                o = lops[oid]
+                val = lambda sid: pk.state_value(i, sid) if sid != N.LC_STATE_NONE else "NONE"
+                if o.f == "read":
+                    if o.value is None:
+                        assert f == N.LC_T_READ_ANY
+                    else:
+                        assert f == N.LC_T_READ and val(a) in (o.value, "NONE")
+                elif o.f == "write":
+                    assert f == N.LC_T_WRITE and val(b) == o.value
+                else:
+                    assert f == N.LC_T_CAS and val(b) == o.value[1] and val(a) in (o.value[0], "NONE")
+            else:
+                assert w & N.LC_EV_OK_BIT
+                s = slot_of.pop(oid)
+                assert (w >> 24) & 0x7F == s
+                free.append(s)
+        assert width[i] == maxw
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.integers(0, 2**31 - 1))
+def test_pack_matches_restatement_random(seed):
+    check_packed_against_oracle(random_history(seed, n_keys=3, max_ops=10, procs=4))
+
+
+@pytest.mark.parametrize("kw", [
+    dict(n_keys=5, ops_per_key=100, concurrency=10, seed=2),
+    dict(n_keys=3, ops_per_key=100, concurrency=30, info_rate=0.05, seed=4),
+    dict(n_keys=4, ops_per_key=80, concurrency=10, interleave=True, nemesis_period=2.0, seed=1),
+    dict(n_keys=3, ops_per_key=200, concurrency=4, n_values=400, seed=8),   # per-key state tables
+])
+def test_pack_matches_restatement_synthetic(kw):
+    check_packed_against_oracle(H.synth(**kw).to_ops())
+
+
+def test_many_values_use_per_key_tables():
+    h = H.synth(n_keys=3, ops_per_key=400, concurrency=4, n_values=1000, seed=8)
+    pk = Packed(h)
+    assert pk.view.trans_off  # > 254 distinct values: per-key state numbering
+    states = np.ctypeslib.as_array(pk.view.key_states, shape=(pk.n_keys,))
+    assert (states > 100).all()
+
+
+def test_completion_without_invocation_is_an_error():
+    ops = [{"type": "ok", "f": "write", "value": Tuple(0, 1), "process": 0}]
+    with pytest.raises(N.LincheckError, match="without a prior invocation"):
+        Packed(H.History.from_ops(ops))
+
+
+def test_non_tuple_client_op_is_unsupported():
+    ops = [{"type": "invoke", "f": "write", "value": 1, "process": 0}]
+    with pytest.raises(N.LincheckError, match="unsupported"):
+        Packed(H.History.from_ops(ops))
+
+
+def test_unknown_f_is_unsupported():
+    ops = [{"type": "invoke", "f": "append", "value": Tuple(0, 1), "process": 0}]
+    with pytest.raises(N.LincheckError, match="unsupported"):
+        Packed(H.History.from_ops(ops))
+
+
+def test_non_integer_values_rejected_on_host():
+    with pytest.raises(ValueError):
+        H.History.from_ops([{"type": "invoke", "f": "write", "value": Tuple(0, "x"), "process": 0}])
+
+
+def test_empty_history():
+    pk = Packed(H.History.from_ops([]))
+    assert pk.n_keys == 0
+
+
+def test_double_invoke_leaves_first_pending_forever():
+    ops = [{"type": "invoke", "f": "write", "value": Tuple(0, 1), "process": 0},
+           {"type": "invoke", "f": "write", "value": Tuple(0, 2), "process": 0},
+           {"type": "ok", "f": "write", "value": Tuple(0, 2), "process": 0}]
+    pk = Packed(H.History.from_ops(ops))
+    ev = pk.events(0)
+    assert [(int(w) >> 31, (int(w) >> 24) & 0x7F) for w in ev] == [(0, 0), (0, 1), (1, 1)]
