@@ -360,7 +360,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     a.ev_off = d->ev_off; a.events = d->events; a.trans = d->trans; a.trans_off = d->trans_off;
     a.key_width = d->key_width; a.key_states = d->key_states;
     a.init_state = d->init_state; a.shared_states = d->shared_states;
-    a.budget = c->o.max_configs; a.max_final = c->o.max_final;
+    a.budget = c->o.max_configs; a.max_final = c->o.max_final; a.debug_mode = c->o.reserved[0];
     if (dev_result) {
         a.valid = r->valid; a.fail_event = r->fail_event; a.cause = r->cause;
         a.peak = r->peak_configs; a.final_cfg = r->final_configs; a.n_final = r->n_final;

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/lincheck.h"
 #include "device_common.hpp"
@@ -60,6 +61,48 @@ __device__ __forceinline__ uint32_t legal_cnt(uint32_t M, uint32_t d) {
     return a < 32u ? (M >> a) & 1u : 0u;
 }
 
+// Branch-free form of an op's state transfer: T(M) = (M & pass) | (M & keep ? set : 0)
+//   read-any: pass = all         read a: pass = {a}
+//   write b:  keep = all, set = {b}      cas a->b: keep = {a}, set = {b}
+// and the number of configs of M where the op is legal is popc(M & (pass | keep)).
+struct Xfer { uint32_t pass, keep, set; };
+
+__device__ __forceinline__ Xfer xfer_of(uint32_t d) {
+    const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
+    const uint32_t abit = a < 32u ? 1u << a : 0u, bbit = b < 32u ? 1u << b : 0u;
+    if (f == LC_T_READ_ANY) return {0xFFFFFFFFu, 0u, 0u};
+    if (f == LC_T_READ) return {abit, 0u, 0u};
+    if (f == LC_T_WRITE) return {0u, 0xFFFFFFFFu, bbit};
+    return {0u, abit, bbit};
+}
+
+__device__ __forceinline__ uint32_t xapply(uint32_t M, uint32_t pass, uint32_t keep, uint32_t set) {
+    return (M & pass) | ((M & keep) ? set : 0u);
+}
+
+// x from lane (lane ^ 2^Q), Q < 6, in VALU only (DPP row shifts, gfx950
+// permlane swaps): no LDS round trip.
+template <int Q>
+__device__ __forceinline__ uint32_t xv(uint32_t x, uint32_t lane) {
+    if constexpr (Q == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+    else if constexpr (Q == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+    else if constexpr (Q == 2) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104, 0xF, 0xF, true);  // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+        return (lane & 4u) ? dn : up;
+    } else if constexpr (Q == 3) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x108, 0xF, 0xF, true);  // row_shl:8
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+        return (lane & 8u) ? dn : up;
+    } else if constexpr (Q == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane & 16u) ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane & 32u) ? r[0] : r[1];
+    }
+}
+
 // x from lane (lane ^ 2^Q), Q < 6.
 template <int Q>
 __device__ __forceinline__ uint32_t xchg(uint32_t x) {
@@ -71,9 +114,15 @@ __device__ __forceinline__ uint32_t xchg(uint32_t x) {
     else return (uint32_t)__shfl_xor((int)x, 32);
 }
 
+// Every helper below works on the first RL registers of a T0_RMAX array
+// (RL = registers that can hold configs for the current pending count); the
+// ok-event handler is instantiated once per RL, so its loops carry no
+// run-time register guards.
+using Lat = uint32_t[T0_RMAX];
+
 // Partner of register k of X along subset bit Q (lane exchange or register pair).
-template <int Q, int R>
-__device__ __forceinline__ uint32_t partner(const uint32_t (&X)[R], int k) {
+template <int Q>
+__device__ __forceinline__ uint32_t partner(const Lat &X, int k) {
     if constexpr (Q < 6) return xchg<Q>(X[k]);
     else return X[k ^ (1 << (Q - 6))];
 }
@@ -84,132 +133,218 @@ __device__ __forceinline__ bool has_bit(uint32_t lane, int k) {
     else return (k >> (Q - 6)) & 1;
 }
 
-// One closure step along candidate op Q: X[L u {Q}] |= T_Q(X[L]).  Returns
-// whether this lane changed.  live = registers that can be non-zero.
-template <int Q, int R>
-__device__ __forceinline__ bool expand(uint32_t (&X)[R], uint32_t dq, uint32_t lane, int live) {
-    bool ch = false;
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-        bool on = k < live;
-        if constexpr (Q >= 6) on = on && ((k >> (Q - 6)) & 1);
-        if (on) {
-            const uint32_t src = partner<Q, R>(X, k);
-            uint32_t up = tmask(src, dq);
-            if constexpr (Q < 6) up = has_bit<Q>(lane, k) ? up : 0u;
-            const uint32_t nv = X[k] | up;
-            ch |= nv != X[k];
-            X[k] = nv;
-        }
-    }
-    return ch;
-}
-
-template <int R>
-__device__ __forceinline__ bool expand_any(uint32_t q, uint32_t (&X)[R], uint32_t dq, uint32_t lane, int live) {
+// Dispatch a templated functor on a run-time subset bit q < 6 + log2(RL).
+template <int RL, class F>
+__device__ __forceinline__ auto on_bit(uint32_t q, F &&f) {
     switch (q) {
-        case 0: return expand<0, R>(X, dq, lane, live);
-        case 1: return expand<1, R>(X, dq, lane, live);
-        case 2: return expand<2, R>(X, dq, lane, live);
-        case 3: return expand<3, R>(X, dq, lane, live);
-        case 4: return expand<4, R>(X, dq, lane, live);
-        case 5: return expand<5, R>(X, dq, lane, live);
-        case 6: if constexpr (R > 1) return expand<6, R>(X, dq, lane, live); else return false;
-        case 7: if constexpr (R > 2) return expand<7, R>(X, dq, lane, live); else return false;
-        case 8: if constexpr (R > 4) return expand<8, R>(X, dq, lane, live); else return false;
-        default: if constexpr (R > 8) return expand<9, R>(X, dq, lane, live); else return false;
+        case 0: return f(std::integral_constant<int, 0>{});
+        case 1: return f(std::integral_constant<int, 1>{});
+        case 2: return f(std::integral_constant<int, 2>{});
+        case 3: return f(std::integral_constant<int, 3>{});
+        case 4: return f(std::integral_constant<int, 4>{});
+        case 5: return f(std::integral_constant<int, 5>{});
+        case 6: if constexpr (RL > 1) return f(std::integral_constant<int, 6>{}); [[fallthrough]];
+        case 7: if constexpr (RL > 2) return f(std::integral_constant<int, 7>{}); [[fallthrough]];
+        case 8: if constexpr (RL > 4) return f(std::integral_constant<int, 8>{}); [[fallthrough]];
+        default: if constexpr (RL > 8) return f(std::integral_constant<int, 9>{});
+                 return f(std::integral_constant<int, 0>{});  // unreachable: q < n
     }
 }
 
-// Probe count of candidate q: configs of subsets without q where q is legal.
-template <int Q, int R>
-__device__ __forceinline__ uint32_t probes_q(const uint32_t (&X)[R], uint32_t dq, uint32_t lane, int live) {
-    uint32_t n = 0;
-#pragma unroll
-    for (int k = 0; k < R; ++k)
-        if (k < live && !has_bit<Q>(lane, k)) n += legal_cnt(X[k], dq);
-    return n;
-}
-
-template <int R>
-__device__ __forceinline__ uint32_t probes_any(uint32_t q, const uint32_t (&X)[R], uint32_t dq, uint32_t lane, int live) {
-    switch (q) {
-        case 0: return probes_q<0, R>(X, dq, lane, live);
-        case 1: return probes_q<1, R>(X, dq, lane, live);
-        case 2: return probes_q<2, R>(X, dq, lane, live);
-        case 3: return probes_q<3, R>(X, dq, lane, live);
-        case 4: return probes_q<4, R>(X, dq, lane, live);
-        case 5: return probes_q<5, R>(X, dq, lane, live);
-        case 6: if constexpr (R > 1) return probes_q<6, R>(X, dq, lane, live); else return 0;
-        case 7: if constexpr (R > 2) return probes_q<7, R>(X, dq, lane, live); else return 0;
-        case 8: if constexpr (R > 4) return probes_q<8, R>(X, dq, lane, live); else return 0;
-        default: if constexpr (R > 8) return probes_q<9, R>(X, dq, lane, live); else return 0;
-    }
-}
-
-// Ret (configs holding p, moved to L without p) and I seed (configs without p).
-template <int Q, int R>
-__device__ __forceinline__ void split_p(const uint32_t (&W)[R], uint32_t (&Ret)[R], uint32_t (&I)[R], uint32_t lane,
-                                        int live) {
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-        if (k >= live) { Ret[k] = 0; I[k] = 0; continue; }
-        const uint32_t src = partner<Q, R>(W, k);
-        const bool hp = has_bit<Q>(lane, k);
-        Ret[k] = hp ? 0u : src;
-        I[k] = hp ? 0u : W[k];
-    }
-}
-
-template <int R>
-__device__ __forceinline__ void split_any(uint32_t p, const uint32_t (&W)[R], uint32_t (&Ret)[R], uint32_t (&I)[R],
-                                          uint32_t lane, int live) {
-    switch (p) {
-        case 0: split_p<0, R>(W, Ret, I, lane, live); break;
-        case 1: split_p<1, R>(W, Ret, I, lane, live); break;
-        case 2: split_p<2, R>(W, Ret, I, lane, live); break;
-        case 3: split_p<3, R>(W, Ret, I, lane, live); break;
-        case 4: split_p<4, R>(W, Ret, I, lane, live); break;
-        case 5: split_p<5, R>(W, Ret, I, lane, live); break;
-        case 6: if constexpr (R > 1) split_p<6, R>(W, Ret, I, lane, live); break;
-        case 7: if constexpr (R > 2) split_p<7, R>(W, Ret, I, lane, live); break;
-        case 8: if constexpr (R > 4) split_p<8, R>(W, Ret, I, lane, live); break;
-        default: if constexpr (R > 8) split_p<9, R>(W, Ret, I, lane, live); break;
-    }
-}
-
-template <int R>
-__device__ __forceinline__ uint32_t wave_count(const uint32_t (&X)[R], int live) {
+template <int RL>
+__device__ __forceinline__ uint32_t lat_count(const Lat &X) {
     uint32_t c = 0;
 #pragma unroll
-    for (int k = 0; k < R; ++k)
-        if (k < live) c += (uint32_t)__popc(X[k]);
-    return __ockl_wfred_add_u32(c);
+    for (int k = 0; k < RL; ++k) c += (uint32_t)__popc(X[k]);
+    return c;
 }
 
-// First max_final configs of the lattice, in (register, lane, state) order.
-template <int R>
-__device__ __forceinline__ void write_final_lattice(const Args &a, int32_t key, const uint32_t (&W)[R], uint32_t lane) {
+// One :ok(p) event on a lattice of RL registers.  W = S on entry, S' on a
+// normal exit (relocated so index n-1 is free).  Returns 0 normal,
+// 1 invalid, 2 budget exceeded.
+template <int RL>
+__device__ __forceinline__ int ok_event(Lat &W, uint32_t p, uint32_t n, uint32_t desc_v, uint32_t lane,
+                                        uint64_t budget, uint32_t &probes, uint32_t &nSn_out, int dbg) {
+    Lat Ret, I;
+    const uint32_t dp = __builtin_amdgcn_readlane(desc_v, p);
+    probes += lat_count<RL>(W);  // oracle: one probe per config of S
+    on_bit<RL>(p, [&](auto QC) {
+        constexpr int Q = decltype(QC)::value;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) {
+            const uint32_t src = partner<Q>(W, k);
+            const bool hp = has_bit<Q>(lane, k);
+            Ret[k] = hp ? 0u : src;
+            I[k] = hp ? 0u : W[k];
+        }
+        return 0;
+    });
+    // JIT closure over the other pending ops, Gauss-Seidel to a fixpoint
+    const uint64_t cand = ((1ull << n) - 1ull) & ~(1ull << p);
+    for (int sweep = 0;; ++sweep) {
+        uint32_t ch = 0;
+        for (uint64_t m = cand; m; m &= m - 1) {
+            const uint32_t q = (uint32_t)__builtin_ctzll(m);
+            const uint32_t dq = __builtin_amdgcn_readlane(desc_v, q);
+            ch |= on_bit<RL>(q, [&](auto QC) -> uint32_t {
+                constexpr int Q = decltype(QC)::value;
+                uint32_t c = 0;
+                uint32_t src[RL];
+#pragma unroll
+                for (int k = 0; k < RL; ++k) src[k] = partner<Q>(I, k);
+#pragma unroll
+                for (int k = 0; k < RL; ++k) {
+                    if (!has_bit<Q>(lane, k)) continue;  // compile-time for Q >= 6
+                    const uint32_t nv = I[k] | tmask(src[k], dq);
+                    c |= nv ^ I[k];
+                    I[k] = nv;
+                }
+                return c;
+            });
+        }
+        if (!__any(ch != 0) || (dbg == 4 && sweep == 0)) break;
+    }
+    const uint32_t nI = __ockl_wfred_add_u32(lat_count<RL>(I));
+    for (uint64_t m = dbg == 3 ? 0 : cand; m; m &= m - 1) {
+        const uint32_t q = (uint32_t)__builtin_ctzll(m);
+        const uint32_t dq = __builtin_amdgcn_readlane(desc_v, q);
+        probes += on_bit<RL>(q, [&](auto QC) -> uint32_t {
+            constexpr int Q = decltype(QC)::value;
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < RL; ++k)
+                if (!has_bit<Q>(lane, k)) c += legal_cnt(I[k], dq);
+            return c;
+        });
+    }
+#pragma unroll
+    for (int k = 0; k < RL; ++k) {
+        Ret[k] |= tmask(I[k], dp);  // Ret becomes S'
+        probes += legal_cnt(I[k], dp);
+    }
+    const uint32_t nSn = __ockl_wfred_add_u32(lat_count<RL>(Ret));
+    nSn_out = nSn;
+    if (nI > budget) return 2;
+    if (nSn == 0) return 1;
+    if (nSn > budget) return 2;
+    const uint32_t last = n - 1;
+    if (p == last) {
+#pragma unroll
+        for (int k = 0; k < RL; ++k) W[k] = Ret[k];
+        return 0;
+    }
+    // the op at index `last` moves to index p: S'[L] for L with p comes from
+    // L ^ {p, last}; no config keeps bit `last`
+    on_bit<RL>(p, [&](auto QC) {
+        constexpr int Q = decltype(QC)::value;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) I[k] = partner<Q>(Ret, k);
+        return 0;
+    });
+    on_bit<RL>(last, [&](auto LC) {
+        constexpr int QL = decltype(LC)::value;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) W[k] = partner<QL>(I, k);
+        return 0;
+    });
+#pragma unroll
+    for (int k = 0; k < RL; ++k) {
+        const bool hp = p < 6 ? ((lane >> p) & 1u) : (((uint32_t)k >> (p - 6)) & 1u);
+        const bool hl = last < 6 ? ((lane >> last) & 1u) : (((uint32_t)k >> (last - 6)) & 1u);
+        W[k] = hl ? 0u : (hp ? W[k] : Ret[k]);
+    }
+    return 0;
+}
+
+
+// One :ok(p) event when at most 6 ops are pending: the whole lattice is one
+// register, every subset bit is a lane bit, and each closure sweep applies
+// all six bit positions branch-free (non-candidates carry zero masks).
+__device__ __forceinline__ int ok_event_1(uint32_t &W, uint32_t p, uint32_t n, uint32_t pass_v, uint32_t keep_v,
+                                          uint32_t set_v, uint32_t lane, uint64_t budget, uint32_t &probes,
+                                          uint32_t &nSn_out) {
+    const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
+    uint32_t ps[6], kp[6], st[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const bool on = (cand >> q) & 1u;
+        ps[q] = on ? __builtin_amdgcn_readlane(pass_v, q) : 0u;
+        kp[q] = on ? __builtin_amdgcn_readlane(keep_v, q) : 0u;
+        st[q] = on ? __builtin_amdgcn_readlane(set_v, q) : 0u;
+    }
+    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
+                   pt = __builtin_amdgcn_readlane(set_v, p);
+    probes += (uint32_t)__popc(W);
+    const bool hp = (lane >> p) & 1u;
+    const uint32_t wp = (uint32_t)__shfl_xor((int)W, 1 << p);
+    uint32_t Ret = hp ? 0u : wp;
+    uint32_t I = hp ? 0u : W;
+    for (;;) {
+        uint32_t ch = 0;
+#define LC_EXPAND(Q)                                                          \
+        {                                                                     \
+            uint32_t t = xapply(xv<Q>(I, lane), ps[Q], kp[Q], st[Q]);         \
+            t = ((lane >> Q) & 1u) ? t : 0u;                                  \
+            ch |= t & ~I;                                                     \
+            I |= t;                                                           \
+        }
+        LC_EXPAND(0) LC_EXPAND(1) LC_EXPAND(2) LC_EXPAND(3) LC_EXPAND(4) LC_EXPAND(5)
+#undef LC_EXPAND
+        if (!__any(ch != 0)) break;
+    }
+    const uint32_t nI = __ockl_wfred_add_u32((uint32_t)__popc(I));
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+        if (!((lane >> q) & 1u)) probes += (uint32_t)__popc(I & (ps[q] | kp[q]));
+    Ret |= xapply(I, pp, pk, pt);
+    probes += (uint32_t)__popc(I & (pp | pk));
+    const uint32_t nSn = __ockl_wfred_add_u32((uint32_t)__popc(Ret));
+    nSn_out = nSn;
+    if (nI > budget) return 2;
+    if (nSn == 0) return 1;
+    if (nSn > budget) return 2;
+    const uint32_t last = n - 1;
+    if (p == last) { W = Ret; return 0; }
+    // op at index `last` moves to index p
+    const uint32_t r2 = (uint32_t)__shfl_xor((int)Ret, (1 << p) | (1 << last));
+    const bool hl = (lane >> last) & 1u;
+    W = hl ? 0u : (hp ? r2 : Ret);
+    return 0;
+}
+
+// First max_final configs of the lattice, in (register, lane, state) order,
+// with dense op indices translated back to window slots (slot_v: lane j holds
+// the slot of dense index j).
+__device__ __forceinline__ void write_final_lattice(const Args &a, int32_t key, const Lat &W, uint32_t lane,
+                                                    uint32_t slot_v, uint32_t n) {
     if (!a.final_cfg) return;
     const uint32_t mf = (uint32_t)a.max_final;
+    const int live = n <= 6 ? 1 : (1 << (n - 6));
     uint32_t base = 0;
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-        const uint32_t c = (uint32_t)__popc(W[k]);
-        // exclusive prefix over lanes of c
-        uint32_t x = c;
+    for (int k = 0; k < T0_RMAX; ++k) {
+        if (k >= live) continue;
+        const uint32_t w = W[k];
+        const uint32_t c = (uint32_t)__popc(w);
+        uint32_t x = c;  // inclusive prefix over lanes
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o);
             if (lane >= (uint32_t)o) x += y;
         }
         const uint32_t tot = __shfl(x, 63);
         uint32_t r = base + x - c;
-        uint32_t m = W[k];
+        uint64_t smask = 0;
+        const uint32_t L = lane + 64u * (uint32_t)k;
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint32_t sj = __builtin_amdgcn_readlane(slot_v, j);
+            if ((L >> j) & 1u) smask |= 1ull << sj;
+        }
+        uint32_t m = w;
         while (m && r < mf) {
-            const uint32_t s = (uint32_t)__ffs(m) - 1;
+            const uint32_t st = (uint32_t)__ffs(m) - 1;
             m &= m - 1;
-            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 0] = (uint64_t)(lane + 64u * (uint32_t)k);
-            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 1] = (uint64_t)s << 48;
+            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 0] = smask;
+            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 1] = (uint64_t)st << 48;
             ++r;
         }
         base += tot;
@@ -217,7 +352,10 @@ __device__ __forceinline__ void write_final_lattice(const Args &a, int32_t key, 
     if (lane == 0 && a.n_final) a.n_final[key] = base < mf ? base : mf;
 }
 
-template <int R>
+// The lattice is indexed by DENSE op indices 0..n-1 (n = ops pending), not by
+// window slots: an invoke appends index n; when the op at index j returns, the
+// op at index n-1 takes index j (its configs move from bit n-1 to bit j, a
+// two-bit exchange).  So the lattice spans 2^n subsets, n = pending count.
 __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
     const uint32_t lane = lane_id();
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
@@ -227,15 +365,20 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
         return K_DONE;
     }
     const uint32_t nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
-    const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;
+    const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;  // = max ops pending at once
     if (nstates > T0_MAX_STATES || width > T0_MAX_WIDTH || a.init_state >= T0_MAX_STATES) return K_SPILL;
+    const uint64_t budget = a.budget;
+    const int dbg = a.debug_mode;  // 0 in every real run (ablation builds only)
 
-    uint32_t W[R];
+    Lat W;
 #pragma unroll
-    for (int k = 0; k < R; ++k) W[k] = 0;
+    for (int k = 0; k < T0_RMAX; ++k) W[k] = 0;
     if (lane == 0) W[0] = 1u << a.init_state;
-    uint32_t desc_v = 0;  // lane q: descriptor of the op in slot q
-    uint64_t pending = 0;
+    uint32_t desc_v = 0;   // lane j: descriptor of the op at dense index j
+    uint32_t pass_v = 0, keep_v = 0, set_v = 0;  // lane j: its Xfer masks
+    uint32_t slot_v = 0;   // lane j: window slot of the op at dense index j
+    uint32_t dense_v = 0;  // lane s: dense index of the op in window slot s
+    uint32_t n = 0;        // ops pending
     uint32_t peak = 1, probes = 0;
 
     for (uint64_t base = b; base < e; base += 64) {
@@ -246,61 +389,55 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
             const uint32_t slot = LC_EV_SLOT(evi);
             if (!(evi & LC_EV_OK_BIT)) {
-                if (slot >= T0_MAX_WIDTH) return K_SPILL;
+                if (n >= T0_MAX_WIDTH || slot >= 64) return K_SPILL;
                 const uint32_t d = __builtin_amdgcn_readlane(dsc, i);
-                if (lane == slot) desc_v = d;
-                pending |= 1ull << slot;
+                if (lane == n) {
+                    const Xfer x = xfer_of(d);
+                    desc_v = d; slot_v = slot; pass_v = x.pass; keep_v = x.keep; set_v = x.set;
+                }
+                if (lane == slot) dense_v = n;
+                ++n;
                 continue;
             }
-            const uint32_t p = slot;
-            const int32_t evno = (int32_t)(base + i - b);
-            const uint64_t pbit = 1ull << p;
-            const uint32_t dp = __builtin_amdgcn_readlane(desc_v, p);
-            // registers that can hold configs: subsets of slots < hi
-            const uint32_t hi = 64u - (uint32_t)__builtin_clzll(pending);  // pending != 0 (p is pending)
-            const int live = hi <= 6 ? 1 : (1 << (hi - 6));
-            uint32_t Ret[R], I[R];
-#pragma unroll
-            for (int k = 0; k < R; ++k)
-                if (k < live) probes += (uint32_t)__popc(W[k]);  // |S| (oracle: one probe per config of S)
-            split_any<R>(p, W, Ret, I, lane, live);
-            const uint64_t cand = pending & ~pbit;
-            for (;;) {
-                bool ch = false;
-                for (uint64_t m = cand; m; m &= m - 1) {
-                    const uint32_t q = (uint32_t)__builtin_ctzll(m);
-                    ch |= expand_any<R>(q, I, __builtin_amdgcn_readlane(desc_v, q), lane, live);
-                }
-                if (!__any(ch)) break;
+            const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
+            uint32_t nSn = 0;
+            int r = 0;
+            if (dbg == 1) {  // ablation: bookkeeping only
+                const uint32_t last = n - 1;
+                const uint32_t d_last = __builtin_amdgcn_readlane(desc_v, last);
+                const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
+                if (lane == p) { desc_v = d_last; slot_v = s_last; }
+                if (lane == s_last) dense_v = p;
+                --n;
+                continue;
             }
-            const uint32_t nI = wave_count<R>(I, live);
-            for (uint64_t m = cand; m; m &= m - 1) {
-                const uint32_t q = (uint32_t)__builtin_ctzll(m);
-                probes += probes_any<R>(q, I, __builtin_amdgcn_readlane(desc_v, q), lane, live);
-            }
-            uint32_t Sn[R];
-#pragma unroll
-            for (int k = 0; k < R; ++k) {
-                if (k >= live) { Sn[k] = 0; continue; }
-                Sn[k] = Ret[k] | tmask(I[k], dp);
-                probes += legal_cnt(I[k], dp);
-            }
-            const uint32_t nSn = wave_count<R>(Sn, live);
-            if (nI > a.budget || nSn == 0 || nSn > a.budget) {
-                const bool invalid = nI <= a.budget && nSn == 0;
-                write_final_lattice<R>(a, key, W, lane);
+            if (n <= 6) r = ok_event_1(W[0], p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn);
+            else if (n == 7) r = ok_event<2>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
+            else if (n == 8) r = ok_event<4>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
+            else if (n == 9) r = ok_event<8>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
+            else r = ok_event<16>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
+            if (r) {
+                const int32_t evno = (int32_t)(base + i - b);
+                write_final_lattice(a, key, W, lane, slot_v, n);
                 const uint32_t pr = __ockl_wfred_add_u32(probes);
-                finish_key(a, key, invalid ? LC_INVALID : LC_UNKNOWN, invalid ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET,
-                           evno, peak, pr, (uint64_t)evno + (invalid ? 1u : 0u));
+                finish_key(a, key, r == 1 ? LC_INVALID : LC_UNKNOWN, r == 1 ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET,
+                           evno, peak, pr, (uint64_t)evno + (r == 1 ? 1u : 0u));
                 return K_DONE;
             }
-#pragma unroll
-            for (int k = 0; k < R; ++k) W[k] = Sn[k];
             peak = nSn > peak ? nSn : peak;
-            pending &= ~pbit;
+            const uint32_t last = n - 1;
+            if (p != last) {
+                const uint32_t d_last = __builtin_amdgcn_readlane(desc_v, last);
+                const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
+                const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last), x1 = __builtin_amdgcn_readlane(keep_v, last),
+                               x2 = __builtin_amdgcn_readlane(set_v, last);
+                if (lane == p) { desc_v = d_last; slot_v = s_last; pass_v = x0; keep_v = x1; set_v = x2; }
+                if (lane == s_last) dense_v = p;
+            }
+            --n;
         }
     }
-    write_final_lattice<R>(a, key, W, lane);
+    write_final_lattice(a, key, W, lane, slot_v, n);
     const uint32_t pr = __ockl_wfred_add_u32(probes);
     finish_key(a, key, LC_VALID, LC_CAUSE_NONE, -1, peak, pr, e - b);
     return K_DONE;
@@ -310,7 +447,7 @@ __global__ __launch_bounds__(64) void k_search_lattice(Args a) {
     const int32_t n = a.n_in ? *a.n_in : a.n_order;
     for (int32_t w = next_work(a); w < n; w = next_work(a)) {
         const int32_t key = a.order[w];
-        const int r = lattice_key<T0_RMAX>(a, key);
+        const int r = lattice_key(a, key);
         if (r == K_SPILL) push_list(a.spill, a.n_spill, key);
     }
 }

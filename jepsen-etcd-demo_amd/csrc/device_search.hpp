@@ -21,6 +21,7 @@ struct Args {
     uint32_t shared_states;      // state ids used by the shared table (trans_off == null)
     uint64_t budget;
     int32_t max_final;
+    int32_t debug_mode;          // 0; ablation builds only (lc_opts.reserved[0])
     // work list of this launch: keys order[0 .. n) with n = n_in ? *n_in : n_order
     const int32_t *order;
     int32_t n_order;
