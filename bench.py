@@ -95,11 +95,10 @@ def main():
     valid = torch.empty(K, dtype=torch.int8, device=tdev)
     fail_event = torch.empty(K, dtype=torch.int32, device=tdev)
     cause = torch.empty(K, dtype=torch.uint8, device=tdev)
-    peak = torch.empty(K, dtype=torch.int32, device=tdev)
     import ctypes as C
+    # verdict records only: no peak sizes, no counterexample configs in the step
     res = N.LcResult(C.cast(valid.data_ptr(), N.P(C.c_int8)), C.cast(fail_event.data_ptr(), N.P(C.c_int32)),
-                     C.cast(cause.data_ptr(), N.P(C.c_uint8)), C.cast(peak.data_ptr(), N.P(C.c_uint32)),
-                     None, None)
+                     C.cast(cause.data_ptr(), N.P(C.c_uint8)), None, None, None)
     gathered = torch.empty(K * world, dtype=torch.int64, device=tdev) if world > 1 else None
 
     from lincheck import parallel as P

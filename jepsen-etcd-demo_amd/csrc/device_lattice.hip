@@ -41,7 +41,7 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 namespace lcd {
 
 constexpr int T0_RMAX = 16;       // registers per lane -> 1024 subsets
-constexpr uint32_t T0_MAX_WIDTH = 10;
+constexpr uint32_t T0_MAX_WIDTH = 10;  // = 6 + log2(T0_RMAX)
 constexpr uint32_t T0_MAX_STATES = 32;
 
 // Mask of states reachable from mask M through op d (0 if illegal for all).
@@ -114,119 +114,113 @@ __device__ __forceinline__ uint32_t xchg(uint32_t x) {
     else return (uint32_t)__shfl_xor((int)x, 32);
 }
 
-// Every helper below works on the first RL registers of a T0_RMAX array
-// (RL = registers that can hold configs for the current pending count); the
-// ok-event handler is instantiated once per RL, so its loops carry no
-// run-time register guards.
 using Lat = uint32_t[T0_RMAX];
 
-// Partner of register k of X along subset bit Q (lane exchange or register pair).
-template <int Q>
-__device__ __forceinline__ uint32_t partner(const Lat &X, int k) {
-    if constexpr (Q < 6) return xchg<Q>(X[k]);
-    else return X[k ^ (1 << (Q - 6))];
-}
-
-template <int Q>
-__device__ __forceinline__ bool has_bit(uint32_t lane, int k) {
-    if constexpr (Q < 6) return (lane >> Q) & 1u;
-    else return (k >> (Q - 6)) & 1;
-}
-
-// Dispatch a templated functor on a run-time subset bit q < 6 + log2(RL).
-template <int RL, class F>
-__device__ __forceinline__ auto on_bit(uint32_t q, F &&f) {
-    switch (q) {
-        case 0: return f(std::integral_constant<int, 0>{});
-        case 1: return f(std::integral_constant<int, 1>{});
-        case 2: return f(std::integral_constant<int, 2>{});
-        case 3: return f(std::integral_constant<int, 3>{});
-        case 4: return f(std::integral_constant<int, 4>{});
-        case 5: return f(std::integral_constant<int, 5>{});
-        case 6: if constexpr (RL > 1) return f(std::integral_constant<int, 6>{}); [[fallthrough]];
-        case 7: if constexpr (RL > 2) return f(std::integral_constant<int, 7>{}); [[fallthrough]];
-        case 8: if constexpr (RL > 4) return f(std::integral_constant<int, 8>{}); [[fallthrough]];
-        default: if constexpr (RL > 8) return f(std::integral_constant<int, 9>{});
-                 return f(std::integral_constant<int, 0>{});  // unreachable: q < n
-    }
-}
-
+// P[k] = X[k's partner along subset bit `bit`] (run-time bit; lanes active).
 template <int RL>
-__device__ __forceinline__ uint32_t lat_count(const Lat &X) {
-    uint32_t c = 0;
+__device__ __forceinline__ void xchg_rt(const Lat &X, Lat &P, uint32_t bit) {
+    if (bit < 6) {
+        const int m = 1 << bit;
 #pragma unroll
-    for (int k = 0; k < RL; ++k) c += (uint32_t)__popc(X[k]);
-    return c;
-}
-
-// One :ok(p) event on a lattice of RL registers.  W = S on entry, S' on a
-// normal exit (relocated so index n-1 is free).  Returns 0 normal,
-// 1 invalid, 2 budget exceeded.
-template <int RL>
-__device__ __forceinline__ int ok_event(Lat &W, uint32_t p, uint32_t n, uint32_t desc_v, uint32_t lane,
-                                        uint64_t budget, uint32_t &probes, uint32_t &nSn_out, int dbg) {
-    Lat Ret, I;
-    const uint32_t dp = __builtin_amdgcn_readlane(desc_v, p);
-    probes += lat_count<RL>(W);  // oracle: one probe per config of S
-    on_bit<RL>(p, [&](auto QC) {
-        constexpr int Q = decltype(QC)::value;
-#pragma unroll
-        for (int k = 0; k < RL; ++k) {
-            const uint32_t src = partner<Q>(W, k);
-            const bool hp = has_bit<Q>(lane, k);
-            Ret[k] = hp ? 0u : src;
-            I[k] = hp ? 0u : W[k];
-        }
-        return 0;
-    });
-    // JIT closure over the other pending ops, Gauss-Seidel to a fixpoint
-    const uint64_t cand = ((1ull << n) - 1ull) & ~(1ull << p);
-    for (int sweep = 0;; ++sweep) {
-        uint32_t ch = 0;
-        for (uint64_t m = cand; m; m &= m - 1) {
-            const uint32_t q = (uint32_t)__builtin_ctzll(m);
-            const uint32_t dq = __builtin_amdgcn_readlane(desc_v, q);
-            ch |= on_bit<RL>(q, [&](auto QC) -> uint32_t {
-                constexpr int Q = decltype(QC)::value;
-                uint32_t c = 0;
-                uint32_t src[RL];
-#pragma unroll
-                for (int k = 0; k < RL; ++k) src[k] = partner<Q>(I, k);
-#pragma unroll
-                for (int k = 0; k < RL; ++k) {
-                    if (!has_bit<Q>(lane, k)) continue;  // compile-time for Q >= 6
-                    const uint32_t nv = I[k] | tmask(src[k], dq);
-                    c |= nv ^ I[k];
-                    I[k] = nv;
-                }
-                return c;
-            });
-        }
-        if (!__any(ch != 0) || (dbg == 4 && sweep == 0)) break;
+        for (int k = 0; k < RL; ++k) P[k] = (uint32_t)__shfl_xor((int)X[k], m);
+        return;
     }
-    const uint32_t nI = __ockl_wfred_add_u32(lat_count<RL>(I));
-    for (uint64_t m = dbg == 3 ? 0 : cand; m; m &= m - 1) {
-        const uint32_t q = (uint32_t)__builtin_ctzll(m);
-        const uint32_t dq = __builtin_amdgcn_readlane(desc_v, q);
-        probes += on_bit<RL>(q, [&](auto QC) -> uint32_t {
-            constexpr int Q = decltype(QC)::value;
-            uint32_t c = 0;
-#pragma unroll
-            for (int k = 0; k < RL; ++k)
-                if (!has_bit<Q>(lane, k)) c += legal_cnt(I[k], dq);
-            return c;
-        });
-    }
+    const uint32_t r = bit - 6;
 #pragma unroll
     for (int k = 0; k < RL; ++k) {
-        Ret[k] |= tmask(I[k], dp);  // Ret becomes S'
-        probes += legal_cnt(I[k], dp);
+        uint32_t v = X[k];
+        if constexpr (RL > 1) v = r == 0 ? X[k ^ 1] : v;
+        if constexpr (RL > 2) v = r == 1 ? X[k ^ 2] : v;
+        if constexpr (RL > 4) v = r == 2 ? X[k ^ 4] : v;
+        if constexpr (RL > 8) v = r == 3 ? X[k ^ 8] : v;
+        P[k] = v;
     }
-    const uint32_t nSn = __ockl_wfred_add_u32(lat_count<RL>(Ret));
-    nSn_out = nSn;
-    if (nI > budget) return 2;
-    if (nSn == 0) return 1;
-    if (nSn > budget) return 2;
+}
+
+__device__ __forceinline__ bool idx_has(uint32_t lane, int k, uint32_t q) {
+    return q < 6 ? ((lane >> q) & 1u) : (((uint32_t)k >> (q - 6)) & 1u);
+}
+
+template <int RL>
+constexpr int lat_bits() { return RL == 1 ? 6 : RL == 2 ? 7 : RL == 4 ? 8 : RL == 8 ? 9 : 10; }
+
+// One :ok(p) event on a lattice of RL registers (n <= 6 + log2 RL pending
+// ops).  Every subset bit position is applied in every sweep, branch-free:
+// positions that are not candidates carry zero transfer masks.  Lane bits
+// move through VALU exchanges (xv), register bits through register pairs.
+// W = S on entry, S' (relocated so index n-1 is free) on a normal return.
+// Returns 0 normal, 1 invalid, 2 budget exceeded.
+template <int RL>
+__device__ __forceinline__ int ok_event_r(Lat &W, uint32_t p, uint32_t n, uint32_t pass_v, uint32_t keep_v,
+                                          uint32_t set_v, uint32_t lane, uint64_t budget, uint32_t &probes,
+                                          uint32_t &nSn_out, bool want_size) {
+    constexpr int NB = lat_bits<RL>();
+    const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
+    uint32_t ps[NB], kp[NB], st[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        const bool on = (cand >> q) & 1u;
+        ps[q] = on ? __builtin_amdgcn_readlane(pass_v, q) : 0u;
+        kp[q] = on ? __builtin_amdgcn_readlane(keep_v, q) : 0u;
+        st[q] = on ? __builtin_amdgcn_readlane(set_v, q) : 0u;
+    }
+    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
+                   pt = __builtin_amdgcn_readlane(set_v, p);
+    Lat Ret, I;  // with W: the only three lattice arrays (register budget)
+#pragma unroll
+    for (int k = 0; k < RL; ++k) probes += (uint32_t)__popc(W[k]);
+    xchg_rt<RL>(W, Ret, p);
+#pragma unroll
+    for (int k = 0; k < RL; ++k) {
+        const bool hp = idx_has(lane, k, p);
+        Ret[k] = hp ? 0u : Ret[k];
+        I[k] = hp ? 0u : W[k];
+    }
+    for (;;) {  // Jacobi sweeps to the fixpoint; W is scratch from here on
+        bool ch = false;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) {
+            uint32_t acc = I[k];
+#define LC_LANEBIT(Q)                                                                  \
+            {                                                                          \
+                const uint32_t x = xv<Q>(I[k], lane);                                  \
+                acc |= ((lane >> Q) & 1u) ? xapply(x, ps[Q], kp[Q], st[Q]) : 0u;      \
+            }
+            LC_LANEBIT(0) LC_LANEBIT(1) LC_LANEBIT(2) LC_LANEBIT(3) LC_LANEBIT(4) LC_LANEBIT(5)
+#undef LC_LANEBIT
+#pragma unroll
+            for (int q = 6; q < NB; ++q)
+                if ((k >> (q - 6)) & 1) acc |= xapply(I[k ^ (1 << (q - 6))], ps[q], kp[q], st[q]);
+            W[k] = acc;
+        }
+#pragma unroll
+        for (int k = 0; k < RL; ++k) { ch |= W[k] != I[k]; I[k] = W[k]; }
+        if (!__any(ch)) break;
+    }
+    uint32_t cI = 0, cS = 0;
+#pragma unroll
+    for (int k = 0; k < RL; ++k) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+            if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(I[k] & (ps[q] | kp[q]));
+        Ret[k] |= xapply(I[k], pp, pk, pt);
+        probes += (uint32_t)__popc(I[k] & (pp | pk));
+        cI += (uint32_t)__popc(I[k]);
+        cS += (uint32_t)__popc(Ret[k]);
+    }
+    // The lattice holds at most RL*64*32 configs: below that budget sizes
+    // decide :unknown; above it only emptiness matters (one ballot), and the
+    // exact |S'| is reduced only when a peak was asked for.
+    if (budget < (uint64_t)RL * 64u * 32u) {
+        const uint32_t nI = __ockl_wfred_add_u32(cI);
+        if (nI > budget) return 2;
+    }
+    if (!__any(cS != 0u)) { nSn_out = 0; return 1; }
+    if (budget < (uint64_t)RL * 64u * 32u || want_size) {
+        const uint32_t nSn = __ockl_wfred_add_u32(cS);
+        nSn_out = nSn;
+        if (nSn > budget) return 2;
+    }
     const uint32_t last = n - 1;
     if (p == last) {
 #pragma unroll
@@ -235,34 +229,22 @@ __device__ __forceinline__ int ok_event(Lat &W, uint32_t p, uint32_t n, uint32_t
     }
     // the op at index `last` moves to index p: S'[L] for L with p comes from
     // L ^ {p, last}; no config keeps bit `last`
-    on_bit<RL>(p, [&](auto QC) {
-        constexpr int Q = decltype(QC)::value;
-#pragma unroll
-        for (int k = 0; k < RL; ++k) I[k] = partner<Q>(Ret, k);
-        return 0;
-    });
-    on_bit<RL>(last, [&](auto LC) {
-        constexpr int QL = decltype(LC)::value;
-#pragma unroll
-        for (int k = 0; k < RL; ++k) W[k] = partner<QL>(I, k);
-        return 0;
-    });
+    xchg_rt<RL>(Ret, W, p);
+    xchg_rt<RL>(W, I, last);
 #pragma unroll
     for (int k = 0; k < RL; ++k) {
-        const bool hp = p < 6 ? ((lane >> p) & 1u) : (((uint32_t)k >> (p - 6)) & 1u);
-        const bool hl = last < 6 ? ((lane >> last) & 1u) : (((uint32_t)k >> (last - 6)) & 1u);
-        W[k] = hl ? 0u : (hp ? W[k] : Ret[k]);
+        const bool hp = idx_has(lane, k, p), hl = idx_has(lane, k, last);
+        W[k] = hl ? 0u : (hp ? I[k] : Ret[k]);
     }
     return 0;
 }
-
 
 // One :ok(p) event when at most 6 ops are pending: the whole lattice is one
 // register, every subset bit is a lane bit, and each closure sweep applies
 // all six bit positions branch-free (non-candidates carry zero masks).
 __device__ __forceinline__ int ok_event_1(uint32_t &W, uint32_t p, uint32_t n, uint32_t pass_v, uint32_t keep_v,
                                           uint32_t set_v, uint32_t lane, uint64_t budget, uint32_t &probes,
-                                          uint32_t &nSn_out) {
+                                          uint32_t &nSn_out, bool want_size) {
     const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
     uint32_t ps[6], kp[6], st[6];
 #pragma unroll
@@ -279,30 +261,37 @@ __device__ __forceinline__ int ok_event_1(uint32_t &W, uint32_t p, uint32_t n, u
     const uint32_t wp = (uint32_t)__shfl_xor((int)W, 1 << p);
     uint32_t Ret = hp ? 0u : wp;
     uint32_t I = hp ? 0u : W;
+    // Jacobi sweeps: the six bit positions read the same I, so their lane
+    // exchanges are independent (ILP); the exchange runs with every lane
+    // active, only its result is masked.  Repeat until nothing new.
     for (;;) {
-        uint32_t ch = 0;
-#define LC_EXPAND(Q)                                                          \
-        {                                                                     \
-            uint32_t t = xapply(xv<Q>(I, lane), ps[Q], kp[Q], st[Q]);         \
-            t = ((lane >> Q) & 1u) ? t : 0u;                                  \
-            ch |= t & ~I;                                                     \
-            I |= t;                                                           \
-        }
+#define LC_EXPAND(Q) \
+        const uint32_t x##Q = xv<Q>(I, lane); \
+        const uint32_t t##Q = ((lane >> Q) & 1u) ? xapply(x##Q, ps[Q], kp[Q], st[Q]) : 0u;
         LC_EXPAND(0) LC_EXPAND(1) LC_EXPAND(2) LC_EXPAND(3) LC_EXPAND(4) LC_EXPAND(5)
 #undef LC_EXPAND
-        if (!__any(ch != 0)) break;
+        const uint32_t nv = I | t0 | t1 | t2 | t3 | t4 | t5;
+        const bool ch = nv != I;
+        I = nv;
+        if (!__any(ch)) break;
     }
-    const uint32_t nI = __ockl_wfred_add_u32((uint32_t)__popc(I));
 #pragma unroll
     for (int q = 0; q < 6; ++q)
         if (!((lane >> q) & 1u)) probes += (uint32_t)__popc(I & (ps[q] | kp[q]));
     Ret |= xapply(I, pp, pk, pt);
     probes += (uint32_t)__popc(I & (pp | pk));
-    const uint32_t nSn = __ockl_wfred_add_u32((uint32_t)__popc(Ret));
-    nSn_out = nSn;
-    if (nI > budget) return 2;
-    if (nSn == 0) return 1;
-    if (nSn > budget) return 2;
+    // One register holds at most 64 x 32 configs: with a larger budget only
+    // emptiness matters (a ballot); exact sizes only when asked for (peak).
+    if (budget < 64u * 32u) {
+        const uint32_t nI = __ockl_wfred_add_u32((uint32_t)__popc(I));
+        if (nI > budget) return 2;
+    }
+    if (!__any(Ret != 0u)) { nSn_out = 0; return 1; }
+    if (budget < 64u * 32u || want_size) {
+        const uint32_t nSn = __ockl_wfred_add_u32((uint32_t)__popc(Ret));
+        nSn_out = nSn;
+        if (nSn > budget) return 2;
+    }
     const uint32_t last = n - 1;
     if (p == last) { W = Ret; return 0; }
     // op at index `last` moves to index p
@@ -356,7 +345,9 @@ __device__ __forceinline__ void write_final_lattice(const Args &a, int32_t key, 
 // window slots: an invoke appends index n; when the op at index j returns, the
 // op at index n-1 takes index j (its configs move from bit n-1 to bit j, a
 // two-bit exchange).  So the lattice spans 2^n subsets, n = pending count.
+template <int RMAX>
 __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
+    constexpr uint32_t MAXW = 6 + (RMAX == 1 ? 0 : RMAX == 2 ? 1 : RMAX == 4 ? 2 : RMAX == 8 ? 3 : 4);
     const uint32_t lane = lane_id();
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
@@ -369,6 +360,7 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
     if (nstates > T0_MAX_STATES || width > T0_MAX_WIDTH || a.init_state >= T0_MAX_STATES) return K_SPILL;
     const uint64_t budget = a.budget;
     const int dbg = a.debug_mode;  // 0 in every real run (ablation builds only)
+    const bool want_peak = a.peak != nullptr;
 
     Lat W;
 #pragma unroll
@@ -381,15 +373,19 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
     uint32_t n = 0;        // ops pending
     uint32_t peak = 1, probes = 0;
 
+    // events arrive 64 at a time, one per lane; the next chunk's words and
+    // descriptors are loaded while this chunk is searched
+    uint32_t ev_next = b + lane < e ? a.events[b + lane] : 0u;
     for (uint64_t base = b; base < e; base += 64) {
         const uint32_t cnt = (uint32_t)((e - base) < 64 ? (e - base) : 64);
-        const uint32_t ev = lane < cnt ? a.events[base + lane] : 0u;
+        const uint32_t ev = ev_next;
         const uint32_t dsc = (lane < cnt && !(ev & LC_EV_OK_BIT)) ? a.trans[tb + LC_EV_TRANS(ev)] : 0u;
+        ev_next = base + 64 + lane < e ? a.events[base + 64 + lane] : 0u;
         for (uint32_t i = 0; i < cnt; ++i) {
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
             const uint32_t slot = LC_EV_SLOT(evi);
             if (!(evi & LC_EV_OK_BIT)) {
-                if (n >= T0_MAX_WIDTH || slot >= 64) return K_SPILL;
+                if (n >= MAXW || slot >= 64) return K_SPILL;
                 const uint32_t d = __builtin_amdgcn_readlane(dsc, i);
                 if (lane == n) {
                     const Xfer x = xfer_of(d);
@@ -402,7 +398,7 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
             const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
             uint32_t nSn = 0;
             int r = 0;
-            if (dbg == 1) {  // ablation: bookkeeping only
+            if (dbg == 1 || (dbg == 5 && n > 6)) {  // ablation: bookkeeping only
                 const uint32_t last = n - 1;
                 const uint32_t d_last = __builtin_amdgcn_readlane(desc_v, last);
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
@@ -411,11 +407,12 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
                 --n;
                 continue;
             }
-            if (n <= 6) r = ok_event_1(W[0], p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn);
-            else if (n == 7) r = ok_event<2>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
-            else if (n == 8) r = ok_event<4>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
-            else if (n == 9) r = ok_event<8>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
-            else r = ok_event<16>(W, p, n, desc_v, lane, budget, probes, nSn, dbg);
+            if (n <= 6) r = ok_event_1(W[0], p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
+            else if (n == 7) r = ok_event_r<2>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
+            else if (n == 8) r = ok_event_r<4>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
+            else if constexpr (RMAX == 8) r = ok_event_r<8>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
+            else if (n == 9) r = ok_event_r<8>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
+            else r = ok_event_r<16>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
             if (r) {
                 const int32_t evno = (int32_t)(base + i - b);
                 write_final_lattice(a, key, W, lane, slot_v, n);
@@ -443,11 +440,12 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
     return K_DONE;
 }
 
+// T0 over a work list: one wavefront per key, lattice of up to 16 registers.
 __global__ __launch_bounds__(64) void k_search_lattice(Args a) {
     const int32_t n = a.n_in ? *a.n_in : a.n_order;
     for (int32_t w = next_work(a); w < n; w = next_work(a)) {
         const int32_t key = a.order[w];
-        const int r = lattice_key(a, key);
+        const int r = lattice_key<T0_RMAX>(a, key);
         if (r == K_SPILL) push_list(a.spill, a.n_spill, key);
     }
 }
