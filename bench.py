@@ -115,11 +115,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, probes, deep = [], 0, 0
+    kernel_ms, tier0_ms, probes, deep = [], [], 0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
         kernel_ms.append(st.kernel_ms)
+        tier0_ms.append(st.tier0_ms)
         probes = st.probes
         deep = st.deep_keys
     torch.cuda.synchronize()
@@ -140,11 +141,20 @@ def main():
         n_ops_total = K * ops * world
         value = n_ops_total * args.steps / elapsed
         avg_kernel_ms = float(np.mean(kernel_ms))
+        avg_t0_ms = float(np.mean(tier0_ms))
         n_events = int(packed.ev_off[-1])
-        # algorithmic HBM bytes per launch: event words + key offsets + LPT
-        # order read, verdict records written (Measurement)
-        alg_bytes = 4 * n_events + 8 * (K + 1) + 4 * K + (1 + 4 + 1 + 4) * K
-        achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        max_events = int(np.diff(packed.ev_off.astype(np.int64)).max()) if K else 0
+        # Algorithmic HBM bytes of one launch of the dominant kernel (the
+        # register-lattice tier, DESIGN.md "Measurement"): every event word
+        # (4 B), the key offsets (8 B) and LPT order (4 B) read, the
+        # transition table read once, a verdict record (valid 1 B + failing
+        # event 4 B + cause 1 B) written per key.
+        alg_bytes = 4 * n_events + 8 * (K + 1) + 4 * K + 4 * int(packed.view.n_trans) + 6 * K
+        achieved = alg_bytes / (avg_t0_ms * 1e-3) / 1e9
+        # SURVEY.md 8(d) D-4's notional model (16 B A3 record per op, 17 B per
+        # key, one 64 B HBM line per probe) for comparison only: in T0 the
+        # probes never leave registers.
+        d4_bytes = 16 * K * ops + 17 * K + 64 * probes
         traffic = None
         for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
             try:
@@ -185,7 +195,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
             "cpu_baseline": cpu,
             "kernel_ms": avg_kernel_ms,
+            "tier0_ms": avg_t0_ms,
+            "ns_per_event_critical_path": avg_t0_ms * 1e6 / max(max_events, 1),
             "probes_per_s": probes / (avg_kernel_ms * 1e-3),
+            "d4_model_gbs": d4_bytes / (avg_t0_ms * 1e-3) / 1e9,
             "deep_keys": deep,
             "verdicts": {"valid": int((v_host == 1).sum()), "invalid": int((v_host == 0).sum()),
                          "unknown": int((v_host == -1).sum())},

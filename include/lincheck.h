@@ -220,6 +220,7 @@ typedef struct lc_stats {
     uint64_t lds_keys;        /* keys finished in the LDS tier                  */
     uint64_t deep_keys;       /* keys (re)searched in the HBM tier              */
     uint64_t events;          /* events processed                               */
+    double   tier0_ms;        /* device time of the register-lattice tier alone */
 } lc_stats;
 
 typedef struct lc_ctx lc_ctx;

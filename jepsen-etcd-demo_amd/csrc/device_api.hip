@@ -71,7 +71,7 @@ struct lc_ctx {
     int device = 0;
     int cu_count = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr;
     std::mutex mu;
     // scratch, grown on demand
     int64_t cap_keys = 0;
@@ -97,6 +97,7 @@ struct lc_ctx {
         dfree(ws[0].base); dfree(ws[1].base);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
+        if (et0) (void)hipEventDestroy(et0);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -195,6 +196,7 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&c->e0));
         HIPCHK(hipEventCreate(&c->e1));
+        HIPCHK(hipEventCreate(&c->et0));
         HIPCHK(dalloc(&c->counters, 16));
         HIPCHK(dalloc(&c->acc, 4));
         return LC_OK;
@@ -385,6 +387,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
         int g0 = (int)std::min<int64_t>(K, (int64_t)c->cu_count * 16);
         HIPCHK(lcd::launch_t0(a0, g0, c->stream));
+        HIPCHK(hipEventRecord(c->et0, c->stream));
         // T1: LDS hash sets
         lcd::Args a1 = a;
         a1.order = spill0; a1.n_order = 0; a1.n_in = n_spill0; a1.ticket = c->counters + 9;
@@ -438,10 +441,12 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
             HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
-    float ms = 0;
+    float ms = 0, ms0 = 0;
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    if (K > 0) HIPCHK(hipEventElapsedTime(&ms0, c->e0, c->et0));
     if (st) {
         st->kernel_ms = ms;
+        st->tier0_ms = ms0;
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         st->probes = acc[0];
         st->events = acc[1];

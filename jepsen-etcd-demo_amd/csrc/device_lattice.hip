@@ -67,13 +67,14 @@ __device__ __forceinline__ uint32_t legal_cnt(uint32_t M, uint32_t d) {
 // and the number of configs of M where the op is legal is popc(M & (pass | keep)).
 struct Xfer { uint32_t pass, keep, set; };
 
-__device__ __forceinline__ Xfer xfer_of(uint32_t d) {
+__device__ __forceinline__ Xfer xfer_of(uint32_t d) {  // branch-free (uniform d: scalar selects)
     const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
-    const uint32_t abit = a < 32u ? 1u << a : 0u, bbit = b < 32u ? 1u << b : 0u;
-    if (f == LC_T_READ_ANY) return {0xFFFFFFFFu, 0u, 0u};
-    if (f == LC_T_READ) return {abit, 0u, 0u};
-    if (f == LC_T_WRITE) return {0u, 0xFFFFFFFFu, bbit};
-    return {0u, abit, bbit};
+    const uint32_t abit = a < 32u ? 1u << (a & 31u) : 0u, bbit = b < 32u ? 1u << (b & 31u) : 0u;
+    Xfer x;
+    x.pass = f == LC_T_READ_ANY ? 0xFFFFFFFFu : (f == LC_T_READ ? abit : 0u);
+    x.keep = f == LC_T_WRITE ? 0xFFFFFFFFu : (f == LC_T_CAS ? abit : 0u);
+    x.set = f >= LC_T_WRITE ? bbit : 0u;
+    return x;
 }
 
 __device__ __forceinline__ uint32_t xapply(uint32_t M, uint32_t pass, uint32_t keep, uint32_t set) {
@@ -387,10 +388,8 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
             if (!(evi & LC_EV_OK_BIT)) {
                 if (n >= MAXW || slot >= 64) return K_SPILL;
                 const uint32_t d = __builtin_amdgcn_readlane(dsc, i);
-                if (lane == n) {
-                    const Xfer x = xfer_of(d);
-                    desc_v = d; slot_v = slot; pass_v = x.pass; keep_v = x.keep; set_v = x.set;
-                }
+                const Xfer x = xfer_of(d);
+                if (lane == n) { desc_v = d; slot_v = slot; pass_v = x.pass; keep_v = x.keep; set_v = x.set; }
                 if (lane == slot) dense_v = n;
                 ++n;
                 continue;

@@ -66,7 +66,8 @@ class LcResult(C.Structure):
 
 class LcStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("total_ms", C.c_double), ("probes", C.c_uint64),
-                ("lds_keys", C.c_uint64), ("deep_keys", C.c_uint64), ("events", C.c_uint64)]
+                ("lds_keys", C.c_uint64), ("deep_keys", C.c_uint64), ("events", C.c_uint64),
+                ("tier0_ms", C.c_double)]
 
 
 class LcSynthOpts(C.Structure):

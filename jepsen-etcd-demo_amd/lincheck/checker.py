@@ -117,7 +117,7 @@ class Device:
     def _results(self, arrs, K, st) -> KeyResults:
         return KeyResults(arrs["valid"][:K], arrs["fail_event"][:K], arrs["cause"][:K],
                           arrs["peak"][:K], arrs["final"][:K], arrs["n_final"][:K],
-                          dict(kernel_ms=st.kernel_ms, total_ms=st.total_ms, probes=st.probes,
+                          dict(kernel_ms=st.kernel_ms, tier0_ms=st.tier0_ms, total_ms=st.total_ms, probes=st.probes,
                                keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events))
 
     def check(self, packed: Packed) -> KeyResults:
