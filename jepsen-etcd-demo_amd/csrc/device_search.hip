@@ -62,9 +62,10 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
         finish_key(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
     }
-    if ((a.key_width && a.key_width[key] > LC_NARROW_MAX_SLOTS) ||
-        (a.trans_off && a.key_states && a.key_states[key] > LC_NARROW_MAX_STATES))
-        return K_WIDE;
+    // Too many register states for an 8-bit state field: wide configs.  A
+    // wide window is decided per invoke (slot >= 56), not from key_width: a
+    // key often ends (budget, failure) long before its widest moment.
+    if (a.trans_off && a.key_states && a.key_states[key] > LC_NARROW_MAX_STATES) return K_WIDE;
 
     // fresh tables for this key
     for (int i = (int)lane; i < T::HS; i += 64) t.hS[i] = EMPTY;
