@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--budget", type=int, default=1 << 20)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--keys", type=int, default=0, help="override keys per GPU (exploration only)")
+    ap.add_argument("--ops", type=int, default=0, help="override ops per key (exploration only)")
     return ap.parse_args()
 
 
@@ -80,7 +82,11 @@ def main():
     from lincheck import _native as N
     from lincheck.checker import Device, Packed
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.keys or args.ops:
+        cfg["keys"] = args.keys or cfg["keys"]
+        cfg["ops"] = args.ops or cfg["ops"]
+        cfg["desc"] += f" [overridden: {cfg['keys']} keys x {cfg['ops']} ops]"
     K, ops = cfg["keys"], cfg["ops"]
     t_gen = time.time()
     hist = H.synth(n_keys=K, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],

@@ -84,6 +84,8 @@ struct lc_ctx {
     uint32_t *peak = nullptr;
     uint64_t *final_cfg = nullptr;
     uint32_t *n_final = nullptr;
+    uint32_t *lat_ws = nullptr;    // T0 workspace (lattices of 9-10 pending ops)
+    int lat_ws_blocks = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
     struct Ws {
         char *base = nullptr;
@@ -94,7 +96,7 @@ struct lc_ctx {
     ~lc_ctx() {
         dfree(lists); dfree(counters); dfree(acc); dfree(valid); dfree(fail_event);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
-        dfree(ws[0].base); dfree(ws[1].base);
+        dfree(ws[0].base); dfree(ws[1].base); dfree(lat_ws);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (et0) (void)hipEventDestroy(et0);
@@ -386,6 +388,13 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         a0.order = d->order; a0.n_order = (int32_t)K; a0.n_in = nullptr; a0.ticket = c->counters + 8;
         a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
         int g0 = (int)std::min<int64_t>(K, (int64_t)c->cu_count * 16);
+        if (g0 > c->lat_ws_blocks) {
+            dfree(c->lat_ws);
+            c->lat_ws_blocks = 0;
+            HIPCHK(dalloc(&c->lat_ws, (size_t)g0 * lcd::lat_ws_words()));
+            c->lat_ws_blocks = g0;
+        }
+        a0.lat_ws = c->lat_ws;
         HIPCHK(lcd::launch_t0(a0, g0, c->stream));
         HIPCHK(hipEventRecord(c->et0, c->stream));
         // T1: LDS hash sets

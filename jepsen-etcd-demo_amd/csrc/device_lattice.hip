@@ -40,8 +40,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 
 namespace lcd {
 
-constexpr int T0_RMAX = 16;       // registers per lane -> 1024 subsets
-constexpr uint32_t T0_MAX_WIDTH = 10;  // = 6 + log2(T0_RMAX)
+constexpr int T0_RMAX = 4;        // lattice registers per lane: n <= 8 pending ops
+constexpr int T0_RMEM = 16;       // workspace lattice (global memory): n <= 10
+constexpr uint32_t T0_MAX_WIDTH = 10;  // = 6 + log2(T0_RMEM)
 constexpr uint32_t T0_MAX_STATES = 32;
 
 // Mask of states reachable from mask M through op d (0 if illegal for all).
@@ -302,19 +303,114 @@ __device__ __forceinline__ int ok_event_1(uint32_t &W, uint32_t p, uint32_t n, u
     return 0;
 }
 
-// First max_final configs of the lattice, in (register, lane, state) order,
-// with dense op indices translated back to window slots (slot_v: lane j holds
-// the slot of dense index j).
-__device__ __forceinline__ void write_final_lattice(const Args &a, int32_t key, const Lat &W, uint32_t lane,
-                                                    uint32_t slot_v, uint32_t n) {
+// Lattice of a key with 9 or 10 ops pending: 16 x 64 words per array in a
+// per-block global workspace, index k * 64 + lane.  Every lane reads and
+// writes only its own column (register-bit partners are in the same lane;
+// lane-bit partners are exchanged in registers), so no cross-lane memory
+// ordering is involved.  Such events are rare (< 0.2 % of C2's); keeping
+// them out of registers keeps T0 at 4 waves per SIMD.
+struct LatMem {
+    uint32_t *W, *R, *I;
+};
+
+template <int RL>
+__device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_t n, uint32_t pass_v,
+                                            uint32_t keep_v, uint32_t set_v, uint32_t lane, uint64_t budget,
+                                            uint32_t &probes, uint32_t &nSn_out, bool want_size) {
+    constexpr int NB = lat_bits<RL>();
+    const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
+    // transfer of candidate q: lane q of pass_v/keep_v/set_v, read at use
+    // (not hoisted: 3 x NB scalars would spill SGPRs into the VGPR budget)
+    const uint32_t cpass = pass_v & (((cand >> lane) & 1u) ? ~0u : 0u);
+    const uint32_t ckeep = keep_v & (((cand >> lane) & 1u) ? ~0u : 0u);
+#define PS(Q) __builtin_amdgcn_readlane(cpass, Q)
+#define KP(Q) __builtin_amdgcn_readlane(ckeep, Q)
+#define ST(Q) __builtin_amdgcn_readlane(set_v, Q)
+    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
+                   pt = __builtin_amdgcn_readlane(set_v, p);
+    const uint32_t plm = p < 6 ? 1u << p : 0u, prm = p >= 6 ? 1u << (p - 6) : 0u;
+#pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t w = m.W[k * 64 + lane];
+        probes += (uint32_t)__popc(w);
+        const uint32_t src = (uint32_t)__shfl_xor((int)m.W[(k ^ prm) * 64 + lane], (int)plm);
+        const bool hp = (lane & plm) || ((uint32_t)k & prm);
+        m.R[k * 64 + lane] = hp ? 0u : src;
+        m.I[k * 64 + lane] = hp ? 0u : w;
+    }
+    for (;;) {  // sweeps in place (monotone: any order reaches the fixpoint)
+        bool ch = false;
+    #pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+            const uint32_t x = m.I[k * 64 + lane];
+            uint32_t acc = x;
+#define LC_LANEBIT(Q)                                                                  \
+            {                                                                          \
+                const uint32_t y = xv<Q>(x, lane);                                     \
+                acc |= ((lane >> Q) & 1u) ? xapply(y, PS(Q), KP(Q), ST(Q)) : 0u;      \
+            }
+            LC_LANEBIT(0) LC_LANEBIT(1) LC_LANEBIT(2) LC_LANEBIT(3) LC_LANEBIT(4) LC_LANEBIT(5)
+#undef LC_LANEBIT
+#pragma unroll
+            for (int q = 6; q < NB; ++q)
+                if ((k >> (q - 6)) & 1) acc |= xapply(m.I[(k ^ (1 << (q - 6))) * 64 + lane], PS(q), KP(q), ST(q));
+            if (acc != x) { m.I[k * 64 + lane] = acc; ch = true; }
+        }
+        if (!__any(ch)) break;
+    }
+    uint32_t cI = 0, cS = 0;
+#pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t x = m.I[k * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+            if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(x & (PS(q) | KP(q)));
+        const uint32_t r = m.R[k * 64 + lane] | xapply(x, pp, pk, pt);
+        probes += (uint32_t)__popc(x & (pp | pk));
+        m.R[k * 64 + lane] = r;
+        cI += (uint32_t)__popc(x);
+        cS += (uint32_t)__popc(r);
+    }
+    if (budget < (uint64_t)RL * 64u * 32u) {
+        const uint32_t nI = __ockl_wfred_add_u32(cI);
+        if (nI > budget) return 2;
+    }
+    if (!__any(cS != 0u)) { nSn_out = 0; return 1; }
+    if (budget < (uint64_t)RL * 64u * 32u || want_size) {
+        const uint32_t nSn = __ockl_wfred_add_u32(cS);
+        nSn_out = nSn;
+        if (nSn > budget) return 2;
+    }
+#undef PS
+#undef KP
+#undef ST
+    // relocation: the op at index `last` moves to index p
+    const uint32_t last = n - 1;
+    const uint32_t llm = last < 6 ? 1u << last : 0u, lrm = last >= 6 ? 1u << (last - 6) : 0u;
+#pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t r = m.R[k * 64 + lane];
+        const uint32_t src = (uint32_t)__shfl_xor((int)m.R[(k ^ (prm | lrm)) * 64 + lane], (int)(plm | llm));
+        const bool hp = (lane & plm) || ((uint32_t)k & prm);
+        const bool hl = (lane & llm) || ((uint32_t)k & lrm);
+        m.W[k * 64 + lane] = p == last ? r : (hl ? 0u : (hp ? src : r));
+    }
+    return 0;
+}
+
+// First max_final configs of the lattice held in m.W (register lattices are
+// stored there first), in (register, lane, state) order, with dense op
+// indices translated back to window slots (slot_v: lane j holds the slot of
+// dense index j).
+__device__ __forceinline__ void write_final_mem(const Args &a, int32_t key, const LatMem &m, uint32_t lane,
+                                                uint32_t slot_v, uint32_t n) {
     if (!a.final_cfg) return;
     const uint32_t mf = (uint32_t)a.max_final;
     const int live = n <= 6 ? 1 : (1 << (n - 6));
     uint32_t base = 0;
-#pragma unroll
-    for (int k = 0; k < T0_RMAX; ++k) {
-        if (k >= live) continue;
-        const uint32_t w = W[k];
+#pragma unroll 1
+    for (int k = 0; k < live; ++k) {
+        const uint32_t w = m.W[k * 64 + lane];
         const uint32_t c = (uint32_t)__popc(w);
         uint32_t x = c;  // inclusive prefix over lanes
         for (int o = 1; o < 64; o <<= 1) {
@@ -329,10 +425,10 @@ __device__ __forceinline__ void write_final_lattice(const Args &a, int32_t key, 
             const uint32_t sj = __builtin_amdgcn_readlane(slot_v, j);
             if ((L >> j) & 1u) smask |= 1ull << sj;
         }
-        uint32_t m = w;
-        while (m && r < mf) {
-            const uint32_t st = (uint32_t)__ffs(m) - 1;
-            m &= m - 1;
+        uint32_t mm = w;
+        while (mm && r < mf) {
+            const uint32_t st = (uint32_t)__ffs(mm) - 1;
+            mm &= mm - 1;
             a.final_cfg[((size_t)key * a.max_final + r) * 2 + 0] = smask;
             a.final_cfg[((size_t)key * a.max_final + r) * 2 + 1] = (uint64_t)st << 48;
             ++r;
@@ -348,8 +444,11 @@ __device__ __forceinline__ void write_final_lattice(const Args &a, int32_t key, 
 // two-bit exchange).  So the lattice spans 2^n subsets, n = pending count.
 template <int RMAX>
 __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
-    constexpr uint32_t MAXW = 6 + (RMAX == 1 ? 0 : RMAX == 2 ? 1 : RMAX == 4 ? 2 : RMAX == 8 ? 3 : 4);
     const uint32_t lane = lane_id();
+    const LatMem m{a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64),
+                   a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64) + T0_RMEM * 64,
+                   a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64) + 2 * T0_RMEM * 64};
+    bool in_mem = false;  // lattice lives in m.W (9 or 10 ops pending)
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
@@ -386,7 +485,12 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
             const uint32_t slot = LC_EV_SLOT(evi);
             if (!(evi & LC_EV_OK_BIT)) {
-                if (n >= MAXW || slot >= 64) return K_SPILL;
+                if (n >= T0_MAX_WIDTH || slot >= 64) return K_SPILL;
+                if (n == 8) {  // 9 pending: move the lattice to the workspace
+#pragma unroll
+                    for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < T0_RMAX ? W[k < T0_RMAX ? k : 0] : 0u;
+                    in_mem = true;
+                }
                 const uint32_t d = __builtin_amdgcn_readlane(dsc, i);
                 const Xfer x = xfer_of(d);
                 if (lane == n) { desc_v = d; slot_v = slot; pass_v = x.pass; keep_v = x.keep; set_v = x.set; }
@@ -397,7 +501,7 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
             const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
             uint32_t nSn = 0;
             int r = 0;
-            if (dbg == 1 || (dbg == 5 && n > 6)) {  // ablation: bookkeeping only
+            if (dbg == 1) {  // ablation: bookkeeping only
                 const uint32_t last = n - 1;
                 const uint32_t d_last = __builtin_amdgcn_readlane(desc_v, last);
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
@@ -409,12 +513,15 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
             if (n <= 6) r = ok_event_1(W[0], p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
             else if (n == 7) r = ok_event_r<2>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
             else if (n == 8) r = ok_event_r<4>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            else if constexpr (RMAX == 8) r = ok_event_r<8>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            else if (n == 9) r = ok_event_r<8>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            else r = ok_event_r<16>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
+            else if (n == 9) r = ok_event_mem<8>(m, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
+            else r = ok_event_mem<16>(m, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
             if (r) {
                 const int32_t evno = (int32_t)(base + i - b);
-                write_final_lattice(a, key, W, lane, slot_v, n);
+                if (!in_mem) {
+#pragma unroll
+                    for (int k = 0; k < T0_RMAX; ++k) m.W[k * 64 + lane] = W[k];
+                }
+                write_final_mem(a, key, m, lane, slot_v, n);
                 const uint32_t pr = __ockl_wfred_add_u32(probes);
                 finish_key(a, key, r == 1 ? LC_INVALID : LC_UNKNOWN, r == 1 ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET,
                            evno, peak, pr, (uint64_t)evno + (r == 1 ? 1u : 0u));
@@ -431,15 +538,25 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
                 if (lane == s_last) dense_v = p;
             }
             --n;
+            if (in_mem && n == 8) {  // back to registers: no config holds index 8 or 9
+#pragma unroll
+                for (int k = 0; k < T0_RMAX; ++k) W[k] = m.W[k * 64 + lane];
+                in_mem = false;
+            }
         }
     }
-    write_final_lattice(a, key, W, lane, slot_v, n);
+    if (!in_mem) {
+#pragma unroll
+        for (int k = 0; k < T0_RMAX; ++k) m.W[k * 64 + lane] = W[k];
+    }
+    write_final_mem(a, key, m, lane, slot_v, n);
     const uint32_t pr = __ockl_wfred_add_u32(probes);
     finish_key(a, key, LC_VALID, LC_CAUSE_NONE, -1, peak, pr, e - b);
     return K_DONE;
 }
 
-// T0 over a work list: one wavefront per key, lattice of up to 16 registers.
+// T0 over a work list: one wavefront per key (lattice in 4 registers, or the
+// workspace for 9-10 pending ops).
 __global__ __launch_bounds__(64) void k_search_lattice(Args a) {
     const int32_t n = a.n_in ? *a.n_in : a.n_order;
     for (int32_t w = next_work(a); w < n; w = next_work(a)) {
@@ -448,6 +565,8 @@ __global__ __launch_bounds__(64) void k_search_lattice(Args a) {
         if (r == K_SPILL) push_list(a.spill, a.n_spill, key);
     }
 }
+
+size_t lat_ws_words() { return 3 * T0_RMEM * 64; }
 
 hipError_t launch_t0(const Args &a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_search_lattice, dim3(grid), dim3(64), 0, s, a);

@@ -34,6 +34,7 @@ struct Args {
     uint32_t *peak;          // may be null
     uint64_t *final_cfg;     // may be null: [key][max_final][2]
     uint32_t *n_final;       // may be null
+    uint32_t *lat_ws;            // T0 workspace: lat_ws_words() per resident block
     // counters
     unsigned long long *probes;
     unsigned long long *ev_count;
@@ -57,6 +58,7 @@ struct HbmWs {
 size_t lds_bytes_t1();
 size_t lds_bytes_t2();
 hipError_t launch_t0(const Args &a, int grid, hipStream_t s);
+size_t lat_ws_words();
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t2(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t3_narrow(const Args &a, const HbmWs &w, int grid, hipStream_t s);
