@@ -127,7 +127,6 @@ def main():
         st = step()
         kernel_ms.append(st.kernel_ms)
         tier0_ms.append(st.tier0_ms)
-        probes = st.probes
         deep = st.deep_keys
     torch.cuda.synchronize()
     if world > 1:
@@ -142,6 +141,12 @@ def main():
     # results of the last step (host copy, outside the timed region)
     v_host = valid.cpu().numpy()
     fe_host = fail_event.cpu().numpy()
+    if rank == 0:
+        # probe count from one extra, untimed pass with
+        # LC_OPT_COUNT_PROBES: the timed steps skip the per-event popcounts
+        dev_c = Device(local, budget=args.budget, count_probes=True)
+        probes = dev_c.upload(packed).check(peak=False).stats["probes"]
+        del dev_c
 
     if rank == 0:
         n_ops_total = K * ops * world
@@ -177,9 +182,18 @@ def main():
             tc = time.perf_counter()
             keys, orc = cref.check_history(hist.as_c(), budget=args.budget, threads=threads)
             tcpu = time.perf_counter() - tc
+            # one thread on a bounded sample (the first keys, ~1/8 of the batch)
+            k1 = max(1, K // 8)
+            h1 = H.synth(n_keys=k1, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
+                         anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"], key_base=0)
+            t1 = time.perf_counter()
+            cref.check_history(h1.as_c(), budget=args.budget, threads=1)
+            t1 = time.perf_counter() - t1
             cpu = {"value": K * ops / tcpu, "unit": "ops/s", "cores": threads, "kind": "port",
                    "sample": f"full {args.config} batch ({K} keys x {ops} ops), oracle/linear_ref.c, "
-                             f"{threads} threads, {tcpu:.2f} s"}
+                             f"{threads} threads, {tcpu:.2f} s",
+                   "one_thread": {"value": k1 * ops / t1, "cores": 1,
+                                  "sample": f"first {k1} keys of the batch, 1 thread, {t1:.2f} s"}}
             parity = bool(np.array_equal(orc["valid"], v_host) and np.array_equal(orc["fail_event"], fe_host))
         line = {
             "metric": "history ops linearizability-checked/sec (whole node)",

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 1
+#define LC_ABI_VERSION 2
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -185,8 +185,15 @@ typedef struct lc_opts {
                                the truncation of jepsen.checker/linearizable)   */
     int32_t  lds_configs;   /* per-wave LDS frontier capacity (0 = default)     */
     int32_t  deep_slots;    /* concurrently searched HBM-tier keys (0 = auto)    */
-    int32_t  reserved[6];
+    int32_t  flags;         /* LC_OPT_*                                          */
+    int32_t  debug_mode;    /* 0 (ablation builds only)                          */
+    int32_t  reserved[4];   /* must be 0                                         */
 } lc_opts;
+
+/* lc_opts.flags */
+#define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,
+                                    SURVEY.md 8(d) D-4); off, the register-lattice
+                                    tier skips the per-event popcounts          */
 
 /* :valid? per key */
 #define LC_VALID    1
@@ -216,7 +223,8 @@ typedef struct lc_result {
 typedef struct lc_stats {
     double   kernel_ms;       /* device time of the search kernels (HIP events) */
     double   total_ms;        /* wall time of the call                          */
-    uint64_t probes;          /* successor-config insert attempts (all tiers)   */
+    uint64_t probes;          /* successor-config insert attempts (all tiers);
+                                 0 unless lc_opts.flags has LC_OPT_COUNT_PROBES */
     uint64_t lds_keys;        /* keys finished in the LDS tier                  */
     uint64_t deep_keys;       /* keys (re)searched in the HBM tier              */
     uint64_t events;          /* events processed                               */

@@ -85,6 +85,9 @@ struct lc_ctx {
     uint64_t *final_cfg = nullptr;
     uint32_t *n_final = nullptr;
     uint32_t *lat_ws = nullptr;    // T0 workspace (lattices of 9-10 pending ops)
+    lcd::Args *dargs = nullptr;    // device copy of T0's Args (read once per key)
+    lcd::Args *hargs = nullptr;    // its pinned host staging copy (copied only when it changes)
+    bool hargs_valid = false;
     int lat_ws_blocks = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
     struct Ws {
@@ -96,7 +99,8 @@ struct lc_ctx {
     ~lc_ctx() {
         dfree(lists); dfree(counters); dfree(acc); dfree(valid); dfree(fail_event);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
-        dfree(ws[0].base); dfree(ws[1].base); dfree(lat_ws);
+        dfree(ws[0].base); dfree(ws[1].base); dfree(lat_ws); dfree(dargs);
+        if (hargs) (void)hipHostFree(hargs);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (et0) (void)hipEventDestroy(et0);
@@ -179,6 +183,9 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
     if (o.max_configs > (1ull << 31)) return lc::fail(LC_E_INVALID, "lc_create: max_configs above 2^31");
     if (o.max_final <= 0) o.max_final = 10;
     if (o.max_final > 16) return lc::fail(LC_E_INVALID, "lc_create: max_final above 16");
+    if (o.flags & ~LC_OPT_COUNT_PROBES) return lc::fail(LC_E_INVALID, "lc_create: unknown flags 0x%x", o.flags);
+    for (int32_t r : o.reserved)
+        if (r) return lc::fail(LC_E_INVALID, "lc_create: reserved fields must be 0");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return lc::fail(LC_E_DEVICE, "lc_create: no HIP device visible");
@@ -201,6 +208,8 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         HIPCHK(hipEventCreate(&c->et0));
         HIPCHK(dalloc(&c->counters, 16));
         HIPCHK(dalloc(&c->acc, 4));
+        HIPCHK(dalloc(&c->dargs, 1));
+        HIPCHK(hipHostMalloc((void **)&c->hargs, sizeof(lcd::Args), hipHostMallocDefault));
         return LC_OK;
     };
     rc = init();
@@ -364,7 +373,8 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     a.ev_off = d->ev_off; a.events = d->events; a.trans = d->trans; a.trans_off = d->trans_off;
     a.key_width = d->key_width; a.key_states = d->key_states;
     a.init_state = d->init_state; a.shared_states = d->shared_states;
-    a.budget = c->o.max_configs; a.max_final = c->o.max_final; a.debug_mode = c->o.reserved[0];
+    a.budget = c->o.max_configs; a.max_final = c->o.max_final; a.debug_mode = c->o.debug_mode;
+    a.count_probes = (c->o.flags & LC_OPT_COUNT_PROBES) ? 1 : 0;
     if (dev_result) {
         a.valid = r->valid; a.fail_event = r->fail_event; a.cause = r->cause;
         a.peak = r->peak_configs; a.final_cfg = r->final_configs; a.n_final = r->n_final;
@@ -381,21 +391,28 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     HIPCHK(hipMemsetAsync(c->counters, 0, 16 * sizeof(int32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->acc, 0, 4 * sizeof(unsigned long long), c->stream));
     if (a.n_final && K > 0) HIPCHK(hipMemsetAsync(a.n_final, 0, (size_t)K * 4, c->stream));
+    // T0: every key, LPT order; keys outside the register lattice spill to T1
+    lcd::Args a0 = a;
+    a0.order = d->order; a0.n_order = (int32_t)K; a0.n_in = nullptr; a0.ticket = c->counters + 8;
+    a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
+    const int g0 = (int)std::max<int64_t>(1, std::min<int64_t>(K, (int64_t)c->cu_count * 16));
+    if (g0 > c->lat_ws_blocks) {
+        dfree(c->lat_ws);
+        c->lat_ws_blocks = 0;
+        HIPCHK(dalloc(&c->lat_ws, (size_t)g0 * lcd::lat_ws_words()));
+        c->lat_ws_blocks = g0;
+    }
+    a0.lat_ws = c->lat_ws;
+    // T0 reads the result/counter/list pointers from a device copy of its
+    // Args, refreshed (outside the timed region) only when they change
+    if (!c->hargs_valid || std::memcmp(c->hargs, &a0, sizeof a0) != 0) {
+        std::memcpy(c->hargs, &a0, sizeof a0);
+        HIPCHK(hipMemcpyAsync(c->dargs, c->hargs, sizeof(lcd::Args), hipMemcpyHostToDevice, c->stream));
+        c->hargs_valid = true;
+    }
     HIPCHK(hipEventRecord(c->e0, c->stream));
     if (K > 0) {
-        // T0: every key, LPT order; keys outside the register lattice spill to T1
-        lcd::Args a0 = a;
-        a0.order = d->order; a0.n_order = (int32_t)K; a0.n_in = nullptr; a0.ticket = c->counters + 8;
-        a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
-        int g0 = (int)std::min<int64_t>(K, (int64_t)c->cu_count * 16);
-        if (g0 > c->lat_ws_blocks) {
-            dfree(c->lat_ws);
-            c->lat_ws_blocks = 0;
-            HIPCHK(dalloc(&c->lat_ws, (size_t)g0 * lcd::lat_ws_words()));
-            c->lat_ws_blocks = g0;
-        }
-        a0.lat_ws = c->lat_ws;
-        HIPCHK(lcd::launch_t0(a0, g0, c->stream));
+        HIPCHK(lcd::launch_t0(a0, c->dargs, g0, c->stream));
         HIPCHK(hipEventRecord(c->et0, c->stream));
         // T1: LDS hash sets
         lcd::Args a1 = a;

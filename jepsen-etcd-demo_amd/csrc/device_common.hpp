@@ -82,7 +82,7 @@ __device__ __forceinline__ void finish_key(const Args &a, int32_t key, int verdi
         a.cause[key] = (uint8_t)cause;
         a.fail_event[key] = fev;
         if (a.peak) a.peak[key] = peak;
-        atomicAdd(a.probes, (unsigned long long)probes);
+        if (a.count_probes) atomicAdd(a.probes, (unsigned long long)probes);
         atomicAdd(a.ev_count, (unsigned long long)nev);
         atomicAdd(a.keys_done, 1ull);
     }

@@ -3,34 +3,40 @@
 //
 // Same sets as every other tier (semantics: oracle/linear_ref.py).  The
 // representation exploits two facts of the packed form:
-//   * a config is (register state, set L of linearized pending ops), and ops
-//     are named by their pending-window slot (lowest free slot at invoke,
-//     lc_pack), so L is a subset of {0 .. width-1} with width = the key's
-//     largest concurrency (<= 10 for the demo's 10 client threads);
+//   * a config is (register state, set L of linearized pending ops), and the
+//     pending ops are numbered densely 0..n-1 (n = ops pending; when op j
+//     returns, op n-1 takes number j), so L is a subset of {0 .. n-1} and
+//     n <= the key's concurrency (10 for the demo's 10 client threads);
 //   * the register has few states (6 for the demo's values 0..4 + nil).
 // So S is stored as W[L] = bitmask of states s with (s, L) in S, one 32-bit
-// mask per subset L, subset index = lane + 64 * register.  A wave's 64 lanes
-// x R registers cover 2^(6 + log2 R) subsets (R = 16: width 10).
+// mask per subset L, subset index = lane + 64 * register.
 //
 // Per :ok(p) event:
 //   Ret[L]  = W[L u {p}]              (configs that already linearized p)
 //   I[L]    = W[L]          for p not in L; then the JIT closure
 //   I[L u {q}] |= T_q(I[L]) for every pending q != p, to a fixpoint,
 //   S'[L]   = Ret[L] | T_p(I[L])
-// where T_q maps a state mask through op q's cas-register step (read a: keep
-// bit a; write b: any -> {b}; cas a->b: bit a -> {b}).  "L u {q}" is the
-// lane/register whose index differs in bit q: a DPP / ds_swizzle / bpermute
-// exchange for q < 6, a register pair for q >= 6.  Set sizes (for the budget,
-// the peak and the probe count) are popcounts reduced over the wave, so every
-// number reported equals the oracle's.
+// where T_q maps a state mask through op q's cas-register step, branch-free:
+//   T(M) = (M & pass) | (min(M & keep, 1) << b)
+//   (read nil: pass = all; read a: pass = {a}; write b: keep = all;
+//    cas a->b: keep = {a}).
+// The closure runs as Gauss-Seidel sweeps over the subset-bit positions:
+// lanes (subsets) WITH bit q gather I from the subset without it -- one
+// DPP / permlane instruction for a lane bit, a register for a register bit --
+// and positions are applied in place, so one sweep follows every path that
+// adds ops in increasing index order.  A sweep that changes nothing ends the
+// closure, and n - 1 sweeps always suffice (a path has at most n - 1 steps).
+// Transfer masks are lane-masked once per event (zero on lanes without bit
+// q and for q = p), so a sweep position is 5 VALU instructions.
 //
-// Keys outside T0's reach (width > 10, > 32 register states, or a caller
-// batch whose slots exceed its key_width) go to the hash-set tiers.
+// Set sizes (budget, peak) are wave popcount reductions and the probe count
+// (LC_OPT_COUNT_PROBES) is accumulated per lane, so every number reported
+// equals the oracle's.  Keys outside T0's reach (more than 10 ops pending,
+// more than 32 register states) go to the hash-set tiers.
 
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <type_traits>
 
 #include "../../include/lincheck.h"
 #include "device_common.hpp"
@@ -40,103 +46,97 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 
 namespace lcd {
 
-constexpr int T0_RMAX = 4;        // lattice registers per lane: n <= 8 pending ops
-constexpr int T0_RMEM = 16;       // workspace lattice (global memory): n <= 10
-constexpr uint32_t T0_MAX_WIDTH = 10;  // = 6 + log2(T0_RMEM)
+constexpr int T0_RMAX = 4;             // lattice registers per lane: n <= 8 pending ops
+constexpr int T0_RMEM = 16;            // workspace lattice (global memory): n <= 10
+#ifndef LC_T0_MAX_WIDTH
+#define LC_T0_MAX_WIDTH 10
+#endif
+constexpr uint32_t T0_MAX_WIDTH = LC_T0_MAX_WIDTH;  // <= 6 + log2(T0_RMEM)
 constexpr uint32_t T0_MAX_STATES = 32;
 
-// Mask of states reachable from mask M through op d (0 if illegal for all).
-__device__ __forceinline__ uint32_t tmask(uint32_t M, uint32_t d) {
+struct Xfer { uint32_t pass, keep, b; };
+
+__device__ __forceinline__ Xfer xfer_of(uint32_t d) {  // uniform d: scalar selects
     const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
-    const uint32_t abit = a < 32u ? (M >> a) & 1u : 0u;
-    if (f == LC_T_READ_ANY) return M;
-    if (f == LC_T_READ) return abit << (a & 31u);
-    if (f == LC_T_WRITE) return M ? (1u << b) : 0u;
-    return abit ? (1u << b) : 0u;  // CAS
-}
-
-// Number of configs of mask M for which op d is legal (probe count).
-__device__ __forceinline__ uint32_t legal_cnt(uint32_t M, uint32_t d) {
-    const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu;
-    if (f == LC_T_READ_ANY || f == LC_T_WRITE) return (uint32_t)__popc(M);
-    return a < 32u ? (M >> a) & 1u : 0u;
-}
-
-// Branch-free form of an op's state transfer: T(M) = (M & pass) | (M & keep ? set : 0)
-//   read-any: pass = all         read a: pass = {a}
-//   write b:  keep = all, set = {b}      cas a->b: keep = {a}, set = {b}
-// and the number of configs of M where the op is legal is popc(M & (pass | keep)).
-struct Xfer { uint32_t pass, keep, set; };
-
-__device__ __forceinline__ Xfer xfer_of(uint32_t d) {  // branch-free (uniform d: scalar selects)
-    const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
-    const uint32_t abit = a < 32u ? 1u << (a & 31u) : 0u, bbit = b < 32u ? 1u << (b & 31u) : 0u;
+    const uint32_t abit = a < 32u ? 1u << (a & 31u) : 0u;
     Xfer x;
     x.pass = f == LC_T_READ_ANY ? 0xFFFFFFFFu : (f == LC_T_READ ? abit : 0u);
     x.keep = f == LC_T_WRITE ? 0xFFFFFFFFu : (f == LC_T_CAS ? abit : 0u);
-    x.set = f >= LC_T_WRITE ? bbit : 0u;
+    x.b = f >= LC_T_WRITE ? (b & 31u) : 0u;
     return x;
+}
+
+// min(t, 1) as one v_min_u32 (the compiler would otherwise turn it into a
+// compare + select through an SGPR pair, which also costs a hazard nop)
+__device__ __forceinline__ uint32_t umin1(uint32_t t) {
+    uint32_t r;
+    asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
+// acc | T(x): v_and_or_b32, v_and_b32, v_min_u32, v_lshl_or_b32
+__device__ __forceinline__ uint32_t xacc(uint32_t acc, uint32_t x, uint32_t pass, uint32_t keep, uint32_t b) {
+    acc = (x & pass) | acc;
+    return (umin1(x & keep) << b) | acc;
+}
+
+// One-directional gathers along subset bit q < 6 (a lane-index bit):
+//   gdown<q>(x)[L] = x[L - 2^q]   (meaningful on lanes WITH bit q)
+//   gup<q>(x)[L]   = x[L + 2^q]   (meaningful on lanes WITHOUT bit q)
+// One VALU instruction each: DPP quad_perm (q = 0, 1), DPP row_shr / row_shl
+// (q = 2, 3; lanes whose source leaves the row read garbage, which every
+// caller masks), gfx950 v_permlane16_swap / v_permlane32_swap (q = 4, 5).
+template <int Q>
+__device__ __forceinline__ uint32_t gdown(uint32_t x) {
+    if constexpr (Q == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
+    else if constexpr (Q == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x44, 0xF, 0xF, false);  // [0,1,0,1]
+    else if constexpr (Q == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    else if constexpr (Q == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    else if constexpr (Q == 4) return __builtin_amdgcn_permlane16_swap(x, x, false, false)[0];
+    else return __builtin_amdgcn_permlane32_swap(x, x, false, false)[0];
+}
+template <int Q>
+__device__ __forceinline__ uint32_t gup(uint32_t x) {
+    if constexpr (Q == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
+    else if constexpr (Q == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xEE, 0xF, 0xF, false);  // [2,3,2,3]
+    else if constexpr (Q == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104, 0xF, 0xF, false);  // row_shl:4
+    else if constexpr (Q == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x108, 0xF, 0xF, false);  // row_shl:8
+    else if constexpr (Q == 4) return __builtin_amdgcn_permlane16_swap(x, x, false, false)[1];
+    else return __builtin_amdgcn_permlane32_swap(x, x, false, false)[1];
+}
+// Run-time bit (uniform q < 6): a scalar branch to one of the above.
+__device__ __forceinline__ uint32_t gdown_rt(uint32_t x, uint32_t q) {
+    switch (q) {
+        case 0: return gdown<0>(x);
+        case 1: return gdown<1>(x);
+        case 2: return gdown<2>(x);
+        case 3: return gdown<3>(x);
+        case 4: return gdown<4>(x);
+        default: return gdown<5>(x);
+    }
+}
+__device__ __forceinline__ uint32_t gup_rt(uint32_t x, uint32_t q) {
+    switch (q) {
+        case 0: return gup<0>(x);
+        case 1: return gup<1>(x);
+        case 2: return gup<2>(x);
+        case 3: return gup<3>(x);
+        case 4: return gup<4>(x);
+        default: return gup<5>(x);
+    }
+}
+
+// x from lane (lane ^ 2^Q), both directions (workspace path).  Both gathers
+// are evaluated unconditionally: a cross-lane op written inside `c ? a : b`
+// would run under a divergent EXEC mask and read inactive source lanes.
+template <int Q>
+__device__ __forceinline__ uint32_t xv(uint32_t x, uint32_t lane) {
+    const uint32_t d = gdown<Q>(x), u = gup<Q>(x);
+    return ((lane >> Q) & 1u) ? d : u;
 }
 
 __device__ __forceinline__ uint32_t xapply(uint32_t M, uint32_t pass, uint32_t keep, uint32_t set) {
     return (M & pass) | ((M & keep) ? set : 0u);
-}
-
-// x from lane (lane ^ 2^Q), Q < 6, in VALU only (DPP row shifts, gfx950
-// permlane swaps): no LDS round trip.
-template <int Q>
-__device__ __forceinline__ uint32_t xv(uint32_t x, uint32_t lane) {
-    if constexpr (Q == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
-    else if constexpr (Q == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
-    else if constexpr (Q == 2) {
-        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104, 0xF, 0xF, true);  // row_shl:4
-        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
-        return (lane & 4u) ? dn : up;
-    } else if constexpr (Q == 3) {
-        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x108, 0xF, 0xF, true);  // row_shl:8
-        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
-        return (lane & 8u) ? dn : up;
-    } else if constexpr (Q == 4) {
-        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-        return (lane & 16u) ? r[0] : r[1];
-    } else {
-        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-        return (lane & 32u) ? r[0] : r[1];
-    }
-}
-
-// x from lane (lane ^ 2^Q), Q < 6.
-template <int Q>
-__device__ __forceinline__ uint32_t xchg(uint32_t x) {
-    if constexpr (Q == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-    else if constexpr (Q == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
-    else if constexpr (Q == 2) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);  // xor 4
-    else if constexpr (Q == 3) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x201F);  // xor 8
-    else if constexpr (Q == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);  // xor 16
-    else return (uint32_t)__shfl_xor((int)x, 32);
-}
-
-using Lat = uint32_t[T0_RMAX];
-
-// P[k] = X[k's partner along subset bit `bit`] (run-time bit; lanes active).
-template <int RL>
-__device__ __forceinline__ void xchg_rt(const Lat &X, Lat &P, uint32_t bit) {
-    if (bit < 6) {
-        const int m = 1 << bit;
-#pragma unroll
-        for (int k = 0; k < RL; ++k) P[k] = (uint32_t)__shfl_xor((int)X[k], m);
-        return;
-    }
-    const uint32_t r = bit - 6;
-#pragma unroll
-    for (int k = 0; k < RL; ++k) {
-        uint32_t v = X[k];
-        if constexpr (RL > 1) v = r == 0 ? X[k ^ 1] : v;
-        if constexpr (RL > 2) v = r == 1 ? X[k ^ 2] : v;
-        if constexpr (RL > 4) v = r == 2 ? X[k ^ 4] : v;
-        if constexpr (RL > 8) v = r == 3 ? X[k ^ 8] : v;
-        P[k] = v;
-    }
 }
 
 __device__ __forceinline__ bool idx_has(uint32_t lane, int k, uint32_t q) {
@@ -146,142 +146,116 @@ __device__ __forceinline__ bool idx_has(uint32_t lane, int k, uint32_t q) {
 template <int RL>
 constexpr int lat_bits() { return RL == 1 ? 6 : RL == 2 ? 7 : RL == 4 ? 8 : RL == 8 ? 9 : 10; }
 
-// One :ok(p) event on a lattice of RL registers (n <= 6 + log2 RL pending
-// ops).  Every subset bit position is applied in every sweep, branch-free:
-// positions that are not candidates carry zero transfer masks.  Lane bits
-// move through VALU exchanges (xv), register bits through register pairs.
-// W = S on entry, S' (relocated so index n-1 is free) on a normal return.
-// Returns 0 normal, 1 invalid, 2 budget exceeded.
-template <int RL>
-__device__ __forceinline__ int ok_event_r(Lat &W, uint32_t p, uint32_t n, uint32_t pass_v, uint32_t keep_v,
-                                          uint32_t set_v, uint32_t lane, uint64_t budget, uint32_t &probes,
-                                          uint32_t &nSn_out, bool want_size) {
-    constexpr int NB = lat_bits<RL>();
-    const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
-    uint32_t ps[NB], kp[NB], st[NB];
+using Lat = uint32_t[T0_RMAX];
+
+// T0's kernel arguments: only what the event loop reads, so the loop keeps
+// its scalar registers (the full Args would spill SGPRs into VGPR lanes).
+constexpr uint32_t T0_COUNT = 1, T0_WANT_PEAK = 2, T0_DBG_NOEVENTS = 4, T0_DBG_NOFINAL = 8;
+struct T0Args {
+    const uint64_t *ev_off;
+    const uint32_t *events;
+    const uint32_t *trans;
+    const uint32_t *trans_off;   // may be null
+    const uint8_t *key_width;    // may be null
+    const uint16_t *key_states;  // may be null
+    const int32_t *order;
+    int32_t *ticket;
+    uint32_t *lat_ws;
+    const Args *full;            // device copy: results, counters, spill list
+    uint64_t budget;
+    int32_t n_order;
+    uint32_t init_state, shared_states, flags;
+};
+
+// Lane-masked transfer masks of one event: vp/vk[q] = op q's pass/keep on
+// lanes with bit q (0 elsewhere and for q = p); sb[q] = op q's shift.
+struct LaneMasks {
+    uint32_t vp[6], vk[6], sb[8];
+};
+
+template <int N>
+__device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t pass_v, uint32_t keep_v, uint32_t b_v,
+                                           uint32_t lane) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-        const bool on = (cand >> q) & 1u;
-        ps[q] = on ? __builtin_amdgcn_readlane(pass_v, q) : 0u;
-        kp[q] = on ? __builtin_amdgcn_readlane(keep_v, q) : 0u;
-        st[q] = on ? __builtin_amdgcn_readlane(set_v, q) : 0u;
+    for (int q = 0; q < 6; ++q) { m.vp[q] = 0u; m.vk[q] = 0u; }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) m.sb[q] = 0u;
+#pragma unroll
+    for (int q = 0; q < (N < 6 ? N : 6); ++q) {
+        const bool on = ((lane >> q) & 1u) && (uint32_t)q != p;
+        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, q), sk = __builtin_amdgcn_readlane(keep_v, q);
+        m.vp[q] = on ? sp : 0u;
+        m.vk[q] = on ? sk : 0u;
     }
-    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
-                   pt = __builtin_amdgcn_readlane(set_v, p);
-    Lat Ret, I;  // with W: the only three lattice arrays (register budget)
 #pragma unroll
-    for (int k = 0; k < RL; ++k) probes += (uint32_t)__popc(W[k]);
-    xchg_rt<RL>(W, Ret, p);
-#pragma unroll
-    for (int k = 0; k < RL; ++k) {
-        const bool hp = idx_has(lane, k, p);
-        Ret[k] = hp ? 0u : Ret[k];
-        I[k] = hp ? 0u : W[k];
-    }
-    for (;;) {  // Jacobi sweeps to the fixpoint; W is scratch from here on
-        bool ch = false;
-#pragma unroll
-        for (int k = 0; k < RL; ++k) {
-            uint32_t acc = I[k];
-#define LC_LANEBIT(Q)                                                                  \
-            {                                                                          \
-                const uint32_t x = xv<Q>(I[k], lane);                                  \
-                acc |= ((lane >> Q) & 1u) ? xapply(x, ps[Q], kp[Q], st[Q]) : 0u;      \
-            }
-            LC_LANEBIT(0) LC_LANEBIT(1) LC_LANEBIT(2) LC_LANEBIT(3) LC_LANEBIT(4) LC_LANEBIT(5)
-#undef LC_LANEBIT
-#pragma unroll
-            for (int q = 6; q < NB; ++q)
-                if ((k >> (q - 6)) & 1) acc |= xapply(I[k ^ (1 << (q - 6))], ps[q], kp[q], st[q]);
-            W[k] = acc;
-        }
-#pragma unroll
-        for (int k = 0; k < RL; ++k) { ch |= W[k] != I[k]; I[k] = W[k]; }
-        if (!__any(ch)) break;
-    }
-    uint32_t cI = 0, cS = 0;
-#pragma unroll
-    for (int k = 0; k < RL; ++k) {
-#pragma unroll
-        for (int q = 0; q < NB; ++q)
-            if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(I[k] & (ps[q] | kp[q]));
-        Ret[k] |= xapply(I[k], pp, pk, pt);
-        probes += (uint32_t)__popc(I[k] & (pp | pk));
-        cI += (uint32_t)__popc(I[k]);
-        cS += (uint32_t)__popc(Ret[k]);
-    }
-    // The lattice holds at most RL*64*32 configs: below that budget sizes
-    // decide :unknown; above it only emptiness matters (one ballot), and the
-    // exact |S'| is reduced only when a peak was asked for.
-    if (budget < (uint64_t)RL * 64u * 32u) {
-        const uint32_t nI = __ockl_wfred_add_u32(cI);
-        if (nI > budget) return 2;
-    }
-    if (!__any(cS != 0u)) { nSn_out = 0; return 1; }
-    if (budget < (uint64_t)RL * 64u * 32u || want_size) {
-        const uint32_t nSn = __ockl_wfred_add_u32(cS);
-        nSn_out = nSn;
-        if (nSn > budget) return 2;
-    }
-    const uint32_t last = n - 1;
-    if (p == last) {
-#pragma unroll
-        for (int k = 0; k < RL; ++k) W[k] = Ret[k];
-        return 0;
-    }
-    // the op at index `last` moves to index p: S'[L] for L with p comes from
-    // L ^ {p, last}; no config keeps bit `last`
-    xchg_rt<RL>(Ret, W, p);
-    xchg_rt<RL>(W, I, last);
-#pragma unroll
-    for (int k = 0; k < RL; ++k) {
-        const bool hp = idx_has(lane, k, p), hl = idx_has(lane, k, last);
-        W[k] = hl ? 0u : (hp ? I[k] : Ret[k]);
-    }
-    return 0;
+    for (int q = 0; q < (N < 8 ? N : 8); ++q) m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
 }
 
-// One :ok(p) event when at most 6 ops are pending: the whole lattice is one
-// register, every subset bit is a lane bit, and each closure sweep applies
-// all six bit positions branch-free (non-candidates carry zero masks).
-__device__ __forceinline__ int ok_event_1(uint32_t &W, uint32_t p, uint32_t n, uint32_t pass_v, uint32_t keep_v,
-                                          uint32_t set_v, uint32_t lane, uint64_t budget, uint32_t &probes,
-                                          uint32_t &nSn_out, bool want_size) {
+// One Gauss-Seidel pass over lane-bit positions Q .. min(N, 6) - 1.
+template <int Q, int N>
+__device__ __forceinline__ uint32_t sweep_lanes(uint32_t cur, const LaneMasks &m) {
+    if constexpr (Q >= N || Q >= 6) {
+        return cur;
+    } else {
+        const uint32_t x = gdown<Q>(cur);
+        return sweep_lanes<Q + 1, N>(xacc(cur, x, m.vp[Q], m.vk[Q], m.sb[Q]), m);
+    }
+}
+
+// Probe count of the oracle for one event (LC_OPT_COUNT_PROBES only): legal
+// successors over I plus legal applications of p.
+template <int RL, int NB>
+__device__ __forceinline__ uint32_t event_probes(const uint32_t *I, uint32_t p, uint32_t cand, uint32_t pass_v,
+                                                 uint32_t keep_v, uint32_t lane) {
+    uint32_t pr = 0;
+    const uint32_t pm = __builtin_amdgcn_readlane(pass_v, p) | __builtin_amdgcn_readlane(keep_v, p);
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        const uint32_t m = ((cand >> q) & 1u) ? (__builtin_amdgcn_readlane(pass_v, q) | __builtin_amdgcn_readlane(keep_v, q)) : 0u;
+#pragma unroll
+        for (int k = 0; k < RL; ++k)
+            if (!idx_has(lane, k, (uint32_t)q)) pr += (uint32_t)__popc(I[k] & m);
+    }
+#pragma unroll
+    for (int k = 0; k < RL; ++k) pr += (uint32_t)__popc(I[k] & pm);
+    return pr;
+}
+
+// One :ok(p) event when n <= 6 ops are pending: the whole lattice is one
+// register and every subset bit is a lane bit.  One code path for every n
+// (positions >= n and p carry zero masks), so an event costs no dispatch
+// branches; the two gathers along the run-time bits p and p^last are one
+// ds_bpermute each.  W = S on entry, S' (relocated so index n-1 is free) on
+// a normal return.  Returns 0 normal, 1 invalid, 2 budget exceeded.
+__device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t n, uint32_t pass_v, uint32_t keep_v,
+                                       uint32_t b_v, uint32_t lane, uint64_t budget, bool count, uint32_t &probes,
+                                       uint32_t &nSn_out, bool want_size) {
     const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
-    uint32_t ps[6], kp[6], st[6];
+    const uint32_t wup = (uint32_t)__shfl_xor((int)W, 1 << p);  // issued first: its latency hides under the masks
+    LaneMasks m;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-        const bool on = (cand >> q) & 1u;
-        ps[q] = on ? __builtin_amdgcn_readlane(pass_v, q) : 0u;
-        kp[q] = on ? __builtin_amdgcn_readlane(keep_v, q) : 0u;
-        st[q] = on ? __builtin_amdgcn_readlane(set_v, q) : 0u;
+        const bool on = ((lane >> q) & 1u) && ((cand >> q) & 1u);
+        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, q), sk = __builtin_amdgcn_readlane(keep_v, q);
+        m.vp[q] = on ? sp : 0u;
+        m.vk[q] = on ? sk : 0u;
+        m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
     }
     const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
-                   pt = __builtin_amdgcn_readlane(set_v, p);
-    probes += (uint32_t)__popc(W);
+                   pb = __builtin_amdgcn_readlane(b_v, p);
     const bool hp = (lane >> p) & 1u;
-    const uint32_t wp = (uint32_t)__shfl_xor((int)W, 1 << p);
-    uint32_t Ret = hp ? 0u : wp;
+    if (count) probes += (uint32_t)__popc(W);
+    uint32_t Ret = hp ? 0u : wup;
     uint32_t I = hp ? 0u : W;
-    // Jacobi sweeps: the six bit positions read the same I, so their lane
-    // exchanges are independent (ILP); the exchange runs with every lane
-    // active, only its result is masked.  Repeat until nothing new.
-    for (;;) {
-#define LC_EXPAND(Q) \
-        const uint32_t x##Q = xv<Q>(I, lane); \
-        const uint32_t t##Q = ((lane >> Q) & 1u) ? xapply(x##Q, ps[Q], kp[Q], st[Q]) : 0u;
-        LC_EXPAND(0) LC_EXPAND(1) LC_EXPAND(2) LC_EXPAND(3) LC_EXPAND(4) LC_EXPAND(5)
-#undef LC_EXPAND
-        const uint32_t nv = I | t0 | t1 | t2 | t3 | t4 | t5;
+#pragma unroll 1
+    for (uint32_t s = 1; s < n; ++s) {
+        const uint32_t nv = sweep_lanes<0, 6>(I, m);
         const bool ch = nv != I;
         I = nv;
         if (!__any(ch)) break;
     }
-#pragma unroll
-    for (int q = 0; q < 6; ++q)
-        if (!((lane >> q) & 1u)) probes += (uint32_t)__popc(I & (ps[q] | kp[q]));
-    Ret |= xapply(I, pp, pk, pt);
-    probes += (uint32_t)__popc(I & (pp | pk));
+    if (count) probes += event_probes<1, 6>(&I, p, cand, pass_v, keep_v, lane);
+    Ret = xacc(Ret, I, pp, pk, pb);
     // One register holds at most 64 x 32 configs: with a larger budget only
     // emptiness matters (a ballot); exact sizes only when asked for (peak).
     if (budget < 64u * 32u) {
@@ -294,12 +268,120 @@ __device__ __forceinline__ int ok_event_1(uint32_t &W, uint32_t p, uint32_t n, u
         nSn_out = nSn;
         if (nSn > budget) return 2;
     }
+    // the op at index `last` moves to index p: lanes with p (and not last)
+    // take Ret[L ^ p ^ last]; with p == last this is the identity
     const uint32_t last = n - 1;
-    if (p == last) { W = Ret; return 0; }
-    // op at index `last` moves to index p
-    const uint32_t r2 = (uint32_t)__shfl_xor((int)Ret, (1 << p) | (1 << last));
+    const uint32_t src = (uint32_t)__shfl_xor((int)Ret, (1 << p) | (1 << last));
     const bool hl = (lane >> last) & 1u;
-    W = hl ? 0u : (hp ? r2 : Ret);
+    W = hl ? 0u : (hp ? src : Ret);
+    return 0;
+}
+
+// One :ok(p) event on a lattice of RL registers (N = 7 or 8 ops pending):
+// lane bits 0..5 as in ok_lane, register bits 6.. through register pairs.
+template <int RL>
+__device__ __forceinline__ int ok_reg(Lat &W, uint32_t p, uint32_t pass_v, uint32_t keep_v, uint32_t b_v,
+                                      uint32_t lane, uint64_t budget, bool count, uint32_t &probes,
+                                      uint32_t &nSn_out, bool want_size) {
+    constexpr int NB = lat_bits<RL>();  // = ops pending
+    constexpr int NR = NB - 6;          // register bits
+    LaneMasks m;
+    lane_masks<NB>(m, p, pass_v, keep_v, b_v, lane);
+    uint32_t rp[NR], rk[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const bool on = (uint32_t)(6 + r) != p;
+        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, 6 + r), sk = __builtin_amdgcn_readlane(keep_v, 6 + r);
+        rp[r] = on ? sp : 0u;
+        rk[r] = on ? sk : 0u;
+    }
+    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
+                   pb = __builtin_amdgcn_readlane(b_v, p);
+    Lat Ret, I;
+    if (count) {
+#pragma unroll
+        for (int k = 0; k < RL; ++k) probes += (uint32_t)__popc(W[k]);
+    }
+    if (p < 6) {
+        const bool hp = (lane >> p) & 1u;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) {
+            const uint32_t u = gup_rt(W[k], p);
+            Ret[k] = hp ? 0u : u;
+            I[k] = hp ? 0u : W[k];
+        }
+    } else {
+        const uint32_t r = p - 6;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) {
+            uint32_t src = W[k];
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr)
+                if (r == (uint32_t)rr) src = W[k | (1 << rr)];
+            const bool hk = ((uint32_t)k >> r) & 1u;
+            Ret[k] = hk ? 0u : src;
+            I[k] = hk ? 0u : W[k];
+        }
+    }
+#pragma unroll 1
+    for (int s = 1; s < NB; ++s) {
+        Lat nv;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6>(I[k], m);
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int k = 0; k < RL; ++k)
+                if ((k >> r) & 1) nv[k] = xacc(nv[k], nv[k ^ (1 << r)], rp[r], rk[r], m.sb[6 + r]);
+        bool ch = false;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) { ch |= nv[k] != I[k]; I[k] = nv[k]; }
+        if (!__any(ch)) break;
+    }
+    if (count) probes += event_probes<RL, NB>(I, p, ((1u << NB) - 1u) & ~(1u << p), pass_v, keep_v, lane);
+    uint32_t cI = 0, cS = 0;
+#pragma unroll
+    for (int k = 0; k < RL; ++k) {
+        Ret[k] = xacc(Ret[k], I[k], pp, pk, pb);
+        cI += (uint32_t)__popc(I[k]);
+        cS += (uint32_t)__popc(Ret[k]);
+    }
+    if (budget < (uint64_t)RL * 64u * 32u) {
+        const uint32_t nI = __ockl_wfred_add_u32(cI);
+        if (nI > budget) return 2;
+    }
+    if (!__any(cS != 0u)) { nSn_out = 0; return 1; }
+    if (budget < (uint64_t)RL * 64u * 32u || want_size) {
+        const uint32_t nSn = __ockl_wfred_add_u32(cS);
+        nSn_out = nSn;
+        if (nSn > budget) return 2;
+    }
+    constexpr int rl = NR - 1;  // `last` = NB - 1 is register bit rl
+    if (p == (uint32_t)(NB - 1)) {
+#pragma unroll
+        for (int k = 0; k < RL; ++k) W[k] = Ret[k];
+        return 0;
+    }
+    if (p < 6) {
+        const bool hp = (lane >> p) & 1u;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) {
+            if ((k >> rl) & 1) { W[k] = 0u; continue; }
+            const uint32_t z = gdown_rt(Ret[k | (1 << rl)], p);
+            W[k] = hp ? z : Ret[k];
+        }
+    } else {
+        const uint32_t r = p - 6;
+#pragma unroll
+        for (int k = 0; k < RL; ++k) {
+            if ((k >> rl) & 1) { W[k] = 0u; continue; }
+            uint32_t src = Ret[k];
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr)
+                if (r == (uint32_t)rr) src = Ret[(k ^ (1 << rr)) | (1 << rl)];
+            W[k] = (((uint32_t)k >> r) & 1u) ? src : Ret[k];
+        }
+    }
     return 0;
 }
 
@@ -308,31 +390,31 @@ __device__ __forceinline__ int ok_event_1(uint32_t &W, uint32_t p, uint32_t n, u
 // writes only its own column (register-bit partners are in the same lane;
 // lane-bit partners are exchanged in registers), so no cross-lane memory
 // ordering is involved.  Such events are rare (< 0.2 % of C2's); keeping
-// them out of registers keeps T0 at 4 waves per SIMD.
+// them out of registers keeps T0's register budget small.
 struct LatMem {
     uint32_t *W, *R, *I;
 };
 
 template <int RL>
 __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_t n, uint32_t pass_v,
-                                            uint32_t keep_v, uint32_t set_v, uint32_t lane, uint64_t budget,
-                                            uint32_t &probes, uint32_t &nSn_out, bool want_size) {
+                                            uint32_t keep_v, uint32_t b_v, uint32_t lane, uint64_t budget,
+                                            bool count, uint32_t &probes, uint32_t &nSn_out, bool want_size) {
     constexpr int NB = lat_bits<RL>();
     const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
-    // transfer of candidate q: lane q of pass_v/keep_v/set_v, read at use
+    // transfer of candidate q: lane q of pass_v/keep_v/b_v, read at use
     // (not hoisted: 3 x NB scalars would spill SGPRs into the VGPR budget)
     const uint32_t cpass = pass_v & (((cand >> lane) & 1u) ? ~0u : 0u);
     const uint32_t ckeep = keep_v & (((cand >> lane) & 1u) ? ~0u : 0u);
 #define PS(Q) __builtin_amdgcn_readlane(cpass, Q)
 #define KP(Q) __builtin_amdgcn_readlane(ckeep, Q)
-#define ST(Q) __builtin_amdgcn_readlane(set_v, Q)
+#define ST(Q) (1u << __builtin_amdgcn_readlane(b_v, Q))
     const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
-                   pt = __builtin_amdgcn_readlane(set_v, p);
+                   pt = 1u << __builtin_amdgcn_readlane(b_v, p);
     const uint32_t plm = p < 6 ? 1u << p : 0u, prm = p >= 6 ? 1u << (p - 6) : 0u;
 #pragma unroll 1
     for (int k = 0; k < RL; ++k) {
         const uint32_t w = m.W[k * 64 + lane];
-        probes += (uint32_t)__popc(w);
+        if (count) probes += (uint32_t)__popc(w);
         const uint32_t src = (uint32_t)__shfl_xor((int)m.W[(k ^ prm) * 64 + lane], (int)plm);
         const bool hp = (lane & plm) || ((uint32_t)k & prm);
         m.R[k * 64 + lane] = hp ? 0u : src;
@@ -340,8 +422,8 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
     }
     for (;;) {  // sweeps in place (monotone: any order reaches the fixpoint)
         bool ch = false;
-    #pragma unroll 1
-    for (int k = 0; k < RL; ++k) {
+#pragma unroll 1
+        for (int k = 0; k < RL; ++k) {
             const uint32_t x = m.I[k * 64 + lane];
             uint32_t acc = x;
 #define LC_LANEBIT(Q)                                                                  \
@@ -362,11 +444,13 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 #pragma unroll 1
     for (int k = 0; k < RL; ++k) {
         const uint32_t x = m.I[k * 64 + lane];
+        if (count) {
 #pragma unroll
-        for (int q = 0; q < NB; ++q)
-            if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(x & (PS(q) | KP(q)));
+            for (int q = 0; q < NB; ++q)
+                if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(x & (PS(q) | KP(q)));
+            probes += (uint32_t)__popc(x & (pp | pk));
+        }
         const uint32_t r = m.R[k * 64 + lane] | xapply(x, pp, pk, pt);
-        probes += (uint32_t)__popc(x & (pp | pk));
         m.R[k * 64 + lane] = r;
         cI += (uint32_t)__popc(x);
         cS += (uint32_t)__popc(r);
@@ -442,45 +526,53 @@ __device__ __forceinline__ void write_final_mem(const Args &a, int32_t key, cons
 // window slots: an invoke appends index n; when the op at index j returns, the
 // op at index n-1 takes index j (its configs move from bit n-1 to bit j, a
 // two-bit exchange).  So the lattice spans 2^n subsets, n = pending count.
-template <int RMAX>
-__device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
+//
+// Register budget: the event loop only touches the T0Args fields it needs;
+// result pointers, counters and work lists are read through `full` (a copy
+// of the tier's Args in device memory) once per key, so they never occupy
+// scalar registers across the loop.
+__device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key) {
     const uint32_t lane = lane_id();
-    const LatMem m{a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64),
-                   a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64) + T0_RMEM * 64,
-                   a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64) + 2 * T0_RMEM * 64};
-    bool in_mem = false;  // lattice lives in m.W (9 or 10 ops pending)
+    uint32_t *const ws = a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64);
+    const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
-        finish_key(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
+        finish_key(*a.full, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
     }
     const uint32_t nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
     const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;  // = max ops pending at once
     if (nstates > T0_MAX_STATES || width > T0_MAX_WIDTH || a.init_state >= T0_MAX_STATES) return K_SPILL;
     const uint64_t budget = a.budget;
-    const int dbg = a.debug_mode;  // 0 in every real run (ablation builds only)
-    const bool want_peak = a.peak != nullptr;
+    const bool want_peak = (a.flags & T0_WANT_PEAK) != 0;
+    const bool count = (a.flags & T0_COUNT) != 0;
+    const uint32_t *const evp = a.events + b;
+    const uint32_t *const trp = a.trans + tb;
+    const uint32_t nev = (uint32_t)(e - b);
 
     Lat W;
 #pragma unroll
     for (int k = 0; k < T0_RMAX; ++k) W[k] = 0;
     if (lane == 0) W[0] = 1u << a.init_state;
-    uint32_t desc_v = 0;   // lane j: descriptor of the op at dense index j
-    uint32_t pass_v = 0, keep_v = 0, set_v = 0;  // lane j: its Xfer masks
+    bool in_mem = false;   // lattice lives in m.W (9 or 10 ops pending)
+    uint32_t pass_v = 0, keep_v = 0, b_v = 0;  // lane j: transfer of the op at dense index j
     uint32_t slot_v = 0;   // lane j: window slot of the op at dense index j
     uint32_t dense_v = 0;  // lane s: dense index of the op in window slot s
     uint32_t n = 0;        // ops pending
     uint32_t peak = 1, probes = 0;
+    int status = 0;        // 1 invalid, 2 budget
+    uint32_t fev = 0;
 
-    // events arrive 64 at a time, one per lane; the next chunk's words and
-    // descriptors are loaded while this chunk is searched
-    uint32_t ev_next = b + lane < e ? a.events[b + lane] : 0u;
-    for (uint64_t base = b; base < e; base += 64) {
-        const uint32_t cnt = (uint32_t)((e - base) < 64 ? (e - base) : 64);
+    // events arrive 64 at a time, one per lane; the next chunk's words are
+    // loaded while this chunk is searched
+    uint32_t ev_next = lane < nev ? evp[lane] : 0u;
+    const uint32_t nev_loop = (a.flags & T0_DBG_NOEVENTS) ? 0u : nev;
+    for (uint32_t base = 0; base < nev_loop; base += 64) {
+        const uint32_t cnt = nev - base < 64u ? nev - base : 64u;
         const uint32_t ev = ev_next;
-        const uint32_t dsc = (lane < cnt && !(ev & LC_EV_OK_BIT)) ? a.trans[tb + LC_EV_TRANS(ev)] : 0u;
-        ev_next = base + 64 + lane < e ? a.events[base + 64 + lane] : 0u;
+        const uint32_t dsc = (lane < cnt && !(ev & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev)] : 0u;
+        ev_next = base + 64 + lane < nev ? evp[base + 64 + lane] : 0u;
         for (uint32_t i = 0; i < cnt; ++i) {
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
             const uint32_t slot = LC_EV_SLOT(evi);
@@ -491,52 +583,39 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
                     for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < T0_RMAX ? W[k < T0_RMAX ? k : 0] : 0u;
                     in_mem = true;
                 }
-                const uint32_t d = __builtin_amdgcn_readlane(dsc, i);
-                const Xfer x = xfer_of(d);
-                if (lane == n) { desc_v = d; slot_v = slot; pass_v = x.pass; keep_v = x.keep; set_v = x.set; }
-                if (lane == slot) dense_v = n;
+                const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
+                const bool me = lane == n;
+                slot_v = me ? slot : slot_v;
+                pass_v = me ? x.pass : pass_v;
+                keep_v = me ? x.keep : keep_v;
+                b_v = me ? x.b : b_v;
+                dense_v = lane == slot ? n : dense_v;
                 ++n;
                 continue;
             }
             const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
             uint32_t nSn = 0;
-            int r = 0;
-            if (dbg == 1) {  // ablation: bookkeeping only
-                const uint32_t last = n - 1;
-                const uint32_t d_last = __builtin_amdgcn_readlane(desc_v, last);
-                const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
-                if (lane == p) { desc_v = d_last; slot_v = s_last; }
-                if (lane == s_last) dense_v = p;
-                --n;
-                continue;
-            }
-            if (n <= 6) r = ok_event_1(W[0], p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            else if (n == 7) r = ok_event_r<2>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            else if (n == 8) r = ok_event_r<4>(W, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            else if (n == 9) r = ok_event_mem<8>(m, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            else r = ok_event_mem<16>(m, p, n, pass_v, keep_v, set_v, lane, budget, probes, nSn, want_peak);
-            if (r) {
-                const int32_t evno = (int32_t)(base + i - b);
-                if (!in_mem) {
-#pragma unroll
-                    for (int k = 0; k < T0_RMAX; ++k) m.W[k * 64 + lane] = W[k];
-                }
-                write_final_mem(a, key, m, lane, slot_v, n);
-                const uint32_t pr = __ockl_wfred_add_u32(probes);
-                finish_key(a, key, r == 1 ? LC_INVALID : LC_UNKNOWN, r == 1 ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET,
-                           evno, peak, pr, (uint64_t)evno + (r == 1 ? 1u : 0u));
-                return K_DONE;
-            }
+            int r;
+            if (n <= 6) r = ok_lane(W[0], p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+            else if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+            else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+            else if (n == 9)
+                r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+            else
+                r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+            if (r) { status = r; fev = base + i; break; }
             peak = nSn > peak ? nSn : peak;
+            // the op at index `last` takes index p (a no-op when p == last)
             const uint32_t last = n - 1;
-            if (p != last) {
-                const uint32_t d_last = __builtin_amdgcn_readlane(desc_v, last);
-                const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
-                const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last), x1 = __builtin_amdgcn_readlane(keep_v, last),
-                               x2 = __builtin_amdgcn_readlane(set_v, last);
-                if (lane == p) { desc_v = d_last; slot_v = s_last; pass_v = x0; keep_v = x1; set_v = x2; }
-                if (lane == s_last) dense_v = p;
-            }
+            const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
+            const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last), x1 = __builtin_amdgcn_readlane(keep_v, last),
+                           x2 = __builtin_amdgcn_readlane(b_v, last);
+            const bool mp = lane == p;
+            slot_v = mp ? s_last : slot_v;
+            pass_v = mp ? x0 : pass_v;
+            keep_v = mp ? x1 : keep_v;
+            b_v = mp ? x2 : b_v;
+            dense_v = lane == s_last ? p : dense_v;
             --n;
             if (in_mem && n == 8) {  // back to registers: no config holds index 8 or 9
 #pragma unroll
@@ -544,32 +623,52 @@ __device__ __forceinline__ int lattice_key(const Args &a, int32_t key) {
                 in_mem = false;
             }
         }
+        if (status) break;
     }
+    // per-key epilogue: results through `full`
+    const Args &f = *a.full;
     if (!in_mem) {
 #pragma unroll
         for (int k = 0; k < T0_RMAX; ++k) m.W[k * 64 + lane] = W[k];
     }
-    write_final_mem(a, key, m, lane, slot_v, n);
+    if (!(a.flags & T0_DBG_NOFINAL)) write_final_mem(f, key, m, lane, slot_v, n);
     const uint32_t pr = __ockl_wfred_add_u32(probes);
-    finish_key(a, key, LC_VALID, LC_CAUSE_NONE, -1, peak, pr, e - b);
+    if (status)
+        finish_key(f, key, status == 1 ? LC_INVALID : LC_UNKNOWN, status == 1 ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET,
+                   (int32_t)fev, peak, pr, (uint64_t)fev + (status == 1 ? 1u : 0u));
+    else
+        finish_key(f, key, LC_VALID, LC_CAUSE_NONE, -1, peak, pr, nev);
     return K_DONE;
 }
 
 // T0 over a work list: one wavefront per key (lattice in 4 registers, or the
-// workspace for 9-10 pending ops).
-__global__ __launch_bounds__(64) void k_search_lattice(Args a) {
-    const int32_t n = a.n_in ? *a.n_in : a.n_order;
-    for (int32_t w = next_work(a); w < n; w = next_work(a)) {
+// workspace for 9-10 pending ops); a persistent grid so the workspace stays
+// one slot per resident block.
+__global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
+    for (int32_t guard = 0; guard <= a.n_order; ++guard) {  // every wave takes at most n_order keys
+        int32_t w = 0;
+        if (lane_id() == 0) w = atomicAdd(a.ticket, 1);
+        w = __builtin_amdgcn_readfirstlane(w);
+        if (w >= a.n_order) break;
         const int32_t key = a.order[w];
-        const int r = lattice_key<T0_RMAX>(a, key);
-        if (r == K_SPILL) push_list(a.spill, a.n_spill, key);
+        if (lattice_key(a, key) == K_SPILL) {
+            const Args &f = *a.full;
+            push_list(f.spill, f.n_spill, key);
+        }
     }
 }
 
 size_t lat_ws_words() { return 3 * T0_RMEM * 64; }
 
-hipError_t launch_t0(const Args &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_search_lattice, dim3(grid), dim3(64), 0, s, a);
+hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, hipStream_t s) {
+    T0Args t{};
+    t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
+    t.key_width = a.key_width; t.key_states = a.key_states; t.order = a.order; t.ticket = a.ticket;
+    t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
+    t.init_state = a.init_state; t.shared_states = a.shared_states;
+    t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) |
+              (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u);
+    hipLaunchKernelGGL(k_search_lattice, dim3(grid), dim3(64), 0, s, t);
     return hipGetLastError();
 }
 

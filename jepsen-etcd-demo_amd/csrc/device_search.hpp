@@ -21,7 +21,8 @@ struct Args {
     uint32_t shared_states;      // state ids used by the shared table (trans_off == null)
     uint64_t budget;
     int32_t max_final;
-    int32_t debug_mode;          // 0; ablation builds only (lc_opts.reserved[0])
+    int32_t debug_mode;          // 0; ablation builds only (lc_opts.debug_mode)
+    int32_t count_probes;        // lc_opts.flags & LC_OPT_COUNT_PROBES
     // work list of this launch: keys order[0 .. n) with n = n_in ? *n_in : n_order
     const int32_t *order;
     int32_t n_order;
@@ -57,7 +58,7 @@ struct HbmWs {
 
 size_t lds_bytes_t1();
 size_t lds_bytes_t2();
-hipError_t launch_t0(const Args &a, int grid, hipStream_t s);
+hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, hipStream_t s);
 size_t lat_ws_words();
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t2(const Args &a, int grid, hipStream_t s);

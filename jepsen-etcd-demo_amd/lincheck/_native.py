@@ -14,10 +14,11 @@ from typing import Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblincheck.so")
+LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 1
+LC_ABI_VERSION = 2
+LC_OPT_COUNT_PROBES = 0x1
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
 LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER = 0, 1, 2, 3
 LC_NIL = -(1 << 63)
@@ -55,7 +56,7 @@ class LcPackOpts(C.Structure):
 class LcOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("algorithm", C.c_int32), ("max_configs", C.c_uint64),
                 ("max_final", C.c_int32), ("lds_configs", C.c_int32), ("deep_slots", C.c_int32),
-                ("reserved", C.c_int32 * 6)]
+                ("flags", C.c_int32), ("debug_mode", C.c_int32), ("reserved", C.c_int32 * 4)]
 
 
 class LcResult(C.Structure):

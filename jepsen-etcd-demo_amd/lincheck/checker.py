@@ -90,13 +90,15 @@ class Device:
     """An lc_ctx on one GPU (lc_create)."""
 
     def __init__(self, device: int = 0, budget: int = DEFAULT_BUDGET, max_final: int = TRUNCATE,
-                 debug_mode: int = 0):
+                 debug_mode: int = 0, count_probes: bool = False):
         o = N.LcOpts()
         o.device, o.algorithm, o.max_configs, o.max_final = device, 0, budget, max_final
-        o.reserved[0] = debug_mode  # ablation builds only; 0 = the real search
+        o.flags = N.LC_OPT_COUNT_PROBES if count_probes else 0
+        o.debug_mode = debug_mode  # ablation builds only; 0 = the real search
         h = C.c_void_p()
         N.check(N.lib().lc_create(C.byref(o), C.byref(h)))
         self.handle, self.device, self.budget, self.max_final = h, device, budget, max_final
+        self.count_probes = count_probes
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -35,4 +35,4 @@ def device():
     if not gpu_available():
         pytest.fail("no GPU visible: -m gpu tests need an MI355X")
     from lincheck.checker import Device
-    return Device(0)
+    return Device(0, count_probes=True)
