@@ -396,13 +396,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     a0.order = d->order; a0.n_order = (int32_t)K; a0.n_in = nullptr; a0.ticket = c->counters + 8;
     a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
     const int g0 = (int)std::max<int64_t>(1, std::min<int64_t>(K, (int64_t)c->cu_count * 16));
-    if (g0 > c->lat_ws_blocks) {
-        dfree(c->lat_ws);
-        c->lat_ws_blocks = 0;
-        HIPCHK(dalloc(&c->lat_ws, (size_t)g0 * lcd::lat_ws_words()));
-        c->lat_ws_blocks = g0;
-    }
-    a0.lat_ws = c->lat_ws;
+    a0.lat_ws = nullptr;
     // T0 reads the result/counter/list pointers from a device copy of its
     // Args, refreshed (outside the timed region) only when they change
     if (!c->hargs_valid || std::memcmp(c->hargs, &a0, sizeof a0) != 0) {

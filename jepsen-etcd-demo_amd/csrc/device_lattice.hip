@@ -74,10 +74,26 @@ __device__ __forceinline__ uint32_t umin1(uint32_t t) {
     return r;
 }
 
+// s & v as one v_and_b32 (kept opaque: the compiler would turn an AND with a
+// 0/~0 lane mask into a select through an SGPR pair)
+__device__ __forceinline__ uint32_t vand(uint32_t s, uint32_t v) {
+    uint32_t r;
+    asm("v_and_b32 %0, %1, %2" : "=v"(r) : "s"(s), "v"(v));
+    return r;
+}
+
 // acc | T(x): v_and_or_b32, v_and_b32, v_min_u32, v_lshl_or_b32
 __device__ __forceinline__ uint32_t xacc(uint32_t acc, uint32_t x, uint32_t pass, uint32_t keep, uint32_t b) {
     acc = (x & pass) | acc;
     return (umin1(x & keep) << b) | acc;
+}
+// The same with `one` an opaque scalar 1 (a kernel argument): min(t, one)
+// stays one v_min_u32 the compiler can see (no hazard padding around inline
+// asm), where min(t, 1) would become a compare + select.
+__device__ __forceinline__ uint32_t xacc1(uint32_t acc, uint32_t x, uint32_t pass, uint32_t keep, uint32_t b,
+                                          uint32_t one) {
+    acc = (x & pass) | acc;
+    return (__builtin_elementwise_min(x & keep, one) << b) | acc;
 }
 
 // One-directional gathers along subset bit q < 6 (a lane-index bit):
@@ -94,6 +110,14 @@ __device__ __forceinline__ uint32_t gdown(uint32_t x) {
     else if constexpr (Q == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
     else if constexpr (Q == 4) return __builtin_amdgcn_permlane16_swap(x, x, false, false)[0];
     else return __builtin_amdgcn_permlane32_swap(x, x, false, false)[0];
+}
+// gdown with a dead register as the permlane's other operand: the swap
+// clobbers both, so this saves one copy of x
+template <int Q>
+__device__ __forceinline__ uint32_t gdown_j(uint32_t x, uint32_t junk) {
+    if constexpr (Q == 4) return __builtin_amdgcn_permlane16_swap(junk, x, false, false)[0];
+    else if constexpr (Q == 5) return __builtin_amdgcn_permlane32_swap(junk, x, false, false)[0];
+    else return gdown<Q>(x);
 }
 template <int Q>
 __device__ __forceinline__ uint32_t gup(uint32_t x) {
@@ -160,11 +184,12 @@ struct T0Args {
     const uint16_t *key_states;  // may be null
     const int32_t *order;
     int32_t *ticket;
-    uint32_t *lat_ws;
+    uint32_t *lat_ws;            // unused (the 9-10-pending workspace is in LDS)
     const Args *full;            // device copy: results, counters, spill list
     uint64_t budget;
     int32_t n_order;
     uint32_t init_state, shared_states, flags;
+    uint32_t one;                // 1 (opaque to the compiler: see xacc1)
 };
 
 // Lane-masked transfer masks of one event: vp/vk[q] = op q's pass/keep on
@@ -191,14 +216,15 @@ __device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t pa
     for (int q = 0; q < (N < 8 ? N : 8); ++q) m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
 }
 
-// One Gauss-Seidel pass over lane-bit positions Q .. min(N, 6) - 1.
+// One Gauss-Seidel pass over lane-bit positions Q .. min(N, 6) - 1 (`prev`:
+// the previous position's gathered value, dead by now, feeds the permlanes).
 template <int Q, int N>
-__device__ __forceinline__ uint32_t sweep_lanes(uint32_t cur, const LaneMasks &m) {
+__device__ __forceinline__ uint32_t sweep_lanes(uint32_t cur, const LaneMasks &m, uint32_t one, uint32_t prev = 0) {
     if constexpr (Q >= N || Q >= 6) {
         return cur;
     } else {
-        const uint32_t x = gdown<Q>(cur);
-        return sweep_lanes<Q + 1, N>(xacc(cur, x, m.vp[Q], m.vk[Q], m.sb[Q]), m);
+        const uint32_t x = gdown_j<Q>(cur, prev);
+        return sweep_lanes<Q + 1, N>(xacc1(cur, x, m.vp[Q], m.vk[Q], m.sb[Q], one), m, one, x);
     }
 }
 
@@ -221,24 +247,37 @@ __device__ __forceinline__ uint32_t event_probes(const uint32_t *I, uint32_t p, 
     return pr;
 }
 
-// One :ok(p) event when n <= 6 ops are pending: the whole lattice is one
-// register and every subset bit is a lane bit.  One code path for every n
-// (positions >= n and p carry zero masks), so an event costs no dispatch
-// branches; the two gathers along the run-time bits p and p^last are one
-// ds_bpermute each.  W = S on entry, S' (relocated so index n-1 is free) on
-// a normal return.  Returns 0 normal, 1 invalid, 2 budget exceeded.
-__device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t n, uint32_t pass_v, uint32_t keep_v,
-                                       uint32_t b_v, uint32_t lane, uint64_t budget, bool count, uint32_t &probes,
-                                       uint32_t &nSn_out, bool want_size) {
-    const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
-    const uint32_t wup = (uint32_t)__shfl_xor((int)W, 1 << p);  // issued first: its latency hides under the masks
+// One :ok(p) event while every live op index is < 6: the whole lattice is
+// one register and every subset bit is a lane bit.  Op indices are assigned
+// lowest-free at invoke (not compacted), so an :ok only frees index p -- no
+// relocation: S' lands on the lanes without bit p and lanes with bit p stay
+// empty, which is exactly the state a later invoke into index p needs.  One
+// code path for every live set (free positions and p carry zero masks), so an
+// event costs no dispatch branches; the gather along the run-time bit p is one
+// ds_bpermute, issued first so its latency hides under the mask setup.
+// lm[q] (0 / ~0) is lane bit q as a VGPR mask.  W = S on entry, S' on a
+// normal return.  Returns 0 normal, 1 invalid, 2 budget exceeded.
+__device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, uint32_t pass_v, uint32_t keep_v,
+                                       uint32_t b_v, uint32_t lane, const uint32_t (&lm)[6], uint32_t one,
+                                       uint64_t budget, bool count, uint32_t &probes, uint32_t &nSn_out,
+                                       bool want_size) {
+    const uint32_t cand = live & ~(1u << p);
+#ifdef LC_GUP_SELECT
+    // branch-free: every gather evaluated, the one for p selected
+    const uint32_t g0 = gup<0>(W), g1 = gup<1>(W), g2 = gup<2>(W), g3 = gup<3>(W), g4 = gup<4>(W), g5 = gup<5>(W);
+    uint32_t wup = g0;
+    wup = p == 1 ? g1 : wup; wup = p == 2 ? g2 : wup; wup = p == 3 ? g3 : wup;
+    wup = p == 4 ? g4 : wup; wup = p == 5 ? g5 : wup;
+#else
+    const uint32_t wup = (uint32_t)__shfl_xor((int)W, 1 << p);
+#endif
     LaneMasks m;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-        const bool on = ((lane >> q) & 1u) && ((cand >> q) & 1u);
-        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, q), sk = __builtin_amdgcn_readlane(keep_v, q);
-        m.vp[q] = on ? sp : 0u;
-        m.vk[q] = on ? sk : 0u;
+        const uint32_t cq = ((cand >> q) & 1u) ? ~0u : 0u;  // scalar
+        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, q) & cq, sk = __builtin_amdgcn_readlane(keep_v, q) & cq;
+        m.vp[q] = vand(sp, lm[q]);
+        m.vk[q] = vand(sk, lm[q]);
         m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
     }
     const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
@@ -247,9 +286,14 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t n, uint
     if (count) probes += (uint32_t)__popc(W);
     uint32_t Ret = hp ? 0u : wup;
     uint32_t I = hp ? 0u : W;
+#ifdef LC_ABL_NOSWEEP
+    const uint32_t nc = 0;  // ablation build: closure skipped
+#else
+    const uint32_t nc = (uint32_t)__popc(cand);  // a closure path has at most nc steps
+#endif
 #pragma unroll 1
-    for (uint32_t s = 1; s < n; ++s) {
-        const uint32_t nv = sweep_lanes<0, 6>(I, m);
+    for (uint32_t s = 0; s < nc; ++s) {
+        const uint32_t nv = sweep_lanes<0, 6>(I, m, one);
         const bool ch = nv != I;
         I = nv;
         if (!__any(ch)) break;
@@ -258,22 +302,17 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t n, uint
     Ret = xacc(Ret, I, pp, pk, pb);
     // One register holds at most 64 x 32 configs: with a larger budget only
     // emptiness matters (a ballot); exact sizes only when asked for (peak).
-    if (budget < 64u * 32u) {
+    if (__builtin_expect(budget < 64u * 32u, 0)) {
         const uint32_t nI = __ockl_wfred_add_u32((uint32_t)__popc(I));
         if (nI > budget) return 2;
     }
     if (!__any(Ret != 0u)) { nSn_out = 0; return 1; }
-    if (budget < 64u * 32u || want_size) {
+    if (__builtin_expect(budget < 64u * 32u || want_size, 0)) {
         const uint32_t nSn = __ockl_wfred_add_u32((uint32_t)__popc(Ret));
         nSn_out = nSn;
         if (nSn > budget) return 2;
     }
-    // the op at index `last` moves to index p: lanes with p (and not last)
-    // take Ret[L ^ p ^ last]; with p == last this is the identity
-    const uint32_t last = n - 1;
-    const uint32_t src = (uint32_t)__shfl_xor((int)Ret, (1 << p) | (1 << last));
-    const bool hl = (lane >> last) & 1u;
-    W = hl ? 0u : (hp ? src : Ret);
+    W = Ret;
     return 0;
 }
 
@@ -327,7 +366,7 @@ __device__ __forceinline__ int ok_reg(Lat &W, uint32_t p, uint32_t pass_v, uint3
     for (int s = 1; s < NB; ++s) {
         Lat nv;
 #pragma unroll
-        for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6>(I[k], m);
+        for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6>(I[k], m, 1u);
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
@@ -385,12 +424,12 @@ __device__ __forceinline__ int ok_reg(Lat &W, uint32_t p, uint32_t pass_v, uint3
     return 0;
 }
 
-// Lattice of a key with 9 or 10 ops pending: 16 x 64 words per array in a
-// per-block global workspace, index k * 64 + lane.  Every lane reads and
-// writes only its own column (register-bit partners are in the same lane;
-// lane-bit partners are exchanged in registers), so no cross-lane memory
-// ordering is involved.  Such events are rare (< 0.2 % of C2's); keeping
-// them out of registers keeps T0's register budget small.
+// Lattice of a key with 9 or 10 ops pending: 16 x 64 words per array in the
+// block's LDS workspace, index k * 64 + lane.  Every lane reads and writes
+// only its own column (register-bit partners are in the same lane; lane-bit
+// partners are exchanged in registers), so no cross-lane memory ordering is
+// involved.  Such events are rare (< 0.2 % of C2's); keeping them out of
+// registers keeps T0's register budget small.
 struct LatMem {
     uint32_t *W, *R, *I;
 };
@@ -483,14 +522,15 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 }
 
 // First max_final configs of the lattice held in m.W (register lattices are
-// stored there first), in (register, lane, state) order, with dense op
-// indices translated back to window slots (slot_v: lane j holds the slot of
-// dense index j).
+// stored there first), in (register, lane, state) order, with op indices
+// translated back to window slots (slot_v: lane j holds the slot of the op at
+// index j; `live` = the occupied indices).
 __device__ __forceinline__ void write_final_mem(const Args &a, int32_t key, const LatMem &m, uint32_t lane,
-                                                uint32_t slot_v, uint32_t n) {
+                                                uint32_t slot_v, uint32_t live_ops) {
     if (!a.final_cfg) return;
     const uint32_t mf = (uint32_t)a.max_final;
-    const int live = n <= 6 ? 1 : (1 << (n - 6));
+    const uint32_t top = live_ops ? 32u - (uint32_t)__clz(live_ops) : 0u;  // index bits in use
+    const int live = top <= 6 ? 1 : (1 << (top - 6));
     uint32_t base = 0;
 #pragma unroll 1
     for (int k = 0; k < live; ++k) {
@@ -505,9 +545,9 @@ __device__ __forceinline__ void write_final_mem(const Args &a, int32_t key, cons
         uint32_t r = base + x - c;
         uint64_t smask = 0;
         const uint32_t L = lane + 64u * (uint32_t)k;
-        for (uint32_t j = 0; j < n; ++j) {
+        for (uint32_t j = 0; j < top; ++j) {
             const uint32_t sj = __builtin_amdgcn_readlane(slot_v, j);
-            if ((L >> j) & 1u) smask |= 1ull << sj;
+            if (((L & live_ops) >> j) & 1u) smask |= 1ull << sj;
         }
         uint32_t mm = w;
         while (mm && r < mf) {
@@ -522,18 +562,22 @@ __device__ __forceinline__ void write_final_mem(const Args &a, int32_t key, cons
     if (lane == 0 && a.n_final) a.n_final[key] = base < mf ? base : mf;
 }
 
-// The lattice is indexed by DENSE op indices 0..n-1 (n = ops pending), not by
-// window slots: an invoke appends index n; when the op at index j returns, the
-// op at index n-1 takes index j (its configs move from bit n-1 to bit j, a
-// two-bit exchange).  So the lattice spans 2^n subsets, n = pending count.
+// Op indices: an invoke takes the lowest free index.  While at most 6 ops are
+// pending every live index is < 6 and an :ok just frees its index (ok_lane);
+// from 7 pending on the indices are dense (0..n-1) and an :ok refills the
+// freed index p with the op at index n-1 (a two-bit exchange of the lattice),
+// so the lattice spans 2^n subsets.
 //
-// Register budget: the event loop only touches the T0Args fields it needs;
-// result pointers, counters and work lists are read through `full` (a copy
-// of the tier's Args in device memory) once per key, so they never occupy
-// scalar registers across the loop.
-__device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key) {
+// The event loop has one exit test per event and no early returns: the
+// compiler then keeps one flat loop (no state-machine phi copies), and with
+// the 9-10-pending workspace in LDS there are no global stores in the loop,
+// so the prefetch of the next chunk is never waited for early.
+//
+// Register budget: the loop only touches the T0Args fields it needs; result
+// pointers, counters and work lists are read through `full` (a copy of the
+// tier's Args in device memory) once per key.
+__device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_t *ws) {
     const uint32_t lane = lane_id();
-    uint32_t *const ws = a.lat_ws + (size_t)blockIdx.x * (3 * T0_RMEM * 64);
     const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
@@ -549,89 +593,114 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key) {
     const bool count = (a.flags & T0_COUNT) != 0;
     const uint32_t *const evp = a.events + b;
     const uint32_t *const trp = a.trans + tb;
-    const uint32_t nev = (uint32_t)(e - b);
+    const uint32_t nev = (a.flags & T0_DBG_NOEVENTS) ? 0u : (uint32_t)(e - b);
 
     Lat W;
 #pragma unroll
     for (int k = 0; k < T0_RMAX; ++k) W[k] = 0;
     if (lane == 0) W[0] = 1u << a.init_state;
     bool in_mem = false;   // lattice lives in m.W (9 or 10 ops pending)
-    uint32_t pass_v = 0, keep_v = 0, b_v = 0;  // lane j: transfer of the op at dense index j
-    uint32_t slot_v = 0;   // lane j: window slot of the op at dense index j
-    uint32_t dense_v = 0;  // lane s: dense index of the op in window slot s
+    uint32_t pass_v = 0, keep_v = 0, b_v = 0;  // lane j: transfer of the op at index j
+    uint32_t slot_v = 0;   // lane j: window slot of the op at index j
+    uint32_t dense_v = 0;  // lane s: index of the op in window slot s
     uint32_t n = 0;        // ops pending
+    uint32_t live = 0;     // occupied op indices (all < 6 while n <= 6; 0..n-1 beyond)
+    uint32_t lm[6];        // lane bit q as a 0 / ~0 mask
+#pragma unroll
+    for (int q = 0; q < 6; ++q) lm[q] = (uint32_t)__builtin_amdgcn_sbfe((int)lane, q, 1);
     uint32_t peak = 1, probes = 0;
-    int status = 0;        // 1 invalid, 2 budget
+    int status = 0;        // 1 invalid, 2 budget, 3 spill
     uint32_t fev = 0;
 
-    // events arrive 64 at a time, one per lane; the next chunk's words are
-    // loaded while this chunk is searched
-    uint32_t ev_next = lane < nev ? evp[lane] : 0u;
-    const uint32_t nev_loop = (a.flags & T0_DBG_NOEVENTS) ? 0u : nev;
-    for (uint32_t base = 0; base < nev_loop; base += 64) {
+    // events arrive 64 at a time, one per lane; chunk c+1's words and
+    // descriptors are in flight while chunk c is searched
+    uint32_t ev = lane < nev ? evp[lane] : 0u;
+    uint32_t dsc = (lane < nev && !(ev & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev)] : 0u;
+    uint32_t ev_n = 64 + lane < nev ? evp[64 + lane] : 0u;
+    for (uint32_t base = 0; base < nev; base += 64) {
         const uint32_t cnt = nev - base < 64u ? nev - base : 64u;
-        const uint32_t ev = ev_next;
-        const uint32_t dsc = (lane < cnt && !(ev & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev)] : 0u;
-        ev_next = base + 64 + lane < nev ? evp[base + 64 + lane] : 0u;
+        // next chunk's descriptors (its words arrived during this chunk's
+        // predecessor) and the words of the chunk after it
+        const uint32_t dsc_n = (base + 64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
+        const uint32_t ev_nn = base + 128 + lane < nev ? evp[base + 128 + lane] : 0u;
         for (uint32_t i = 0; i < cnt; ++i) {
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
             const uint32_t slot = LC_EV_SLOT(evi);
             if (!(evi & LC_EV_OK_BIT)) {
-                if (n >= T0_MAX_WIDTH || slot >= 64) return K_SPILL;
-                if (n == 8) {  // 9 pending: move the lattice to the workspace
+                if (n >= T0_MAX_WIDTH || slot >= 64) {
+                    status = 3;
+                } else {
+                    if (n == 8) {  // 9 pending: move the lattice to the workspace
 #pragma unroll
-                    for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < T0_RMAX ? W[k < T0_RMAX ? k : 0] : 0u;
-                    in_mem = true;
+                        for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < T0_RMAX ? W[k < T0_RMAX ? k : 0] : 0u;
+                        in_mem = true;
+                    }
+                    const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
+                    const uint32_t idx = (uint32_t)__builtin_ctz(~live);  // lowest free index (= n once dense)
+                    const bool me = lane == idx;
+                    slot_v = me ? slot : slot_v;
+                    pass_v = me ? x.pass : pass_v;
+                    keep_v = me ? x.keep : keep_v;
+                    b_v = me ? x.b : b_v;
+                    dense_v = lane == slot ? idx : dense_v;
+                    live |= 1u << idx;
+                    ++n;
                 }
-                const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
-                const bool me = lane == n;
-                slot_v = me ? slot : slot_v;
-                pass_v = me ? x.pass : pass_v;
-                keep_v = me ? x.keep : keep_v;
-                b_v = me ? x.b : b_v;
-                dense_v = lane == slot ? n : dense_v;
-                ++n;
-                continue;
-            }
-            const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
-            uint32_t nSn = 0;
-            int r;
-            if (n <= 6) r = ok_lane(W[0], p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-            else if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-            else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-            else if (n == 9)
-                r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-            else
-                r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-            if (r) { status = r; fev = base + i; break; }
-            peak = nSn > peak ? nSn : peak;
-            // the op at index `last` takes index p (a no-op when p == last)
-            const uint32_t last = n - 1;
-            const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
-            const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last), x1 = __builtin_amdgcn_readlane(keep_v, last),
-                           x2 = __builtin_amdgcn_readlane(b_v, last);
-            const bool mp = lane == p;
-            slot_v = mp ? s_last : slot_v;
-            pass_v = mp ? x0 : pass_v;
-            keep_v = mp ? x1 : keep_v;
-            b_v = mp ? x2 : b_v;
-            dense_v = lane == s_last ? p : dense_v;
-            --n;
-            if (in_mem && n == 8) {  // back to registers: no config holds index 8 or 9
+            } else {
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
+                uint32_t nSn = 0;
+                int r;
+                if (__builtin_expect(n <= 6, 1)) {  // every live index < 6: no relocation
+#ifdef LC_ABL_NOOK
+                    r = 0;  // ablation build: bookkeeping only
+#else
+                    r = ok_lane(W[0], p, live, pass_v, keep_v, b_v, lane, lm, a.one, budget, count, probes, nSn, want_peak);
+#endif
+                    live = r ? live : live & ~(1u << p);
+                } else {
+                    if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    else if (n == 9)
+                        r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    else
+                        r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    // the op at index `last` takes index p (a no-op when p == last)
+                    const uint32_t last = n - 1;
+                    const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
+                    const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last),
+                                   x1 = __builtin_amdgcn_readlane(keep_v, last), x2 = __builtin_amdgcn_readlane(b_v, last);
+                    const bool mp = lane == p && !r;
+                    slot_v = mp ? s_last : slot_v;
+                    pass_v = mp ? x0 : pass_v;
+                    keep_v = mp ? x1 : keep_v;
+                    b_v = mp ? x2 : b_v;
+                    dense_v = (lane == s_last && !r) ? p : dense_v;
+                    live = r ? live : (1u << last) - 1u;
+                    if (in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
 #pragma unroll
-                for (int k = 0; k < T0_RMAX; ++k) W[k] = m.W[k * 64 + lane];
-                in_mem = false;
+                        for (int k = 0; k < T0_RMAX; ++k) W[k] = m.W[k * 64 + lane];
+                        in_mem = false;
+                    }
+                }
+                n = r ? n : n - 1;
+                peak = nSn > peak ? nSn : peak;
+                status = r;
+                fev = base + i;
             }
+            if (status) break;
         }
         if (status) break;
+        ev = ev_n; dsc = dsc_n; ev_n = ev_nn;
     }
-    // per-key epilogue: results through `full`
+    if (status == 3) return K_SPILL;
+    // per-key epilogue (results through `full`); on a failure W / live still
+    // hold the set before the failing event, which is what is reported
     const Args &f = *a.full;
     if (!in_mem) {
 #pragma unroll
         for (int k = 0; k < T0_RMAX; ++k) m.W[k * 64 + lane] = W[k];
     }
-    if (!(a.flags & T0_DBG_NOFINAL)) write_final_mem(f, key, m, lane, slot_v, n);
+    if (!(a.flags & T0_DBG_NOFINAL)) write_final_mem(f, key, m, lane, slot_v, live);
     const uint32_t pr = __ockl_wfred_add_u32(probes);
     if (status)
         finish_key(f, key, status == 1 ? LC_INVALID : LC_UNKNOWN, status == 1 ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET,
@@ -644,19 +713,46 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key) {
 // T0 over a work list: one wavefront per key (lattice in 4 registers, or the
 // workspace for 9-10 pending ops); a persistent grid so the workspace stays
 // one slot per resident block.
+#ifdef LC_T0_STAMPS
+// Diagnostic build only: per-block clock stamps and hardware placement.
+__device__ unsigned long long lc_t0_stamps[8192 * 6];
+#endif
+
 __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
+    __shared__ uint32_t ws[3 * T0_RMEM * 64];  // lattices of 9-10 pending ops (12 KB)
+#ifdef LC_T0_STAMPS
+    const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t nkeys = 0;
+#endif
     for (int32_t guard = 0; guard <= a.n_order; ++guard) {  // every wave takes at most n_order keys
         int32_t w = 0;
         if (lane_id() == 0) w = atomicAdd(a.ticket, 1);
         w = __builtin_amdgcn_readfirstlane(w);
         if (w >= a.n_order) break;
         const int32_t key = a.order[w];
-        if (lattice_key(a, key) == K_SPILL) {
+        if (lattice_key(a, key, ws) == K_SPILL) {
             const Args &f = *a.full;
             push_list(f.spill, f.n_spill, key);
         }
+#ifdef LC_T0_STAMPS
+        ++nkeys;
+#endif
     }
+#ifdef LC_T0_STAMPS
+    if (lane_id() == 0 && blockIdx.x < 8192) {
+        unsigned long long *o = lc_t0_stamps + blockIdx.x * 6;
+        o[0] = st0; o[1] = __builtin_amdgcn_s_memtime(); o[2] = rt0; o[3] = __builtin_amdgcn_s_memrealtime();
+        o[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        o[5] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) | ((unsigned long long)nkeys << 32);  // XCC_ID
+    }
+#endif
 }
+
+#ifdef LC_T0_STAMPS
+extern "C" int lc_debug_t0_stamps(unsigned long long *host, int n_blocks) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(lc_t0_stamps), (size_t)n_blocks * 6 * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 size_t lat_ws_words() { return 3 * T0_RMEM * 64; }
 
@@ -665,7 +761,7 @@ hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, hipStream_t s) 
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
     t.key_width = a.key_width; t.key_states = a.key_states; t.order = a.order; t.ticket = a.ticket;
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
-    t.init_state = a.init_state; t.shared_states = a.shared_states;
+    t.init_state = a.init_state; t.shared_states = a.shared_states; t.one = 1u;
     t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) |
               (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u);
     hipLaunchKernelGGL(k_search_lattice, dim3(grid), dim3(64), 0, s, t);

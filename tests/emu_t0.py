@@ -81,6 +81,30 @@ def sweep_lanes(cur, vp, vk, sb, N):
     return cur
 
 
+def ok_lane(W0, p, live, ops):
+    """ok_lane: every live index < 6, lowest-free indices, no relocation."""
+    cand = live & ~(1 << p)
+    vp, vk = [], []
+    for q in range(6):
+        on = ((LANES >> q) & 1 == 1) & bool((cand >> q) & 1)
+        vp.append(np.where(on, np.uint32(ops.pas[q]), np.uint32(0)).astype(np.uint32))
+        vk.append(np.where(on, np.uint32(ops.keep[q]), np.uint32(0)).astype(np.uint32))
+    sb = [ops.b[q] for q in range(6)]
+    hp = (LANES >> p) & 1 == 1
+    Ret = np.where(hp, 0, gup(W0, p)).astype(np.uint32)
+    I = np.where(hp, 0, W0).astype(np.uint32)
+    for _s in range(bin(cand).count("1")):
+        nv = sweep_lanes(I, vp, vk, sb, 6)
+        ch = (nv != I).any()
+        I = nv
+        if not ch:
+            break
+    Ret = xacc(Ret, I, ops.pas[p], ops.keep[p], ops.b[p])
+    if not Ret.any():
+        return 1, W0
+    return 0, Ret
+
+
 def ok_event(W, p, n, ops):
     """One :ok(p) with n pending; W = list of RL lane arrays. Returns (status, W')."""
     RL = 1 if n <= 6 else 1 << (n - 6)
@@ -213,6 +237,7 @@ def check_key(events, trans, tb=0, init_state=0):
     slot_v = [0] * 64
     dense = [0] * 128
     n = 0
+    live = 0
     for j, ev in enumerate(events):
         ev = int(ev)
         slot = (ev >> 24) & 0x7F
@@ -220,12 +245,22 @@ def check_key(events, trans, tb=0, init_state=0):
             if n >= 10 or slot >= 64:
                 return None
             pas, keep, b = xfer_of(int(trans[tb + (ev & 0xFFFFFF)]))
-            ops.pas[n], ops.keep[n], ops.b[n] = pas, keep, b
-            slot_v[n] = slot
-            dense[slot] = n
+            idx = (~live & -~live).bit_length() - 1
+            ops.pas[idx], ops.keep[idx], ops.b[idx] = pas, keep, b
+            slot_v[idx] = slot
+            dense[slot] = idx
+            live |= 1 << idx
             n += 1
             continue
         p = dense[slot]
+        if n <= 6:
+            st, W0 = ok_lane(W[0], p, live, ops)
+            if st == 1:
+                return 0, j
+            W[0] = W0
+            live &= ~(1 << p)
+            n -= 1
+            continue
         RL = 1 if n <= 6 else 1 << (n - 6)
         st, Wn = (ok_event_mem if n >= 9 else ok_event)(W[:RL], p, n, ops)
         if st == 1:
@@ -239,4 +274,5 @@ def check_key(events, trans, tb=0, init_state=0):
             slot_v[p] = s_last
             dense[s_last] = p
         n -= 1
+        live = (1 << n) - 1
     return 1, -1

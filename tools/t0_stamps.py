@@ -1,0 +1,31 @@
+"""Per-block clock stamps of T0 (diagnostic build liblincheck_stamps.so)."""
+import os, sys, ctypes as C, collections
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(root, "jepsen-etcd-demo_amd")]
+import numpy as np
+from lincheck import history as H
+from lincheck import _native as N
+from lincheck.checker import Device, Packed
+keys = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+h = H.synth(n_keys=keys, ops_per_key=1000, concurrency=10, seed=2)
+pk = Packed(h)
+db = Device(0).upload(pk)
+for _ in range(20):
+    st = db.check(False).stats
+nb = min(keys, 4096)
+buf = np.zeros(nb * 6, np.uint64)
+rc = N.lib().lc_debug_t0_stamps(buf.ctypes.data_as(C.c_void_p), nb)
+b = buf.reshape(nb, 6).astype(np.int64)
+cyc = b[:, 1] - b[:, 0]; rt = b[:, 3] - b[:, 2]
+print("rc", rc, "T0 ms", st["tier0_ms"])
+print("per-block cycles: min %d median %d max %d" % (cyc.min(), np.median(cyc), cyc.max()))
+print("per-block realtime ticks (100MHz): min %d median %d max %d" % (rt.min(), np.median(rt), rt.max()))
+print("clock GHz (cycles/realtime*0.1):", np.median(cyc / np.maximum(rt, 1)) * 0.1)
+start_rt = b[:, 2] - b[:, 2].min(); end_rt = b[:, 3] - b[:, 2].min()
+print("start spread us: max %.1f ; end max us %.1f" % (start_rt.max() / 100, end_rt.max() / 100))
+hw = b[:, 4]; xcc = b[:, 5] & 0xFFFFFFFF; nk = b[:, 5] >> 32
+simd = (hw >> 4) & 3; cu = (hw >> 8) & 15; sh = (hw >> 12) & 1; se = (hw >> 13) & 7
+place = collections.Counter(zip(xcc, se, sh, cu, simd))
+print("distinct SIMDs", len(place), "max blocks on one SIMD", max(place.values()), "keys per block max", nk.max())
+cuc = collections.Counter(zip(xcc, se, sh, cu))
+print("distinct CUs", len(cuc), "max blocks per CU", max(cuc.values()))
