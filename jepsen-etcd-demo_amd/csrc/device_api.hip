@@ -419,48 +419,56 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         a2.order = spill1; a2.n_order = 0; a2.n_in = n_spill1; a2.ticket = c->counters + 10;
         a2.spill = spill2; a2.n_spill = n_spill2; a2.wide = wide; a2.n_wide = n_wide;
         HIPCHK(lcd::launch_t2(a2, c->cu_count, c->stream));
-        // T3 (HBM tier): keys beyond T2, then keys needing wide configs.
-        // The work-list lengths size the workspace, so read them back first.
-        int32_t cnt3[4];
-        HIPCHK(hipMemcpyAsync(cnt3, c->counters, sizeof cnt3, hipMemcpyDeviceToHost, c->stream));
+    }
+    // One readback for the common case.  The T3 (HBM) tier is launched only
+    // when T2 left keys for it (its workspace is sized from those counts),
+    // after which the readback is repeated.
+    unsigned long long acc[4] = {0, 0, 0, 0};
+    int32_t cnt[16];
+    auto readback = [&]() -> int {
+        HIPCHK(hipEventRecord(c->e1, c->stream));
+        HIPCHK(hipMemcpyAsync(acc, c->acc, sizeof acc, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(cnt, c->counters, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+        if (!dev_result && K > 0) {
+            HIPCHK(hipMemcpyAsync(r->valid, c->valid, (size_t)K, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(r->fail_event, c->fail_event, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(r->cause, c->cause, (size_t)K, hipMemcpyDeviceToHost, c->stream));
+            if (r->peak_configs)
+                HIPCHK(hipMemcpyAsync(r->peak_configs, c->peak, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+            if (r->final_configs)
+                HIPCHK(hipMemcpyAsync(r->final_configs, c->final_cfg, (size_t)K * c->o.max_final * 16,
+                                      hipMemcpyDeviceToHost, c->stream));
+            if (r->n_final)
+                HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+        }
         HIPCHK(hipStreamSynchronize(c->stream));
+        return LC_OK;
+    };
+    rc = readback();
+    if (rc) return rc;
+    if (K > 0 && (cnt[2] > 0 || cnt[3] > 0)) {
+        // T3 (HBM tier): keys beyond T2, then keys needing wide configs
         lcd::Args a3 = a;
         a3.wide = wide; a3.n_wide = n_wide;
-        if (cnt3[2] > 0) {
+        if (cnt[2] > 0) {
             int slots = 0;
-            rc = ensure_ws(c, 0, cnt3[2], &slots);
+            rc = ensure_ws(c, 0, cnt[2], &slots);
             if (rc) return rc;
             a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 11;
             HIPCHK(lcd::launch_t3_narrow(a3, c->ws[0].w, slots, c->stream));
-            HIPCHK(hipMemcpyAsync(cnt3, c->counters, sizeof cnt3, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(cnt, c->counters, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
         }
-        if (cnt3[3] > 0) {
+        if (cnt[3] > 0) {
             int slots = 0;
-            rc = ensure_ws(c, 1, cnt3[3], &slots);
+            rc = ensure_ws(c, 1, cnt[3], &slots);
             if (rc) return rc;
             a3.order = wide; a3.n_order = 0; a3.n_in = n_wide; a3.ticket = c->counters + 12;
             HIPCHK(lcd::launch_t3_wide(a3, c->ws[1].w, slots, c->stream));
         }
+        rc = readback();
+        if (rc) return rc;
     }
-    HIPCHK(hipEventRecord(c->e1, c->stream));
-    unsigned long long acc[4] = {0, 0, 0, 0};
-    int32_t cnt[16];
-    HIPCHK(hipMemcpyAsync(acc, c->acc, sizeof acc, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(cnt, c->counters, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
-    if (!dev_result && K > 0) {
-        HIPCHK(hipMemcpyAsync(r->valid, c->valid, (size_t)K, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(r->fail_event, c->fail_event, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(r->cause, c->cause, (size_t)K, hipMemcpyDeviceToHost, c->stream));
-        if (r->peak_configs)
-            HIPCHK(hipMemcpyAsync(r->peak_configs, c->peak, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
-        if (r->final_configs)
-            HIPCHK(hipMemcpyAsync(r->final_configs, c->final_cfg, (size_t)K * c->o.max_final * 16,
-                                  hipMemcpyDeviceToHost, c->stream));
-        if (r->n_final)
-            HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
-    }
-    HIPCHK(hipStreamSynchronize(c->stream));
     float ms = 0, ms0 = 0;
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
     if (K > 0) HIPCHK(hipEventElapsedTime(&ms0, c->e0, c->et0));
