@@ -65,6 +65,8 @@ extern "C" {
 #define LC_F_WRITE 1
 #define LC_F_CAS   2
 #define LC_F_OTHER 3   /* nemesis :start/:stop and anything else */
+#define LC_F_ACQUIRE 4 /* (model/mutex) :acquire                  */
+#define LC_F_RELEASE 5 /* (model/mutex) :release                  */
 
 #define LC_NIL        INT64_MIN  /* a nil value                                */
 #define LC_NO_KEY     INT64_MIN  /* :value is not an independent tuple [k v]   */
@@ -146,8 +148,19 @@ typedef struct lc_batch {
     uint32_t        init_state; /* state id of the initial value (0 = nil)    */
 } lc_batch;
 
+/* The Knossos model a batch is checked against (knossos.model, SURVEY.md
+ * 8(f) F-4).  The demo uses (model/cas-register) at etcdemo.clj:117; the
+ * other two map onto the same transition descriptors:
+ *   register     read / write of integer values (no cas)
+ *   mutex        two states, unlocked (state 0, the initial one) and locked:
+ *                :acquire = cas unlocked -> locked, :release = cas locked ->
+ *                unlocked; :value is ignored                            */
+#define LC_MODEL_CAS_REGISTER 0
+#define LC_MODEL_REGISTER     1
+#define LC_MODEL_MUTEX        2
+
 typedef struct lc_pack_opts {
-    int32_t reserved;  /* must be 0 */
+    int32_t model;     /* LC_MODEL_* (0 = cas-register) */
 } lc_pack_opts;
 
 typedef struct lc_packed lc_packed;  /* library-owned */

@@ -172,6 +172,8 @@ bool read_op(Parser &ps, RawOp &op) {
                 if (v.kind == Val::KW && v.kw == "read") op.f = LC_F_READ;
                 else if (v.kind == Val::KW && v.kw == "write") op.f = LC_F_WRITE;
                 else if (v.kind == Val::KW && v.kw == "cas") op.f = LC_F_CAS;
+                else if (v.kind == Val::KW && v.kw == "acquire") op.f = LC_F_ACQUIRE;  // (model/mutex)
+                else if (v.kind == Val::KW && v.kw == "release") op.f = LC_F_RELEASE;
                 else {
                     op.f = LC_F_OTHER;
                     if (v.kind == Val::KW) op.value.kw = v.kw;  // remembered for nemesis :start/:stop
@@ -235,7 +237,9 @@ int build(std::vector<RawOp> &ops, lc_hist **out) {
                 if (!ok || key == LC_NIL) { delete h; return lc::fail(LC_E_UNSUPPORTED, "lc_edn: op %zu: tuple key is not an integer", i); }
                 val = &o.value.v[1];
             }
-            if (o.f == LC_F_CAS) {
+            if (o.f == LC_F_ACQUIRE || o.f == LC_F_RELEASE) {
+                // mutex ops carry no register value (knossos.model/mutex ignores it)
+            } else if (o.f == LC_F_CAS) {
                 if (val->kind == Val::VEC && val->v.size() == 2) {
                     v0 = scalar(val->v[0], ok);
                     v1 = scalar(val->v[1], ok);
@@ -307,11 +311,11 @@ extern "C" int lc_edn_write(const char *path, const lc_history *h) {
     FILE *f = std::fopen(path, "wb");
     if (!f) return lc::fail(LC_E_IO, "lc_edn_write: cannot open %s", path);
     static const char *types[] = {"invoke", "ok", "fail", "info"};
-    static const char *fs[] = {"read", "write", "cas"};
+    static const char *fs[] = {"read", "write", "cas", "", "acquire", "release"};
     std::string line;
     for (int64_t r = 0; r < h->n; ++r) {
         line.clear();
-        if (h->type[r] > LC_INFO || h->f[r] > LC_F_OTHER) { std::fclose(f); return lc::fail(LC_E_INVALID, "lc_edn_write: bad row %lld", (long long)r); }
+        if (h->type[r] > LC_INFO || h->f[r] > LC_F_RELEASE) { std::fclose(f); return lc::fail(LC_E_INVALID, "lc_edn_write: bad row %lld", (long long)r); }
         line += "{:type :"; line += types[h->type[r]];
         if (h->f[r] == LC_F_OTHER) {
             line += ", :f :"; line += h->v0[r] == 1 ? "start" : h->v0[r] == 0 ? "stop" : "nemesis";
@@ -320,7 +324,9 @@ extern "C" int lc_edn_write(const char *path, const lc_history *h) {
             line += ", :f :"; line += fs[h->f[r]];
             line += ", :value ";
             std::string v;
-            if (h->f[r] == LC_F_CAS) {
+            if (h->f[r] == LC_F_ACQUIRE || h->f[r] == LC_F_RELEASE) {
+                v = "nil";
+            } else if (h->f[r] == LC_F_CAS) {
                 if (h->v0[r] == LC_NIL && h->v1[r] == LC_NIL && h->type[r] == LC_INVOKE) v = "nil";
                 else { v = "["; put_scalar(v, h->v0[r]); v += " "; put_scalar(v, h->v1[r]); v += "]"; }
             } else {

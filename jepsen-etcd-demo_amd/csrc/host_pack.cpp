@@ -32,7 +32,12 @@
 
 namespace {
 
-inline bool is_client_f(uint8_t f) { return f == LC_F_READ || f == LC_F_WRITE || f == LC_F_CAS; }
+// Ops a model can step (knossos.model: cas-register, register, mutex).
+inline bool is_client_f(uint8_t f, int model) {
+    if (model == LC_MODEL_MUTEX) return f == LC_F_ACQUIRE || f == LC_F_RELEASE;
+    if (model == LC_MODEL_REGISTER) return f == LC_F_READ || f == LC_F_WRITE;
+    return f == LC_F_READ || f == LC_F_WRITE || f == LC_F_CAS;
+}
 
 // Small process -> outstanding-op map; linear scan while small, hash beyond.
 struct ProcMap {
@@ -78,7 +83,7 @@ struct KeyOut {
 };
 
 // Pairing + event emission for one key (rows in history order).
-void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, KeyOut &out) {
+void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model, KeyOut &out) {
     ProcMap pm;
     out.ops.clear();
     out.ops.reserve((size_t)nrows / 2 + 1);
@@ -88,9 +93,10 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, KeyOut &o
         uint8_t t = h.type[r];
         int64_t p = h.process[r];
         if (t == LC_INVOKE) {
-            if (!is_client_f(h.f[r])) {
+            if (!is_client_f(h.f[r], model)) {
+                static const char *names[] = {"cas-register", "register", "mutex"};
                 out.err = LC_E_UNSUPPORTED;
-                out.msg = "row " + std::to_string(r) + ": cas-register cannot step this :f";
+                out.msg = "row " + std::to_string(r) + ": " + names[model] + " cannot step this :f";
                 return;
             }
             int32_t id = (int32_t)out.ops.size();
@@ -180,7 +186,9 @@ struct lc_packed {
 
 extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed **out) {
     if (!h || !out) return lc::fail(LC_E_INVALID, "lc_pack: null argument");
-    if (opts && opts->reserved != 0) return lc::fail(LC_E_INVALID, "lc_pack: opts.reserved must be 0");
+    const int model = opts ? opts->model : LC_MODEL_CAS_REGISTER;
+    if (model < LC_MODEL_CAS_REGISTER || model > LC_MODEL_MUTEX)
+        return lc::fail(LC_E_INVALID, "lc_pack: unknown model %d", model);
     if (h->n < 0 || (h->n > 0 && (!h->type || !h->f || !h->process || !h->key || !h->v0 || !h->v1)))
         return lc::fail(LC_E_INVALID, "lc_pack: history arrays missing");
     const int64_t n = h->n;
@@ -193,7 +201,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         int64_t last_key = LC_NO_KEY;
         int32_t last_idx = -1;
         for (int64_t r = 0; r < n; ++r) {
-            if (h->type[r] > LC_INFO || h->f[r] > LC_F_OTHER) {
+            if (h->type[r] > LC_INFO || h->f[r] > LC_F_RELEASE) {
                 delete P;
                 return lc::fail(LC_E_INVALID, "lc_pack: row %lld has a bad :type/:f code", (long long)r);
             }
@@ -243,7 +251,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             auto work = [&](unsigned t) {
                 for (int64_t k = t; k < K; k += nt)
                     pack_key(*h, P->krows.data() + P->krow_off[(size_t)k],
-                             (int64_t)(P->krow_off[(size_t)k + 1] - P->krow_off[(size_t)k]), ko[(size_t)k]);
+                             (int64_t)(P->krow_off[(size_t)k + 1] - P->krow_off[(size_t)k]), model, ko[(size_t)k]);
             };
             std::vector<std::thread> pool;
             for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
@@ -262,6 +270,10 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         // ---- A4/A5: register states + transition descriptors ----
         // A state is a value some surviving write / cas could install.
         auto state_values = [&](const KeyOut &o, std::vector<int64_t> &vals) {
+            if (model == LC_MODEL_MUTEX) {  // state 1 = locked (state 0, "nil", = unlocked)
+                vals.push_back(1);
+                return;
+            }
             for (const KOp &op : o.ops) {
                 if (op.fate == 2) continue;
                 if (op.f == LC_F_WRITE && op.v0 != LC_NIL) vals.push_back(op.v0);
@@ -297,6 +309,8 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             return it == m.end() ? LC_STATE_NONE : it->second;
         };
         auto make_desc = [&](const std::unordered_map<int64_t, uint32_t> &m, const KOp &op) -> uint32_t {
+            if (op.f == LC_F_ACQUIRE) return LC_DESC(LC_T_CAS, 0, sid(m, 1));  // unlocked -> locked
+            if (op.f == LC_F_RELEASE) return LC_DESC(LC_T_CAS, sid(m, 1), 0);  // locked -> unlocked
             if (op.f == LC_F_READ)
                 return op.v0 == LC_NIL ? LC_DESC(LC_T_READ_ANY, 0, 0) : LC_DESC(LC_T_READ, sid(m, op.v0), 0);
             if (op.f == LC_F_WRITE) return LC_DESC(LC_T_WRITE, 0, sid(m, op.v0));

@@ -20,7 +20,8 @@ LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblin
 LC_ABI_VERSION = 2
 LC_OPT_COUNT_PROBES = 0x1
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
-LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER = 0, 1, 2, 3
+LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE = 0, 1, 2, 3, 4, 5
+LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX = 0, 1, 2
 LC_NIL = -(1 << 63)
 LC_NO_KEY = LC_NIL
 LC_NO_PROCESS = LC_NIL
@@ -50,7 +51,7 @@ class LcBatch(C.Structure):
 
 
 class LcPackOpts(C.Structure):
-    _fields_ = [("reserved", C.c_int32)]
+    _fields_ = [("model", C.c_int32)]
 
 
 class LcOpts(C.Structure):

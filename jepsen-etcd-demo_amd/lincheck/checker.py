@@ -27,7 +27,7 @@ import numpy as np
 
 from . import _native as N
 from .history import History
-from .model import CASRegister, fmt
+from .model import MODELS, CASRegister, fmt
 
 DEFAULT_BUDGET = 1 << 20
 TRUNCATE = 10  # jepsen.checker/linearizable truncates :final-paths and :configs
@@ -37,11 +37,13 @@ TRUNCATE = 10  # jepsen.checker/linearizable truncates :final-paths and :configs
 class Packed:
     """lc_pack output: per-key event streams plus the row maps back to ops."""
 
-    def __init__(self, hist: History):
+    def __init__(self, hist: History, model=None):
         self.hist = hist
+        self.model = model if model is not None else CASRegister()
         self._c = hist.as_c()
         handle = C.c_void_p()
-        N.check(N.lib().lc_pack(C.byref(self._c), None, C.byref(handle)))
+        opts = N.LcPackOpts(self.model.code)
+        N.check(N.lib().lc_pack(C.byref(self._c), C.byref(opts), C.byref(handle)))
         self.handle = handle
         v = N.LcBatch()
         N.check(N.lib().lc_packed_view(self.handle, C.byref(v)))
@@ -213,7 +215,8 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
         mask = lo | ((hi & ((1 << 48) - 1)) << 64)
         pend = [hist.op(packed.event_row(i, slot_op[s])) for s in sorted(slot_op) if not (mask >> s) & 1]
         lin = [hist.op(packed.event_row(i, slot_op[s])) for s in sorted(slot_op) if (mask >> s) & 1]
-        configs.append({"model": {"value": packed.state_value(i, st)}, "pending": pend, "linearized": lin})
+        configs.append({"model": packed.model.of_state(packed.state_value(i, st)).render(),
+                        "pending": pend, "linearized": lin})
     out: Dict[str, Any] = {"analyzer": "linear", "configs": configs[:TRUNCATE], "final-paths": []}
     if v == N.LC_VALID:
         out["valid?"] = True
@@ -240,8 +243,8 @@ class Linearizable:
         model = opts.get("model")
         if model is None:
             raise ValueError("The linearizable checker requires a model.")
-        if not isinstance(model, CASRegister):
-            raise NotImplementedError("only (model/cas-register) is supported")
+        if not isinstance(model, MODELS):
+            raise NotImplementedError("supported models: (model/cas-register), (model/register), (model/mutex)")
         algo = opts.get("algorithm", "linear")
         if algo not in ("linear", ":linear"):
             raise NotImplementedError(f"algorithm {algo!r}: only :linear is implemented")
@@ -255,7 +258,7 @@ class Linearizable:
     def check(self, test: Dict, history, opts: Dict | None = None) -> Dict:
         """One key's (unwrapped) sub-history, as at etcdemo.clj:117."""
         hist = history if isinstance(history, History) else History.from_ops(history, default_key=0)
-        packed = Packed(hist)
+        packed = Packed(hist, self.model)
         if packed.n_keys == 0:
             return {"valid?": True, "configs": [], "final-paths": [], "analyzer": "linear"}
         res = self._dev().check(packed)
@@ -265,7 +268,7 @@ class Linearizable:
     def check_independent(self, test, history, opts, inner) -> Dict:
         from .independent import merge_results, subhistory
         hist = history if isinstance(history, History) else History.from_ops(history)
-        packed = Packed(hist)
+        packed = Packed(hist, self.model)
         res = self._dev().check(packed) if packed.n_keys else None
         results = {}
         ops_cache = None

@@ -21,7 +21,8 @@ from .independent import Tuple, is_tuple
 
 TYPES = {"invoke": N.LC_INVOKE, "ok": N.LC_OK_T, "fail": N.LC_FAIL, "info": N.LC_INFO}
 TYPE_NAMES = {v: k for k, v in TYPES.items()}
-FS = {"read": N.LC_F_READ, "write": N.LC_F_WRITE, "cas": N.LC_F_CAS}
+FS = {"read": N.LC_F_READ, "write": N.LC_F_WRITE, "cas": N.LC_F_CAS,
+      "acquire": N.LC_F_ACQUIRE, "release": N.LC_F_RELEASE}
 F_NAMES = {v: k for k, v in FS.items()}
 NIL = N.LC_NIL
 
@@ -83,7 +84,9 @@ class History:
                 k[i] = default_key
             else:
                 k[i] = N.LC_NO_KEY
-            if f[i] == N.LC_F_CAS:
+            if f[i] in (N.LC_F_ACQUIRE, N.LC_F_RELEASE):
+                a[i] = b[i] = NIL          # (model/mutex) ignores the value
+            elif f[i] == N.LC_F_CAS:
                 if v is None:
                     a[i] = b[i] = NIL
                 else:
@@ -135,7 +138,7 @@ class History:
         nil = lambda x: None if x == NIL else int(x)
         if f == N.LC_F_CAS:
             val = [nil(self.v0[i]), nil(self.v1[i])]
-        elif f == N.LC_F_OTHER:
+        elif f in (N.LC_F_OTHER, N.LC_F_ACQUIRE, N.LC_F_RELEASE):
             val = None
         else:
             val = nil(self.v0[i])

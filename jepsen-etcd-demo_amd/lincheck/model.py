@@ -1,7 +1,12 @@
-"""Mirror of knossos.model for this path: (model/cas-register) at etcdemo.clj:117.
+"""Mirror of knossos.model for this path.
 
-Only the cas-register is implemented; the device search
-takes its transition descriptors (include/lincheck.h LC_T_*).
+The demo checks (model/cas-register) (etcdemo.clj:117).
+(model/register) and (model/mutex) are the other Knossos models whose state
+space maps onto the device's transition descriptors (include/lincheck.h
+LC_T_*, LC_MODEL_*).  The step functions here only
+produce the result maps' :model values and "can't ..." messages on the host;
+the search itself runs on the device.  Messages follow the public knossos
+0.3.7 source as recalled (not verifiable here: knossos is absent).
 """
 
 from __future__ import annotations
@@ -9,14 +14,26 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+from . import _native as N
+
+
+@dataclass(frozen=True)
+class Inconsistent:
+    msg: str
+
+
+def fmt(v) -> str:
+    return "nil" if v is None else str(v)
+
 
 @dataclass(frozen=True)
 class CASRegister:
     """knossos.model/cas-register: nil initial value unless given."""
     value: Optional[int] = None
+    code = N.LC_MODEL_CAS_REGISTER
+    name = "cas-register"
 
     def step(self, f: str, v):
-        """Sequential spec, as knossos.model's CASRegister step (for docs/tests)."""
         if f == "write":
             return CASRegister(v)
         if f == "cas":
@@ -30,17 +47,72 @@ class CASRegister:
             return Inconsistent(f"can't read {fmt(v)} from register {fmt(self.value)}")
         raise ValueError(f"cas-register cannot step {f!r}")
 
+    def of_state(self, value):
+        return CASRegister(value)
+
+    def render(self) -> dict:
+        return {"value": self.value}
+
 
 @dataclass(frozen=True)
-class Inconsistent:
-    msg: str
+class Register:
+    """knossos.model/register: read / write, nil initial value."""
+    value: Optional[int] = None
+    code = N.LC_MODEL_REGISTER
+    name = "register"
+
+    def step(self, f: str, v):
+        if f == "write":
+            return Register(v)
+        if f == "read":
+            if v is None or v == self.value:
+                return self
+            return Inconsistent(f"{fmt(self.value)}≠{fmt(v)}")
+        raise ValueError(f"register cannot step {f!r}")
+
+    def of_state(self, value):
+        return Register(value)
+
+    def render(self) -> dict:
+        return {"value": self.value}
 
 
-def fmt(v) -> str:
-    return "nil" if v is None else str(v)
+@dataclass(frozen=True)
+class Mutex:
+    """knossos.model/mutex: unlocked initially."""
+    locked: bool = False
+    code = N.LC_MODEL_MUTEX
+    name = "mutex"
+
+    def step(self, f: str, v=None):
+        if f == "acquire":
+            return Inconsistent("already held") if self.locked else Mutex(True)
+        if f == "release":
+            return Mutex(False) if self.locked else Inconsistent("not held")
+        raise ValueError(f"mutex cannot step {f!r}")
+
+    def of_state(self, value):
+        # lc_pack numbers the mutex states 0 = unlocked (nil), 1 = locked
+        return Mutex(value is not None)
+
+    def render(self) -> dict:
+        return {"locked?": self.locked}
 
 
 def cas_register(value: Optional[int] = None) -> CASRegister:
     if value is not None:
         raise NotImplementedError("only the nil initial value of (model/cas-register) is supported")
     return CASRegister(value)
+
+
+def register(value: Optional[int] = None) -> Register:
+    if value is not None:
+        raise NotImplementedError("only the nil initial value of (model/register) is supported")
+    return Register(value)
+
+
+def mutex() -> Mutex:
+    return Mutex(False)
+
+
+MODELS = (CASRegister, Register, Mutex)

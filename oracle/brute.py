@@ -11,7 +11,8 @@ linearizable iff there is a sequence of ops that
   * contains every op whose :ok is at or before e,
   * may contain any other op invoked before e (it is still pending at e),
   * respects real time: if a's :ok precedes b's :invoke, a comes first,
-  * is legal for the cas-register model from the nil initial value.
+  * is legal for the model (cas-register, register or mutex) from its
+    initial value.
 The history is valid iff every prefix ending at an :ok is linearizable; the
 reported failure is the first :ok whose prefix is not.  That event is what
 knossos.linear reports as :op (its config set empties exactly there).
@@ -24,10 +25,10 @@ from __future__ import annotations
 from functools import lru_cache
 from typing import Optional, Sequence
 
-from linear_ref import INCONSISTENT, cas_register_step, complete
+from linear_ref import INCONSISTENT, complete, model_step
 
 
-def prefix_linearizable(ops, events, e: int, initial=None) -> bool:
+def prefix_linearizable(ops, events, e: int, initial=None, step=None) -> bool:
     inv_at = {}
     ok_at = {}
     for i, (kind, oid, _pos) in enumerate(events[: e + 1]):
@@ -48,7 +49,7 @@ def prefix_linearizable(ops, events, e: int, initial=None) -> bool:
         for q in cand:
             if q in done or not must[q] <= done:
                 continue
-            s2 = cas_register_step(state, ops[q].f, ops[q].value)
+            s2 = step(state, ops[q].f, ops[q].value)
             if s2 is INCONSISTENT:
                 continue
             if search((s2 is None, s2), done | {q}):
@@ -58,10 +59,13 @@ def prefix_linearizable(ops, events, e: int, initial=None) -> bool:
     return search((initial is None, initial), frozenset())
 
 
-def brute_check(history: Sequence[dict], initial=None):
+def brute_check(history: Sequence[dict], initial=None, model: str = "cas-register"):
     """Returns (valid, fail_event_ordinal or None) over the reduced events."""
-    ops, events = complete(history)
+    ops, events = complete(history, model)
+    step, init = model_step(model)
+    if initial is None:
+        initial = init
     for e, (kind, _oid, _pos) in enumerate(events):
-        if kind == "ok" and not prefix_linearizable(ops, events, e, initial):
+        if kind == "ok" and not prefix_linearizable(ops, events, e, initial, step):
             return False, e
     return True, None

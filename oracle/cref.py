@@ -30,21 +30,28 @@ def lib():
         L = C.CDLL(SO)
         L.oracle_check_history.restype = C.c_int64
         L.oracle_check_history.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_check_history_model.restype = C.c_int64
+        L.oracle_check_history_model.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
+                                                 C.c_int64]
         _lib = L
     return _lib
 
 
-def check_history(hist_c, budget: int = 1 << 20, threads: int = 1):
+MODELS = {"cas-register": 0, "register": 1, "mutex": 2}
+
+
+def check_history(hist_c, budget: int = 1 << 20, threads: int = 1, model: str = "cas-register"):
     """Run the C restatement over an lc_history struct (lincheck.history.History.as_c()).
 
     Returns (keys, structured numpy array of per-key results)."""
     L = lib()
-    nk = L.oracle_check_history(C.byref(hist_c), budget, threads, None, None, 0)
+    m = MODELS[model]
+    nk = L.oracle_check_history_model(C.byref(hist_c), m, budget, threads, None, None, 0)
     if nk < 0:
         raise RuntimeError(f"oracle_check_history failed: {nk}")
     keys = np.zeros(max(nk, 1), np.int64)
     res = (OracleKeyResult * max(nk, 1))()
-    rc = L.oracle_check_history(C.byref(hist_c), budget, threads, keys.ctypes.data, C.addressof(res), nk)
+    rc = L.oracle_check_history_model(C.byref(hist_c), m, budget, threads, keys.ctypes.data, C.addressof(res), nk)
     if rc < 0:
         raise RuntimeError(f"oracle_check_history failed: {rc}")
     dt = np.dtype({"names": [f[0] for f in OracleKeyResult._fields_],

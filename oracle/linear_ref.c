@@ -134,8 +134,15 @@ static void vmap_put(vent *tab, uint64_t cap, int64_t v, uint32_t *next) {
     tab[h].used = 1; tab[h].v = v; tab[h].id = (*next)++;
 }
 
+/* Ops each model can step (knossos.model cas-register / register / mutex). */
+static int model_steps(int model, uint8_t f) {
+    if (model == LC_MODEL_MUTEX) return f == LC_F_ACQUIRE || f == LC_F_RELEASE;
+    if (model == LC_MODEL_REGISTER) return f == LC_F_READ || f == LC_F_WRITE;
+    return f == LC_F_READ || f == LC_F_WRITE || f == LC_F_CAS;
+}
+
 /* Check one key: rows[] are its sub-history rows (history order). */
-static int check_key(const lc_history *h, const int64_t *rows, int64_t nr, uint64_t budget,
+static int check_key(const lc_history *h, const int64_t *rows, int64_t nr, uint64_t budget, int model,
                      oracle_key_result *res) {
     memset(res, 0, sizeof *res);
     res->valid = 1; res->fail_event = -1; res->peak = 1;
@@ -153,7 +160,7 @@ static int check_key(const lc_history *h, const int64_t *rows, int64_t nr, uint6
         int64_t j;
         for (j = 0; j < npm; ++j) if (pm[j].p == p) break;
         if (t == LC_INVOKE) {
-            if (h->f[r] > LC_F_CAS) { free(ops); free(row_op); free(pm); return LC_E_UNSUPPORTED; }
+            if (!model_steps(model, h->f[r])) { free(ops); free(row_op); free(pm); return LC_E_UNSUPPORTED; }
             ops[nops].f = h->f[r]; ops[nops].v0 = h->v0[r]; ops[nops].v1 = h->v1[r]; ops[nops].fate = 0;
             if (j < npm) pm[j].op = (int32_t)nops; else { pm[npm].p = p; pm[npm].op = (int32_t)nops; npm++; }
             row_op[i] = (int32_t)nops++;
@@ -187,9 +194,14 @@ static int check_key(const lc_history *h, const int64_t *rows, int64_t nr, uint6
     }
     desc_t *desc = (desc_t *)malloc((size_t)(nops + 1) * sizeof(desc_t));
     if (!desc) { free(vt); free(ops); free(row_op); return LC_E_NOMEM; }
+    if (model == LC_MODEL_MUTEX) nstates = 2;  /* 0 unlocked (initial), 1 locked */
     for (int64_t k = 0; k < nops; ++k) {
         desc_t d;
-        if (ops[k].f == LC_F_READ) {
+        if (ops[k].f == LC_F_ACQUIRE) {        /* legal iff unlocked */
+            d.kind = LC_T_CAS; d.a = 0; d.b = 1;
+        } else if (ops[k].f == LC_F_RELEASE) { /* legal iff locked */
+            d.kind = LC_T_CAS; d.a = 1; d.b = 0;
+        } else if (ops[k].f == LC_F_READ) {
             d.kind = ops[k].v0 == LC_NIL ? LC_T_READ_ANY : LC_T_READ;
             d.a = vmap_get(vt, vcap, ops[k].v0); d.b = 0;
         } else if (ops[k].f == LC_F_WRITE) {
@@ -299,6 +311,7 @@ typedef struct {
     const uint64_t *off;
     int64_t nkeys;
     uint64_t budget;
+    int model;
     oracle_key_result *out;
     int64_t next;
     int rc;
@@ -312,7 +325,8 @@ static void *worker(void *arg) {
         int64_t k = j->next++;
         pthread_mutex_unlock(&j->mu);
         if (k >= j->nkeys) break;
-        int rc = check_key(j->h, j->rows + j->off[k], (int64_t)(j->off[k + 1] - j->off[k]), j->budget, &j->out[k]);
+        int rc = check_key(j->h, j->rows + j->off[k], (int64_t)(j->off[k + 1] - j->off[k]), j->budget, j->model,
+                           &j->out[k]);
         if (rc) { pthread_mutex_lock(&j->mu); j->rc = rc; pthread_mutex_unlock(&j->mu); }
     }
     return NULL;
@@ -323,8 +337,8 @@ static void *worker(void *arg) {
  * appearance (as lc_pack).  Returns the key count (or a negative LC_E_*);
  * out_keys / out must hold max_keys entries (call with max_keys = 0 to count).
  */
-int64_t oracle_check_history(const lc_history *h, uint64_t budget, int n_threads,
-                             int64_t *out_keys, oracle_key_result *out, int64_t max_keys) {
+int64_t oracle_check_history_model(const lc_history *h, int model, uint64_t budget, int n_threads,
+                                   int64_t *out_keys, oracle_key_result *out, int64_t max_keys) {
     if (!h || h->n < 0) return LC_E_INVALID;
     int64_t n = h->n;
     uint64_t cap = 64;
@@ -362,7 +376,7 @@ int64_t oracle_check_history(const lc_history *h, uint64_t budget, int n_threads
         free(cur);
     }
     free(rk);
-    job_t j = {h, rows, off, nk, budget ? budget : (1ull << 20), out, 0, 0, PTHREAD_MUTEX_INITIALIZER};
+    job_t j = {h, rows, off, nk, budget ? budget : (1ull << 20), model, out, 0, 0, PTHREAD_MUTEX_INITIALIZER};
     if (n_threads < 1) n_threads = 1;
     if (n_threads > 256) n_threads = 256;
     pthread_t th[256];
@@ -372,4 +386,10 @@ int64_t oracle_check_history(const lc_history *h, uint64_t budget, int n_threads
     if (out_keys) memcpy(out_keys, keys, (size_t)nk * sizeof(int64_t));
     free(keys); free(off); free(rows);
     return j.rc ? j.rc : nk;
+}
+
+/* The demo's model, (model/cas-register) (etcdemo.clj:117). */
+int64_t oracle_check_history(const lc_history *h, uint64_t budget, int n_threads,
+                             int64_t *out_keys, oracle_key_result *out, int64_t max_keys) {
+    return oracle_check_history_model(h, LC_MODEL_CAS_REGISTER, budget, n_threads, out_keys, out, max_keys);
 }

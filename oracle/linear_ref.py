@@ -26,6 +26,10 @@ What is restated, from the published knossos 0.3.7 / jepsen 0.2.x sources
   knossos.model/cas-register  (etcdemo.clj:15,117)
       nil initial value; write v -> v; cas [a b] legal iff cur = a; read v
       legal iff v is nil or v = cur.
+  knossos.model/register, knossos.model/mutex  
+      register: the cas-register without cas.  mutex: unlocked initially;
+      :acquire legal iff unlocked (-> locked), :release legal iff locked
+      (-> unlocked).
   knossos.linear/analysis with :algorithm :linear  (etcdemo.clj:118)
       the just-in-time config-set search.  A config is (model state, set of
       pending ops already linearized).  :invoke adds the op to the pending
@@ -105,7 +109,11 @@ class HistoryError(Exception):
     """knossos.history/complete's assertion (or an op the model cannot step)."""
 
 
-def complete(history: Sequence[dict]) -> Tuple[List[Op], List[Tuple[str, int, int]]]:
+MODEL_FS = {"cas-register": ("read", "write", "cas"), "register": ("read", "write"),
+            "mutex": ("acquire", "release")}
+
+
+def complete(history: Sequence[dict], model: str = "cas-register") -> Tuple[List[Op], List[Tuple[str, int, int]]]:
     """knossos.history/complete + without-failures.
 
     Returns (ops, events) where events is the sub-history reduced to the
@@ -118,8 +126,8 @@ def complete(history: Sequence[dict]) -> Tuple[List[Op], List[Tuple[str, int, in
     for pos, op in enumerate(history):
         t, p = op.get("type"), op.get("process")
         if t == "invoke":
-            if op.get("f") not in ("read", "write", "cas"):
-                raise HistoryError(f"cas-register cannot step {op.get('f')!r}")
+            if op.get("f") not in MODEL_FS[model]:
+                raise HistoryError(f"{model} cannot step {op.get('f')!r}")
             ops.append(Op(len(ops), op["f"], op.get("value"), pos, None))
             outstanding[p] = len(ops) - 1   # assoc! overwrites an older one
         elif t in ("ok", "fail"):
@@ -172,6 +180,22 @@ def cas_register_step(state, f: str, value):
     raise HistoryError(f"cas-register cannot step {f!r}")
 
 
+def mutex_step(locked: bool, f: str, value=None):
+    """knossos.model/mutex's Mutex step (locked? = True / False)."""
+    if f == "acquire":
+        return INCONSISTENT if locked else True
+    if f == "release":
+        return False if locked else INCONSISTENT
+    raise HistoryError(f"mutex cannot step {f!r}")
+
+
+def model_step(model: str):
+    """(step fn, initial state) of a model."""
+    if model == "mutex":
+        return mutex_step, False
+    return cas_register_step, None
+
+
 def register_values(ops: Iterable[Op]) -> set:
     """Values a surviving write / cas can install (the key's state count - 1)."""
     vals = set()
@@ -205,9 +229,12 @@ class Analysis:
 
 
 def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
-             initial=None) -> Analysis:
-    """knossos.linear/analysis (cas-register) over one key's sub-history."""
-    ops, events = complete(history)
+             initial=None, model: str = "cas-register") -> Analysis:
+    """knossos.linear/analysis over one key's sub-history (default: cas-register)."""
+    ops, events = complete(history, model)
+    step, init = model_step(model)
+    if initial is None:
+        initial = init
     res = Analysis(valid=True, ops=ops, events=events)
     if len(register_values(ops)) + 1 > WIDE_MAX_STATES:
         res.valid, res.cause = "unknown", "states"
@@ -245,7 +272,7 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
                 for q in pending:
                     if q == p or q in L:
                         continue
-                    s2 = cas_register_step(st, ops[q].f, ops[q].value)
+                    s2 = step(st, ops[q].f, ops[q].value)
                     if s2 is INCONSISTENT:
                         continue
                     res.probes += 1
@@ -259,7 +286,7 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
                         nxt.append(c)
             frontier = nxt
         for (st, L) in I:
-            s2 = cas_register_step(st, ops[p].f, ops[p].value)
+            s2 = step(st, ops[p].f, ops[p].value)
             if s2 is INCONSISTENT:
                 continue
             res.probes += 1
@@ -284,9 +311,10 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
 
 def config_sort_key(c: Config):
     st, L = c
-    return (-1 if st is None else st, sorted(L))
+    return (-1 if st is None else int(st), sorted(L))
 
 
-def check_independent(history: Sequence[dict], budget: int = DEFAULT_BUDGET) -> Dict[Any, Analysis]:
-    """independent/checker over linearizable(cas-register): per-key analyses."""
-    return {k: analysis(subhistory(history, k), budget) for k in history_keys(history)}
+def check_independent(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
+                      model: str = "cas-register") -> Dict[Any, Analysis]:
+    """independent/checker over linearizable(model): per-key analyses."""
+    return {k: analysis(subhistory(history, k), budget, model=model) for k in history_keys(history)}

@@ -65,8 +65,8 @@ class H:
 def kats():
     out = []
 
-    def case(name, h, expect, note):
-        out.append({"name": name, "note": note, "history": h.ops, "expect": expect})
+    def case(name, h, expect, note, model="cas-register"):
+        out.append({"name": name, "note": note, "history": h.ops, "expect": expect, "model": model})
 
     # 1: the tutorial's stale read -- "can't read 1 from register 3"
     h = H(); h.seq(0, "write", 1, 1); prev = h.seq(1, "write", 3, 3); bad = h.seq(2, "read", None, 1)
@@ -139,6 +139,40 @@ def kats():
     bad = h.seq(1, "read", None, 1)
     case("crashed-cas-cannot-land", h, {"0": {"valid?": False, "op": bad, "previous-ok": prev}},
          "crashed cas nil->1 needs nil, so it cannot land after write 3 and is overwritten before it")
+    # --- other Knossos models: (model/mutex), (model/register)
+    # 21: acquire / release in turn
+    h = H(); h.seq(0, "acquire", None, None); h.seq(0, "release", None, None)
+    h.seq(1, "acquire", None, None); h.seq(1, "release", None, None)
+    case("mutex-in-turn", h, {"0": {"valid?": True}}, "", model="mutex")
+    # 22: a second acquire completes while the lock is held
+    h = H(); prev = h.seq(0, "acquire", None, None); bad = h.seq(1, "acquire", None, None)
+    case("mutex-double-acquire", h, {"0": {"valid?": False, "op": bad, "previous-ok": prev}}, "already held",
+         model="mutex")
+    # 23: two overlapping acquires both complete, nobody releases
+    h = H(); h.inv(0, "acquire"); h.inv(1, "acquire"); prev = h.ok(0, "acquire"); bad = h.ok(1, "acquire")
+    case("mutex-concurrent-acquires", h, {"0": {"valid?": False, "op": bad, "previous-ok": prev}},
+         "whichever goes first, the other finds the lock held", model="mutex")
+    # 24: release of a lock nobody holds
+    h = H(); h.seq(0, "acquire", None, None); prev = h.seq(0, "release", None, None)
+    bad = h.seq(1, "release", None, None)
+    case("mutex-release-unheld", h, {"0": {"valid?": False, "op": bad, "previous-ok": prev}}, "not held",
+         model="mutex")
+    # 25: a crashed release may have taken effect
+    h = H(); h.seq(0, "acquire", None, None); h.inv(0, "release"); h.info(0, "release")
+    h.seq(1, "acquire", None, None)
+    case("mutex-crashed-release", h, {"0": {"valid?": True}}, ":info release stays callable", model="mutex")
+    # 26: a failed acquire is dropped
+    h = H(); h.seq(0, "acquire", None, None); h.inv(1, "acquire"); h.fail(1, "acquire")
+    h.seq(0, "release", None, None)
+    case("mutex-failed-acquire-dropped", h, {"0": {"valid?": True}}, "", model="mutex")
+    # 27: the register model: the tutorial's stale read
+    h = H(); h.seq(0, "write", 1, 1); prev = h.seq(1, "write", 3, 3); bad = h.seq(2, "read", None, 1)
+    case("register-stale-read", h, {"0": {"valid?": False, "op": bad, "previous-ok": prev}}, "3 vs 1",
+         model="register")
+    # 28: the register model, concurrent write and read
+    h = H(); h.inv(0, "write", 1); h.inv(1, "read"); h.ok(1, "read", 1); h.ok(0, "write", 1)
+    h.seq(2, "read", None, None)
+    case("register-concurrent", h, {"0": {"valid?": True}}, "", model="register")
     return out
 
 
@@ -168,13 +202,13 @@ def main():
         keys = LR.history_keys(ops)
         for k in keys:
             sub = LR.subhistory(ops, k)
-            ok, fe = brute.brute_check(sub)
-            a = LR.analysis(sub)
+            ok, fe = brute.brute_check(sub, model=c["model"])
+            a = LR.analysis(sub, model=c["model"])
             exp = c["expect"][str(k)]
             assert ok == exp["valid?"], (c["name"], k, ok)
             assert a.valid == exp["valid?"], (c["name"], k, a.valid)
             if not ok:
-                _ops, events = LR.complete(sub)
+                _ops, events = LR.complete(sub, c["model"])
                 assert fe == a.fail_event, (c["name"], fe, a.fail_event)
                 assert sub[events[fe][2]]["index"] == exp["op"], (c["name"], sub[events[fe][2]]["index"], exp["op"])
                 assert sub[a.previous_ok_pos]["index"] == exp["previous-ok"], c["name"]

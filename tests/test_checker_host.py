@@ -76,6 +76,17 @@ def test_linearizable_options():
     assert ck.batched_linearizable(comp) is lin
 
 
+def test_other_model_messages():
+    m = model.mutex()
+    assert m.step("acquire").locked is True
+    assert m.step("release").msg == "not held"
+    assert m.step("acquire").step("acquire").msg == "already held"
+    r = model.register()
+    assert r.step("write", 3).step("read", 1).msg == "3≠1"
+    with pytest.raises(ValueError):
+        r.step("cas", [1, 2])
+
+
 def test_model_messages():
     r = model.cas_register()
     assert r.step("write", 3).value == 3
@@ -99,8 +110,10 @@ def test_result_maps_from_verdict_records(case):
     """Knossos-shaped maps (A8) from verdict records: :op / :previous-ok are
     the original op maps (their :index), :configs render the model value."""
     h = H.History.from_ops(case["history"])
-    pk = Packed(h)
-    keys, r = cref.check_history(h.as_c())
+    mdl = {"cas-register": model.cas_register(), "register": model.register(),
+           "mutex": model.mutex()}[case.get("model", "cas-register")]
+    pk = Packed(h, mdl)
+    keys, r = cref.check_history(h.as_c(), model=mdl.name)
     K = pk.n_keys
     res = KeyResults(r["valid"], r["fail_event"], r["cause"], r["peak"],
                      np.zeros((K, 10, 2), np.uint64), np.zeros(K, np.uint32), {})

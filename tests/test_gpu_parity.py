@@ -70,3 +70,28 @@ def test_window_overflow(device):
     _, res, _ = device_vs_oracle(H.History.from_ops(ops), device)
     assert list(res.valid) == [-1, 1]
     assert list(res.cause) == [3, 0]
+
+
+@pytest.mark.parametrize("mname", ["mutex", "register"])
+def test_other_models(device, mname):
+    """(model/mutex) and (model/register) on the same kernels (SURVEY.md 8(f)
+    F-4): bit-exact verdicts, failing events and peak set sizes."""
+    import cref
+    from histgen import mutex_history, random_history
+    from lincheck import model
+    from lincheck.checker import Packed
+    mdl = {"mutex": model.mutex(), "register": model.register()}[mname]
+    if mname == "mutex":
+        ops = mutex_history(3, n_keys=400, rounds=60, procs=8)
+    else:
+        ops = random_history(77, n_keys=200, max_ops=60, procs=10, model=mname, p_garbage_read=0.05,
+                             p_open=0.0, p_info=0.05)
+    h = H.History.from_ops(ops)
+    pk = Packed(h, mdl)
+    res = device.check(pk)
+    keys, orc = cref.check_history(h.as_c(), model=mname, threads=8)
+    assert list(keys) == pk.keys
+    np.testing.assert_array_equal(res.valid, orc["valid"])
+    np.testing.assert_array_equal(res.fail_event, orc["fail_event"])
+    np.testing.assert_array_equal(res.peak, orc["peak"])
+    assert (res.valid == 1).any() and (res.valid == 0).any()

@@ -34,19 +34,20 @@ def load_kats():
 @pytest.mark.parametrize("case", load_kats(), ids=lambda c: c["name"])
 def test_known_answers(case):
     ops = case["history"]
+    model = case.get("model", "cas-register")
     # Python restatement + brute force
     for k in LR.history_keys(ops):
         sub = LR.subhistory(ops, k)
         exp = case["expect"][str(k)]
-        a = LR.analysis(sub)
+        a = LR.analysis(sub, model=model)
         assert a.valid == exp["valid?"]
-        assert brute.brute_check(sub)[0] == exp["valid?"]
+        assert brute.brute_check(sub, model=model)[0] == exp["valid?"]
         if not exp["valid?"]:
             assert sub[a.fail_pos]["index"] == exp["op"]
             assert sub[a.previous_ok_pos]["index"] == exp["previous-ok"]
     # C restatement
     h = H.History.from_ops(ops)
-    keys, r = cref.check_history(h.as_c())
+    keys, r = cref.check_history(h.as_c(), model=model)
     for k, rr in zip(keys, r):
         exp = case["expect"][str(k)]
         assert bool(rr["valid"] == 1) == (exp["valid?"] is True)
@@ -111,3 +112,24 @@ def test_budget_semantics_exact():
     assert r["valid"][0] == 1
     keys, r = cref.check_history(H.History.from_ops(ops).as_c(), budget=b - 1)
     assert r["valid"][0] == -1
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.integers(0, 2**31 - 1), st.sampled_from(["mutex", "register"]))
+def test_other_models_restatement_matches_brute_force(seed, model):
+    """(model/mutex), (model/register): JIT restatement =
+    definition, and the C restatement agrees with the Python one."""
+    ops = random_history(seed, model=model)
+    for k in LR.history_keys(ops):
+        sub = LR.subhistory(ops, k)
+        a = LR.analysis(sub, model=model)
+        ok, fe = brute.brute_check(sub, model=model)
+        assert a.valid == ok
+        assert a.fail_event == fe
+    h = H.History.from_ops(ops)
+    keys, r = cref.check_history(h.as_c(), model=model)
+    for k, rr in zip(keys, r):
+        a = LR.analysis(LR.subhistory(ops, k), model=model)
+        assert rr["valid"] == {True: 1, False: 0, "unknown": -1}[a.valid]
+        assert rr["fail_event"] == (-1 if a.fail_event is None else a.fail_event)
+        assert rr["peak"] == a.peak_configs and rr["probes"] == a.probes

@@ -128,3 +128,24 @@ def test_double_invoke_leaves_first_pending_forever():
     pk = Packed(H.History.from_ops(ops))
     ev = pk.events(0)
     assert [(int(w) >> 31, (int(w) >> 24) & 0x7F) for w in ev] == [(0, 0), (0, 1), (1, 1)]
+
+
+def test_models_pack():
+    """(model/mutex) packs acquire / release as cas over {unlocked, locked};
+    (model/register) refuses a cas, as knossos's Register cannot step it."""
+    from lincheck import _native as N
+    from lincheck import model
+    from lincheck.checker import Packed
+    from lincheck.independent import Tuple
+    ops = [{"type": "invoke", "f": "acquire", "value": Tuple(0, None), "process": 0},
+           {"type": "ok", "f": "acquire", "value": Tuple(0, None), "process": 0},
+           {"type": "invoke", "f": "release", "value": Tuple(0, None), "process": 0},
+           {"type": "ok", "f": "release", "value": Tuple(0, None), "process": 0}]
+    pk = Packed(H.History.from_ops(ops), model.mutex())
+    trans = np.ctypeslib.as_array(pk.view.trans, shape=(int(pk.view.n_trans),))
+    assert sorted(int(t) for t in trans) == sorted([N.LC_T_CAS | (0 << 2) | (1 << 17), N.LC_T_CAS | (1 << 2) | (0 << 17)])
+    cas = [{"type": "invoke", "f": "cas", "value": Tuple(0, [1, 2]), "process": 0}]
+    with pytest.raises(N.LincheckError):
+        Packed(H.History.from_ops(cas), model.register())
+    with pytest.raises(N.LincheckError):
+        Packed(H.History.from_ops(ops), model.cas_register())
