@@ -39,7 +39,10 @@
 (def ^:private nil-long Long/MIN_VALUE)  ; LC_NIL / LC_NO_KEY / LC_NO_PROCESS
 
 (def ^:private type-code {:invoke 0 :ok 1 :fail 2 :info 3})
-(def ^:private f-code    {:read 0 :write 1 :cas 2})
+(def ^:private f-code    {:read 0 :write 1 :cas 2 :acquire 4 :release 5})
+
+;; LC_MODEL_*: which knossos.model the device checks against
+(def ^:private model-code {:cas-register 0 :register 1 :mutex 2})
 
 (defn- long-or-nil [x] (if (nil? x) nil-long (long x)))
 
@@ -60,7 +63,9 @@
       (let [value         (:value op)
             [k v]         (if (independent/tuple? value) [(key value) (val value)] [nil value])
             fc            (f-code (:f op) 3)
-            [a b]         (if (= fc 2) (if (nil? v) [nil nil] v) [v nil])]
+            [a b]         (cond (= fc 2) (if (nil? v) [nil nil] v)
+                                (<= 4 fc) [nil nil]      ; mutex ops carry no value
+                                :else     [v nil])]
         (.setByte type i (byte (type-code (:type op))))
         (.setByte fn i (byte fc))
         (.setLong proc (* 8 i) (if (integer? (:process op)) (long (:process op)) nil-long))
@@ -85,10 +90,12 @@
 
 (defn check-history
   "Runs the device search over every key; returns per-key verdict maps."
-  [history {:keys [device budget] :or {device 0 budget (bit-shift-left 1 20)}}]
+  [history {:keys [device budget model]
+            :or {device 0 budget (bit-shift-left 1 20) model :cas-register}}]
   (let [{:keys [hist]} (marshal history)
+        pack-opts      (doto (Memory. 4) (.setInt 0 (int (model-code model))))
         packed-ref     (PointerByReference.)
-        _              (call-int "lc_pack" hist nil packed-ref)
+        _              (call-int "lc_pack" hist pack-opts packed-ref)
         packed         (.getValue packed-ref)
         batch          (Memory. 72)
         _              (call-int "lc_packed_view" packed batch)
@@ -125,7 +132,9 @@
 
 (defn checker
   "independent/checker over compose{:linear linearizable(cas-register),
-  :timeline html}, with the :linear part batched on the GPU."
+  :timeline html}, with the :linear part batched on the GPU.  opts:
+  :device, :budget, and :model (:cas-register, the default and the demo's;
+  :register or :mutex for the other Knossos models, SURVEY.md 8(f) F-4)."
   ([] (checker {}))
   ([opts]
    (reify checker/Checker
