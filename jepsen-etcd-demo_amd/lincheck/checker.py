@@ -70,6 +70,14 @@ class Packed:
     def event_row(self, i: int, j: int) -> int:
         return int(N.check(N.lib().lc_packed_event_row(self.handle, i, j)))
 
+    def desc(self, i: int, t: int) -> int:
+        """Transition descriptor t of key i (LC_EV_TRANS + trans_off[i])."""
+        if not hasattr(self, "_trans"):
+            self._trans = N.carray(self.view.trans, max(int(self.view.n_trans), 1), np.uint32)
+            self._trans_off = N.carray(self.view.trans_off, self.n_keys, np.uint32)
+        base = int(self._trans_off[i]) if len(self._trans_off) else 0
+        return int(self._trans[base + t])
+
     def state_value(self, i: int, s: int):
         v = C.c_int64(); nil = C.c_int()
         N.check(N.lib().lc_packed_state_value(self.handle, i, s, C.byref(v), C.byref(nil)))
@@ -190,48 +198,170 @@ def merge_valid(vals: Sequence[Any]) -> Any:
     return True
 
 
+def desc_step(d: int, st: int) -> Optional[int]:
+    """One interned transition (include/lincheck.h LC_DESC) from state id st:
+    the next state id, or None when the model step is inconsistent."""
+    t, a, b = d & 3, (d >> 2) & 0x7FFF, d >> 17
+    if t == N.LC_T_READ_ANY:
+        return st
+    if t == N.LC_T_READ:
+        return st if st == a else None
+    if t == N.LC_T_WRITE:
+        return b
+    return b if st == a else None
+
+
+def _sub_op(packed: Packed, row: int) -> Dict:
+    """Row as it appears in the key's sub-history (independent/subhistory
+    unwraps the tuple value)."""
+    op = packed.hist.op(row)
+    v = op.get("value")
+    if getattr(v, "_lc_tuple", False):
+        op["value"] = v[1]
+    return op
+
+
+class _KeyView:
+    """Key i's event stream around the failing (or last) event, for result
+    shaping: which invoke holds each window slot, its completed op map and
+    its transition descriptor."""
+
+    def __init__(self, packed: Packed, i: int, upto: int):
+        self.packed, self.i = packed, i
+        self.ev = packed.events(i)
+        self.slot_ev: Dict[int, int] = {}     # slot -> invoke event ordinal
+        self.last_ok: Optional[int] = None
+        for j in range(upto):
+            w = int(self.ev[j]); s = (w >> 24) & 0x7F
+            if w & N.LC_EV_OK_BIT:
+                self.slot_ev.pop(s, None)
+                self.last_ok = j
+            else:
+                self.slot_ev[s] = j
+        self._ops: Dict[int, Dict] = {}
+
+    def op(self, j: int) -> Dict:
+        """Event j's op map; an invocation carries its completion's value
+        when it has none (knossos.history/complete)."""
+        if j not in self._ops:
+            op = _sub_op(self.packed, self.packed.event_row(self.i, j))
+            w = int(self.ev[j])
+            if not (w & N.LC_EV_OK_BIT) and op.get("value") is None:
+                s = (w >> 24) & 0x7F
+                for k in range(j + 1, len(self.ev)):
+                    wk = int(self.ev[k])
+                    if (wk >> 24) & 0x7F == s:   # the slot's next event is its :ok
+                        if wk & N.LC_EV_OK_BIT:
+                            op["value"] = _sub_op(self.packed, self.packed.event_row(self.i, k)).get("value")
+                        break
+            self._ops[j] = op
+        return self._ops[j]
+
+    def desc(self, j: int) -> int:
+        return self.packed.desc(self.i, int(self.ev[j]) & 0x00FFFFFF)
+
+
+def _final_paths(kv: _KeyView, fe: int, finals: List, prev_op, limit: int = TRUNCATE,
+                 max_visits: int = 1 << 16) -> List[List[Dict]]:
+    """knossos.linear's :final-paths for an invalid key.
+
+    From each final config (model state, linearized pending ops), every
+    sequence of further pending ops that the model allows, followed by the
+    failing op, whose step is inconsistent in every state so reached (that is
+    what made the config set empty).  A path is [{"op": previous-ok, "model":
+    config state}, {"op": op, "model": state after it} ..., {"op": failing op,
+    "model": {"msg": "can't ..."}}].  Paths are generated depth-first, shortest
+    first, from the configs in device order; at most `limit` distinct ones are
+    kept (jepsen.checker/linearizable truncates to 10).  Knossos iterates a
+    hash set here, so only the SET of paths is comparable (SURVEY.md 8(a) A8);
+    its exact element shape is unpinned (knossos is absent)."""
+    packed, i = kv.packed, kv.i
+    fw = int(kv.ev[fe])
+    p_slot = (fw >> 24) & 0x7F
+    p_desc = kv.desc(kv.slot_ev[p_slot])
+    fail_op = _sub_op(packed, packed.event_row(i, fe))
+    others = [(s, kv.slot_ev[s], kv.desc(kv.slot_ev[s])) for s in sorted(kv.slot_ev) if s != p_slot]
+    out: List[List[Dict]] = []
+    seen = set()
+    visits = 0
+    state_cache: Dict[int, Any] = {}
+
+    def model_of(st):
+        if st not in state_cache:
+            state_cache[st] = packed.model.of_state(packed.state_value(i, st))
+        return state_cache[st]
+
+    def emit(st0, steps, st):
+        key = (st0, tuple(steps))
+        if key in seen:
+            return
+        seen.add(key)
+        f, v = fail_op["f"], fail_op.get("value")
+        bad = model_of(st).step(f, v)
+        msg = getattr(bad, "msg", None) or f"can't {f} {fmt(v)}"
+        path = [{"op": prev_op, "model": model_of(st0).render()}]
+        path += [{"op": kv.op(j), "model": model_of(s2).render()} for j, s2 in steps]
+        path.append({"op": fail_op, "model": {"msg": msg}})
+        out.append(path)
+
+    def dfs(st0, st, used, steps):
+        nonlocal visits
+        visits += 1
+        if len(out) >= limit or visits > max_visits:
+            return
+        if desc_step(p_desc, st) is None:
+            emit(st0, steps, st)
+        for s, j, d in others:
+            if (used >> s) & 1:
+                continue
+            st2 = desc_step(d, st)
+            if st2 is not None:
+                steps.append((j, st2))
+                dfs(st0, st2, used | (1 << s), steps)
+                steps.pop()
+                if len(out) >= limit or visits > max_visits:
+                    return
+
+    for st, mask in finals:
+        if len(out) >= limit:
+            break
+        dfs(st, st, mask, [])
+    return out
+
+
 def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.ndarray]) -> Dict:
-    """Knossos-shaped result for key i (SURVEY.md 8(a) A8)."""
-    hist = packed.hist
+    """Knossos-shaped result for key i (SURVEY.md 8(a) A8, 8(f) F-2)."""
     v = int(res.valid[i])
     cause = N.CAUSES.get(int(res.cause[i]), "error")
-    ev = packed.events(i)
     fe = int(res.fail_event[i])
-    upto = fe if fe >= 0 else len(ev)
-    # which op holds each window slot just before event `upto`
-    slot_op: Dict[int, int] = {}
-    last_ok = None
-    for j in range(upto):
-        w = int(ev[j]); s = (w >> 24) & 0x7F
-        if w & N.LC_EV_OK_BIT:
-            slot_op.pop(s, None)
-            last_ok = j
-        else:
-            slot_op[s] = j
-    configs = []
+    upto = fe if fe >= 0 else packed.n_events(i)
+    kv = _KeyView(packed, i, upto)
+    prev = _sub_op(packed, packed.event_row(i, kv.last_ok)) if kv.last_ok is not None else None
+    finals = []
     for c in range(int(res.n_final[i])):
         lo, hi = int(res.final[i, c, 0]), int(res.final[i, c, 1])
-        st = (hi >> 48) & 0x7FFF
-        mask = lo | ((hi & ((1 << 48) - 1)) << 64)
-        pend = [hist.op(packed.event_row(i, slot_op[s])) for s in sorted(slot_op) if not (mask >> s) & 1]
-        lin = [hist.op(packed.event_row(i, slot_op[s])) for s in sorted(slot_op) if (mask >> s) & 1]
+        finals.append(((hi >> 48) & 0x7FFF, lo | ((hi & ((1 << 48) - 1)) << 64)))
+    configs = []
+    for st, mask in finals[:TRUNCATE]:
+        slots = sorted(kv.slot_ev)
         configs.append({"model": packed.model.of_state(packed.state_value(i, st)).render(),
-                        "pending": pend, "linearized": lin})
-    out: Dict[str, Any] = {"analyzer": "linear", "configs": configs[:TRUNCATE], "final-paths": []}
+                        "last-op": prev,
+                        "pending": [kv.op(kv.slot_ev[s]) for s in slots if not (mask >> s) & 1],
+                        "linearized": [kv.op(kv.slot_ev[s]) for s in slots if (mask >> s) & 1]})
+    out: Dict[str, Any] = {"analyzer": "linear", "configs": configs, "final-paths": []}
     if v == N.LC_VALID:
         out["valid?"] = True
     elif v == N.LC_INVALID:
         out["valid?"] = False
-        op = hist.op(packed.event_row(i, fe))
-        out["op"] = op
-        prev = hist.op(packed.event_row(i, last_ok)) if last_ok is not None else None
+        out["op"] = _sub_op(packed, packed.event_row(i, fe))
         out["previous-ok"] = prev
         out["last-op"] = prev
+        out["final-paths"] = _final_paths(kv, fe, finals, prev)
     else:
         out["valid?"] = "unknown"
         out["cause"] = cause
         if fe >= 0:
-            out["op"] = hist.op(packed.event_row(i, fe))
+            out["op"] = _sub_op(packed, packed.event_row(i, fe))
     return out
 
 

@@ -222,6 +222,7 @@ class Analysis:
     fail_pos: Optional[int] = None  # position in the sub-history
     previous_ok_pos: Optional[int] = None
     final_configs: List[Config] = field(default_factory=list)
+    final_slots: Dict[int, int] = field(default_factory=dict)  # op id -> window slot at failure
     peak_configs: int = 1
     probes: int = 0
     ops: List[Op] = field(default_factory=list)
@@ -296,6 +297,7 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
             res.op_id, res.fail_event, res.fail_pos = p, ei, pos
             res.previous_ok_pos = last_ok_pos
             res.final_configs = sorted(S, key=config_sort_key)
+            res.final_slots = dict(slot_of)
             return res
         if len(S_next) > budget:
             res.valid, res.cause = "unknown", "budget"
@@ -307,6 +309,43 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
         free_slots.append(slot_of.pop(p))
         last_ok_pos = pos
     return res
+
+
+def final_paths(res: Analysis, sub: Sequence[dict], model: str = "cas-register",
+                cap: int = 1 << 16) -> set:
+    """Every final path of an invalid analysis, as a set
+    of tuples ((index, state), ..., (index, "inconsistent")): from each final
+    config, each sequence of further pending ops (other than the failing op p)
+    that the model allows, then p, which is inconsistent in every state so
+    reached.  The first element is (previous-ok's :index or None, config
+    state); ops are named by their invocation's :index, p by its :ok's.
+    None when there are more than `cap` paths (the set is then not known)."""
+    assert res.valid is False
+    step, _ = model_step(model)
+    ops = res.ops
+    p = res.op_id
+    idx = lambda pos: sub[pos].get("index", pos)
+    prev = idx(res.previous_ok_pos) if res.previous_ok_pos is not None else None
+    pend = sorted((q for q in res.final_slots if q != p), key=lambda q: res.final_slots[q])
+    out = set()
+
+    def dfs(st0, st, L, steps):
+        if len(out) >= cap:
+            return
+        if step(st, ops[p].f, ops[p].value) is INCONSISTENT:
+            out.add(((prev, st0),) + tuple(steps) + ((idx(res.fail_pos), "inconsistent"),))
+        for q in pend:
+            if q in L:
+                continue
+            s2 = step(st, ops[q].f, ops[q].value)
+            if s2 is not INCONSISTENT:
+                steps.append((idx(ops[q].invoke_pos), s2))
+                dfs(st0, s2, L | {q}, steps)
+                steps.pop()
+
+    for st, L in res.final_configs:
+        dfs(st, st, L, [])
+    return None if len(out) >= cap else out
 
 
 def config_sort_key(c: Config):

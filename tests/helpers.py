@@ -24,3 +24,56 @@ def device_vs_oracle(hist: H.History, dev: Device, budget=None, check_peak=True)
     if done.all() and dev.count_probes:
         assert res.stats["probes"] == int(orc["probes"].sum())
     return packed, res, orc
+
+
+# ---- counterexample shaping -----------------------------
+def state_ids(packed: Packed, i: int) -> dict:
+    """Model-state value -> packed state id for key i (ids may come from a
+    table shared by every key, so walk it to its end)."""
+    out = {}
+    for s in range(1 << 16):
+        try:
+            out[packed.state_value(i, s)] = s
+        except Exception:
+            break
+    return out
+
+
+def oracle_state_value(st, model: str):
+    """The restatement's state as the value lc_pack interns (mutex: locked -> 1)."""
+    if model == "mutex":
+        return 1 if st else None
+    return st
+
+
+def encode_finals(packed: Packed, i: int, a, model: str, limit: int = 10):
+    """The restatement's final configs in the device's record layout
+    (lo = slots 0..63, hi = slots 64..111 | state << 48)."""
+    ids = state_ids(packed, i)
+    out = np.zeros((limit, 2), np.uint64)
+    n = 0
+    for st, L in a.final_configs[:limit]:
+        mask = 0
+        for q in L:
+            mask |= 1 << a.final_slots[q]
+        out[n, 0] = mask & ((1 << 64) - 1)
+        out[n, 1] = (mask >> 64) | (ids[oracle_state_value(st, model)] << 48)
+        n += 1
+    return out, n
+
+
+def path_tuple(path, model: str):
+    """A rendered :final-paths entry as the restatement's tuple form."""
+    def state(m):
+        if "msg" in m:
+            return "inconsistent"
+        v = m["locked?"] if model == "mutex" else m["value"]
+        return v
+    return tuple(((e["op"]["index"] if e["op"] is not None else None), state(e["model"])) for e in path)
+
+
+def config_tuple(cfg, model: str):
+    """A rendered :configs entry as (state, frozenset of linearized :index)."""
+    m = cfg["model"]
+    v = m["locked?"] if model == "mutex" else m["value"]
+    return (v, frozenset(o["index"] for o in cfg["linearized"]))

@@ -126,3 +126,73 @@ def test_result_maps_from_verdict_records(case):
             assert m["op"]["index"] == exp["op"]
             assert m["op"]["type"] == "ok"
             assert m["previous-ok"]["index"] == exp["previous-ok"]
+
+
+def _final_paths_case(ops, model_name):
+    """Render :configs / :final-paths from the restatement's final configs and
+    compare them with the restatement's own enumeration."""
+    import linear_ref as LR
+    from helpers import config_tuple, encode_finals, path_tuple
+    mdl = {"cas-register": model.cas_register(), "register": model.register(),
+           "mutex": model.mutex()}[model_name]
+    h = H.History.from_ops(ops)
+    pk = Packed(h, mdl)
+    checked = 0
+    for i, k in enumerate(pk.keys):
+        sub = LR.subhistory(ops, k)
+        a = LR.analysis(sub, model=model_name)
+        if a.valid is not False:
+            continue
+        fin, n = encode_finals(pk, i, a, model_name)
+        K = pk.n_keys
+        final = np.zeros((K, 10, 2), np.uint64); final[i] = fin
+        nf = np.zeros(K, np.uint32); nf[i] = n
+        valid = np.ones(K, np.int8); valid[i] = 0
+        fev = np.full(K, -1, np.int32); fev[i] = a.fail_event
+        res = KeyResults(valid, fev, np.zeros(K, np.uint8), np.zeros(K, np.uint32), final, nf, {})
+        m = _render_key(pk, i, res, None)
+        exp_paths = LR.final_paths(a, sub, model_name)
+        got = [path_tuple(p, model_name) for p in m["final-paths"]]
+        assert len(set(got)) == len(got)
+        assert set(got) <= exp_paths
+        if len(exp_paths) <= 10 and len(a.final_configs) <= 10:
+            assert set(got) == exp_paths
+        else:
+            assert len(got) == 10
+        # every path replays under the host model: legal steps, then the failure
+        for p in m["final-paths"]:
+            st = mdl.of_state(None)
+            st = type(mdl)(**{f: v for f, v in zip(p[0]["model"].keys(), p[0]["model"].values())}) \
+                if model_name != "mutex" else model.Mutex(p[0]["model"]["locked?"])
+            for e in p[1:-1]:
+                st = st.step(e["op"]["f"], e["op"]["value"])
+                assert not isinstance(st, model.Inconsistent)
+                assert st.render() == e["model"]
+            bad = st.step(p[-1]["op"]["f"], p[-1]["op"]["value"])
+            assert isinstance(bad, model.Inconsistent) and bad.msg == p[-1]["model"]["msg"]
+        cfgs = {config_tuple(c, model_name) for c in m["configs"]}
+        exp_cfgs = {(oracle_v(st, model_name), frozenset(sub[a.ops[q].invoke_pos]["index"] for q in L))
+                    for st, L in a.final_configs[:10]}
+        assert cfgs == exp_cfgs
+        checked += 1
+    return checked
+
+
+def oracle_v(st, model_name):
+    return bool(st) if model_name == "mutex" else st
+
+
+@pytest.mark.parametrize("case", kats(), ids=lambda c: c["name"])
+def test_final_paths_known_answers(case):
+    """:final-paths / :configs on the known answers."""
+    _final_paths_case(case["history"], case.get("model", "cas-register"))
+
+
+@pytest.mark.parametrize("model_name", ["cas-register", "register", "mutex"])
+def test_final_paths_random(model_name):
+    from histgen import random_history
+    checked = 0
+    for seed in range(400):
+        ops = random_history(seed, n_keys=2, max_ops=8, procs=4, model=model_name)
+        checked += _final_paths_case(ops, model_name)
+    assert checked > 20

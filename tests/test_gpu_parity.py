@@ -95,3 +95,52 @@ def test_other_models(device, mname):
     np.testing.assert_array_equal(res.fail_event, orc["fail_event"])
     np.testing.assert_array_equal(res.peak, orc["peak"])
     assert (res.valid == 1).any() and (res.valid == 0).any()
+
+
+@pytest.mark.parametrize("shape", ["lattice", "wide_window", "mutex"])
+def test_counterexamples(device, shape):
+    """:configs and :final-paths of invalid keys from the
+    device's final config records, against the restatement's final config set
+    and its full path enumeration: the device's (first <= 10) configs and the
+    paths built from them are subsets, and equal when the restatement has no
+    more than 10 of each."""
+    import linear_ref as LR
+    from helpers import config_tuple, path_tuple
+    from histgen import mutex_history
+    from lincheck import model
+    from lincheck.checker import Packed, _render_key
+    mname = "mutex" if shape == "mutex" else "cas-register"
+    if shape == "lattice":      # <= 10 pending: the register-lattice tier
+        h = H.synth(n_keys=300, ops_per_key=80, concurrency=6, anomaly_rate=0.3, seed=31)
+    elif shape == "wide_window":  # 12-16 pending: the LDS / HBM set tiers
+        h = H.synth(n_keys=150, ops_per_key=120, concurrency=14, anomaly_rate=0.3, seed=32)
+    else:
+        h = H.History.from_ops(mutex_history(5, n_keys=200, rounds=30, procs=6, corrupt=0.3))
+    mdl = model.mutex() if mname == "mutex" else model.cas_register()
+    ops = h.to_ops()
+    pk = Packed(h, mdl)
+    res = device.check(pk)
+    n_bad = 0
+    for i, k in enumerate(pk.keys):
+        if res.valid[i] != 0:
+            continue
+        sub = LR.subhistory(ops, k)
+        a = LR.analysis(sub, model=mname)
+        assert a.valid is False and a.fail_event == res.fail_event[i]
+        m = _render_key(pk, i, res, None)
+        exp_cfgs = {(bool(st) if mname == "mutex" else st,
+                     frozenset(sub[a.ops[q].invoke_pos]["index"] for q in L)) for st, L in a.final_configs}
+        got_cfgs = [config_tuple(c, mname) for c in m["configs"]]
+        assert len(set(got_cfgs)) == len(got_cfgs) == min(10, len(exp_cfgs)), f"key {k}"
+        assert set(got_cfgs) <= exp_cfgs, f"key {k}"
+        exp_paths = LR.final_paths(a, sub, mname)
+        got_paths = {path_tuple(p, mname) for p in m["final-paths"]}
+        assert len(got_paths) == len(m["final-paths"]) > 0
+        if exp_paths is None:   # too many to enumerate: 10 distinct paths
+            assert len(got_paths) == 10
+            continue
+        assert got_paths <= exp_paths, f"key {k}"
+        if len(exp_cfgs) <= 10 and len(exp_paths) <= 10:
+            assert got_paths == exp_paths, f"key {k}"
+        n_bad += 1
+    assert n_bad > 5
