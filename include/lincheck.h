@@ -185,11 +185,16 @@ int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows);
 int lc_packed_state_value(const lc_packed *p, int64_t i, uint32_t s, int64_t *value, int *is_nil);
 
 /* ---- device checking (rows A6-A9) ------------------------------------------ */
-#define LC_ALGO_LINEAR 0   /* :algorithm :linear (etcdemo.clj:118) */
+#define LC_ALGO_LINEAR      0  /* :algorithm :linear (etcdemo.clj:118)              */
+#define LC_ALGO_WGL         1  /* :algorithm :wgl              */
+#define LC_ALGO_COMPETITION 2  /* jepsen.checker/linearizable's default             */
+/* The three run the same device search: :valid? and the first :ok that cannot
+ * be linearized are properties of the history, not of the algorithm.  Only
+ * the host-side result shaping (:analyzer) differs. */
 
 typedef struct lc_opts {
     int32_t  device;        /* HIP device ordinal                               */
-    int32_t  algorithm;     /* LC_ALGO_LINEAR                                   */
+    int32_t  algorithm;     /* LC_ALGO_*                                        */
     uint64_t max_configs;   /* search budget B (0 = default 1<<20): a key whose
                                config set or JIT closure exceeds B configs is
                                :unknown (LC_CAUSE_BUDGET); replaces

@@ -78,11 +78,16 @@
       (.setPointer hist off m))
     {:hist hist :keep [type fn proc key v0 v1 index]}))
 
-(defn- lc-create [device budget]
+;; LC_ALGO_*: jepsen.checker/linearizable's :algorithm (:linear, :wgl, else
+;; competition).  All three run the same device search; only :analyzer differs.
+(defn- algo-code [algorithm] (case algorithm :linear 0 :wgl 1 2))
+
+(defn- lc-create [device budget algorithm]
   (let [opts (Memory. 56)
         out  (PointerByReference.)]
     (.clear opts)
     (.setInt opts 0 (int device))
+    (.setInt opts 4 (int (algo-code algorithm)))
     (.setLong opts 8 (long budget))
     (.setInt opts 16 (int 10))          ; max_final: jepsen truncates to 10
     (call-int "lc_create" opts out)
@@ -90,8 +95,9 @@
 
 (defn check-history
   "Runs the device search over every key; returns per-key verdict maps."
-  [history {:keys [device budget model]
-            :or {device 0 budget (bit-shift-left 1 20) model :cas-register}}]
+  [history {:keys [device budget model algorithm]
+            :or {device 0 budget (bit-shift-left 1 20) model :cas-register
+                 algorithm :linear}}]
   (let [{:keys [hist]} (marshal history)
         pack-opts      (doto (Memory. 4) (.setInt 0 (int (model-code model))))
         packed-ref     (PointerByReference.)
@@ -100,7 +106,7 @@
         batch          (Memory. 72)
         _              (call-int "lc_packed_view" packed batch)
         n-keys         (.getLong batch 0)
-        ctx            (lc-create device budget)
+        ctx            (lc-create device budget algorithm)
         valid          (Memory. (max 1 n-keys))
         fail-ev        (Memory. (* 4 (max 1 n-keys)))
         cause          (Memory. (max 1 n-keys))
@@ -120,7 +126,7 @@
                          (history (.invokeLong (f "lc_packed_event_row")
                                                (object-array [packed (long i) (long fe)]))))]
                 [k (cond-> {:valid?   (case v 1 true 0 false :unknown)
-                            :analyzer :linear
+                            :analyzer (if (= algorithm :wgl) :wgl :linear)
                             :configs  []
                             :final-paths []}
                      (zero? v) (assoc :op op)
@@ -133,8 +139,9 @@
 (defn checker
   "independent/checker over compose{:linear linearizable(cas-register),
   :timeline html}, with the :linear part batched on the GPU.  opts:
-  :device, :budget, and :model (:cas-register, the default and the demo's;
-  :register or :mutex for the other Knossos models, SURVEY.md 8(f) F-4)."
+  :device, :budget, :model (:cas-register, the default and the demo's;
+  :register or :mutex for the other Knossos models, SURVEY.md 8(f) F-4) and
+  :algorithm (:linear, the demo's; :wgl; anything else = competition)."
   ([] (checker {}))
   ([opts]
    (reify checker/Checker

@@ -178,7 +178,8 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
     if (!out) return lc::fail(LC_E_INVALID, "lc_create: null out");
     lc_opts o{};
     if (opts) o = *opts;
-    if (o.algorithm != LC_ALGO_LINEAR) return lc::fail(LC_E_INVALID, "lc_create: only :algorithm :linear is supported");
+    if (o.algorithm < LC_ALGO_LINEAR || o.algorithm > LC_ALGO_COMPETITION)
+        return lc::fail(LC_E_INVALID, "lc_create: algorithm must be LC_ALGO_LINEAR, _WGL or _COMPETITION");
     if (o.max_configs == 0) o.max_configs = 1ull << 20;
     if (o.max_configs > (1ull << 31)) return lc::fail(LC_E_INVALID, "lc_create: max_configs above 2^31");
     if (o.max_final <= 0) o.max_final = 10;

@@ -22,6 +22,7 @@ LC_OPT_COUNT_PROBES = 0x1
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
 LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE = 0, 1, 2, 3, 4, 5
 LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX = 0, 1, 2
+LC_ALGO_LINEAR, LC_ALGO_WGL, LC_ALGO_COMPETITION = 0, 1, 2
 LC_NIL = -(1 << 63)
 LC_NO_KEY = LC_NIL
 LC_NO_PROCESS = LC_NIL

@@ -100,9 +100,9 @@ class Device:
     """An lc_ctx on one GPU (lc_create)."""
 
     def __init__(self, device: int = 0, budget: int = DEFAULT_BUDGET, max_final: int = TRUNCATE,
-                 debug_mode: int = 0, count_probes: bool = False):
+                 debug_mode: int = 0, count_probes: bool = False, algorithm: int = N.LC_ALGO_LINEAR):
         o = N.LcOpts()
-        o.device, o.algorithm, o.max_configs, o.max_final = device, 0, budget, max_final
+        o.device, o.algorithm, o.max_configs, o.max_final = device, algorithm, budget, max_final
         o.flags = N.LC_OPT_COUNT_PROBES if count_probes else 0
         o.debug_mode = debug_mode  # ablation builds only; 0 = the real search
         h = C.c_void_p()
@@ -179,11 +179,11 @@ _devices: Dict[tuple, Device] = {}
 _devices_lock = threading.Lock()
 
 
-def device_for(device: int = 0, budget: int = DEFAULT_BUDGET) -> Device:
+def device_for(device: int = 0, budget: int = DEFAULT_BUDGET, algorithm: int = N.LC_ALGO_LINEAR) -> Device:
     with _devices_lock:
-        key = (device, budget)
+        key = (device, budget, algorithm)
         if key not in _devices:
-            _devices[key] = Device(device, budget)
+            _devices[key] = Device(device, budget, algorithm=algorithm)
         return _devices[key]
 
 
@@ -229,15 +229,16 @@ class _KeyView:
     def __init__(self, packed: Packed, i: int, upto: int):
         self.packed, self.i = packed, i
         self.ev = packed.events(i)
-        self.slot_ev: Dict[int, int] = {}     # slot -> invoke event ordinal
-        self.last_ok: Optional[int] = None
-        for j in range(upto):
-            w = int(self.ev[j]); s = (w >> 24) & 0x7F
-            if w & N.LC_EV_OK_BIT:
-                self.slot_ev.pop(s, None)
-                self.last_ok = j
-            else:
-                self.slot_ev[s] = j
+        e = self.ev[:upto]
+        slots = (e >> 24) & 0x7F
+        # each slot's last event before `upto`: an invoke means the slot is held
+        rev_slots = slots[::-1]
+        u, first_rev = np.unique(rev_slots, return_index=True)
+        last = upto - 1 - first_rev
+        held = (e[last] & N.LC_EV_OK_BIT) == 0
+        self.slot_ev: Dict[int, int] = {int(s): int(j) for s, j in zip(u[held], last[held])}
+        oks = np.flatnonzero(e & N.LC_EV_OK_BIT)
+        self.last_ok: Optional[int] = int(oks[-1]) if len(oks) else None
         self._ops: Dict[int, Dict] = {}
 
     def op(self, j: int) -> Dict:
@@ -329,8 +330,9 @@ def _final_paths(kv: _KeyView, fe: int, finals: List, prev_op, limit: int = TRUN
     return out
 
 
-def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.ndarray]) -> Dict:
-    """Knossos-shaped result for key i (SURVEY.md 8(a) A8, 8(f) F-2)."""
+def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.ndarray],
+                analyzer: str = "linear") -> Dict:
+    """Knossos-shaped result for key i (SURVEY.md 8(a) A8, 8(f) F-2/F-3)."""
     v = int(res.valid[i])
     cause = N.CAUSES.get(int(res.cause[i]), "error")
     fe = int(res.fail_event[i])
@@ -348,7 +350,7 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
                         "last-op": prev,
                         "pending": [kv.op(kv.slot_ev[s]) for s in slots if not (mask >> s) & 1],
                         "linearized": [kv.op(kv.slot_ev[s]) for s in slots if (mask >> s) & 1]})
-    out: Dict[str, Any] = {"analyzer": "linear", "configs": configs, "final-paths": []}
+    out: Dict[str, Any] = {"analyzer": analyzer, "configs": configs, "final-paths": []}
     if v == N.LC_VALID:
         out["valid?"] = True
     elif v == N.LC_INVALID:
@@ -375,24 +377,27 @@ class Linearizable:
             raise ValueError("The linearizable checker requires a model.")
         if not isinstance(model, MODELS):
             raise NotImplementedError("supported models: (model/cas-register), (model/register), (model/mutex)")
-        algo = opts.get("algorithm", "linear")
-        if algo not in ("linear", ":linear"):
-            raise NotImplementedError(f"algorithm {algo!r}: only :linear is implemented")
+        # jepsen.checker/linearizable: :linear, :wgl, anything else -> competition
+        algo = str(opts.get("algorithm", "competition")).lstrip(":")
+        self.algorithm = {"linear": N.LC_ALGO_LINEAR, "wgl": N.LC_ALGO_WGL}.get(algo, N.LC_ALGO_COMPETITION)
+        # knossos.competition returns whichever analysis finishes first; here
+        # the device's :linear search always answers
+        self.analyzer = "wgl" if self.algorithm == N.LC_ALGO_WGL else "linear"
         self.model = model
         self.budget = int(opts.get("max-configs", DEFAULT_BUDGET))
         self.device = int(opts.get("device", 0))
 
     def _dev(self) -> Device:
-        return device_for(self.device, self.budget)
+        return device_for(self.device, self.budget, self.algorithm)
 
     def check(self, test: Dict, history, opts: Dict | None = None) -> Dict:
         """One key's (unwrapped) sub-history, as at etcdemo.clj:117."""
         hist = history if isinstance(history, History) else History.from_ops(history, default_key=0)
         packed = Packed(hist, self.model)
         if packed.n_keys == 0:
-            return {"valid?": True, "configs": [], "final-paths": [], "analyzer": "linear"}
+            return {"valid?": True, "configs": [], "final-paths": [], "analyzer": self.analyzer}
         res = self._dev().check(packed)
-        return _render_key(packed, 0, res, None)
+        return _render_key(packed, 0, res, None, self.analyzer)
 
     # batched form, used by independent.checker
     def check_independent(self, test, history, opts, inner) -> Dict:
@@ -403,7 +408,7 @@ class Linearizable:
         results = {}
         ops_cache = None
         for i, k in enumerate(packed.keys):
-            lin = _render_key(packed, i, res, None)
+            lin = _render_key(packed, i, res, None, self.analyzer)
             if inner is self:
                 results[k] = lin
                 continue

@@ -52,3 +52,17 @@ def test_bad_options_rejected():
     h = C.c_void_p()
     assert N.lib().lc_create(C.byref(o), C.byref(h)) == -1
     assert b"algorithm" in N.lib().lc_last_error()
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+def test_wgl_and_competition_accepted(algo):
+    """LC_ALGO_WGL / _COMPETITION pass option validation (F-3); without a GPU
+    the call then fails on the device, not on the option."""
+    o = N.LcOpts()
+    o.algorithm = algo
+    h = C.c_void_p()
+    rc = N.lib().lc_create(C.byref(o), C.byref(h))
+    if rc == 0:
+        N.lib().lc_destroy(h)
+    else:
+        assert b"algorithm" not in N.lib().lc_last_error()

@@ -68,8 +68,10 @@ def test_independent_checker_generic_inner():
 def test_linearizable_options():
     with pytest.raises(ValueError):
         ck.linearizable({})
-    with pytest.raises(NotImplementedError):
-        ck.linearizable({"model": model.cas_register(), "algorithm": "wgl"})
+    # F-3: :wgl and the default (competition) run the same device search
+    assert ck.linearizable({"model": model.cas_register(), "algorithm": "wgl"}).analyzer == "wgl"
+    comp = ck.linearizable({"model": model.cas_register()})
+    assert comp.algorithm == 2 and comp.analyzer == "linear"
     lin = ck.linearizable({"model": model.cas_register(), "algorithm": "linear"})
     assert ck.batched_linearizable(lin) is lin
     comp = ck.compose({"linear": lin, "timeline": ck.unbridled_optimism()})
