@@ -247,6 +247,14 @@ __device__ __forceinline__ uint32_t event_probes(const uint32_t *I, uint32_t p, 
     return pr;
 }
 
+#ifdef LC_T0_COUNT_SWEEPS
+// Diagnostic build only: histogram of (closure width nc, sweeps run).
+__device__ unsigned long long lc_sweep_hist[8 * 8];
+extern "C" int lc_debug_sweep_hist(unsigned long long *host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(lc_sweep_hist), sizeof(lc_sweep_hist), 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 // One :ok(p) event while every live op index is < 6: the whole lattice is
 // one register and every subset bit is a lane bit.  Op indices are assigned
 // lowest-free at invoke (not compacted), so an :ok only frees index p -- no
@@ -262,15 +270,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
                                        uint64_t budget, bool count, uint32_t &probes, uint32_t &nSn_out,
                                        bool want_size) {
     const uint32_t cand = live & ~(1u << p);
-#ifdef LC_GUP_SELECT
-    // branch-free: every gather evaluated, the one for p selected
-    const uint32_t g0 = gup<0>(W), g1 = gup<1>(W), g2 = gup<2>(W), g3 = gup<3>(W), g4 = gup<4>(W), g5 = gup<5>(W);
-    uint32_t wup = g0;
-    wup = p == 1 ? g1 : wup; wup = p == 2 ? g2 : wup; wup = p == 3 ? g3 : wup;
-    wup = p == 4 ? g4 : wup; wup = p == 5 ? g5 : wup;
-#else
     const uint32_t wup = (uint32_t)__shfl_xor((int)W, 1 << p);
-#endif
     LaneMasks m;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
@@ -291,13 +291,24 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 #else
     const uint32_t nc = (uint32_t)__popc(cand);  // a closure path has at most nc steps
 #endif
+#ifdef LC_T0_COUNT_SWEEPS
+    uint32_t done_s = nc;
+#endif
 #pragma unroll 1
     for (uint32_t s = 0; s < nc; ++s) {
         const uint32_t nv = sweep_lanes<0, 6>(I, m, one);
         const bool ch = nv != I;
         I = nv;
-        if (!__any(ch)) break;
+        if (!__any(ch)) {
+#ifdef LC_T0_COUNT_SWEEPS
+            done_s = s + 1;
+#endif
+            break;
+        }
     }
+#ifdef LC_T0_COUNT_SWEEPS
+    if (lane == 0) atomicAdd(&lc_sweep_hist[nc * 8 + (done_s < 7 ? done_s : 7)], 1ull);
+#endif
     if (count) probes += event_probes<1, 6>(&I, p, cand, pass_v, keep_v, lane);
     Ret = xacc(Ret, I, pp, pk, pb);
     // One register holds at most 64 x 32 configs: with a larger budget only
@@ -576,6 +587,16 @@ __device__ __forceinline__ void write_final_mem(const Args &a, int32_t key, cons
 // Register budget: the loop only touches the T0Args fields it needs; result
 // pointers, counters and work lists are read through `full` (a copy of the
 // tier's Args in device memory) once per key.
+#ifdef LC_T0_PROFILE
+// Diagnostic build only: cycles and counts per event class (invoke, :ok with
+// <= 6, 7, 8, 9, 10 pending), summed over every key.
+__device__ unsigned long long lc_t0_prof[12];
+__shared__ unsigned long long lc_t0_prof_lds[12];
+extern "C" int lc_debug_t0_prof(unsigned long long *host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(lc_t0_prof), sizeof(lc_t0_prof), 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_t *ws) {
     const uint32_t lane = lane_id();
     const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
@@ -624,6 +645,10 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
         const uint32_t dsc_n = (base + 64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
         const uint32_t ev_nn = base + 128 + lane < nev ? evp[base + 128 + lane] : 0u;
         for (uint32_t i = 0; i < cnt; ++i) {
+#ifdef LC_T0_PROFILE
+            const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
+            const uint32_t pn0 = n;
+#endif
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
             const uint32_t slot = LC_EV_SLOT(evi);
             if (!(evi & LC_EV_OK_BIT)) {
@@ -651,19 +676,23 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 uint32_t nSn = 0;
                 int r;
                 if (__builtin_expect(n <= 6, 1)) {  // every live index < 6: no relocation
-#ifdef LC_ABL_NOOK
+#if defined(LC_ABL_NOOK) || defined(LC_ABL_NOOKALL)
                     r = 0;  // ablation build: bookkeeping only
 #else
                     r = ok_lane(W[0], p, live, pass_v, keep_v, b_v, lane, lm, a.one, budget, count, probes, nSn, want_peak);
 #endif
                     live = r ? live : live & ~(1u << p);
                 } else {
+#ifdef LC_ABL_NOOKALL
+                    r = 0;  // ablation build: bookkeeping only, every width
+#else
                     if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
                     else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
                     else if (n == 9)
                         r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
                     else
                         r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+#endif
                     // the op at index `last` takes index p (a no-op when p == last)
                     const uint32_t last = n - 1;
                     const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
@@ -687,6 +716,16 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 status = r;
                 fev = base + i;
             }
+#ifdef LC_T0_PROFILE
+            {
+                const unsigned long long pt1 = __builtin_amdgcn_s_memtime();
+                const uint32_t cat = !(evi & LC_EV_OK_BIT) ? 0u : (pn0 <= 6 ? 1u : pn0 - 5u);
+                if (lane == 0 && cat < 6) {
+                    lc_t0_prof_lds[cat] += pt1 - pt0;
+                    lc_t0_prof_lds[6 + cat] += 1;
+                }
+            }
+#endif
             if (status) break;
         }
         if (status) break;
@@ -722,7 +761,10 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
     __shared__ uint32_t ws[3 * T0_RMEM * 64];  // lattices of 9-10 pending ops (12 KB)
 #ifdef LC_T0_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t nkeys = 0;
+    uint32_t nkeys = 0, lastkey = 0;
+#endif
+#ifdef LC_T0_PROFILE
+    if (lane_id() < 12) lc_t0_prof_lds[lane_id()] = 0;
 #endif
     for (int32_t guard = 0; guard <= a.n_order; ++guard) {  // every wave takes at most n_order keys
         int32_t w = 0;
@@ -736,13 +778,18 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
         }
 #ifdef LC_T0_STAMPS
         ++nkeys;
+        lastkey = (uint32_t)key;
 #endif
     }
+#ifdef LC_T0_PROFILE
+    if (lane_id() < 12) atomicAdd(&lc_t0_prof[lane_id()], lc_t0_prof_lds[lane_id()]);
+#endif
 #ifdef LC_T0_STAMPS
     if (lane_id() == 0 && blockIdx.x < 8192) {
         unsigned long long *o = lc_t0_stamps + blockIdx.x * 6;
         o[0] = st0; o[1] = __builtin_amdgcn_s_memtime(); o[2] = rt0; o[3] = __builtin_amdgcn_s_memrealtime();
-        o[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        o[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4)    // HW_REG_HW_ID
+               | ((unsigned long long)lastkey << 32);
         o[5] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) | ((unsigned long long)nkeys << 32);  // XCC_ID
     }
 #endif

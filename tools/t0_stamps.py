@@ -23,9 +23,33 @@ print("per-block realtime ticks (100MHz): min %d median %d max %d" % (rt.min(), 
 print("clock GHz (cycles/realtime*0.1):", np.median(cyc / np.maximum(rt, 1)) * 0.1)
 start_rt = b[:, 2] - b[:, 2].min(); end_rt = b[:, 3] - b[:, 2].min()
 print("start spread us: max %.1f ; end max us %.1f" % (start_rt.max() / 100, end_rt.max() / 100))
-hw = b[:, 4]; xcc = b[:, 5] & 0xFFFFFFFF; nk = b[:, 5] >> 32
+hw = b[:, 4] & 0xFFFFFFFF; xcc = b[:, 5] & 0xFFFFFFFF; nk = b[:, 5] >> 32
 simd = (hw >> 4) & 3; cu = (hw >> 8) & 15; sh = (hw >> 12) & 1; se = (hw >> 13) & 7
 place = collections.Counter(zip(xcc, se, sh, cu, simd))
 print("distinct SIMDs", len(place), "max blocks on one SIMD", max(place.values()), "keys per block max", nk.max())
 cuc = collections.Counter(zip(xcc, se, sh, cu))
 print("distinct CUs", len(cuc), "max blocks per CU", max(cuc.values()))
+
+# per-key critical path vs the key's shape (one key per block when keys <= grid)
+if nk.max() == 1:
+    kid = b[:, 4] >> 32
+    width = np.ctypeslib.as_array(pk.view.key_width, shape=(pk.n_keys,))
+    nev = np.diff(pk.ev_off.astype(np.int64))
+    hi = np.zeros(pk.n_keys, np.int64)   # :ok events with >= 7 ops pending
+    for i in range(pk.n_keys):
+        ev = pk.events(i)
+        okb = (ev & N.LC_EV_OK_BIT) != 0
+        pend = np.cumsum(np.where(okb, -1, 1))  # pending after each event
+        hi[i] = int(((pend + 1 >= 7) & okb).sum())
+    c = cyc.astype(np.float64)
+    w = width[kid]; hk = hi[kid]; ne = nev[kid]
+    print("cycles per event: median %.0f max %.0f" % (np.median(c / ne), (c / ne).max()))
+    for wv in sorted(set(w.tolist())):
+        m = w == wv
+        print("width %2d: keys %4d  cycles median %9.0f max %9.0f  ok>=7 pending median %d" %
+              (wv, m.sum(), np.median(c[m]), c[m].max(), np.median(hk[m])))
+    order = np.argsort(-c)[:10]
+    print("slowest keys: cycles / width / ok>=7 / events")
+    for j in order:
+        print("  %9d %3d %5d %6d" % (c[j], w[j], hk[j], ne[j]))
+    print("corr(cycles, ok>=7 pending) = %.3f" % np.corrcoef(c, hk)[0, 1])
