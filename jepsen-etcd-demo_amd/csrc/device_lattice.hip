@@ -600,7 +600,7 @@ extern "C" int lc_debug_t0_prof(unsigned long long *host) {
 __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_t *ws) {
     const uint32_t lane = lane_id();
     const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
-    const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
+    const uint64_t eb = a.ev_off[key], ee = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
         finish_key(*a.full, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
@@ -612,9 +612,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     const uint64_t budget = a.budget;
     const bool want_peak = (a.flags & T0_WANT_PEAK) != 0;
     const bool count = (a.flags & T0_COUNT) != 0;
-    const uint32_t *const evp = a.events + b;
+    const uint32_t *const evp = a.events + eb;
     const uint32_t *const trp = a.trans + tb;
-    const uint32_t nev = (a.flags & T0_DBG_NOEVENTS) ? 0u : (uint32_t)(e - b);
+    const uint32_t nev = (a.flags & T0_DBG_NOEVENTS) ? 0u : (uint32_t)(ee - eb);
 
     Lat W;
 #pragma unroll
@@ -633,22 +633,91 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     int status = 0;        // 1 invalid, 2 budget, 3 spill
     uint32_t fev = 0;
 
-    // events arrive 64 at a time, one per lane; chunk c+1's words and
-    // descriptors are in flight while chunk c is searched
+    // Event cursor: events arrive 64 at a time, one per lane; the next
+    // chunk's words and descriptors are in flight while this one is searched.
     uint32_t ev = lane < nev ? evp[lane] : 0u;
     uint32_t dsc = (lane < nev && !(ev & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev)] : 0u;
     uint32_t ev_n = 64 + lane < nev ? evp[64 + lane] : 0u;
-    for (uint32_t base = 0; base < nev; base += 64) {
-        const uint32_t cnt = nev - base < 64u ? nev - base : 64u;
-        // next chunk's descriptors (its words arrived during this chunk's
-        // predecessor) and the words of the chunk after it
-        const uint32_t dsc_n = (base + 64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
-        const uint32_t ev_nn = base + 128 + lane < nev ? evp[base + 128 + lane] : 0u;
-        for (uint32_t i = 0; i < cnt; ++i) {
+    uint32_t dsc_n = (64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
+    uint32_t ev_nn = 128 + lane < nev ? evp[128 + lane] : 0u;
+    uint32_t e = 0, i = 0, base = 0;
+    uint32_t lim = nev;  // 0 once the key has a verdict: each loop's only exit is its head
+    auto advance = [&]() {
+        ++e;
+        if (++i == 64u) {
+            i = 0; base += 64;
+            ev = ev_n; dsc = dsc_n; ev_n = ev_nn;
+            dsc_n = (base + 64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
+            ev_nn = base + 128 + lane < nev ? evp[base + 128 + lane] : 0u;
+        }
+    };
 #ifdef LC_T0_PROFILE
-            const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
-            const uint32_t pn0 = n;
+#define T0_PROF_BEGIN const unsigned long long pt0 = __builtin_amdgcn_s_memtime(); const uint32_t pn0 = n;
+#define T0_PROF_END(evi)                                                                   \
+    {                                                                                      \
+        const unsigned long long pt1 = __builtin_amdgcn_s_memtime();                       \
+        const uint32_t cat = !((evi) & LC_EV_OK_BIT) ? 0u : (pn0 <= 6 ? 1u : pn0 - 5u);    \
+        if (lane == 0 && cat < 6) { lc_t0_prof_lds[cat] += pt1 - pt0; lc_t0_prof_lds[6 + cat] += 1; } \
+    }
+#else
+#define T0_PROF_BEGIN
+#define T0_PROF_END(evi)
 #endif
+
+    // Two phases, each a loop of its own, so that neither carries the
+    // other's values through its back edge (one loop for both made the
+    // register allocator copy every loop-carried value twice per event):
+    //   lane phase  -- at most 6 ops pending, every live index < 6, the
+    //                  lattice in one register (W0);
+    //   dense phase -- 7 to 10 pending, dense indices, W[0..3] or the LDS
+    //                  workspace; left after the :ok that brings n back to 6.
+    uint32_t W0 = W[0];
+    for (uint32_t phase = 0; phase <= nev && e < lim; ++phase) {
+        while (e < lim) {
+            T0_PROF_BEGIN
+            const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
+            const uint32_t slot = LC_EV_SLOT(evi);
+            if (!(evi & LC_EV_OK_BIT)) {
+                if (n == 6) break;  // a 7th pending op: the dense phase takes this invoke
+                if (n >= T0_MAX_WIDTH || slot >= 64) {
+                    status = 3;
+                } else {
+                    const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
+                    const uint32_t idx = (uint32_t)__builtin_ctz(~live);  // lowest free index
+                    const bool me = lane == idx;
+                    slot_v = me ? slot : slot_v;
+                    pass_v = me ? x.pass : pass_v;
+                    keep_v = me ? x.keep : keep_v;
+                    b_v = me ? x.b : b_v;
+                    dense_v = lane == slot ? idx : dense_v;
+                    live |= 1u << idx;
+                    ++n;
+                }
+            } else {
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
+                uint32_t nSn = 0;
+#if defined(LC_ABL_NOOK) || defined(LC_ABL_NOOKALL)
+                const int r = 0;  // ablation build: bookkeeping only
+#else
+                const int r = ok_lane(W0, p, live, pass_v, keep_v, b_v, lane, lm, a.one, budget, count, probes, nSn,
+                                      want_peak);
+#endif
+                live = r ? live : live & ~(1u << p);
+                n = r ? n : n - 1;
+                peak = nSn > peak ? nSn : peak;
+                status = r;
+                fev = e;
+            }
+            T0_PROF_END(evi)
+            lim = status ? 0u : lim;
+            advance();
+        }
+        if (e >= lim) break;
+        W[0] = W0;
+#pragma unroll
+        for (int k = 1; k < T0_RMAX; ++k) W[k] = 0u;
+        while (e < lim) {
+            T0_PROF_BEGIN
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
             const uint32_t slot = LC_EV_SLOT(evi);
             if (!(evi & LC_EV_OK_BIT)) {
@@ -661,7 +730,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                         in_mem = true;
                     }
                     const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
-                    const uint32_t idx = (uint32_t)__builtin_ctz(~live);  // lowest free index (= n once dense)
+                    const uint32_t idx = n;  // dense: every index below n is taken
                     const bool me = lane == idx;
                     slot_v = me ? slot : slot_v;
                     pass_v = me ? x.pass : pass_v;
@@ -675,62 +744,48 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
                 uint32_t nSn = 0;
                 int r;
-                if (__builtin_expect(n <= 6, 1)) {  // every live index < 6: no relocation
-#if defined(LC_ABL_NOOK) || defined(LC_ABL_NOOKALL)
-                    r = 0;  // ablation build: bookkeeping only
-#else
-                    r = ok_lane(W[0], p, live, pass_v, keep_v, b_v, lane, lm, a.one, budget, count, probes, nSn, want_peak);
-#endif
-                    live = r ? live : live & ~(1u << p);
-                } else {
 #ifdef LC_ABL_NOOKALL
-                    r = 0;  // ablation build: bookkeeping only, every width
+                r = 0;  // ablation build: bookkeeping only, every width
 #else
-                    if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-                    else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-                    else if (n == 9)
-                        r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-                    else
-                        r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                else if (n == 9)
+                    r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                else
+                    r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
 #endif
-                    // the op at index `last` takes index p (a no-op when p == last)
-                    const uint32_t last = n - 1;
-                    const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
-                    const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last),
-                                   x1 = __builtin_amdgcn_readlane(keep_v, last), x2 = __builtin_amdgcn_readlane(b_v, last);
-                    const bool mp = lane == p && !r;
-                    slot_v = mp ? s_last : slot_v;
-                    pass_v = mp ? x0 : pass_v;
-                    keep_v = mp ? x1 : keep_v;
-                    b_v = mp ? x2 : b_v;
-                    dense_v = (lane == s_last && !r) ? p : dense_v;
-                    live = r ? live : (1u << last) - 1u;
-                    if (in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
+                // the op at index `last` takes index p (a no-op when p == last)
+                const uint32_t last = n - 1;
+                const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
+                const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last),
+                               x1 = __builtin_amdgcn_readlane(keep_v, last), x2 = __builtin_amdgcn_readlane(b_v, last);
+                const bool mp = lane == p && !r;
+                slot_v = mp ? s_last : slot_v;
+                pass_v = mp ? x0 : pass_v;
+                keep_v = mp ? x1 : keep_v;
+                b_v = mp ? x2 : b_v;
+                dense_v = (lane == s_last && !r) ? p : dense_v;
+                live = r ? live : (1u << last) - 1u;
+                if (in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
 #pragma unroll
-                        for (int k = 0; k < T0_RMAX; ++k) W[k] = m.W[k * 64 + lane];
-                        in_mem = false;
-                    }
+                    for (int k = 0; k < T0_RMAX; ++k) W[k] = m.W[k * 64 + lane];
+                    in_mem = false;
                 }
                 n = r ? n : n - 1;
                 peak = nSn > peak ? nSn : peak;
                 status = r;
-                fev = base + i;
+                fev = e;
             }
-#ifdef LC_T0_PROFILE
-            {
-                const unsigned long long pt1 = __builtin_amdgcn_s_memtime();
-                const uint32_t cat = !(evi & LC_EV_OK_BIT) ? 0u : (pn0 <= 6 ? 1u : pn0 - 5u);
-                if (lane == 0 && cat < 6) {
-                    lc_t0_prof_lds[cat] += pt1 - pt0;
-                    lc_t0_prof_lds[6 + cat] += 1;
-                }
-            }
-#endif
-            if (status) break;
+            T0_PROF_END(evi)
+            lim = status ? 0u : lim;
+            advance();
+            if (n <= 6) break;  // dense indices 0..5: the lane phase's invariant holds
         }
-        if (status) break;
-        ev = ev_n; dsc = dsc_n; ev_n = ev_nn;
+        W0 = W[0];
     }
+#undef T0_PROF_BEGIN
+#undef T0_PROF_END
+    W[0] = W0;
     if (status == 3) return K_SPILL;
     // per-key epilogue (results through `full`); on a failure W / live still
     // hold the set before the failing event, which is what is reported
