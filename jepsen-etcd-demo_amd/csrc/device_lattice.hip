@@ -232,9 +232,8 @@ __device__ __forceinline__ uint32_t sweep_lanes(uint32_t cur, const LaneMasks &m
 // successors over I plus legal applications of p.
 template <int RL, int NB>
 __device__ __forceinline__ uint32_t event_probes(const uint32_t *I, uint32_t p, uint32_t cand, uint32_t pass_v,
-                                                 uint32_t keep_v, uint32_t lane) {
-    uint32_t pr = 0;
-    const uint32_t pm = __builtin_amdgcn_readlane(pass_v, p) | __builtin_amdgcn_readlane(keep_v, p);
+                                                 uint32_t keep_v, uint32_t lane, uint32_t pm) {
+    uint32_t pr = 0;  // pm: p's pass | keep
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
         const uint32_t m = ((cand >> q) & 1u) ? (__builtin_amdgcn_readlane(pass_v, q) | __builtin_amdgcn_readlane(keep_v, q)) : 0u;
@@ -266,22 +265,20 @@ extern "C" int lc_debug_sweep_hist(unsigned long long *host) {
 // lm[q] (0 / ~0) is lane bit q as a VGPR mask.  W = S on entry, S' on a
 // normal return.  Returns 0 normal, 1 invalid, 2 budget exceeded.
 __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, uint32_t pass_v, uint32_t keep_v,
-                                       uint32_t b_v, uint32_t lane, const uint32_t (&lm)[6], uint32_t one,
-                                       uint64_t budget, bool count, uint32_t &probes, uint32_t &nSn_out,
-                                       bool want_size) {
+                                       uint32_t b_v, uint32_t pp, uint32_t pk, uint32_t pb, uint32_t lane,
+                                       const uint32_t (&lm)[6], uint32_t one, uint64_t budget, bool count,
+                                       uint32_t &probes, uint32_t &nSn_out, bool want_size) {
     const uint32_t cand = live & ~(1u << p);
     const uint32_t wup = (uint32_t)__shfl_xor((int)W, 1 << p);
+    // free indices and p hold zero transfers in pass_v / keep_v (the caller
+    // cleared lane p), so a position's masks need no gating by `cand`
     LaneMasks m;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-        const uint32_t cq = ((cand >> q) & 1u) ? ~0u : 0u;  // scalar
-        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, q) & cq, sk = __builtin_amdgcn_readlane(keep_v, q) & cq;
-        m.vp[q] = vand(sp, lm[q]);
-        m.vk[q] = vand(sk, lm[q]);
+        m.vp[q] = vand(__builtin_amdgcn_readlane(pass_v, q), lm[q]);
+        m.vk[q] = vand(__builtin_amdgcn_readlane(keep_v, q), lm[q]);
         m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
     }
-    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
-                   pb = __builtin_amdgcn_readlane(b_v, p);
     const bool hp = (lane >> p) & 1u;
     if (count) probes += (uint32_t)__popc(W);
     uint32_t Ret = hp ? 0u : wup;
@@ -309,7 +306,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 #ifdef LC_T0_COUNT_SWEEPS
     if (lane == 0) atomicAdd(&lc_sweep_hist[nc * 8 + (done_s < 7 ? done_s : 7)], 1ull);
 #endif
-    if (count) probes += event_probes<1, 6>(&I, p, cand, pass_v, keep_v, lane);
+    if (count) probes += event_probes<1, 6>(&I, p, cand, pass_v, keep_v, lane, pp | pk);
     Ret = xacc(Ret, I, pp, pk, pb);
     // One register holds at most 64 x 32 configs: with a larger budget only
     // emptiness matters (a ballot); exact sizes only when asked for (peak).
@@ -388,7 +385,9 @@ __device__ __forceinline__ int ok_reg(Lat &W, uint32_t p, uint32_t pass_v, uint3
         for (int k = 0; k < RL; ++k) { ch |= nv[k] != I[k]; I[k] = nv[k]; }
         if (!__any(ch)) break;
     }
-    if (count) probes += event_probes<RL, NB>(I, p, ((1u << NB) - 1u) & ~(1u << p), pass_v, keep_v, lane);
+    if (count)
+        probes += event_probes<RL, NB>(I, p, ((1u << NB) - 1u) & ~(1u << p), pass_v, keep_v, lane,
+                                       __builtin_amdgcn_readlane(pass_v, p) | __builtin_amdgcn_readlane(keep_v, p));
     uint32_t cI = 0, cS = 0;
 #pragma unroll
     for (int k = 0; k < RL; ++k) {
@@ -699,8 +698,14 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 #if defined(LC_ABL_NOOK) || defined(LC_ABL_NOOKALL)
                 const int r = 0;  // ablation build: bookkeeping only
 #else
-                const int r = ok_lane(W0, p, live, pass_v, keep_v, b_v, lane, lm, a.one, budget, count, probes, nSn,
-                                      want_peak);
+                // p's transfer, then p's lane cleared for good: its index is
+                // free after this :ok (and an invalid key stops here)
+                const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
+                               pb = __builtin_amdgcn_readlane(b_v, p);
+                pass_v = lane == p ? 0u : pass_v;
+                keep_v = lane == p ? 0u : keep_v;
+                const int r = ok_lane(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
+                                      probes, nSn, want_peak);
 #endif
                 live = r ? live : live & ~(1u << p);
                 n = r ? n : n - 1;
@@ -765,6 +770,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 keep_v = mp ? x1 : keep_v;
                 b_v = mp ? x2 : b_v;
                 dense_v = (lane == s_last && !r) ? p : dense_v;
+                // index `last` is free now: zero transfer (the lane phase relies on it)
+                pass_v = (lane == last && !r) ? 0u : pass_v;
+                keep_v = (lane == last && !r) ? 0u : keep_v;
                 live = r ? live : (1u << last) - 1u;
                 if (in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
 #pragma unroll
