@@ -396,7 +396,13 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     lcd::Args a0 = a;
     a0.order = d->order; a0.n_order = (int32_t)K; a0.n_in = nullptr; a0.ticket = c->counters + 8;
     a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
-    const int g0 = (int)std::max<int64_t>(1, std::min<int64_t>(K, (int64_t)c->cu_count * 16));
+    // T0 has two builds: 16 lattice registers (n <= 10 pending in VGPRs, 2
+    // waves per SIMD) when every key can be resident at once -- each key's
+    // events are serial, so there per-key latency is the whole story -- and
+    // 4 registers (9-10 pending in LDS, 4 waves per SIMD) for larger batches,
+    // where occupancy hides latency across keys.
+    const bool t0_wide = K <= (int64_t)c->cu_count * 8;
+    const int g0 = (int)std::max<int64_t>(1, std::min<int64_t>(K, (int64_t)c->cu_count * (t0_wide ? 8 : 16)));
     a0.lat_ws = nullptr;
     // T0 reads the result/counter/list pointers from a device copy of its
     // Args, refreshed (outside the timed region) only when they change
@@ -407,7 +413,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     }
     HIPCHK(hipEventRecord(c->e0, c->stream));
     if (K > 0) {
-        HIPCHK(lcd::launch_t0(a0, c->dargs, g0, c->stream));
+        HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream));
         HIPCHK(hipEventRecord(c->et0, c->stream));
         // T1: LDS hash sets
         lcd::Args a1 = a;

@@ -46,7 +46,11 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 
 namespace lcd {
 
-constexpr int T0_RMAX = 4;             // lattice registers per lane: n <= 8 pending ops
+// Lattice registers per lane: the compact build holds n <= 8 pending ops in
+// 4 registers (9-10 in the LDS workspace) and fits 4 waves per SIMD; the
+// wide build holds n <= 10 in 16 registers (2 waves per SIMD) and is used
+// when every key can be resident at once (launch_t0).
+constexpr int T0_RSMALL = 4, T0_RBIG = 16;
 constexpr int T0_RMEM = 16;            // workspace lattice (global memory): n <= 10
 #ifndef LC_T0_MAX_WIDTH
 #define LC_T0_MAX_WIDTH 10
@@ -170,7 +174,7 @@ __device__ __forceinline__ bool idx_has(uint32_t lane, int k, uint32_t q) {
 template <int RL>
 constexpr int lat_bits() { return RL == 1 ? 6 : RL == 2 ? 7 : RL == 4 ? 8 : RL == 8 ? 9 : 10; }
 
-using Lat = uint32_t[T0_RMAX];
+using Lat = uint32_t[T0_RBIG];
 
 // T0's kernel arguments: only what the event loop reads, so the loop keeps
 // its scalar registers (the full Args would spill SGPRs into VGPR lanes).
@@ -195,7 +199,7 @@ struct T0Args {
 // Lane-masked transfer masks of one event: vp/vk[q] = op q's pass/keep on
 // lanes with bit q (0 elsewhere and for q = p); sb[q] = op q's shift.
 struct LaneMasks {
-    uint32_t vp[6], vk[6], sb[8];
+    uint32_t vp[6], vk[6], sb[10];
 };
 
 template <int N>
@@ -204,7 +208,7 @@ __device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t pa
 #pragma unroll
     for (int q = 0; q < 6; ++q) { m.vp[q] = 0u; m.vk[q] = 0u; }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) m.sb[q] = 0u;
+    for (int q = 0; q < 10; ++q) m.sb[q] = 0u;
 #pragma unroll
     for (int q = 0; q < (N < 6 ? N : 6); ++q) {
         const bool on = ((lane >> q) & 1u) && (uint32_t)q != p;
@@ -213,7 +217,7 @@ __device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t pa
         m.vk[q] = on ? sk : 0u;
     }
 #pragma unroll
-    for (int q = 0; q < (N < 8 ? N : 8); ++q) m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
+    for (int q = 0; q < (N < 10 ? N : 10); ++q) m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
 }
 
 // One Gauss-Seidel pass over lane-bit positions Q .. min(N, 6) - 1 (`prev`:
@@ -326,8 +330,8 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 
 // One :ok(p) event on a lattice of RL registers (N = 7 or 8 ops pending):
 // lane bits 0..5 as in ok_lane, register bits 6.. through register pairs.
-template <int RL>
-__device__ __forceinline__ int ok_reg(Lat &W, uint32_t p, uint32_t pass_v, uint32_t keep_v, uint32_t b_v,
+template <int RL, int RM>
+__device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t pass_v, uint32_t keep_v, uint32_t b_v,
                                       uint32_t lane, uint64_t budget, bool count, uint32_t &probes,
                                       uint32_t &nSn_out, bool want_size) {
     constexpr int NB = lat_bits<RL>();  // = ops pending
@@ -344,7 +348,7 @@ __device__ __forceinline__ int ok_reg(Lat &W, uint32_t p, uint32_t pass_v, uint3
     }
     const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
                    pb = __builtin_amdgcn_readlane(b_v, p);
-    Lat Ret, I;
+    uint32_t Ret[RL], I[RL];
     if (count) {
 #pragma unroll
         for (int k = 0; k < RL; ++k) probes += (uint32_t)__popc(W[k]);
@@ -372,7 +376,7 @@ __device__ __forceinline__ int ok_reg(Lat &W, uint32_t p, uint32_t pass_v, uint3
     }
 #pragma unroll 1
     for (int s = 1; s < NB; ++s) {
-        Lat nv;
+        uint32_t nv[RL];
 #pragma unroll
         for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6>(I[k], m, 1u);
 #pragma unroll
@@ -596,6 +600,7 @@ extern "C" int lc_debug_t0_prof(unsigned long long *host) {
 }
 #endif
 
+template <int RM>
 __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_t *ws) {
     const uint32_t lane = lane_id();
     const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
@@ -615,9 +620,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     const uint32_t *const trp = a.trans + tb;
     const uint32_t nev = (a.flags & T0_DBG_NOEVENTS) ? 0u : (uint32_t)(ee - eb);
 
-    Lat W;
+    uint32_t W[RM];
 #pragma unroll
-    for (int k = 0; k < T0_RMAX; ++k) W[k] = 0;
+    for (int k = 0; k < RM; ++k) W[k] = 0;
     if (lane == 0) W[0] = 1u << a.init_state;
     bool in_mem = false;   // lattice lives in m.W (9 or 10 ops pending)
     uint32_t pass_v = 0, keep_v = 0, b_v = 0;  // lane j: transfer of the op at index j
@@ -720,7 +725,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
         if (e >= lim) break;
         W[0] = W0;
 #pragma unroll
-        for (int k = 1; k < T0_RMAX; ++k) W[k] = 0u;
+        for (int k = 1; k < RM; ++k) W[k] = 0u;
         while (e < lim) {
             T0_PROF_BEGIN
             const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
@@ -729,9 +734,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 if (n >= T0_MAX_WIDTH || slot >= 64) {
                     status = 3;
                 } else {
-                    if (n == 8) {  // 9 pending: move the lattice to the workspace
+                    if (RM < 16 && n == 8) {  // 9 pending: move the lattice to the workspace
 #pragma unroll
-                        for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < T0_RMAX ? W[k < T0_RMAX ? k : 0] : 0u;
+                        for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < RM ? W[k < RM ? k : 0] : 0u;
                         in_mem = true;
                     }
                     const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
@@ -754,10 +759,15 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 #else
                 if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
                 else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-                else if (n == 9)
-                    r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-                else
-                    r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                else if constexpr (RM < 16) {
+                    if (n == 9)
+                        r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    else
+                        r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                } else {
+                    if (n == 9) r = ok_reg<8>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    else r = ok_reg<16>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                }
 #endif
                 // the op at index `last` takes index p (a no-op when p == last)
                 const uint32_t last = n - 1;
@@ -774,9 +784,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 pass_v = (lane == last && !r) ? 0u : pass_v;
                 keep_v = (lane == last && !r) ? 0u : keep_v;
                 live = r ? live : (1u << last) - 1u;
-                if (in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
+                if (RM < 16 && in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
 #pragma unroll
-                    for (int k = 0; k < T0_RMAX; ++k) W[k] = m.W[k * 64 + lane];
+                    for (int k = 0; k < RM; ++k) W[k] = m.W[k * 64 + lane];
                     in_mem = false;
                 }
                 n = r ? n : n - 1;
@@ -800,7 +810,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     const Args &f = *a.full;
     if (!in_mem) {
 #pragma unroll
-        for (int k = 0; k < T0_RMAX; ++k) m.W[k * 64 + lane] = W[k];
+        for (int k = 0; k < RM; ++k) m.W[k * 64 + lane] = W[k];
     }
     if (!(a.flags & T0_DBG_NOFINAL)) write_final_mem(f, key, m, lane, slot_v, live);
     const uint32_t pr = __ockl_wfred_add_u32(probes);
@@ -820,6 +830,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 __device__ unsigned long long lc_t0_stamps[8192 * 6];
 #endif
 
+template <int RM>
 __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
     __shared__ uint32_t ws[3 * T0_RMEM * 64];  // lattices of 9-10 pending ops (12 KB)
 #ifdef LC_T0_STAMPS
@@ -835,7 +846,7 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
         w = __builtin_amdgcn_readfirstlane(w);
         if (w >= a.n_order) break;
         const int32_t key = a.order[w];
-        if (lattice_key(a, key, ws) == K_SPILL) {
+        if (lattice_key<RM>(a, key, ws) == K_SPILL) {
             const Args &f = *a.full;
             push_list(f.spill, f.n_spill, key);
         }
@@ -866,7 +877,7 @@ extern "C" int lc_debug_t0_stamps(unsigned long long *host, int n_blocks) {
 
 size_t lat_ws_words() { return 3 * T0_RMEM * 64; }
 
-hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, hipStream_t s) {
+hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s) {
     T0Args t{};
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
     t.key_width = a.key_width; t.key_states = a.key_states; t.order = a.order; t.ticket = a.ticket;
@@ -874,7 +885,8 @@ hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, hipStream_t s) 
     t.init_state = a.init_state; t.shared_states = a.shared_states; t.one = 1u;
     t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) |
               (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u);
-    hipLaunchKernelGGL(k_search_lattice, dim3(grid), dim3(64), 0, s, t);
+    if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(grid), dim3(64), 0, s, t);
+    else hipLaunchKernelGGL(k_search_lattice<T0_RSMALL>, dim3(grid), dim3(64), 0, s, t);
     return hipGetLastError();
 }
 

@@ -58,7 +58,7 @@ struct HbmWs {
 
 size_t lds_bytes_t1();
 size_t lds_bytes_t2();
-hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, hipStream_t s);
+hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s);
 size_t lat_ws_words();
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t2(const Args &a, int grid, hipStream_t s);

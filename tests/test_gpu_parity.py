@@ -144,3 +144,12 @@ def test_counterexamples(device, shape):
             assert got_paths == exp_paths, f"key {k}"
         n_bad += 1
     assert n_bad > 5
+
+
+def test_compact_t0_build_heavy_widths(device):
+    """More keys than SIMD slots: T0's compact build (4 lattice registers, 9-10
+    pending ops in the LDS workspace) on keys up to 10 ops wide.  Smaller
+    batches take the wide build (16 registers); both must match the oracle."""
+    h = H.synth(n_keys=2600, ops_per_key=120, concurrency=10, anomaly_rate=0.1, seed=41)
+    _, res, _ = device_vs_oracle(h, device)
+    assert (res.valid == 0).any()

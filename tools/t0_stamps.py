@@ -36,11 +36,13 @@ if nk.max() == 1:
     width = np.ctypeslib.as_array(pk.view.key_width, shape=(pk.n_keys,))
     nev = np.diff(pk.ev_off.astype(np.int64))
     hi = np.zeros(pk.n_keys, np.int64)   # :ok events with >= 7 ops pending
+    byn = np.zeros((pk.n_keys, 11), np.int64)  # :ok events by ops pending
     for i in range(pk.n_keys):
         ev = pk.events(i)
         okb = (ev & N.LC_EV_OK_BIT) != 0
         pend = np.cumsum(np.where(okb, -1, 1))  # pending after each event
         hi[i] = int(((pend + 1 >= 7) & okb).sum())
+        byn[i] = np.bincount(np.minimum(pend[okb] + 1, 10), minlength=11)
     c = cyc.astype(np.float64)
     w = width[kid]; hk = hi[kid]; ne = nev[kid]
     print("cycles per event: median %.0f max %.0f" % (np.median(c / ne), (c / ne).max()))
@@ -49,7 +51,12 @@ if nk.max() == 1:
         print("width %2d: keys %4d  cycles median %9.0f max %9.0f  ok>=7 pending median %d" %
               (wv, m.sum(), np.median(c[m]), c[m].max(), np.median(hk[m])))
     order = np.argsort(-c)[:10]
-    print("slowest keys: cycles / width / ok>=7 / events")
+    print("slowest keys: cycles / width / ok>=7 / events / oks at n=7,8,9,10")
     for j in order:
-        print("  %9d %3d %5d %6d" % (c[j], w[j], hk[j], ne[j]))
+        print("  %9d %3d %5d %6d   %s" % (c[j], w[j], hk[j], ne[j], byn[kid[j], 7:11].tolist()))
+    # least squares: cycles ~ a*invokes + b*ok(<=6) + c7*ok7 + c8*ok8 + c9*ok9 + c10*ok10
+    nb = byn[kid]
+    X = np.column_stack([ne - nb.sum(1), nb[:, :7].sum(1), nb[:, 7], nb[:, 8], nb[:, 9], nb[:, 10]]).astype(np.float64)
+    coef, *_ = np.linalg.lstsq(X, c, rcond=None)
+    print("fit cycles per event: invoke %.0f ok<=6 %.0f ok7 %.0f ok8 %.0f ok9 %.0f ok10 %.0f" % tuple(coef))
     print("corr(cycles, ok>=7 pending) = %.3f" % np.corrcoef(c, hk)[0, 1])
