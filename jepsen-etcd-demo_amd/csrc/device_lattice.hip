@@ -60,7 +60,7 @@ constexpr uint32_t T0_MAX_STATES = 32;
 
 struct Xfer { uint32_t pass, keep, b; };
 
-__device__ __forceinline__ Xfer xfer_of(uint32_t d) {  // uniform d: scalar selects
+__device__ __forceinline__ Xfer xfer_of(uint32_t d) {
     const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
     const uint32_t abit = a < 32u ? 1u << (a & 31u) : 0u;
     Xfer x;
@@ -644,6 +644,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     uint32_t ev_n = 64 + lane < nev ? evp[64 + lane] : 0u;
     uint32_t dsc_n = (64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
     uint32_t ev_nn = 128 + lane < nev ? evp[128 + lane] : 0u;
+    // each lane decodes its event's transition once per chunk (VALU, all 64
+    // at a time), so an invoke only reads three lanes
+    Xfer xc = xfer_of(dsc);
     uint32_t e = 0, i = 0, base = 0;
     uint32_t lim = nev;  // 0 once the key has a verdict: each loop's only exit is its head
     auto advance = [&]() {
@@ -651,6 +654,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
         if (++i == 64u) {
             i = 0; base += 64;
             ev = ev_n; dsc = dsc_n; ev_n = ev_nn;
+            xc = xfer_of(dsc);
             dsc_n = (base + 64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
             ev_nn = base + 128 + lane < nev ? evp[base + 128 + lane] : 0u;
         }
@@ -686,7 +690,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 if (n >= T0_MAX_WIDTH || slot >= 64) {
                     status = 3;
                 } else {
-                    const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
+                    const Xfer x{(uint32_t)__builtin_amdgcn_readlane(xc.pass, i),
+                                 (uint32_t)__builtin_amdgcn_readlane(xc.keep, i),
+                                 (uint32_t)__builtin_amdgcn_readlane(xc.b, i)};
                     const uint32_t idx = (uint32_t)__builtin_ctz(~live);  // lowest free index
                     const bool me = lane == idx;
                     slot_v = me ? slot : slot_v;
@@ -739,7 +745,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                         for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < RM ? W[k < RM ? k : 0] : 0u;
                         in_mem = true;
                     }
-                    const Xfer x = xfer_of(__builtin_amdgcn_readlane(dsc, i));
+                    const Xfer x{(uint32_t)__builtin_amdgcn_readlane(xc.pass, i),
+                                 (uint32_t)__builtin_amdgcn_readlane(xc.keep, i),
+                                 (uint32_t)__builtin_amdgcn_readlane(xc.b, i)};
                     const uint32_t idx = n;  // dense: every index below n is taken
                     const bool me = lane == idx;
                     slot_v = me ? slot : slot_v;
