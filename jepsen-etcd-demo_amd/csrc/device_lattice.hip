@@ -268,6 +268,7 @@ extern "C" int lc_debug_sweep_hist(unsigned long long *host) {
 // ds_bpermute, issued first so its latency hides under the mask setup.
 // lm[q] (0 / ~0) is lane bit q as a VGPR mask.  W = S on entry, S' on a
 // normal return.  Returns 0 normal, 1 invalid, 2 budget exceeded.
+template <int T>  // T = 1 + the highest live index (positions T.. are empty)
 __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, uint32_t pass_v, uint32_t keep_v,
                                        uint32_t b_v, uint32_t pp, uint32_t pk, uint32_t pb, uint32_t lane,
                                        const uint32_t (&lm)[6], uint32_t one, uint64_t budget, bool count,
@@ -278,7 +279,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
     // cleared lane p), so a position's masks need no gating by `cand`
     LaneMasks m;
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
+    for (int q = 0; q < T; ++q) {
         m.vp[q] = vand(__builtin_amdgcn_readlane(pass_v, q), lm[q]);
         m.vk[q] = vand(__builtin_amdgcn_readlane(keep_v, q), lm[q]);
         m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
@@ -297,7 +298,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 #endif
 #pragma unroll 1
     for (uint32_t s = 0; s < nc; ++s) {
-        const uint32_t nv = sweep_lanes<0, 6>(I, m, one);
+        const uint32_t nv = sweep_lanes<0, T>(I, m, one);
         const bool ch = nv != I;
         I = nv;
         if (!__any(ch)) {
@@ -715,8 +716,22 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                                pb = __builtin_amdgcn_readlane(b_v, p);
                 pass_v = lane == p ? 0u : pass_v;
                 keep_v = lane == p ? 0u : keep_v;
-                const int r = ok_lane(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
-                                      probes, nSn, want_peak);
+                // Compact build (many keys per SIMD, throughput): sweeps cover
+                // the positions below the highest live index only.  Wide build
+                // (one key per SIMD, latency): one sweep body for every event --
+                // the specialised copies cost more in instruction-cache misses
+                // across a CU's four lone waves than they save.
+                const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
+                int r;
+                if (RM == T0_RBIG || top >= 6)
+                    r = ok_lane<6>(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
+                                   probes, nSn, want_peak);
+                else if (top == 5)
+                    r = ok_lane<5>(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
+                                   probes, nSn, want_peak);
+                else
+                    r = ok_lane<4>(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
+                                   probes, nSn, want_peak);
 #endif
                 live = r ? live : live & ~(1u << p);
                 n = r ? n : n - 1;
