@@ -17,9 +17,11 @@
 //   I[L u {q}] |= T_q(I[L]) for every pending q != p, to a fixpoint,
 //   S'[L]   = Ret[L] | T_p(I[L])
 // where T_q maps a state mask through op q's cas-register step, branch-free:
-//   T(M) = (M & pass) | (min(M & keep, 1) << b)
-//   (read nil: pass = all; read a: pass = {a}; write b: keep = all;
-//    cas a->b: keep = {a}).
+//   T(M) = min(M & k, cap) << b
+//   (k = the states the op accepts, cap = ~0 for reads (T(M) = M & k, b = 0)
+//    and 1 for writes / cas (T(M) = {b} if M & k is not empty):
+//    read nil: k = all; read a: k = {a}; write b: k = all, cap = 1;
+//    cas a->b: k = {a}, cap = 1).
 // The closure runs as Gauss-Seidel sweeps over the subset-bit positions:
 // lanes (subsets) WITH bit q gather I from the subset without it -- one
 // DPP / permlane instruction for a lane bit, a register for a register bit --
@@ -58,24 +60,16 @@ constexpr int T0_RMEM = 16;            // workspace lattice (global memory): n <
 constexpr uint32_t T0_MAX_WIDTH = LC_T0_MAX_WIDTH;  // <= 6 + log2(T0_RMEM)
 constexpr uint32_t T0_MAX_STATES = 32;
 
-struct Xfer { uint32_t pass, keep, b; };
+struct Xfer { uint32_t k, cap, b; };
 
 __device__ __forceinline__ Xfer xfer_of(uint32_t d) {
     const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
     const uint32_t abit = a < 32u ? 1u << (a & 31u) : 0u;
     Xfer x;
-    x.pass = f == LC_T_READ_ANY ? 0xFFFFFFFFu : (f == LC_T_READ ? abit : 0u);
-    x.keep = f == LC_T_WRITE ? 0xFFFFFFFFu : (f == LC_T_CAS ? abit : 0u);
+    x.k = (f == LC_T_READ || f == LC_T_CAS) ? abit : 0xFFFFFFFFu;
+    x.cap = f >= LC_T_WRITE ? 1u : 0xFFFFFFFFu;
     x.b = f >= LC_T_WRITE ? (b & 31u) : 0u;
     return x;
-}
-
-// min(t, 1) as one v_min_u32 (the compiler would otherwise turn it into a
-// compare + select through an SGPR pair, which also costs a hazard nop)
-__device__ __forceinline__ uint32_t umin1(uint32_t t) {
-    uint32_t r;
-    asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(t));
-    return r;
 }
 
 // s & v as one v_and_b32 (kept opaque: the compiler would turn an AND with a
@@ -86,18 +80,9 @@ __device__ __forceinline__ uint32_t vand(uint32_t s, uint32_t v) {
     return r;
 }
 
-// acc | T(x): v_and_or_b32, v_and_b32, v_min_u32, v_lshl_or_b32
-__device__ __forceinline__ uint32_t xacc(uint32_t acc, uint32_t x, uint32_t pass, uint32_t keep, uint32_t b) {
-    acc = (x & pass) | acc;
-    return (umin1(x & keep) << b) | acc;
-}
-// The same with `one` an opaque scalar 1 (a kernel argument): min(t, one)
-// stays one v_min_u32 the compiler can see (no hazard padding around inline
-// asm), where min(t, 1) would become a compare + select.
-__device__ __forceinline__ uint32_t xacc1(uint32_t acc, uint32_t x, uint32_t pass, uint32_t keep, uint32_t b,
-                                          uint32_t one) {
-    acc = (x & pass) | acc;
-    return (__builtin_elementwise_min(x & keep, one) << b) | acc;
+// acc | T(x) = acc | (min(x & k, cap) << b): v_and_b32, v_min_u32, v_lshl_or_b32
+__device__ __forceinline__ uint32_t xacc(uint32_t acc, uint32_t x, uint32_t k, uint32_t cap, uint32_t b) {
+    return (__builtin_elementwise_min(x & k, cap) << b) | acc;
 }
 
 // One-directional gathers along subset bit q < 6 (a lane-index bit):
@@ -106,12 +91,19 @@ __device__ __forceinline__ uint32_t xacc1(uint32_t acc, uint32_t x, uint32_t pas
 // One VALU instruction each: DPP quad_perm (q = 0, 1), DPP row_shr / row_shl
 // (q = 2, 3; lanes whose source leaves the row read garbage, which every
 // caller masks), gfx950 v_permlane16_swap / v_permlane32_swap (q = 4, 5).
+// A DPP move whose lanes without a source read 0 (bound_ctrl): written as
+// update_dpp(0, x) so the compiler folds it into the single VALU op that
+// consumes it (v_and_b32_dpp in a sweep).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
 template <int Q>
 __device__ __forceinline__ uint32_t gdown(uint32_t x) {
-    if constexpr (Q == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
-    else if constexpr (Q == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x44, 0xF, 0xF, false);  // [0,1,0,1]
-    else if constexpr (Q == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
-    else if constexpr (Q == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    if constexpr (Q == 0) return dpp0<0xA0>(x);        // quad_perm [0,0,2,2]
+    else if constexpr (Q == 1) return dpp0<0x44>(x);   // quad_perm [0,1,0,1]
+    else if constexpr (Q == 2) return dpp0<0x114>(x);  // row_shr:4
+    else if constexpr (Q == 3) return dpp0<0x118>(x);  // row_shr:8
     else if constexpr (Q == 4) return __builtin_amdgcn_permlane16_swap(x, x, false, false)[0];
     else return __builtin_amdgcn_permlane32_swap(x, x, false, false)[0];
 }
@@ -125,10 +117,10 @@ __device__ __forceinline__ uint32_t gdown_j(uint32_t x, uint32_t junk) {
 }
 template <int Q>
 __device__ __forceinline__ uint32_t gup(uint32_t x) {
-    if constexpr (Q == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
-    else if constexpr (Q == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xEE, 0xF, 0xF, false);  // [2,3,2,3]
-    else if constexpr (Q == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104, 0xF, 0xF, false);  // row_shl:4
-    else if constexpr (Q == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x108, 0xF, 0xF, false);  // row_shl:8
+    if constexpr (Q == 0) return dpp0<0xF5>(x);        // quad_perm [1,1,3,3]
+    else if constexpr (Q == 1) return dpp0<0xEE>(x);   // quad_perm [2,3,2,3]
+    else if constexpr (Q == 2) return dpp0<0x104>(x);  // row_shl:4
+    else if constexpr (Q == 3) return dpp0<0x108>(x);  // row_shl:8
     else if constexpr (Q == 4) return __builtin_amdgcn_permlane16_swap(x, x, false, false)[1];
     else return __builtin_amdgcn_permlane32_swap(x, x, false, false)[1];
 }
@@ -163,8 +155,8 @@ __device__ __forceinline__ uint32_t xv(uint32_t x, uint32_t lane) {
     return ((lane >> Q) & 1u) ? d : u;
 }
 
-__device__ __forceinline__ uint32_t xapply(uint32_t M, uint32_t pass, uint32_t keep, uint32_t set) {
-    return (M & pass) | ((M & keep) ? set : 0u);
+__device__ __forceinline__ uint32_t xapply(uint32_t M, uint32_t k, uint32_t cap, uint32_t b) {
+    return __builtin_elementwise_min(M & k, cap) << b;
 }
 
 __device__ __forceinline__ bool idx_has(uint32_t lane, int k, uint32_t q) {
@@ -193,54 +185,61 @@ struct T0Args {
     uint64_t budget;
     int32_t n_order;
     uint32_t init_state, shared_states, flags;
-    uint32_t one;                // 1 (opaque to the compiler: see xacc1)
+    uint32_t one;                // 1 (unused)
 };
 
-// Lane-masked transfer masks of one event: vp/vk[q] = op q's pass/keep on
-// lanes with bit q (0 elsewhere and for q = p); sb[q] = op q's shift.
+// Transfer masks of one event: vk[q] = op q's accept mask on lanes with bit
+// q (0 elsewhere and for q = p); sc[q] / sb[q] = op q's cap / shift.
 struct LaneMasks {
-    uint32_t vp[6], vk[6], sb[10];
+    uint32_t vk[6], sc[10], sb[10];
 };
 
 template <int N>
-__device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t pass_v, uint32_t keep_v, uint32_t b_v,
+__device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t k_v, uint32_t cap_v, uint32_t b_v,
                                            uint32_t lane) {
 #pragma unroll
-    for (int q = 0; q < 6; ++q) { m.vp[q] = 0u; m.vk[q] = 0u; }
+    for (int q = 0; q < 6; ++q) m.vk[q] = 0u;
 #pragma unroll
-    for (int q = 0; q < 10; ++q) m.sb[q] = 0u;
+    for (int q = 0; q < 10; ++q) { m.sc[q] = 0u; m.sb[q] = 0u; }
 #pragma unroll
     for (int q = 0; q < (N < 6 ? N : 6); ++q) {
         const bool on = ((lane >> q) & 1u) && (uint32_t)q != p;
-        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, q), sk = __builtin_amdgcn_readlane(keep_v, q);
-        m.vp[q] = on ? sp : 0u;
+        const uint32_t sk = __builtin_amdgcn_readlane(k_v, q);
         m.vk[q] = on ? sk : 0u;
     }
 #pragma unroll
-    for (int q = 0; q < (N < 10 ? N : 10); ++q) m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
+    for (int q = 0; q < (N < 10 ? N : 10); ++q) {
+        m.sc[q] = __builtin_amdgcn_readlane(cap_v, q);
+        m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
+    }
 }
 
-// One Gauss-Seidel pass over lane-bit positions Q .. min(N, 6) - 1 (`prev`:
-// the previous position's gathered value, dead by now, feeds the permlanes).
+// One Gauss-Seidel pass over lane-bit positions Q .. min(N, 6) - 1.  A
+// position is T_Q applied to the gathered word: min(x & k, cap) << b, OR-ed
+// into cur.  The DPP gathers (Q < 4) have a single use and fold into the
+// v_and_b32 (v_and_b32_dpp); the permlane swaps (Q = 4, 5) clobber both
+// operands, so their other operand is `prev`, the previous position's min()
+// result, dead once it has been shifted into cur -- one copy of cur per swap.
 template <int Q, int N>
-__device__ __forceinline__ uint32_t sweep_lanes(uint32_t cur, const LaneMasks &m, uint32_t one, uint32_t prev = 0) {
+__device__ __forceinline__ uint32_t sweep_lanes(uint32_t cur, const LaneMasks &m, uint32_t prev = 0) {
     if constexpr (Q >= N || Q >= 6) {
         return cur;
     } else {
         const uint32_t x = gdown_j<Q>(cur, prev);
-        return sweep_lanes<Q + 1, N>(xacc1(cur, x, m.vp[Q], m.vk[Q], m.sb[Q], one), m, one, x);
+        const uint32_t t = __builtin_elementwise_min(x & m.vk[Q], m.sc[Q]);
+        return sweep_lanes<Q + 1, N>((t << m.sb[Q]) | cur, m, t);
     }
 }
 
 // Probe count of the oracle for one event (LC_OPT_COUNT_PROBES only): legal
 // successors over I plus legal applications of p.
 template <int RL, int NB>
-__device__ __forceinline__ uint32_t event_probes(const uint32_t *I, uint32_t p, uint32_t cand, uint32_t pass_v,
-                                                 uint32_t keep_v, uint32_t lane, uint32_t pm) {
-    uint32_t pr = 0;  // pm: p's pass | keep
+__device__ __forceinline__ uint32_t event_probes(const uint32_t *I, uint32_t p, uint32_t cand, uint32_t k_v,
+                                                 uint32_t lane, uint32_t pm) {
+    uint32_t pr = 0;  // pm: p's accept mask
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
-        const uint32_t m = ((cand >> q) & 1u) ? (__builtin_amdgcn_readlane(pass_v, q) | __builtin_amdgcn_readlane(keep_v, q)) : 0u;
+        const uint32_t m = ((cand >> q) & 1u) ? __builtin_amdgcn_readlane(k_v, q) : 0u;
 #pragma unroll
         for (int k = 0; k < RL; ++k)
             if (!idx_has(lane, k, (uint32_t)q)) pr += (uint32_t)__popc(I[k] & m);
@@ -269,19 +268,19 @@ extern "C" int lc_debug_sweep_hist(unsigned long long *host) {
 // lm[q] (0 / ~0) is lane bit q as a VGPR mask.  W = S on entry, S' on a
 // normal return.  Returns 0 normal, 1 invalid, 2 budget exceeded.
 template <int T>  // T = 1 + the highest live index (positions T.. are empty)
-__device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, uint32_t pass_v, uint32_t keep_v,
-                                       uint32_t b_v, uint32_t pp, uint32_t pk, uint32_t pb, uint32_t lane,
-                                       const uint32_t (&lm)[6], uint32_t one, uint64_t budget, bool count,
-                                       uint32_t &probes, uint32_t &nSn_out, bool want_size) {
+__device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, uint32_t k_v, uint32_t cap_v,
+                                       uint32_t b_v, uint32_t pk, uint32_t pc, uint32_t pb, uint32_t lane,
+                                       const uint32_t (&lm)[6], uint64_t budget, bool count, uint32_t &probes,
+                                       uint32_t &nSn_out, bool want_size) {
     const uint32_t cand = live & ~(1u << p);
     const uint32_t wup = (uint32_t)__shfl_xor((int)W, 1 << p);
-    // free indices and p hold zero transfers in pass_v / keep_v (the caller
-    // cleared lane p), so a position's masks need no gating by `cand`
+    // free indices and p hold zero accept masks in k_v (the caller cleared
+    // lane p), so a position's masks need no gating by `cand`
     LaneMasks m;
 #pragma unroll
     for (int q = 0; q < T; ++q) {
-        m.vp[q] = vand(__builtin_amdgcn_readlane(pass_v, q), lm[q]);
-        m.vk[q] = vand(__builtin_amdgcn_readlane(keep_v, q), lm[q]);
+        m.vk[q] = vand(__builtin_amdgcn_readlane(k_v, q), lm[q]);
+        m.sc[q] = __builtin_amdgcn_readlane(cap_v, q);
         m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
     }
     const bool hp = (lane >> p) & 1u;
@@ -298,7 +297,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 #endif
 #pragma unroll 1
     for (uint32_t s = 0; s < nc; ++s) {
-        const uint32_t nv = sweep_lanes<0, T>(I, m, one);
+        const uint32_t nv = sweep_lanes<0, T>(I, m);
         const bool ch = nv != I;
         I = nv;
         if (!__any(ch)) {
@@ -311,8 +310,8 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 #ifdef LC_T0_COUNT_SWEEPS
     if (lane == 0) atomicAdd(&lc_sweep_hist[nc * 8 + (done_s < 7 ? done_s : 7)], 1ull);
 #endif
-    if (count) probes += event_probes<1, 6>(&I, p, cand, pass_v, keep_v, lane, pp | pk);
-    Ret = xacc(Ret, I, pp, pk, pb);
+    if (count) probes += event_probes<1, 6>(&I, p, cand, k_v, lane, pk);
+    Ret = xacc(Ret, I, pk, pc, pb);
     // One register holds at most 64 x 32 configs: with a larger budget only
     // emptiness matters (a ballot); exact sizes only when asked for (peak).
     if (__builtin_expect(budget < 64u * 32u, 0)) {
@@ -332,22 +331,21 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 // One :ok(p) event on a lattice of RL registers (N = 7 or 8 ops pending):
 // lane bits 0..5 as in ok_lane, register bits 6.. through register pairs.
 template <int RL, int RM>
-__device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t pass_v, uint32_t keep_v, uint32_t b_v,
+__device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t k_v, uint32_t cap_v, uint32_t b_v,
                                       uint32_t lane, uint64_t budget, bool count, uint32_t &probes,
                                       uint32_t &nSn_out, bool want_size) {
     constexpr int NB = lat_bits<RL>();  // = ops pending
     constexpr int NR = NB - 6;          // register bits
     LaneMasks m;
-    lane_masks<NB>(m, p, pass_v, keep_v, b_v, lane);
-    uint32_t rp[NR], rk[NR];
+    lane_masks<NB>(m, p, k_v, cap_v, b_v, lane);
+    uint32_t rk[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const bool on = (uint32_t)(6 + r) != p;
-        const uint32_t sp = __builtin_amdgcn_readlane(pass_v, 6 + r), sk = __builtin_amdgcn_readlane(keep_v, 6 + r);
-        rp[r] = on ? sp : 0u;
+        const uint32_t sk = __builtin_amdgcn_readlane(k_v, 6 + r);
         rk[r] = on ? sk : 0u;
     }
-    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
+    const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
                    pb = __builtin_amdgcn_readlane(b_v, p);
     uint32_t Ret[RL], I[RL];
     if (count) {
@@ -379,24 +377,23 @@ __device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t pa
     for (int s = 1; s < NB; ++s) {
         uint32_t nv[RL];
 #pragma unroll
-        for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6>(I[k], m, 1u);
+        for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6>(I[k], m);
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
             for (int k = 0; k < RL; ++k)
-                if ((k >> r) & 1) nv[k] = xacc(nv[k], nv[k ^ (1 << r)], rp[r], rk[r], m.sb[6 + r]);
+                if ((k >> r) & 1) nv[k] = xacc(nv[k], nv[k ^ (1 << r)], rk[r], m.sc[6 + r], m.sb[6 + r]);
         bool ch = false;
 #pragma unroll
         for (int k = 0; k < RL; ++k) { ch |= nv[k] != I[k]; I[k] = nv[k]; }
         if (!__any(ch)) break;
     }
     if (count)
-        probes += event_probes<RL, NB>(I, p, ((1u << NB) - 1u) & ~(1u << p), pass_v, keep_v, lane,
-                                       __builtin_amdgcn_readlane(pass_v, p) | __builtin_amdgcn_readlane(keep_v, p));
+        probes += event_probes<RL, NB>(I, p, ((1u << NB) - 1u) & ~(1u << p), k_v, lane, pk);
     uint32_t cI = 0, cS = 0;
 #pragma unroll
     for (int k = 0; k < RL; ++k) {
-        Ret[k] = xacc(Ret[k], I[k], pp, pk, pb);
+        Ret[k] = xacc(Ret[k], I[k], pk, pc, pb);
         cI += (uint32_t)__popc(I[k]);
         cS += (uint32_t)__popc(Ret[k]);
     }
@@ -450,20 +447,19 @@ struct LatMem {
 };
 
 template <int RL>
-__device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_t n, uint32_t pass_v,
-                                            uint32_t keep_v, uint32_t b_v, uint32_t lane, uint64_t budget,
+__device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_t n, uint32_t k_v,
+                                            uint32_t cap_v, uint32_t b_v, uint32_t lane, uint64_t budget,
                                             bool count, uint32_t &probes, uint32_t &nSn_out, bool want_size) {
     constexpr int NB = lat_bits<RL>();
     const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
-    // transfer of candidate q: lane q of pass_v/keep_v/b_v, read at use
+    // transfer of candidate q: lane q of k_v/cap_v/b_v, read at use
     // (not hoisted: 3 x NB scalars would spill SGPRs into the VGPR budget)
-    const uint32_t cpass = pass_v & (((cand >> lane) & 1u) ? ~0u : 0u);
-    const uint32_t ckeep = keep_v & (((cand >> lane) & 1u) ? ~0u : 0u);
-#define PS(Q) __builtin_amdgcn_readlane(cpass, Q)
-#define KP(Q) __builtin_amdgcn_readlane(ckeep, Q)
-#define ST(Q) (1u << __builtin_amdgcn_readlane(b_v, Q))
-    const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
-                   pt = 1u << __builtin_amdgcn_readlane(b_v, p);
+    const uint32_t ck = k_v & (((cand >> lane) & 1u) ? ~0u : 0u);
+#define KK(Q) __builtin_amdgcn_readlane(ck, Q)
+#define CP(Q) __builtin_amdgcn_readlane(cap_v, Q)
+#define SB(Q) __builtin_amdgcn_readlane(b_v, Q)
+    const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
+                   pb = __builtin_amdgcn_readlane(b_v, p);
     const uint32_t plm = p < 6 ? 1u << p : 0u, prm = p >= 6 ? 1u << (p - 6) : 0u;
 #pragma unroll 1
     for (int k = 0; k < RL; ++k) {
@@ -483,13 +479,13 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 #define LC_LANEBIT(Q)                                                                  \
             {                                                                          \
                 const uint32_t y = xv<Q>(x, lane);                                     \
-                acc |= ((lane >> Q) & 1u) ? xapply(y, PS(Q), KP(Q), ST(Q)) : 0u;      \
+                acc |= ((lane >> Q) & 1u) ? xapply(y, KK(Q), CP(Q), SB(Q)) : 0u;      \
             }
             LC_LANEBIT(0) LC_LANEBIT(1) LC_LANEBIT(2) LC_LANEBIT(3) LC_LANEBIT(4) LC_LANEBIT(5)
 #undef LC_LANEBIT
 #pragma unroll
             for (int q = 6; q < NB; ++q)
-                if ((k >> (q - 6)) & 1) acc |= xapply(m.I[(k ^ (1 << (q - 6))) * 64 + lane], PS(q), KP(q), ST(q));
+                if ((k >> (q - 6)) & 1) acc |= xapply(m.I[(k ^ (1 << (q - 6))) * 64 + lane], KK(q), CP(q), SB(q));
             if (acc != x) { m.I[k * 64 + lane] = acc; ch = true; }
         }
         if (!__any(ch)) break;
@@ -501,10 +497,10 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
         if (count) {
 #pragma unroll
             for (int q = 0; q < NB; ++q)
-                if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(x & (PS(q) | KP(q)));
-            probes += (uint32_t)__popc(x & (pp | pk));
+                if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(x & KK(q));
+            probes += (uint32_t)__popc(x & pk);
         }
-        const uint32_t r = m.R[k * 64 + lane] | xapply(x, pp, pk, pt);
+        const uint32_t r = m.R[k * 64 + lane] | xapply(x, pk, pc, pb);
         m.R[k * 64 + lane] = r;
         cI += (uint32_t)__popc(x);
         cS += (uint32_t)__popc(r);
@@ -519,9 +515,9 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
         nSn_out = nSn;
         if (nSn > budget) return 2;
     }
-#undef PS
-#undef KP
-#undef ST
+#undef KK
+#undef CP
+#undef SB
     // relocation: the op at index `last` moves to index p
     const uint32_t last = n - 1;
     const uint32_t llm = last < 6 ? 1u << last : 0u, lrm = last >= 6 ? 1u << (last - 6) : 0u;
@@ -601,7 +597,10 @@ extern "C" int lc_debug_t0_prof(unsigned long long *host) {
 }
 #endif
 
-template <int RM>
+// FAST: no probe counting, no peak sizes and a budget no lattice can exceed
+// (>= 16 x 64 x 32 configs), so every size reduction and budget test folds
+// away -- the common case, and the bench's.
+template <int RM, bool FAST>
 __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_t *ws) {
     const uint32_t lane = lane_id();
     const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
@@ -614,9 +613,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     const uint32_t nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
     const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;  // = max ops pending at once
     if (nstates > T0_MAX_STATES || width > T0_MAX_WIDTH || a.init_state >= T0_MAX_STATES) return K_SPILL;
-    const uint64_t budget = a.budget;
-    const bool want_peak = (a.flags & T0_WANT_PEAK) != 0;
-    const bool count = (a.flags & T0_COUNT) != 0;
+    const uint64_t budget = FAST ? ~0ull : a.budget;
+    const bool want_peak = !FAST && (a.flags & T0_WANT_PEAK) != 0;
+    const bool count = !FAST && (a.flags & T0_COUNT) != 0;
     const uint32_t *const evp = a.events + eb;
     const uint32_t *const trp = a.trans + tb;
     const uint32_t nev = (a.flags & T0_DBG_NOEVENTS) ? 0u : (uint32_t)(ee - eb);
@@ -626,7 +625,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     for (int k = 0; k < RM; ++k) W[k] = 0;
     if (lane == 0) W[0] = 1u << a.init_state;
     bool in_mem = false;   // lattice lives in m.W (9 or 10 ops pending)
-    uint32_t pass_v = 0, keep_v = 0, b_v = 0;  // lane j: transfer of the op at index j
+    uint32_t k_v = 0, cap_v = 0, b_v = 0;  // lane j: transfer (k, cap, b) of the op at index j
     uint32_t slot_v = 0;   // lane j: window slot of the op at index j
     uint32_t dense_v = 0;  // lane s: index of the op in window slot s
     uint32_t n = 0;        // ops pending
@@ -691,14 +690,14 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 if (n >= T0_MAX_WIDTH || slot >= 64) {
                     status = 3;
                 } else {
-                    const Xfer x{(uint32_t)__builtin_amdgcn_readlane(xc.pass, i),
-                                 (uint32_t)__builtin_amdgcn_readlane(xc.keep, i),
+                    const Xfer x{(uint32_t)__builtin_amdgcn_readlane(xc.k, i),
+                                 (uint32_t)__builtin_amdgcn_readlane(xc.cap, i),
                                  (uint32_t)__builtin_amdgcn_readlane(xc.b, i)};
                     const uint32_t idx = (uint32_t)__builtin_ctz(~live);  // lowest free index
                     const bool me = lane == idx;
                     slot_v = me ? slot : slot_v;
-                    pass_v = me ? x.pass : pass_v;
-                    keep_v = me ? x.keep : keep_v;
+                    k_v = me ? x.k : k_v;
+                    cap_v = me ? x.cap : cap_v;
                     b_v = me ? x.b : b_v;
                     dense_v = lane == slot ? idx : dense_v;
                     live |= 1u << idx;
@@ -712,10 +711,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 #else
                 // p's transfer, then p's lane cleared for good: its index is
                 // free after this :ok (and an invalid key stops here)
-                const uint32_t pp = __builtin_amdgcn_readlane(pass_v, p), pk = __builtin_amdgcn_readlane(keep_v, p),
+                const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
                                pb = __builtin_amdgcn_readlane(b_v, p);
-                pass_v = lane == p ? 0u : pass_v;
-                keep_v = lane == p ? 0u : keep_v;
+                k_v = lane == p ? 0u : k_v;
                 // Compact build (many keys per SIMD, throughput): sweeps cover
                 // the positions below the highest live index only.  Wide build
                 // (one key per SIMD, latency): one sweep body for every event --
@@ -724,14 +722,14 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
                 int r;
                 if (RM == T0_RBIG || top >= 6)
-                    r = ok_lane<6>(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
-                                   probes, nSn, want_peak);
+                    r = ok_lane<6>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, budget, count, probes, nSn,
+                                   want_peak);
                 else if (top == 5)
-                    r = ok_lane<5>(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
-                                   probes, nSn, want_peak);
+                    r = ok_lane<5>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, budget, count, probes, nSn,
+                                   want_peak);
                 else
-                    r = ok_lane<4>(W0, p, live, pass_v, keep_v, b_v, pp, pk, pb, lane, lm, a.one, budget, count,
-                                   probes, nSn, want_peak);
+                    r = ok_lane<4>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, budget, count, probes, nSn,
+                                   want_peak);
 #endif
                 live = r ? live : live & ~(1u << p);
                 n = r ? n : n - 1;
@@ -760,14 +758,14 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                         for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < RM ? W[k < RM ? k : 0] : 0u;
                         in_mem = true;
                     }
-                    const Xfer x{(uint32_t)__builtin_amdgcn_readlane(xc.pass, i),
-                                 (uint32_t)__builtin_amdgcn_readlane(xc.keep, i),
+                    const Xfer x{(uint32_t)__builtin_amdgcn_readlane(xc.k, i),
+                                 (uint32_t)__builtin_amdgcn_readlane(xc.cap, i),
                                  (uint32_t)__builtin_amdgcn_readlane(xc.b, i)};
                     const uint32_t idx = n;  // dense: every index below n is taken
                     const bool me = lane == idx;
                     slot_v = me ? slot : slot_v;
-                    pass_v = me ? x.pass : pass_v;
-                    keep_v = me ? x.keep : keep_v;
+                    k_v = me ? x.k : k_v;
+                    cap_v = me ? x.cap : cap_v;
                     b_v = me ? x.b : b_v;
                     dense_v = lane == slot ? idx : dense_v;
                     live |= 1u << idx;
@@ -780,32 +778,31 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 #ifdef LC_ABL_NOOKALL
                 r = 0;  // ablation build: bookkeeping only, every width
 #else
-                if (n == 7) r = ok_reg<2>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-                else if (n == 8) r = ok_reg<4>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                if (n == 7) r = ok_reg<2>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                else if (n == 8) r = ok_reg<4>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                 else if constexpr (RM < 16) {
                     if (n == 9)
-                        r = ok_event_mem<8>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                        r = ok_event_mem<8>(m, p, n, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                     else
-                        r = ok_event_mem<16>(m, p, n, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                        r = ok_event_mem<16>(m, p, n, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                 } else {
-                    if (n == 9) r = ok_reg<8>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
-                    else r = ok_reg<16>(W, p, pass_v, keep_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    if (n == 9) r = ok_reg<8>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
+                    else r = ok_reg<16>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                 }
 #endif
                 // the op at index `last` takes index p (a no-op when p == last)
                 const uint32_t last = n - 1;
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
-                const uint32_t x0 = __builtin_amdgcn_readlane(pass_v, last),
-                               x1 = __builtin_amdgcn_readlane(keep_v, last), x2 = __builtin_amdgcn_readlane(b_v, last);
+                const uint32_t x0 = __builtin_amdgcn_readlane(k_v, last),
+                               x1 = __builtin_amdgcn_readlane(cap_v, last), x2 = __builtin_amdgcn_readlane(b_v, last);
                 const bool mp = lane == p && !r;
                 slot_v = mp ? s_last : slot_v;
-                pass_v = mp ? x0 : pass_v;
-                keep_v = mp ? x1 : keep_v;
+                k_v = mp ? x0 : k_v;
+                cap_v = mp ? x1 : cap_v;
                 b_v = mp ? x2 : b_v;
                 dense_v = (lane == s_last && !r) ? p : dense_v;
                 // index `last` is free now: zero transfer (the lane phase relies on it)
-                pass_v = (lane == last && !r) ? 0u : pass_v;
-                keep_v = (lane == last && !r) ? 0u : keep_v;
+                k_v = (lane == last && !r) ? 0u : k_v;
                 live = r ? live : (1u << last) - 1u;
                 if (RM < 16 && in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
 #pragma unroll
@@ -863,13 +860,15 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
 #ifdef LC_T0_PROFILE
     if (lane_id() < 12) lc_t0_prof_lds[lane_id()] = 0;
 #endif
+    const bool fast = !(a.flags & (T0_COUNT | T0_WANT_PEAK)) && a.budget >= 16ull * 64u * 32u;
     for (int32_t guard = 0; guard <= a.n_order; ++guard) {  // every wave takes at most n_order keys
         int32_t w = 0;
         if (lane_id() == 0) w = atomicAdd(a.ticket, 1);
         w = __builtin_amdgcn_readfirstlane(w);
         if (w >= a.n_order) break;
         const int32_t key = a.order[w];
-        if (lattice_key<RM>(a, key, ws) == K_SPILL) {
+        const int kr = fast ? lattice_key<RM, true>(a, key, ws) : lattice_key<RM, false>(a, key, ws);
+        if (kr == K_SPILL) {
             const Args &f = *a.full;
             push_list(f.spill, f.n_spill, key);
         }
