@@ -28,8 +28,9 @@
 // and positions are applied in place, so one sweep follows every path that
 // adds ops in increasing index order.  A sweep that changes nothing ends the
 // closure, and n - 1 sweeps always suffice (a path has at most n - 1 steps).
-// Transfer masks are lane-masked once per event (zero on lanes without bit
-// q and for q = p), so a sweep position is 5 VALU instructions.
+// Accept masks are lane-masked once per event (zero on lanes without bit q
+// and for q = p), so a sweep position is 3 VALU instructions (v_and_b32_dpp
+// with the gather folded in, v_min_u32, v_lshl_or_b32).
 //
 // Set sizes (budget, peak) are wave popcount reductions and the probe count
 // (LC_OPT_COUNT_PROBES) is accumulated per lane, so every number reported
@@ -89,10 +90,11 @@ __device__ __forceinline__ uint32_t xacc(uint32_t acc, uint32_t x, uint32_t k, u
 //   gdown<q>(x)[L] = x[L - 2^q]   (meaningful on lanes WITH bit q)
 //   gup<q>(x)[L]   = x[L + 2^q]   (meaningful on lanes WITHOUT bit q)
 // One VALU instruction each: DPP quad_perm (q = 0, 1), DPP row_shr / row_shl
-// (q = 2, 3; lanes whose source leaves the row read garbage, which every
-// caller masks), gfx950 v_permlane16_swap / v_permlane32_swap (q = 4, 5).
-// A DPP move whose lanes without a source read 0 (bound_ctrl): written as
-// update_dpp(0, x) so the compiler folds it into the single VALU op that
+// (q = 2, 3; lanes whose source leaves the row read 0), gfx950
+// v_permlane16_swap / v_permlane32_swap (q = 4, 5; the other half of the
+// lanes reads garbage, which every caller masks).
+// A DPP move whose lanes without a source read 0 (bound_ctrl) is written as
+// update_dpp(0, x), so the compiler folds it into the single VALU op that
 // consumes it (v_and_b32_dpp in a sweep).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp0(uint32_t x) {
@@ -721,7 +723,10 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 // across a CU's four lone waves than they save.
                 const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
                 int r;
-                if (RM == T0_RBIG || top >= 6)
+#ifndef LC_T0_WIDE_SPEC  // 1: specialise the wide build too (measured slower on C2)
+#define LC_T0_WIDE_SPEC 0
+#endif
+                if ((RM == T0_RBIG && !LC_T0_WIDE_SPEC) || top >= 6)
                     r = ok_lane<6>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, budget, count, probes, nSn,
                                    want_peak);
                 else if (top == 5)
