@@ -66,6 +66,8 @@ struct lc_dev_batch {
     }
 };
 
+constexpr size_t CTL_BYTES = 4 * sizeof(unsigned long long) + 16 * sizeof(int32_t);
+
 struct lc_ctx {
     lc_opts o{};
     int device = 0;
@@ -76,8 +78,13 @@ struct lc_ctx {
     // scratch, grown on demand
     int64_t cap_keys = 0;
     int32_t *lists = nullptr;      // 4 x cap_keys: spill0, spill1, spill2, wide
-    int32_t *counters = nullptr;   // 16 ints: n_spill0, n_spill1, n_spill2, n_wide, -, tickets[8..15]
-    unsigned long long *acc = nullptr;  // probes, events, keys_done
+    // one 96-byte control block, zeroed and read back in one operation each:
+    // acc (4 x u64: probes, events, keys_done) then counters (16 x i32:
+    // n_spill0, n_spill1, n_spill2, n_wide, -, tickets[8..15])
+    unsigned long long *ctl = nullptr;
+    unsigned long long *acc = nullptr;
+    int32_t *counters = nullptr;
+    unsigned long long *hctl = nullptr;  // pinned host copy of ctl
     int8_t *valid = nullptr;
     int32_t *fail_event = nullptr;
     uint8_t *cause = nullptr;
@@ -97,7 +104,8 @@ struct lc_ctx {
         lcd::HbmWs w{};
     } ws[2];
     ~lc_ctx() {
-        dfree(lists); dfree(counters); dfree(acc); dfree(valid); dfree(fail_event);
+        dfree(lists); dfree(ctl); dfree(valid); dfree(fail_event);
+        if (hctl) (void)hipHostFree(hctl);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(lat_ws); dfree(dargs);
         if (hargs) (void)hipHostFree(hargs);
@@ -207,8 +215,10 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         HIPCHK(hipEventCreate(&c->e0));
         HIPCHK(hipEventCreate(&c->e1));
         HIPCHK(hipEventCreate(&c->et0));
-        HIPCHK(dalloc(&c->counters, 16));
-        HIPCHK(dalloc(&c->acc, 4));
+        HIPCHK(dalloc(&c->ctl, 16));
+        c->acc = c->ctl;
+        c->counters = (int32_t *)(c->ctl + 4);
+        HIPCHK(hipHostMalloc((void **)&c->hctl, 16 * sizeof(unsigned long long), hipHostMallocDefault));
         HIPCHK(dalloc(&c->dargs, 1));
         HIPCHK(hipHostMalloc((void **)&c->hargs, sizeof(lcd::Args), hipHostMallocDefault));
         return LC_OK;
@@ -389,8 +399,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     int32_t *n_spill0 = c->counters + 0, *n_spill1 = c->counters + 1, *n_spill2 = c->counters + 2;
     int32_t *n_wide = c->counters + 3;
 
-    HIPCHK(hipMemsetAsync(c->counters, 0, 16 * sizeof(int32_t), c->stream));
-    HIPCHK(hipMemsetAsync(c->acc, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_BYTES, c->stream));
     if (a.n_final && K > 0) HIPCHK(hipMemsetAsync(a.n_final, 0, (size_t)K * 4, c->stream));
     // T0: every key, LPT order; keys outside the register lattice spill to T1
     lcd::Args a0 = a;
@@ -430,12 +439,11 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     // One readback for the common case.  The T3 (HBM) tier is launched only
     // when T2 left keys for it (its workspace is sized from those counts),
     // after which the readback is repeated.
-    unsigned long long acc[4] = {0, 0, 0, 0};
-    int32_t cnt[16];
+    const unsigned long long *acc = c->hctl;
+    const int32_t *cnt = (const int32_t *)(c->hctl + 4);
     auto readback = [&]() -> int {
         HIPCHK(hipEventRecord(c->e1, c->stream));
-        HIPCHK(hipMemcpyAsync(acc, c->acc, sizeof acc, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(cnt, c->counters, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
         if (!dev_result && K > 0) {
             HIPCHK(hipMemcpyAsync(r->valid, c->valid, (size_t)K, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(r->fail_event, c->fail_event, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
@@ -463,7 +471,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
             if (rc) return rc;
             a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 11;
             HIPCHK(lcd::launch_t3_narrow(a3, c->ws[0].w, slots, c->stream));
-            HIPCHK(hipMemcpyAsync(cnt, c->counters, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
         }
         if (cnt[3] > 0) {
