@@ -172,7 +172,7 @@ using Lat = uint32_t[T0_RBIG];
 
 // T0's kernel arguments: only what the event loop reads, so the loop keeps
 // its scalar registers (the full Args would spill SGPRs into VGPR lanes).
-constexpr uint32_t T0_COUNT = 1, T0_WANT_PEAK = 2, T0_DBG_NOEVENTS = 4, T0_DBG_NOFINAL = 8;
+constexpr uint32_t T0_COUNT = 1, T0_WANT_PEAK = 2, T0_DBG_NOEVENTS = 4, T0_DBG_NOFINAL = 8, T0_WANT_FINAL = 16;
 struct T0Args {
     const uint64_t *ev_off;
     const uint32_t *events;
@@ -327,6 +327,45 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
         if (nSn > budget) return 2;
     }
     W = Ret;
+    return 0;
+}
+
+// Fast path (verdicts only): the lane lattice is kept CLOSED under every
+// pending op instead of holding exactly Knossos's set S.  With C(S) the
+// closure of S under the pending ops, the projection
+//     { (s, L \ p) : (s, L) in C(S_k), p in L }  =  C(S_{k+1}),
+// so an :ok(p) is "close W, then keep the lanes with bit p, shifted down":
+// S_{k+1} is empty iff that projection is.  Any W with S <= W <= C(S) closes
+// to C(S), and W is already closed when no op was invoked since the last
+// :ok (`dirty` false): then the :ok is the projection alone.  Sets are
+// supersets of Knossos's, so this path is used only when no set size, probe
+// count or config list is asked for (FAST in lattice_key).
+// Returns 0 normal, 1 invalid (W unchanged).
+template <int T>
+__device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t live, uint32_t k_v, uint32_t cap_v,
+                                              uint32_t b_v, uint32_t lane, const uint32_t (&lm)[6], bool dirty) {
+    uint32_t C = W;
+    if (dirty) {
+        LaneMasks m;
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+            m.vk[q] = vand(__builtin_amdgcn_readlane(k_v, q), lm[q]);
+            m.sc[q] = __builtin_amdgcn_readlane(cap_v, q);
+            m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
+        }
+        const uint32_t nc = (uint32_t)__popc(live);  // a path has at most nc steps
+#pragma unroll 1
+        for (uint32_t s = 0; s < nc; ++s) {
+            const uint32_t nv = sweep_lanes<0, T>(C, m);
+            const bool ch = nv != C;
+            C = nv;
+            if (!__any(ch)) break;
+        }
+    }
+    const uint32_t up = (uint32_t)__shfl_xor((int)C, 1 << p);  // (a DPP switch on p measured slower)
+    const uint32_t Wn = ((lane >> p) & 1u) ? 0u : up;
+    if (!__any(Wn != 0u)) return 1;
+    W = Wn;
     return 0;
 }
 
@@ -682,6 +721,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     //   dense phase -- 7 to 10 pending, dense indices, W[0..3] or the LDS
     //                  workspace; left after the :ok that brings n back to 6.
     uint32_t W0 = W[0];
+    bool dirty = true;  // FAST: an op was invoked since the lattice was last closed
     for (uint32_t phase = 0; phase <= nev && e < lim; ++phase) {
         while (e < lim) {
             T0_PROF_BEGIN
@@ -704,6 +744,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                     dense_v = lane == slot ? idx : dense_v;
                     live |= 1u << idx;
                     ++n;
+                    dirty = true;
                 }
             } else {
                 const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
@@ -711,6 +752,17 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 #if defined(LC_ABL_NOOK) || defined(LC_ABL_NOOKALL)
                 const int r = 0;  // ablation build: bookkeeping only
 #else
+                int r;
+                if constexpr (FAST && RM == T0_RSMALL) {
+                    // closed sets (compact build only: on C2's lone waves the
+                    // projection's exposed bpermute ate the saved sweeps)
+                    const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
+                    if (top >= 6) r = ok_lane_closed<6>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                    else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                    else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                    dirty = false;
+                    k_v = lane == p ? 0u : k_v;
+                } else {
                 // p's transfer, then p's lane cleared for good: its index is
                 // free after this :ok (and an invalid key stops here)
                 const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
@@ -722,7 +774,6 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 // the specialised copies cost more in instruction-cache misses
                 // across a CU's four lone waves than they save.
                 const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
-                int r;
 #ifndef LC_T0_WIDE_SPEC  // 1: specialise the wide build too (measured slower on C2)
 #define LC_T0_WIDE_SPEC 0
 #endif
@@ -735,6 +786,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 else
                     r = ok_lane<4>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, budget, count, probes, nSn,
                                    want_peak);
+                }
 #endif
                 live = r ? live : live & ~(1u << p);
                 n = r ? n : n - 1;
@@ -825,6 +877,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
             if (n <= 6) break;  // dense indices 0..5: the lane phase's invariant holds
         }
         W0 = W[0];
+        dirty = true;  // the dense phase keeps exact sets, not closed ones
     }
 #undef T0_PROF_BEGIN
 #undef T0_PROF_END
@@ -865,7 +918,7 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
 #ifdef LC_T0_PROFILE
     if (lane_id() < 12) lc_t0_prof_lds[lane_id()] = 0;
 #endif
-    const bool fast = !(a.flags & (T0_COUNT | T0_WANT_PEAK)) && a.budget >= 16ull * 64u * 32u;
+    const bool fast = !(a.flags & (T0_COUNT | T0_WANT_PEAK | T0_WANT_FINAL)) && a.budget >= 16ull * 64u * 32u;
     for (int32_t guard = 0; guard <= a.n_order; ++guard) {  // every wave takes at most n_order keys
         int32_t w = 0;
         if (lane_id() == 0) w = atomicAdd(a.ticket, 1);
@@ -910,7 +963,7 @@ hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipS
     t.key_width = a.key_width; t.key_states = a.key_states; t.order = a.order; t.ticket = a.ticket;
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
     t.init_state = a.init_state; t.shared_states = a.shared_states; t.one = 1u;
-    t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) |
+    t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) | (a.final_cfg ? T0_WANT_FINAL : 0u) |
               (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u);
     if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(grid), dim3(64), 0, s, t);
     else hipLaunchKernelGGL(k_search_lattice<T0_RSMALL>, dim3(grid), dim3(64), 0, s, t);

@@ -132,10 +132,14 @@ class Device:
                           dict(kernel_ms=st.kernel_ms, tier0_ms=st.tier0_ms, total_ms=st.total_ms, probes=st.probes,
                                keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events))
 
-    def check(self, packed: Packed) -> KeyResults:
-        """lc_check_batch: H2D, search, D2H."""
+    def check(self, packed: Packed, verdicts_only: bool = False) -> KeyResults:
+        """lc_check_batch: H2D, search, D2H.  verdicts_only: no peak sizes and
+        no final configs are requested (the library's fast path; `peak`,
+        `final` and `n_final` come back zero)."""
         K = packed.n_keys
         arrs, r = self._alloc(K)
+        if verdicts_only:
+            r = N.LcResult(r.valid, r.fail_event, r.cause, None, None, None)
         st = N.LcStats()
         N.check(N.lib().lc_check_batch(self.handle, C.byref(packed.view), C.byref(r), C.byref(st)))
         return self._results(arrs, K, st)

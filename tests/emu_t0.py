@@ -229,8 +229,33 @@ def ok_event_mem(Wm, p, n, ops):
     return 0, Wn
 
 
-def check_key(events, trans, tb=0, init_state=0):
-    """Model of lattice_key: returns (valid, fail_event) or None (spill)."""
+def ok_lane_closed(W0, p, live, ops, dirty):
+    """ok_lane_closed: close W under every live op (p included), then keep the
+    lanes with bit p, shifted down (the fast path's closed-set invariant)."""
+    C = W0
+    if dirty:
+        vp, vk = [], []
+        for q in range(6):
+            on = ((LANES >> q) & 1 == 1) & bool((live >> q) & 1)
+            vp.append(np.where(on, np.uint32(ops.pas[q]), np.uint32(0)).astype(np.uint32))
+            vk.append(np.where(on, np.uint32(ops.keep[q]), np.uint32(0)).astype(np.uint32))
+        sb = [ops.b[q] for q in range(6)]
+        for _s in range(bin(live).count("1")):
+            nv = sweep_lanes(C, vp, vk, sb, 6)
+            ch = (nv != C).any()
+            C = nv
+            if not ch:
+                break
+    hp = (LANES >> p) & 1 == 1
+    Wn = np.where(hp, 0, gup(C, p)).astype(np.uint32)
+    if not Wn.any():
+        return 1, W0
+    return 0, Wn
+
+
+def check_key(events, trans, tb=0, init_state=0, closed=False):
+    """Model of lattice_key: returns (valid, fail_event) or None (spill).
+    closed: the fast path's lane phase (closed sets, ok_lane_closed)."""
     W = [np.zeros(64, np.uint32) for _ in range(16)]
     W[0][0] = 1 << init_state
     ops = Ops()
@@ -238,6 +263,7 @@ def check_key(events, trans, tb=0, init_state=0):
     dense = [0] * 128
     n = 0
     live = 0
+    dirty = True
     for j, ev in enumerate(events):
         ev = int(ev)
         slot = (ev >> 24) & 0x7F
@@ -251,10 +277,15 @@ def check_key(events, trans, tb=0, init_state=0):
             dense[slot] = idx
             live |= 1 << idx
             n += 1
+            dirty = True
             continue
         p = dense[slot]
         if n <= 6:
-            st, W0 = ok_lane(W[0], p, live, ops)
+            if closed:
+                st, W0 = ok_lane_closed(W[0], p, live, ops, dirty)
+                dirty = False
+            else:
+                st, W0 = ok_lane(W[0], p, live, ops)
             if st == 1:
                 return 0, j
             W[0] = W0
@@ -275,4 +306,5 @@ def check_key(events, trans, tb=0, init_state=0):
             dense[s_last] = p
         n -= 1
         live = (1 << n) - 1
+        dirty = True  # the dense phase keeps exact sets
     return 1, -1

@@ -153,3 +153,20 @@ def test_compact_t0_build_heavy_widths(device):
     h = H.synth(n_keys=2600, ops_per_key=120, concurrency=10, anomaly_rate=0.1, seed=41)
     _, res, _ = device_vs_oracle(h, device)
     assert (res.valid == 0).any()
+
+
+@pytest.mark.parametrize("shape", ["c2", "c5", "compact_heavy", "high_concurrency", "many_values"])
+def test_verdicts_only_fast_path(shape):
+    """Verdict-only requests take T0's fast path (the compact build keeps its
+    lane lattice closed under the pending ops instead of holding Knossos's
+    exact set); verdicts, causes and failing events must stay bit-exact."""
+    dev = Device(0)  # no probe counting: the fast path is eligible
+    h = {
+        "c2": lambda: H.synth(n_keys=300, ops_per_key=1000, concurrency=10, seed=2),
+        "c5": lambda: H.synth(n_keys=400, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=5),
+        "compact_heavy": lambda: H.synth(n_keys=2600, ops_per_key=120, concurrency=10, anomaly_rate=0.1, seed=41),
+        "high_concurrency": lambda: H.synth(n_keys=64, ops_per_key=600, concurrency=16, seed=17),
+        "many_values": lambda: H.synth(n_keys=32, ops_per_key=600, concurrency=8, n_values=5000,
+                                       anomaly_rate=0.2, seed=21),
+    }[shape]()
+    device_vs_oracle(h, dev, verdicts_only=True)
