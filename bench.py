@@ -121,12 +121,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, tier0_ms, probes, deep = [], [], 0, 0
+    kernel_ms, tier0_ms, tier3_ms, probes, deep = [], [], [], 0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
         kernel_ms.append(st.kernel_ms)
         tier0_ms.append(st.tier0_ms)
+        tier3_ms.append(st.tier3_ms)
         deep = st.deep_keys
     torch.cuda.synchronize()
     if world > 1:
@@ -145,7 +146,8 @@ def main():
         # probe count from one extra, untimed pass with
         # LC_OPT_COUNT_PROBES: the timed steps skip the per-event popcounts
         dev_c = Device(local, budget=args.budget, count_probes=True)
-        probes = dev_c.upload(packed).check(peak=False).stats["probes"]
+        pst = dev_c.upload(packed).check(peak=False).stats
+        probes, probes_t3 = pst["probes"], pst["probes_t3"]
         del dev_c
 
     if rank == 0:
@@ -162,6 +164,15 @@ def main():
         # event 4 B + cause 1 B) written per key.
         alg_bytes = 4 * n_events + 8 * (K + 1) + 4 * K + 4 * int(packed.view.n_trans) + 6 * K
         achieved = alg_bytes / (avg_t0_ms * 1e-3) / 1e9
+        dominant = "k_search_lattice (T0)"
+        avg_t3_ms = float(np.mean(tier3_ms))
+        if avg_t3_ms > avg_t0_ms:
+            # The HBM tier dominates (deep keys, C4): its algorithmic traffic
+            # is SURVEY.md 8(d) D-4's one 64 B line per hash probe, counted
+            # for that tier alone, over the span of its launches.
+            dominant = "k_search_hbm (T3)"
+            alg_bytes = 64 * probes_t3
+            achieved = alg_bytes / (avg_t3_ms * 1e-3) / 1e9
         # SURVEY.md 8(d) D-4's notional model (16 B A3 record per op, 17 B per
         # key, one 64 B HBM line per probe) for comparison only: in T0 the
         # probes never leave registers.
@@ -212,13 +223,16 @@ def main():
                        "concurrency": cfg["concurrency"], "budget": args.budget,
                        "parallelism": f"keys sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
+                         "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "kernel_ms": avg_kernel_ms,
             "tier0_ms": avg_t0_ms,
+            "tier3_ms": avg_t3_ms,
+            "probes_t3": probes_t3,
             "ns_per_event_critical_path": avg_t0_ms * 1e6 / max(max_events, 1),
             "probes_per_s": probes / (avg_kernel_ms * 1e-3),
-            "d4_model_gbs": d4_bytes / (avg_t0_ms * 1e-3) / 1e9,
+            "d4_model_gbs": d4_bytes / (avg_kernel_ms * 1e-3) / 1e9,
             "deep_keys": deep,
             "verdicts": {"valid": int((v_host == 1).sum()), "invalid": int((v_host == 0).sum()),
                          "unknown": int((v_host == -1).sum())},

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 2
+#define LC_ABI_VERSION 3
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -247,6 +247,8 @@ typedef struct lc_stats {
     uint64_t deep_keys;       /* keys (re)searched in the HBM tier              */
     uint64_t events;          /* events processed                               */
     double   tier0_ms;        /* device time of the register-lattice tier alone */
+    double   tier3_ms;        /* device time of the HBM tier launches (0 if none) */
+    uint64_t probes_t3;       /* the part of `probes` made by the HBM tier      */
 } lc_stats;
 
 typedef struct lc_ctx lc_ctx;

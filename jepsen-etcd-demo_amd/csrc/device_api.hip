@@ -73,7 +73,7 @@ struct lc_ctx {
     int device = 0;
     int cu_count = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr, et3a = nullptr, et3b = nullptr;
     std::mutex mu;
     // scratch, grown on demand
     int64_t cap_keys = 0;
@@ -112,6 +112,8 @@ struct lc_ctx {
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (et0) (void)hipEventDestroy(et0);
+        if (et3a) (void)hipEventDestroy(et3a);
+        if (et3b) (void)hipEventDestroy(et3b);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -215,6 +217,8 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         HIPCHK(hipEventCreate(&c->e0));
         HIPCHK(hipEventCreate(&c->e1));
         HIPCHK(hipEventCreate(&c->et0));
+        HIPCHK(hipEventCreate(&c->et3a));
+        HIPCHK(hipEventCreate(&c->et3b));
         HIPCHK(dalloc(&c->ctl, 16));
         c->acc = c->ctl;
         c->counters = (int32_t *)(c->ctl + 4);
@@ -461,8 +465,12 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     };
     rc = readback();
     if (rc) return rc;
+    bool t3 = false;
+    const unsigned long long probes_pre_t3 = acc[0];
     if (K > 0 && (cnt[2] > 0 || cnt[3] > 0)) {
         // T3 (HBM tier): keys beyond T2, then keys needing wide configs
+        t3 = true;
+        HIPCHK(hipEventRecord(c->et3a, c->stream));
         lcd::Args a3 = a;
         a3.wide = wide; a3.n_wide = n_wide;
         if (cnt[2] > 0) {
@@ -481,15 +489,19 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
             a3.order = wide; a3.n_order = 0; a3.n_in = n_wide; a3.ticket = c->counters + 12;
             HIPCHK(lcd::launch_t3_wide(a3, c->ws[1].w, slots, c->stream));
         }
+        HIPCHK(hipEventRecord(c->et3b, c->stream));
         rc = readback();
         if (rc) return rc;
     }
-    float ms = 0, ms0 = 0;
+    float ms = 0, ms0 = 0, ms3 = 0;
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
     if (K > 0) HIPCHK(hipEventElapsedTime(&ms0, c->e0, c->et0));
+    if (t3) HIPCHK(hipEventElapsedTime(&ms3, c->et3a, c->et3b));
     if (st) {
         st->kernel_ms = ms;
         st->tier0_ms = ms0;
+        st->tier3_ms = ms3;
+        st->probes_t3 = t3 ? acc[0] - probes_pre_t3 : 0;
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         st->probes = acc[0];
         st->events = acc[1];

@@ -29,6 +29,21 @@
 
 namespace lcd {
 
+// Diagnostic build only (make variant VFLAGS=-DLC_T3_PROF): thread 0 of the
+// first blocks accumulates shader cycles per :ok phase and prints them when a
+// key finishes.  Never in the product library.
+#ifdef LC_T3_PROF
+#define T3P_DECL uint64_t t3p[6] = {0, 0, 0, 0, 0, 0}, t3last = 0, t3lev = 0, t3gen = 0, t3nok = 0;
+#define T3P_MARK(i) do { if (tid == 0) { const uint64_t t_ = __builtin_readcyclecounter(); if ((i) >= 0) t3p[(i) < 0 ? 0 : (i)] += t_ - t3last; t3last = t_; } } while (0)
+#define T3P_ADD(v, x) do { if (tid == 0) v += (x); } while (0)
+#define T3P_PRINT() do { if (tid == 0 && blockIdx.x < 4) printf("T3PROF key %d ok %llu erase %llu part %llu close %llu apply %llu lev %llu gen %llu nS %u\n", key, (unsigned long long)t3nok, (unsigned long long)t3p[0], (unsigned long long)t3p[1], (unsigned long long)t3p[2], (unsigned long long)t3p[3], (unsigned long long)t3lev, (unsigned long long)t3gen, nS); } while (0)
+#else
+#define T3P_DECL
+#define T3P_MARK(i) do {} while (0)
+#define T3P_ADD(v, x) do {} while (0)
+#define T3P_PRINT() do {} while (0)
+#endif
+
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr uint64_t BUSY = 1ull << 63;
 
@@ -43,14 +58,57 @@ struct Narrow {
     __device__ static T drop(T c, uint32_t p) { return c & ~(1ull << p); }
     __device__ static void rec(T c, uint64_t &w0, uint64_t &w1) { w0 = c & LMASK; w1 = (c >> 56) << 48; }
     __device__ static void erase(T *tab, uint32_t pos) { tab[pos] = EMPTY; }
+    static constexpr int U = 4;  // inserts in flight per lane
+    // Small :oks keep both hash sets in LDS (LDS_E slots each, at most
+    // LDS_LIM configs per set); larger ones use the HBM tables.
+    static constexpr bool LDS_MODE = true;
+    static constexpr uint32_t LDS_E = 4096, LDS_LIM = 2048;
     __device__ static bool insert(T *tab, uint32_t mask, T key, uint32_t &pos, uint32_t *err) {
-        uint32_t h = hash64(key) & mask;
+        return insert_at(tab, mask, key, hash64(key) & mask, pos);
+    }
+    __device__ static bool insert_at(T *tab, uint32_t mask, T key, uint32_t h, uint32_t &pos) {
         for (;;) {
             unsigned long long old = atomicCAS((unsigned long long *)&tab[h], (unsigned long long)EMPTY,
                                                (unsigned long long)key);
             if (old == EMPTY) { pos = h; return true; }
             if (old == key) { pos = h; return false; }
             h = (h + 1) & mask;
+        }
+    }
+    // U inserts per lane with their first probes in flight together: the
+    // CASes are independent, so one wait covers all of them; a lane whose
+    // first slot holds another config continues serially from there.
+    // Two thirds of the closure's probes meet a config already in the set
+    // (C4), and every atomic executes at the memory side, so the home slots
+    // are read first (L2-served, L1 bypassed): a slot that already holds the
+    // key is a duplicate and costs no atomic.  A stale EMPTY only means one
+    // CAS more; a key cannot read stale, since its slot was erased by this
+    // workgroup's own earlier stores.
+    __device__ static void insert_n(T *tab, uint32_t mask, const T (&key)[U], const bool (&act)[U],
+                                    uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err) {
+        uint32_t h[U];
+        unsigned long long old[U];
+        bool need[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            h[u] = hash64(key[u]) & mask;
+            old[u] = act[u] ? __hip_atomic_load((unsigned long long *)&tab[h[u]], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : (unsigned long long)key[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            need[u] = old[u] != (unsigned long long)key[u];
+            old[u] = need[u] ? atomicCAS((unsigned long long *)&tab[h[u]], (unsigned long long)EMPTY,
+                                         (unsigned long long)key[u])
+                             : old[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pos[u] = h[u];
+            isnew[u] = act[u] && old[u] == EMPTY;
+            if (act[u] && old[u] != EMPTY && old[u] != key[u])
+                isnew[u] = insert_at(tab, mask, key[u], (h[u] + 1) & mask, pos[u]);
         }
     }
 };
@@ -77,6 +135,18 @@ struct Wide {
     __device__ static void rec(T c, uint64_t &w0, uint64_t &w1) { w0 = c.lo; w1 = c.hi; }
     __device__ static void erase(T *tab, uint32_t pos) { tab[pos].hi = EMPTY; }
     __device__ static uint32_t hash(T c) { return hash64(c.lo ^ (c.hi * 0x9E3779B97F4A7C15ull)); }
+    static constexpr int U = 2;
+    static constexpr bool LDS_MODE = false;  // the publish protocol is HBM-only
+    static constexpr uint32_t LDS_E = 1, LDS_LIM = 0;
+    // Wide inserts keep their publish protocol: one at a time.
+    __device__ static void insert_n(T *tab, uint32_t mask, const T (&key)[U], const bool (&act)[U],
+                                    uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pos[u] = NOPOS;
+            isnew[u] = act[u] && insert(tab, mask, key[u], pos[u], err);
+        }
+    }
     __device__ static bool insert(T *tab, uint32_t mask, T key, uint32_t &pos, uint32_t *err) {
         uint32_t h = hash(key) & mask;
         for (;;) {
@@ -115,9 +185,12 @@ struct HbmShared {
     uint32_t slot_desc[128];
     uint32_t cand_slot[128];
     uint32_t cand_desc[128];
-    uint32_t nSn, nI, stop, err;
+    uint32_t nSn, nI, stop, err, redo;
     int32_t work;
     unsigned long long probes;
+    // closure successors staged per wave until 64 x U are ready to insert
+    typename C::T stage[WG / 64][64 * C::U + 64];
+    uint64_t lt[2][C::LDS_E];  // LDS-mode hash sets: [0] S', [1] I
 };
 
 // Sum of one value over the workgroup (every thread gets it).
@@ -192,6 +265,190 @@ __device__ void erase_all(const HbmWs &w, Slot<C> &sl, const uint32_t *posI, uin
     __syncthreads();
 }
 
+// Insert into an LDS-mode hash set (narrow configs).  The probe sequence is
+// bounded: a table that fills up (sets past LDS_LIM, plus other waves'
+// in-flight batches) raises `redo` and the :ok is run again on HBM tables.
+template <class C>
+__device__ __forceinline__ bool lds_set_insert(uint64_t *tab, uint64_t key, bool active, uint32_t &pos,
+                                               uint32_t *redo) {
+    bool isnew = false;
+    uint32_t h = hash64(key) & (C::LDS_E - 1);
+    bool done = !active;
+    for (uint32_t n = 0; !done; ++n) {
+        if (n == C::LDS_E) { *redo = 1; break; }
+        const unsigned long long old = atomicCAS((unsigned long long *)&tab[h], (unsigned long long)EMPTY,
+                                                 (unsigned long long)key);
+        if (old == EMPTY) { isnew = true; done = true; }
+        else if (old == key) { done = true; }
+        else { h = (h + 1) & (C::LDS_E - 1); }
+    }
+    pos = h;
+    return isnew;
+}
+
+template <class C, int WG, bool LDS>
+__device__ __forceinline__ void set_insert_n(HbmShared<C, WG> &sh, typename C::T *htab, int which, uint32_t hmask,
+                                             const typename C::T (&key)[C::U], const bool (&act)[C::U],
+                                             uint32_t (&pos)[C::U], bool (&nw)[C::U]) {
+    if constexpr (LDS) {
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) nw[u] = lds_set_insert<C>(sh.lt[which], key[u], act[u], pos[u], &sh.redo);
+    } else {
+        C::insert_n(htab, hmask, key, act, pos, nw, &sh.err);
+    }
+}
+
+// Position r of a new config: past the set's limit it is an error in HBM
+// mode (cap covers every overshoot) and a redo in LDS mode.
+template <class C, int WG, bool LDS>
+__device__ __forceinline__ bool take_pos(HbmShared<C, WG> &sh, uint32_t r, uint32_t cap) {
+    if (LDS && r >= C::LDS_LIM) { sh.redo = 1; sh.stop = 1; }
+    if (r < cap) return true;
+    sh.err = 1;
+    return false;
+}
+
+// Insert the first n (<= 64 x U) staged successors of this wave into the I
+// set and append the new ones (wave-uniform call).  A stop raised by any wave
+// caps the overshoot past the budget at WG x U configs (cap covers it).
+template <class C, int WG, bool LDS>
+__device__ void flush_stage(typename C::T *stg, uint32_t n, Slot<C> &sl, HbmShared<C, WG> &sh, uint32_t hmask,
+                            uint32_t cap, uint64_t budget) {
+    constexpr int U = C::U;
+    typename C::T key[U];
+    bool act[U], nw[U];
+    uint32_t pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t i = (uint32_t)u * 64u + lane_id();
+        act[u] = i < n;
+        key[u] = act[u] ? stg[i] : C::init(0);
+    }
+    set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, key, act, pos, nw);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t r = block_append<WG>(&sh.nI, nw[u]);
+        if (nw[u]) {
+            if (take_pos<C, WG, LDS>(sh, r, cap)) { sl.I[r] = key[u]; sl.posI[r] = pos[u]; }
+            if (r + 1 > budget) sh.stop = 1;
+        }
+    }
+}
+
+enum { PASS_OK = 0, PASS_CLOSURE_STOP = 1, PASS_REDO = 2 };
+
+// One :ok(p) over the config set S (nS configs): S' into Sn, I in sl.I, with
+// the hash sets in LDS (LDS) or in the block's HBM tables.  Counters sh.nSn /
+// sh.nI / stop / err / redo are zero on entry.
+template <class C, int WG, bool LDS>
+__device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typename C::T *S, uint32_t nS,
+                       typename C::T *Sn, uint32_t *posSn, uint32_t p, uint32_t dp, uint32_t nc, uint32_t cap,
+                       uint32_t hmask, uint64_t &probes) {
+    using T = typename C::T;
+    constexpr int U = C::U;
+    const uint32_t tid = threadIdx.x;
+    if constexpr (LDS) {
+        for (uint32_t j = tid; j < 2 * C::LDS_E; j += WG) (&sh.lt[0][0])[j] = EMPTY;
+        __syncthreads();
+    }
+    // -- partition S (U configs per thread, their inserts in flight together)
+    for (uint32_t j0 = 0; j0 < nS; j0 += WG * U) {
+        T kS[U], kI[U];
+        bool hasp[U], toI[U], ns[U], ni[U];
+        uint32_t pS[U], pI[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = j0 + u * WG + tid;
+            const bool act = j < nS;
+            const T c = act ? S[j] : C::init(0);
+            hasp[u] = act && C::has(c, p);
+            toI[u] = act && !hasp[u];
+            kS[u] = C::drop(c, p);
+            kI[u] = c;
+        }
+        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, kS, hasp, pS, ns);
+        set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, kI, toI, pI, ni);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t rs = block_append<WG>(&sh.nSn, ns[u]);
+            const uint32_t ri = block_append<WG>(&sh.nI, ni[u]);
+            if (ns[u] && take_pos<C, WG, LDS>(sh, rs, cap)) { Sn[rs] = kS[u]; posSn[rs] = pS[u]; }
+            if (ni[u] && take_pos<C, WG, LDS>(sh, ri, cap)) { sl.I[ri] = kI[u]; sl.posI[ri] = pI[u]; }
+        }
+    }
+    if (tid == 0) probes += nS;
+    __syncthreads();
+    // -- JIT closure, level by level.  Each wave stages the legal successors
+    // of its configs in LDS and inserts them 64 x U at a time, so every
+    // insert batch is full whatever fraction of the (config, candidate)
+    // pairs is legal.
+    uint32_t head = 0;
+    T *stg = sh.stage[tid >> 6];
+    while (true) {
+        const uint32_t end = sh.nI < cap ? sh.nI : cap;
+        if (head >= end || sh.stop || nc == 0) break;
+        uint32_t nst = 0;  // wave-uniform
+        bool halt = false;
+        for (uint32_t j0 = head; j0 < end && !halt; j0 += WG) {
+            const uint32_t j = j0 + tid;
+            const bool in = j < end;
+            const T c = in ? sl.I[j] : C::init(0);
+            const uint32_t st = C::state(c);
+            for (uint32_t k = 0; k < nc; ++k) {
+                const uint32_t q = sh.cand_slot[k];
+                uint32_t s2 = 0;
+                const bool act = in && !C::has(c, q) && step(st, sh.cand_desc[k], s2);
+                probes += act;
+                const uint64_t m = __ballot(act);
+                if (m == 0) continue;
+                if (act) stg[nst + rank_of(m)] = C::lin(c, q, s2);
+                nst += (uint32_t)__popcll(m);
+                if (nst >= 64u * U) {
+                    flush_stage<C, WG, LDS>(stg, 64u * U, sl, sh, hmask, cap, a.budget);
+                    nst -= 64u * U;
+                    if (lane_id() < nst) stg[lane_id()] = stg[64u * U + lane_id()];
+                    if (*(volatile uint32_t *)&sh.stop) { halt = true; break; }
+                }
+            }
+        }
+        if (nst && !halt) flush_stage<C, WG, LDS>(stg, nst, sl, sh, hmask, cap, a.budget);
+        __syncthreads();
+        head = end;
+    }
+    __syncthreads();
+    if (LDS && sh.redo) return PASS_REDO;
+    if (sh.nI > a.budget || sh.err) return PASS_CLOSURE_STOP;
+    // -- apply p
+    const uint32_t nI = sh.nI;
+    for (uint32_t j0 = 0; j0 < nI; j0 += WG * U) {
+        if (*(volatile uint32_t *)&sh.stop) break;
+        T k2[U];
+        bool act[U], nw[U];
+        uint32_t pos[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = j0 + u * WG + tid;
+            const T c = j < nI ? sl.I[j] : C::init(0);
+            uint32_t s2 = 0;
+            act[u] = j < nI && step(C::state(c), dp, s2);
+            probes += act[u];
+            k2[u] = C::restate(c, s2);
+        }
+        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, k2, act, pos, nw);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t r = block_append<WG>(&sh.nSn, nw[u]);
+            if (nw[u]) {
+                if (take_pos<C, WG, LDS>(sh, r, cap)) { Sn[r] = k2[u]; posSn[r] = pos[u]; }
+                if (r + 1 > a.budget) sh.stop = 1;
+            }
+        }
+    }
+    __syncthreads();
+    if (LDS && sh.redo) return PASS_REDO;
+    return PASS_OK;
+}
+
 // Search one key with the whole workgroup.  Returns K_DONE or K_WIDE.
 template <class C, int WG>
 __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C> &sl, HbmShared<C, WG> &sh) {
@@ -206,9 +463,10 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
     if (tid == 0) { sl.S[0][0] = C::init(a.init_state); sl.posS[0][0] = NOPOS; sh.err = 0; sh.probes = 0; }
     __syncthreads();
     int cur = 0;
-    uint32_t nS = 1, nSprev = 0, nIlast = 0, peak = 1;
+    uint32_t nS = 1, nSprev = 0, nIlast = 0, peak = 1, nIbig = 0;
     uint64_t pend0 = 0, pend1 = 0;
     uint64_t probes = 0;  // this thread's share
+    T3P_DECL
     for (uint64_t base = b; base < e; base += WG) {
         const uint32_t cnt = (uint32_t)((e - base) < WG ? (e - base) : WG);
         __syncthreads();
@@ -240,6 +498,8 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
             typename C::T *Sn = sl.S[cur ^ 1];
             uint32_t *posSn = sl.posS[cur ^ 1];
             __syncthreads();  // slot_desc of earlier invokes visible
+            T3P_MARK(-1);
+            T3P_ADD(t3nok, 1);
             const uint32_t dp = sh.slot_desc[p];
             for (uint32_t j = tid; j < nIlast; j += WG) C::erase(sl.hI, sl.posI[j]);
             for (uint32_t j = tid; j < nSprev; j += WG) {
@@ -258,98 +518,61 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
                     sh.cand_desc[r] = sh.slot_desc[tid];
                 }
             }
-            if (tid == 0) { sh.nSn = 0; sh.nI = 0; sh.stop = 0; }
-            __threadfence_block();
-            __syncthreads();
-            // -- partition S
-            for (uint32_t j0 = 0; j0 < nS; j0 += WG) {
-                const uint32_t j = j0 + tid;
-                const bool act = j < nS;
-                typename C::T c = act ? S[j] : C::init(0);
-                const bool hasp = act && C::has(c, p);
-                const bool toI = act && !hasp;
-                uint32_t pos = NOPOS;
-                bool ns = false, ni = false;
-                if (hasp) ns = C::insert(sl.hS, hmask, C::drop(c, p), pos, &sh.err);
-                if (toI) ni = C::insert(sl.hI, hmask, c, pos, &sh.err);
-                const uint32_t rs = block_append<WG>(&sh.nSn, ns);
-                const uint32_t ri = block_append<WG>(&sh.nI, ni);
-                if (ns) { Sn[rs] = C::drop(c, p); posSn[rs] = pos; }
-                if (ni) { sl.I[ri] = c; sl.posI[ri] = pos; }
-            }
-            if (tid == 0) probes += nS;
-            __syncthreads();
-            // -- JIT closure, level by level
-            uint32_t head = 0;
-            while (true) {
-                const uint32_t end = sh.nI;
-                if (head >= end || sh.stop || nc == 0) break;
-                const uint32_t total = (end - head) * nc;
-                for (uint32_t it0 = 0; it0 < total; it0 += WG) {
-                    const uint32_t item = it0 + tid;
-                    bool act = item < total && !*(volatile uint32_t *)&sh.stop;
-                    const uint32_t ci = act ? head + item / nc : head;
-                    const uint32_t k = act ? item % nc : 0;
-                    const typename C::T c = sl.I[ci];
-                    const uint32_t q = sh.cand_slot[k];
-                    uint32_t s2 = 0;
-                    act = act && !C::has(c, q) && step(C::state(c), sh.cand_desc[k], s2);
-                    probes += act;
-                    uint32_t pos = NOPOS;
-                    const typename C::T c2 = C::lin(c, q, s2);
-                    const bool nw = act && C::insert(sl.hI, hmask, c2, pos, &sh.err);
-                    const uint32_t r = block_append<WG>(&sh.nI, nw);
-                    if (nw) {
-                        if (r < cap) { sl.I[r] = c2; sl.posI[r] = pos; } else sh.err = 1;
-                        if (r + 1 > a.budget) sh.stop = 1;
-                    }
-                }
+            // Small sets run with both hash sets in LDS; a pass that outgrows
+            // them is discarded (S is untouched) and run again on the HBM
+            // tables, which the erasure above has left clean.
+            bool lds = C::LDS_MODE && nS <= C::LDS_LIM && nIbig <= C::LDS_LIM;
+            const uint64_t probes0 = probes;
+            int pr;
+            for (;;) {
+                if (tid == 0) { sh.nSn = 0; sh.nI = 0; sh.stop = 0; sh.redo = 0; }
+                __threadfence_block();
                 __syncthreads();
-                head = end;
+                T3P_MARK(0);
+                if constexpr (C::LDS_MODE) {
+                    if (lds)
+                        pr = ok_pass<C, WG, true>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, probes);
+                    else
+                        pr = ok_pass<C, WG, false>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, probes);
+                } else {
+                    pr = ok_pass<C, WG, false>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, probes);
+                }
+                if (pr != PASS_REDO) break;
+                lds = false;
+                probes = probes0;
             }
-            __syncthreads();
+            T3P_MARK(2);
             const uint32_t nI = sh.nI < cap ? sh.nI : cap;
-            if (sh.nI > a.budget || sh.err) {
+            nIbig = sh.nI;
+            if (pr == PASS_CLOSURE_STOP) {
+                T3P_PRINT();
                 const int cause = sh.err ? LC_CAUSE_ERROR : LC_CAUSE_BUDGET;
                 const uint32_t nSn_now = sh.nSn;
-                erase_all<C, WG>(w, sl, sl.posI, nI, posSn, nSn_now);
+                if (!lds) erase_all<C, WG>(w, sl, sl.posI, nI, posSn, nSn_now);
                 write_final_hbm<C, WG>(a, key, S, nS);
                 probes = block_sum<WG>(probes, &sh.probes);
                 if (tid == 0) finish_key(a, key, LC_UNKNOWN, cause, evno, peak, probes, (uint64_t)evno);
                 return K_DONE;
             }
-            // -- apply p
-            for (uint32_t j0 = 0; j0 < nI; j0 += WG) {
-                const uint32_t j = j0 + tid;
-                bool act = j < nI && !*(volatile uint32_t *)&sh.stop;
-                const typename C::T c = act ? sl.I[j] : C::init(0);
-                uint32_t s2 = 0;
-                act = act && step(C::state(c), dp, s2);
-                probes += act;
-                uint32_t pos = NOPOS;
-                const typename C::T c2 = C::restate(c, s2);
-                const bool nw = act && C::insert(sl.hS, hmask, c2, pos, &sh.err);
-                const uint32_t r = block_append<WG>(&sh.nSn, nw);
-                if (nw) {
-                    if (r < cap) { Sn[r] = c2; posSn[r] = pos; } else sh.err = 1;
-                    if (r + 1 > a.budget) sh.stop = 1;
-                }
-            }
-            __syncthreads();
+#ifdef LC_T3_PROF
+            if (tid == 0 && blockIdx.x == 0)
+                printf("T3OK key %d ev %d nS %u nI %u nSn %u nc %u lds %d setup %llu pass %llu\n", key, evno, nS, nI, sh.nSn, nc,
+                       (int)lds, (unsigned long long)t3p[0], (unsigned long long)t3p[2]);
+#endif
             const uint32_t nSn_all = sh.nSn;
             const uint32_t nSn = nSn_all < cap ? nSn_all : cap;
-            nIlast = nI;
+            nIlast = lds ? 0u : nI;  // HBM entries the next :ok erases
             if (nSn_all == 0 || nSn_all > a.budget || sh.err) {
                 const int verdict = nSn_all == 0 ? LC_INVALID : LC_UNKNOWN;
                 const int cause = sh.err ? LC_CAUSE_ERROR : (nSn_all == 0 ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET);
-                erase_all<C, WG>(w, sl, sl.posI, nI, posSn, nSn);
+                if (!lds) erase_all<C, WG>(w, sl, sl.posI, nI, posSn, nSn);
                 write_final_hbm<C, WG>(a, key, S, nS);
                 probes = block_sum<WG>(probes, &sh.probes);
                 if (tid == 0)
                     finish_key(a, key, verdict, cause, evno, peak, probes, (uint64_t)evno + (verdict == LC_INVALID));
                 return K_DONE;
             }
-            nSprev = nSn;
+            nSprev = lds ? 0u : nSn;
             cur ^= 1;
             nS = nSn;
             peak = nS > peak ? nS : peak;
@@ -357,6 +580,7 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
         }
     }
     __syncthreads();
+    T3P_PRINT();
     erase_all<C, WG>(w, sl, sl.posI, nIlast, sl.posS[cur], nSprev);
     write_final_hbm<C, WG>(a, key, sl.S[cur], nS);
     probes = block_sum<WG>(probes, &sh.probes);
@@ -386,7 +610,7 @@ __global__ __launch_bounds__(WG) void k_search_hbm(Args a, HbmWs w) {
     }
 }
 
-constexpr int T3_WG = 512;
+constexpr int T3_WG = 1024;
 
 hipError_t launch_t3_narrow(const Args &a, const HbmWs &w, int grid, hipStream_t s) {
     hipLaunchKernelGGL((k_search_hbm<Narrow, T3_WG>), dim3(grid), dim3(T3_WG), 0, s, a, w);
@@ -396,7 +620,9 @@ hipError_t launch_t3_wide(const Args &a, const HbmWs &w, int grid, hipStream_t s
     hipLaunchKernelGGL((k_search_hbm<Wide, T3_WG>), dim3(grid), dim3(T3_WG), 0, s, a, w);
     return hipGetLastError();
 }
-int t3_block() { return T3_WG; }
+// Configs a set can pass the budget by before every wave sees the stop flag:
+// each wave has at most one batch of U inserts per lane in flight.
+int t3_block() { return T3_WG * (Narrow::U > Wide::U ? Narrow::U : Wide::U); }
 size_t cfg_bytes_narrow() { return sizeof(Narrow::T); }
 size_t cfg_bytes_wide() { return sizeof(Wide::T); }
 

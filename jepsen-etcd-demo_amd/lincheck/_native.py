@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 2
+LC_ABI_VERSION = 3
 LC_OPT_COUNT_PROBES = 0x1
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
 LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE = 0, 1, 2, 3, 4, 5
@@ -70,7 +70,8 @@ class LcResult(C.Structure):
 class LcStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("total_ms", C.c_double), ("probes", C.c_uint64),
                 ("lds_keys", C.c_uint64), ("deep_keys", C.c_uint64), ("events", C.c_uint64),
-                ("tier0_ms", C.c_double)]
+                ("tier0_ms", C.c_double), ("tier3_ms", C.c_double),
+                ("probes_t3", C.c_uint64)]
 
 
 class LcSynthOpts(C.Structure):

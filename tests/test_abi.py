@@ -36,7 +36,7 @@ def test_struct_sizes_match_header():
     assert C.sizeof(N.LcBatch) == 8 * 9
     assert C.sizeof(N.LcResult) == 8 * 6
     assert C.sizeof(N.LcOpts) == 4 + 4 + 8 + 4 * 3 + 4 * 6 + 4
-    assert C.sizeof(N.LcStats) == 8 * 7
+    assert C.sizeof(N.LcStats) == 8 * 9
 
 
 @pytest.mark.skipif(N.lib().lc_device_count() > 0, reason="a GPU is visible")

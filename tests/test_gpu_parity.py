@@ -52,6 +52,22 @@ def test_c4_shape_crashed_ops_wide(device):
     assert (res.valid == -1).sum() > 0
 
 
+@pytest.mark.parametrize("conc,info,budget", [(20, 0.005, 1 << 20), (16, 0.01, 1 << 20), (16, 0.01, 8192),
+                                               (16, 0.01, 1000)])
+def test_hbm_tier_narrow_lds_and_hbm_passes(device, conc, info, budget):
+    """Crashed ops, sets of 10^3-10^5 configs: keys reach the HBM tier with
+    narrow configs, where small :oks keep their hash sets in LDS and larger
+    ones are redone on the HBM tables.  Keys finish (valid / invalid) at the
+    full budget, so peaks and probe counts are compared too; the smaller
+    budgets stop inside an LDS pass (1000) and after a redo (8192)."""
+    dev = Device(0, budget=budget, count_probes=True)
+    h = H.synth(n_keys=32, ops_per_key=600, concurrency=conc, info_rate=info, anomaly_rate=0.1, seed=31)
+    _, res, orc = device_vs_oracle(h, dev, budget=budget)
+    assert res.stats["deep_keys"] > 0
+    if budget == 1 << 20:
+        assert (orc["cause"] != 2).all() and orc["peak"].max() > 2048
+
+
 def test_many_register_values_wide(device):
     """> 255 distinct register values in a key: per-key state tables, wide configs."""
     h = H.synth(n_keys=32, ops_per_key=600, concurrency=8, n_values=5000, anomaly_rate=0.2, seed=21)
