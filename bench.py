@@ -40,6 +40,9 @@ CONFIGS = {
                desc="C3 shard: 100,000 keys x 2,000 ops per GPU, concurrency 10"),
     "C4": dict(keys=256, ops=5000, concurrency=30, info_rate=0.02, anomaly_rate=0.0, seed=4,
                desc="C4: 256 keys x 5,000 ops, concurrency 30, 2% crashed write/cas"),
+    "C1": dict(keys=6, ops=100, concurrency=10, info_rate=0.0, anomaly_rate=0.0, seed=1,
+               desc="C1: demo re-check, history.edn of 6 keys x 100 ops, 10 clients, nemesis :info ops "
+                    "(the stored run is absent: synthetic file of the demo's shape)"),
     "C5": dict(keys=1000, ops=1000, concurrency=10, info_rate=0.0, anomaly_rate=0.05, seed=5,
                desc="C5: C2 shape with stale reads / lost cas in 5% of keys"),
 }
@@ -59,8 +62,71 @@ def parse():
     return ap.parse_args()
 
 
+def bench_c1(args):
+    """C1 (BASELINE.json configs[0]): the demo's check phase end to end, as
+    etcdemo.clj:115-119 runs it -- history.edn on disk -> lc_edn_read ->
+    independent/checker over compose {:linear linearizable, :timeline} ->
+    the result map.  A step is that whole call; the latency to a verdict,
+    not the kernel, is what this config measures."""
+    import tempfile
+
+    import numpy as np
+
+    from lincheck import checker as CK
+    from lincheck import history as H
+    from lincheck import independent as IND
+    from lincheck import model as M
+
+    hist = H.synth(n_keys=6, ops_per_key=100, concurrency=10, interleave=True, nemesis_period=5.0, seed=1)
+    path = os.path.join(tempfile.mkdtemp(), "history.edn")
+    H.write_edn(path, hist)
+    lin = CK.linearizable({"model": M.cas_register(), "algorithm": "linear", "max-configs": args.budget})
+    chk = IND.checker(CK.compose({"linear": lin, "timeline": CK.unbridled_optimism()}))
+
+    def step():
+        return chk.check({}, H.read_edn(path), {})
+
+    for _ in range(args.warmup):
+        step()
+    ts = []
+    for _ in range(args.steps):
+        t = time.perf_counter()
+        out = step()
+        ts.append(time.perf_counter() - t)
+    elapsed = float(np.sum(ts))
+    n_ops = 6 * 100
+    cpu = parity = None
+    if not args.no_cpu:
+        import cref
+        tc = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - tc < 2.0:
+            keys, orc = cref.check_history(H.read_edn(path).as_c(), budget=args.budget, threads=1)
+            reps += 1
+        tcpu = (time.perf_counter() - tc) / reps
+        cpu = {"value": n_ops / tcpu, "unit": "ops/s", "cores": 1, "kind": "port",
+               "sample": f"same history.edn read + oracle/linear_ref.c, 1 thread, {reps} reps of {tcpu * 1e3:.2f} ms"}
+        fails = sorted(k for k, r in zip(keys, orc) if r["valid"] == 0)
+        parity = bool(sorted(out["failures"]) == fails and out["valid?"] == (not fails))
+    line = {
+        "metric": "history ops linearizability-checked/sec (whole node)",
+        "value": n_ops * args.steps / elapsed, "unit": "ops/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": CONFIGS["C1"]["desc"], "keys_per_gpu": 6, "ops_per_key": 100, "concurrency": 10,
+                   "budget": args.budget, "parallelism": "1 GPU (latency case)"},
+        "roofline": None,
+        "cpu_baseline": cpu,
+        "step": "lc_edn_read + independent/checker(compose(linearizable, timeline)) -> result map",
+        "valid?": out["valid?"], "failures": out["failures"], "parity_vs_oracle": parity,
+    }
+    print(json.dumps(line, default=str), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "C1":
+        return bench_c1(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -36,12 +36,16 @@ namespace lcd {
 #define T3P_DECL uint64_t t3p[6] = {0, 0, 0, 0, 0, 0}, t3last = 0, t3lev = 0, t3gen = 0, t3nok = 0;
 #define T3P_MARK(i) do { if (tid == 0) { const uint64_t t_ = __builtin_readcyclecounter(); if ((i) >= 0) t3p[(i) < 0 ? 0 : (i)] += t_ - t3last; t3last = t_; } } while (0)
 #define T3P_ADD(v, x) do { if (tid == 0) v += (x); } while (0)
-#define T3P_PRINT() do { if (tid == 0 && blockIdx.x < 4) printf("T3PROF key %d ok %llu erase %llu part %llu close %llu apply %llu lev %llu gen %llu nS %u\n", key, (unsigned long long)t3nok, (unsigned long long)t3p[0], (unsigned long long)t3p[1], (unsigned long long)t3p[2], (unsigned long long)t3p[3], (unsigned long long)t3lev, (unsigned long long)t3gen, nS); } while (0)
+#define T3P_PRINT() do { if (tid == 0) printf("T3KEY blk %d key %d ok %llu setup %llu pass %llu nS %u t1 %llu\n", (int)blockIdx.x, key, (unsigned long long)t3nok, (unsigned long long)t3p[0], (unsigned long long)t3p[2], nS, (unsigned long long)__builtin_readcyclecounter()); } while (0)
 #else
 #define T3P_DECL
 #define T3P_MARK(i) do {} while (0)
 #define T3P_ADD(v, x) do {} while (0)
 #define T3P_PRINT() do {} while (0)
+#endif
+
+#ifndef LC_T3_U
+#define LC_T3_U 2  // measured on C4: 2 beats 4 and 8 (the memory side is the bound, not latency)
 #endif
 
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
@@ -58,7 +62,7 @@ struct Narrow {
     __device__ static T drop(T c, uint32_t p) { return c & ~(1ull << p); }
     __device__ static void rec(T c, uint64_t &w0, uint64_t &w1) { w0 = c & LMASK; w1 = (c >> 56) << 48; }
     __device__ static void erase(T *tab, uint32_t pos) { tab[pos] = EMPTY; }
-    static constexpr int U = 4;  // inserts in flight per lane
+    static constexpr int U = LC_T3_U;  // inserts in flight per lane
     // Small :oks keep both hash sets in LDS (LDS_E slots each, at most
     // LDS_LIM configs per set); larger ones use the HBM tables.
     static constexpr bool LDS_MODE = true;

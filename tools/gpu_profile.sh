@@ -15,4 +15,10 @@ find gpurun_out/prof -name "*.csv" | head -20
 timeout -k 10 300 python bench.py --config C5 --steps 20 --warmup 3 > gpurun_out/bench_c5.log 2>&1 || { echo C5_FAILED; tail -5 gpurun_out/bench_c5.log; exit 1; }
 timeout -k 10 300 python bench.py --config C4 --budget 65536 --steps 3 --warmup 1 > gpurun_out/bench_c4.log 2>&1 || { echo C4_FAILED; tail -5 gpurun_out/bench_c4.log; exit 1; }
 timeout -k 10 300 python bench.py --config C3 --keys 20000 --steps 5 --warmup 1 --no-cpu > gpurun_out/bench_c3s.log 2>&1 || { echo C3_FAILED; tail -5 gpurun_out/bench_c3s.log; exit 1; }
+timeout -k 10 300 python bench.py --config C1 --steps 20 --warmup 3 > gpurun_out/bench_c1.log 2>&1 || { echo C1_FAILED; tail -5 gpurun_out/bench_c1.log; exit 1; }
+tail -1 gpurun_out/bench_c1.log | cut -c1-300
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt4 -o kt4 --output-format csv -- python3 bench.py --config C4 --budget 65536 --steps 3 --warmup 1 --no-cpu > gpurun_out/prof/kt4.log 2>&1 || { echo PROF4_FAILED; tail -20 gpurun_out/prof/kt4.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch4 -o f4 --output-format csv -- python3 bench.py --config C4 --budget 65536 --steps 2 --warmup 1 --no-cpu > gpurun_out/prof/f4.log 2>&1 || { echo PMC41_FAILED; tail -5 gpurun_out/prof/f4.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write4 -o w4 --output-format csv -- python3 bench.py --config C4 --budget 65536 --steps 2 --warmup 1 --no-cpu > gpurun_out/prof/w4.log 2>&1 || { echo PMC42_FAILED; tail -5 gpurun_out/prof/w4.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_ATOMIC_sum -d gpurun_out/prof/atom4 -o a4 --output-format csv -- python3 bench.py --config C4 --budget 65536 --steps 2 --warmup 1 --no-cpu > gpurun_out/prof/a4.log 2>&1 || { echo PMC43_FAILED; tail -5 gpurun_out/prof/a4.log; exit 1; }
 echo ALL_OK
