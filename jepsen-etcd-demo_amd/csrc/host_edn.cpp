@@ -15,290 +15,454 @@
 // tuples (the register workload, etcdemo.clj:90, :120); otherwise values are
 // used as they are.
 
-#include <cerrno>
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <fstream>
-#include <sstream>
 #include <string>
+#include <string_view>
+#include <system_error>
+#include <thread>
 
 #include "common.hpp"
 
+// Parsing is allocation-free per op (string_view tokens, fixed-depth value
+// records) and, for the one-op-per-line form, split at line starts over up to
+// 16 threads whose row blocks are concatenated in order.  Anything the split
+// could misread (an op map spanning a line break inside a string) fails its
+// chunk, and the whole text is then re-read serially, which gives the exact
+// result or error.  LC_EDN_THREADS caps the thread count (1 = serial).
+
 namespace {
 
-// A parsed value, only as deep as this workload needs.
-struct Val {
-    enum Kind { NIL, INT, KW, VEC, OTHER } kind = OTHER;
-    int64_t i = 0;
-    std::string kw;
-    std::vector<Val> v;
+enum : uint8_t { K_NIL, K_INT, K_VEC, K_OTHER };
+
+// A :value, only as deep as the register workloads need: [k [a b]].
+struct Leaf { uint8_t kind = K_OTHER; int64_t i = 0; };
+struct Node { uint8_t kind = K_OTHER; int64_t i = 0; uint32_t n = 0; Leaf e[2]; };
+struct Top { uint8_t kind = K_OTHER; int64_t i = 0; uint32_t n = 0; Node e[2]; };
+
+struct Delims {
+    bool d[256] = {};
+    Delims() {
+        for (unsigned char c : std::string_view(" \t\n\r,)]}([{\";")) d[c] = true;
+    }
 };
+const Delims DELIM;
 
 struct Parser {
-    const char *p, *end;
-    int64_t line = 1;
+    const char *p, *end, *base;
     std::string err;
+    size_t err_off = 0;
 
     bool fail(const std::string &m) {
-        if (err.empty()) err = "line " + std::to_string(line) + ": " + m;
+        if (err.empty()) { err = m; err_off = (size_t)(p - base); }
         return false;
     }
     void ws() {
         while (p < end) {
-            char c = *p;
-            if (c == '\n') { ++line; ++p; }
-            else if (c == ' ' || c == '\t' || c == '\r' || c == ',') ++p;
+            const char c = *p;
+            if (c == ' ' || c == ',' || c == '\n' || c == '\t' || c == '\r') ++p;
             else if (c == ';') { while (p < end && *p != '\n') ++p; }
             else break;
         }
     }
-    static bool delim(char c) {
-        return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == ',' || c == ')' || c == ']' ||
-               c == '}' || c == '(' || c == '[' || c == '{' || c == '"' || c == ';';
-    }
-    std::string token() {
+    std::string_view token() {
         const char *s = p;
-        while (p < end && !delim(*p)) ++p;
-        return std::string(s, p);
-    }
-    bool parse_seq(char close, Val *out) {
-        ++p;  // opening bracket
-        for (;;) {
-            ws();
-            if (p >= end) return fail("unterminated collection");
-            if (*p == close) { ++p; return true; }
-            Val x;
-            if (!value(out ? &x : nullptr)) return false;
-            if (out) out->v.push_back(std::move(x));
-        }
+        while (p < end && !DELIM.d[(unsigned char)*p]) ++p;
+        return std::string_view(s, (size_t)(p - s));
     }
     bool string_lit() {
         ++p;
-        while (p < end && *p != '"') {
-            if (*p == '\\') ++p;
-            else if (*p == '\n') ++line;
-            ++p;
-        }
+        while (p < end && *p != '"') p += (*p == '\\') ? 2 : 1;
         if (p >= end) return fail("unterminated string");
         ++p;
         return true;
     }
-    // Parse one value; out may be null (skip).
-    bool value(Val *out) {
-        ws();
-        if (p >= end) return fail("unexpected end of input");
-        char c = *p;
-        if (out) out->kind = Val::OTHER;
-        switch (c) {
-            case '[':
-                if (out) out->kind = Val::VEC;
-                return parse_seq(']', out);
-            case '(': return parse_seq(')', nullptr);
-            case '{': return parse_seq('}', nullptr);
-            case '"': return string_lit();
-            case '\\': ++p; if (p < end) ++p; token(); return true;  // char literal
-            case '^': ++p; if (!value(nullptr)) return false; return value(out);  // metadata
-            case '#': {
-                ++p;
-                if (p < end && *p == '{') return parse_seq('}', nullptr);  // set
-                if (p < end && *p == '_') { ++p; if (!value(nullptr)) return false; return value(out); }
-                if (p < end && *p == '"') return string_lit();            // regex
-                token();                                                  // tag
-                return value(nullptr);
-            }
-            case ':': {
-                ++p;
-                std::string t = token();
-                if (out) { out->kind = Val::KW; out->kw = t; }
-                return true;
-            }
-            default: break;
-        }
-        std::string t = token();
-        if (t.empty()) return fail(std::string("unexpected character '") + c + "'");
-        if (t == "nil") { if (out) out->kind = Val::NIL; return true; }
-        if (t == "true" || t == "false") return true;
-        char first = t[0];
-        if ((first >= '0' && first <= '9') || ((first == '-' || first == '+') && t.size() > 1 && t[1] >= '0' && t[1] <= '9')) {
-            std::string num = t;
-            if (!num.empty() && (num.back() == 'N' || num.back() == 'M')) num.pop_back();
-            bool integral = num.find_first_of(".eE/") == std::string::npos;
-            if (integral && out) {
-                errno = 0;
-                char *e = nullptr;
-                long long v = std::strtoll(num.c_str(), &e, 10);
-                if (errno || *e) return fail("integer out of range: " + t);
-                if (v == LC_NIL) return fail("integer reserved for nil: " + t);
-                out->kind = Val::INT;
-                out->i = v;
-            }
+    // Metadata (^m) and discards (#_ x) in front of a value.
+    bool prefixes() {
+        for (;;) {
+            ws();
+            if (p >= end) return fail("unexpected end of input");
+            if (*p == '^') { ++p; if (!skip()) return false; continue; }
+            if (*p == '#' && p + 1 < end && p[1] == '_') { p += 2; if (!skip()) return false; continue; }
             return true;
         }
-        return true;  // symbol
+    }
+    bool skip_seq(char close) {
+        ++p;
+        for (;;) {
+            ws();
+            if (p >= end) return fail("unterminated collection");
+            if (*p == close) { ++p; return true; }
+            if (!skip()) return false;
+        }
+    }
+    // Read one scalar token (number / nil / true / false / symbol).
+    bool scalar(uint8_t &kind, int64_t &v) {
+        const char c = *p;
+        std::string_view t = token();
+        kind = K_OTHER;
+        if (t.empty()) return fail(std::string("unexpected character '") + c + "'");
+        if (t == "nil") { kind = K_NIL; return true; }
+        const char f0 = t[0];
+        const bool num = (f0 >= '0' && f0 <= '9') || ((f0 == '-' || f0 == '+') && t.size() > 1 && t[1] >= '0' && t[1] <= '9');
+        if (!num) return true;  // true / false / symbol
+        std::string_view d = t;
+        if (d.back() == 'N' || d.back() == 'M') d.remove_suffix(1);
+        if (d.find_first_of(".eE/") != std::string_view::npos) return true;  // not integral
+        bool neg = false;
+        size_t j = 0;
+        if (d[0] == '-' || d[0] == '+') { neg = d[0] == '-'; j = 1; }
+        unsigned __int128 acc = 0;
+        for (; j < d.size(); ++j) {
+            const char x = d[j];
+            if (x < '0' || x > '9') return fail("integer out of range: " + std::string(t));
+            acc = acc * 10 + (unsigned)(x - '0');
+            if (acc > (unsigned __int128)INT64_MAX + 1) return fail("integer out of range: " + std::string(t));
+        }
+        if (!neg && acc > (unsigned __int128)INT64_MAX) return fail("integer out of range: " + std::string(t));
+        const int64_t val = neg ? (int64_t)(0 - (uint64_t)acc) : (int64_t)acc;
+        if (val == LC_NIL) return fail("integer reserved for nil: " + std::string(t));
+        kind = K_INT;
+        v = val;
+        return true;
+    }
+    // Skip one value of any EDN kind.
+    bool skip() {
+        if (!prefixes()) return false;
+        switch (*p) {
+            case '[': return skip_seq(']');
+            case '(': return skip_seq(')');
+            case '{': return skip_seq('}');
+            case '"': return string_lit();
+            case '\\': ++p; if (p < end) ++p; token(); return true;  // char literal
+            case ':': ++p; token(); return true;
+            case '#': {
+                ++p;
+                if (p < end && *p == '{') return skip_seq('}');  // set
+                if (p < end && *p == '"') return string_lit();   // regex
+                token();                                         // tagged literal
+                return skip();
+            }
+            default: {
+                uint8_t k;
+                int64_t v;
+                return scalar(k, v);
+            }
+        }
+    }
+    // A value whose shape we keep: scalars, and vectors down to `depth`.
+    template <class V>
+    bool shaped(V &out);
+    bool keyword(std::string_view &kw, bool &is_kw) {
+        if (!prefixes()) return false;
+        is_kw = *p == ':';
+        if (!is_kw) return skip();
+        ++p;
+        kw = token();
+        return true;
     }
 };
 
+template <class V>
+bool Parser::shaped(V &out) {
+    if (!prefixes()) return false;
+    out.kind = K_OTHER;
+    const char c = *p;
+    if (c == '[') {
+        out.kind = K_VEC;
+        out.n = 0;
+        ++p;
+        for (;;) {
+            ws();
+            if (p >= end) return fail("unterminated collection");
+            if (*p == ']') { ++p; return true; }
+            bool ok;
+            if constexpr (sizeof(V) == sizeof(Leaf)) {
+                ok = skip();
+            } else {
+                if (out.n < 2) ok = shaped(out.e[out.n]);
+                else ok = skip();
+            }
+            if (!ok) return false;
+            ++out.n;
+        }
+    }
+    if (c == '(' || c == '{' || c == '"' || c == '\\' || c == ':' || c == '#') return skip();
+    return scalar(out.kind, out.i);
+}
+template <>
+bool Parser::shaped<Leaf>(Leaf &out) {
+    if (!prefixes()) return false;
+    out.kind = K_OTHER;
+    const char c = *p;
+    if (c == '[' || c == '(' || c == '{' || c == '"' || c == '\\' || c == ':' || c == '#') return skip();
+    return scalar(out.kind, out.i);
+}
+
 struct RawOp {
     uint8_t type = 255, f = LC_F_OTHER;
+    int8_t nem = -1;  // nemesis :f :start (1) / :stop (0)
     int64_t process = LC_NO_PROCESS, index = -1;
-    Val value;
-    bool has_value = false;
+    Top value;
 };
 
+bool kw_is(std::string_view a, const char *b) { return a == b; }
+
 bool read_op(Parser &ps, RawOp &op) {
-    // at '{'
-    ++ps.p;
+    ++ps.p;  // at '{'
     for (;;) {
         ps.ws();
         if (ps.p >= ps.end) return ps.fail("unterminated op map");
         if (*ps.p == '}') { ++ps.p; break; }
-        Val k;
-        if (!ps.value(&k)) return false;
-        if (k.kind != Val::KW) {  // non-keyword key: skip its value
-            if (!ps.value(nullptr)) return false;
+        std::string_view k;
+        bool is_kw = false;
+        if (!ps.keyword(k, is_kw)) return false;
+        if (!is_kw) {  // non-keyword key: skip its value
+            if (!ps.skip()) return false;
             continue;
         }
-        if (k.kw == "type" || k.kw == "f") {
-            Val v;
-            if (!ps.value(&v)) return false;
-            if (k.kw == "type") {
-                if (v.kind != Val::KW) return ps.fail(":type is not a keyword");
-                if (v.kw == "invoke") op.type = LC_INVOKE;
-                else if (v.kw == "ok") op.type = LC_OK_T;
-                else if (v.kw == "fail") op.type = LC_FAIL;
-                else if (v.kw == "info") op.type = LC_INFO;
-                else return ps.fail("unknown :type :" + v.kw);
+        if (kw_is(k, "type") || kw_is(k, "f")) {
+            std::string_view v;
+            bool vk = false;
+            if (!ps.keyword(v, vk)) return false;
+            if (kw_is(k, "type")) {
+                if (!vk) return ps.fail(":type is not a keyword");
+                if (v == "invoke") op.type = LC_INVOKE;
+                else if (v == "ok") op.type = LC_OK_T;
+                else if (v == "fail") op.type = LC_FAIL;
+                else if (v == "info") op.type = LC_INFO;
+                else return ps.fail("unknown :type :" + std::string(v));
             } else {
-                if (v.kind == Val::KW && v.kw == "read") op.f = LC_F_READ;
-                else if (v.kind == Val::KW && v.kw == "write") op.f = LC_F_WRITE;
-                else if (v.kind == Val::KW && v.kw == "cas") op.f = LC_F_CAS;
-                else if (v.kind == Val::KW && v.kw == "acquire") op.f = LC_F_ACQUIRE;  // (model/mutex)
-                else if (v.kind == Val::KW && v.kw == "release") op.f = LC_F_RELEASE;
-                else {
-                    op.f = LC_F_OTHER;
-                    if (v.kind == Val::KW) op.value.kw = v.kw;  // remembered for nemesis :start/:stop
+                op.f = LC_F_OTHER;
+                op.nem = -1;
+                if (vk) {
+                    if (v == "read") op.f = LC_F_READ;
+                    else if (v == "write") op.f = LC_F_WRITE;
+                    else if (v == "cas") op.f = LC_F_CAS;
+                    else if (v == "acquire") op.f = LC_F_ACQUIRE;  // (model/mutex)
+                    else if (v == "release") op.f = LC_F_RELEASE;
+                    else if (v == "start") op.nem = 1;              // nemesis
+                    else if (v == "stop") op.nem = 0;
                 }
             }
-        } else if (k.kw == "process") {
-            Val v;
-            if (!ps.value(&v)) return false;
-            op.process = v.kind == Val::INT ? v.i : LC_NO_PROCESS;
-        } else if (k.kw == "index") {
-            Val v;
-            if (!ps.value(&v)) return false;
-            op.index = v.kind == Val::INT ? v.i : -1;
-        } else if (k.kw == "value") {
-            std::string keep = op.value.kw;
-            if (!ps.value(&op.value)) return false;
-            if (op.value.kw.empty()) op.value.kw = keep;
-            op.has_value = true;
+        } else if (kw_is(k, "process") || kw_is(k, "index")) {
+            Leaf v;
+            if (!ps.shaped(v)) return false;
+            if (kw_is(k, "process")) op.process = v.kind == K_INT ? v.i : LC_NO_PROCESS;
+            else op.index = v.kind == K_INT ? v.i : -1;
+        } else if (kw_is(k, "value")) {
+            if (!ps.shaped(op.value)) return false;
         } else {
-            if (!ps.value(nullptr)) return false;
+            if (!ps.skip()) return false;
         }
     }
     if (op.type == 255) return ps.fail("op map without :type");
     return true;
 }
 
-int64_t scalar(const Val &v, bool &ok) {
-    if (v.kind == Val::NIL) return LC_NIL;
-    if (v.kind == Val::INT) return v.i;
+enum { CONV_OK = 0, CONV_KEY = 1, CONV_VALUE = 2 };
+
+template <class V>
+int64_t scal(const V &v, bool &ok) {
+    if (v.kind == K_NIL) return LC_NIL;
+    if (v.kind == K_INT) return v.i;
     ok = false;
     return LC_NIL;
 }
 
-int build(std::vector<RawOp> &ops, lc_hist **out) {
-    // independent iff every client op's value is a 2-vector
-    bool indep = false, any_client = false;
-    for (const RawOp &o : ops) {
-        if (o.f == LC_F_OTHER) continue;
-        any_client = true;
-        indep = true;
+template <class V>
+bool register_value(uint8_t f, const V &val, int64_t &v0, int64_t &v1) {
+    bool ok = true;
+    if (f == LC_F_ACQUIRE || f == LC_F_RELEASE) return true;  // mutex ops carry no register value
+    if (f == LC_F_CAS) {
+        if (val.kind == K_VEC && val.n == 2) { v0 = scal(val.e[0], ok); v1 = scal(val.e[1], ok); }
+        else if (val.kind != K_NIL) ok = false;
+        return ok;
     }
-    for (const RawOp &o : ops) {
-        if (o.f == LC_F_OTHER) continue;
-        if (!(o.value.kind == Val::VEC && o.value.v.size() == 2)) { indep = false; break; }
-    }
-    if (!any_client) indep = false;
-    lc_hist *h = new (std::nothrow) lc_hist();
-    if (!h) return lc::fail(LC_E_NOMEM, "lc_edn: out of memory");
-    h->reserve(ops.size());
-    for (size_t i = 0; i < ops.size(); ++i) {
-        const RawOp &o = ops[i];
-        int64_t key = LC_NO_KEY, v0 = LC_NIL, v1 = LC_NIL;
+    v0 = scal(val, ok);
+    return ok;
+}
+
+// One row from a parsed op.  indep: values are [k v] tuples.
+int convert(const RawOp &o, bool indep, lc_hist &h) {
+    int64_t key = LC_NO_KEY, v0 = LC_NIL, v1 = LC_NIL;
+    if (o.f == LC_F_OTHER) {
+        if (o.nem >= 0) v0 = o.nem;
+    } else if (indep) {
         bool ok = true;
-        const Val *val = &o.value;
-        if (o.f == LC_F_OTHER) {
-            if (o.value.kw == "start") v0 = 1;
-            else if (o.value.kw == "stop") v0 = 0;
-        } else {
-            if (indep) {
-                key = scalar(o.value.v[0], ok);
-                if (!ok || key == LC_NIL) { delete h; return lc::fail(LC_E_UNSUPPORTED, "lc_edn: op %zu: tuple key is not an integer", i); }
-                val = &o.value.v[1];
-            }
-            if (o.f == LC_F_ACQUIRE || o.f == LC_F_RELEASE) {
-                // mutex ops carry no register value (knossos.model/mutex ignores it)
-            } else if (o.f == LC_F_CAS) {
-                if (val->kind == Val::VEC && val->v.size() == 2) {
-                    v0 = scalar(val->v[0], ok);
-                    v1 = scalar(val->v[1], ok);
-                } else if (val->kind != Val::NIL) {
-                    ok = false;
-                }
-            } else {
-                v0 = scalar(*val, ok);
-            }
-            if (!ok) { delete h; return lc::fail(LC_E_UNSUPPORTED, "lc_edn: op %zu: value is not an integer, nil or [old new]", i); }
-        }
-        h->push(o.type, o.f, o.process, key, v0, v1, o.index);
+        key = scal(o.value.e[0], ok);
+        if (!ok || key == LC_NIL) return CONV_KEY;
+        if (!register_value(o.f, o.value.e[1], v0, v1)) return CONV_VALUE;
+    } else {
+        if (!register_value(o.f, o.value, v0, v1)) return CONV_VALUE;
     }
-    *out = h;
-    return LC_OK;
+    h.push(o.type, o.f, o.process, key, v0, v1, o.index);
+    return CONV_OK;
+}
+
+// Parse [b, e) of one-op-per-line text (or, whole=true, the full text in
+// either form) into rows.  Tuple mode is assumed; a client op whose value is
+// not a 2-vector ends the chunk with not_indep set.
+struct alignas(256) Chunk {
+    lc_hist rows;
+    std::string err;
+    size_t err_off = 0;
+    int conv_err = CONV_OK;
+    int64_t conv_row = -1;  // chunk-local op number of a conversion error
+    bool not_indep = false, any_client = false;
+};
+
+void parse_range(const char *base, const char *b, const char *e, bool indep, bool whole, Chunk &out) {
+    Parser ps{b, e, base};
+    out.rows.reserve((size_t)(e - b) / 64 + 16);  // ~70-100 bytes per Jepsen op line
+    auto one = [&](void) -> bool {
+        RawOp op;
+        if (!read_op(ps, op)) return false;
+        if (op.f != LC_F_OTHER) {
+            out.any_client = true;
+            if (indep && !(op.value.kind == K_VEC && op.value.n == 2)) { out.not_indep = true; return false; }
+        }
+        const int rc = convert(op, indep, out.rows);
+        if (rc != CONV_OK) { out.conv_err = rc; out.conv_row = out.rows.size(); return false; }
+        return true;
+    };
+    for (;;) {
+        ps.ws();
+        if (ps.p >= ps.end) break;
+        if (*ps.p == '{') {
+            if (!one()) break;
+        } else if (whole && *ps.p == '[') {  // a vector of op maps
+            ++ps.p;
+            bool closed = false;
+            for (;;) {
+                ps.ws();
+                if (ps.p >= ps.end) { ps.fail("unterminated history vector"); break; }
+                if (*ps.p == ']') { ++ps.p; closed = true; break; }
+                if (*ps.p != '{') { ps.fail("expected an op map"); break; }
+                if (!one()) break;
+            }
+            if (!closed) break;
+        } else {
+            ps.fail("expected an op map");
+            break;
+        }
+    }
+    out.err = ps.err;
+    out.err_off = ps.err_off;
+}
+
+int64_t line_of(const char *text, size_t off) {
+    return 1 + (int64_t)std::count(text, text + off, '\n');
+}
+
+int finish_serial(const char *text, int64_t len, lc_hist **out) {
+    // pass 1 assumes [k v] tuples; a client op that is not one means the
+    // history is not independent and it is read again with plain values
+    for (int pass = 0; pass < 2; ++pass) {
+        const bool indep = pass == 0;
+        auto *c = new (std::nothrow) Chunk();
+        if (!c) return lc::fail(LC_E_NOMEM, "lc_edn: out of memory");
+        parse_range(text, text, text + len, indep, true, *c);
+        if (!c->err.empty()) {
+            const int rc = lc::fail(LC_E_PARSE, "lc_edn: line %lld: %s", (long long)line_of(text, c->err_off),
+                                    c->err.c_str());
+            delete c;
+            return rc;
+        }
+        if (indep && (c->not_indep || !c->any_client)) { delete c; continue; }
+        if (c->conv_err != CONV_OK) {
+            const int rc = c->conv_err == CONV_KEY
+                               ? lc::fail(LC_E_UNSUPPORTED, "lc_edn: op %lld: tuple key is not an integer",
+                                          (long long)c->conv_row)
+                               : lc::fail(LC_E_UNSUPPORTED,
+                                          "lc_edn: op %lld: value is not an integer, nil or [old new]",
+                                          (long long)c->conv_row);
+            delete c;
+            return rc;
+        }
+        lc_hist *h = new (std::nothrow) lc_hist(std::move(c->rows));
+        delete c;
+        if (!h) return lc::fail(LC_E_NOMEM, "lc_edn: out of memory");
+        *out = h;
+        return LC_OK;
+    }
+    return lc::fail(LC_E_PARSE, "lc_edn: internal error");  // not reached
 }
 
 }  // namespace
 
 extern "C" int lc_edn_parse(const char *text, int64_t len, lc_hist **out) {
     if (!text || !out || len < 0) return lc::fail(LC_E_INVALID, "lc_edn_parse: null argument");
-    Parser ps{text, text + len};
-    std::vector<RawOp> ops;
     try {
-        for (;;) {
-            ps.ws();
-            if (ps.p >= ps.end) break;
-            if (*ps.p == '{') {
-                RawOp op;
-                if (!read_op(ps, op)) return lc::fail(LC_E_PARSE, "lc_edn: %s", ps.err.c_str());
-                ops.push_back(std::move(op));
-            } else if (*ps.p == '[') {  // a vector of op maps
-                ++ps.p;
-                for (;;) {
-                    ps.ws();
-                    if (ps.p >= ps.end) return lc::fail(LC_E_PARSE, "lc_edn: unterminated history vector");
-                    if (*ps.p == ']') { ++ps.p; break; }
-                    if (*ps.p != '{') return lc::fail(LC_E_PARSE, "lc_edn: line %lld: expected an op map", (long long)ps.line);
-                    RawOp op;
-                    if (!read_op(ps, op)) return lc::fail(LC_E_PARSE, "lc_edn: %s", ps.err.c_str());
-                    ops.push_back(std::move(op));
-                }
-            } else {
-                return lc::fail(LC_E_PARSE, "lc_edn: line %lld: expected an op map", (long long)ps.line);
-            }
+        const char *b = text, *e = text + len;
+        while (b < e && (*b == ' ' || *b == '\n' || *b == '\t' || *b == '\r' || *b == ',')) ++b;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        int T = (int)std::min<int64_t>({16, (int64_t)hw, len >> 20});
+        if (const char *ev = std::getenv("LC_EDN_THREADS")) T = std::min(T, std::atoi(ev));
+        if (T < 2 || b >= e || *b != '{') return finish_serial(text, len, out);
+        // split at line starts that open an op map
+        std::vector<const char *> cut{b};
+        for (int i = 1; i < T; ++i) {
+            const char *q = std::max(cut.back(), text + len * i / T);
+            while (q < e && !(q[-1] == '\n' && *q == '{')) ++q;
+            if (q < e && q > cut.back()) cut.push_back(q);
         }
-        return build(ops, out);
+        cut.push_back(e);
+        const size_t n = cut.size() - 1;
+        std::vector<Chunk> ch(n);
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < n; ++i)
+            th.emplace_back([&, i] { parse_range(text, cut[i], cut[i + 1], true, false, ch[i]); });
+        for (auto &t : th) t.join();
+        bool any_client = false;
+        for (auto &c : ch) {
+            if (!c.err.empty() || c.not_indep || c.conv_err != CONV_OK) return finish_serial(text, len, out);
+            any_client |= c.any_client;
+        }
+        if (!any_client) return finish_serial(text, len, out);
+        lc_hist *h = new (std::nothrow) lc_hist();
+        if (!h) return lc::fail(LC_E_NOMEM, "lc_edn: out of memory");
+        size_t total = 0;
+        for (auto &c : ch) total += c.rows.type.size();
+        h->reserve(total);
+        for (auto &c : ch) {
+            auto app = [](auto &dst, auto &src) { dst.insert(dst.end(), src.begin(), src.end()); };
+            app(h->type, c.rows.type); app(h->f, c.rows.f); app(h->process, c.rows.process);
+            app(h->key, c.rows.key); app(h->v0, c.rows.v0); app(h->v1, c.rows.v1); app(h->index, c.rows.index);
+            c.rows = lc_hist();
+        }
+        *out = h;
+        return LC_OK;
     } catch (const std::bad_alloc &) {
         return lc::fail(LC_E_NOMEM, "lc_edn: out of memory");
+    } catch (const std::system_error &) {
+        return finish_serial(text, len, out);  // no threads: serial read
     }
 }
 
 extern "C" int lc_edn_read(const char *path, lc_hist **out) {
     if (!path || !out) return lc::fail(LC_E_INVALID, "lc_edn_read: null argument");
-    std::ifstream in(path, std::ios::binary);
-    if (!in) return lc::fail(LC_E_IO, "lc_edn_read: cannot open %s", path);
-    std::ostringstream ss;
-    ss << in.rdbuf();
-    std::string s = ss.str();
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return lc::fail(LC_E_IO, "lc_edn_read: cannot open %s", path);
+    std::string s;
+    try {
+        if (std::fseek(f, 0, SEEK_END) == 0) {
+            const long sz = std::ftell(f);
+            if (sz > 0) s.resize((size_t)sz);
+            std::rewind(f);
+        }
+        size_t got = s.empty() ? 0 : std::fread(&s[0], 1, s.size(), f);
+        s.resize(got);
+        char buf[1 << 16];
+        size_t r;
+        while ((r = std::fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, r);  // growing / unseekable files
+    } catch (const std::bad_alloc &) {
+        std::fclose(f);
+        return lc::fail(LC_E_NOMEM, "lc_edn_read: out of memory");
+    }
+    std::fclose(f);
     return lc_edn_parse(s.data(), (int64_t)s.size(), out);
 }
 

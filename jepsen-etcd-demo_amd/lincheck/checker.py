@@ -417,13 +417,19 @@ class Linearizable:
             if inner is self:
                 results[k] = lin
                 continue
-            # compose: run the other checkers per key on the host
-            if ops_cache is None:
-                ops_cache = history if not isinstance(history, History) else history.to_ops()
-            sub = subhistory(ops_cache, k)
+            # compose: run the other checkers per key on the host (the
+            # sub-history is built only for checkers that read one)
+            sub = None
             r = {}
             for name, ch in inner.checkers.items():
-                r[name] = lin if ch is self else check_safe(ch, test, sub, dict(opts or {}, **{"history-key": k}))
+                if ch is self:
+                    r[name] = lin
+                    continue
+                if sub is None and getattr(ch, "needs_history", True):
+                    if ops_cache is None:
+                        ops_cache = history if not isinstance(history, History) else history.to_ops()
+                    sub = subhistory(ops_cache, k)
+                r[name] = check_safe(ch, test, sub, dict(opts or {}, **{"history-key": k}))
             r["valid?"] = merge_valid([x.get("valid?") for x in r.values()])
             results[k] = r
         out = merge_results(results)
@@ -446,6 +452,8 @@ class Compose:
 
 class UnbridledOptimism:
     """jepsen.checker/unbridled-optimism: always valid (stands in for :timeline)."""
+
+    needs_history = False
 
     def check(self, test, history, opts=None) -> Dict:
         return {"valid?": True}

@@ -60,3 +60,61 @@ def test_parse_errors(text):
 def test_missing_file():
     with pytest.raises(N.LincheckError, match="io"):
         H.read_edn("/nonexistent/history.edn")
+
+
+def _parse_with_threads(text: str, threads: int):
+    import os
+    old = os.environ.get("LC_EDN_THREADS")
+    os.environ["LC_EDN_THREADS"] = str(threads)
+    try:
+        return H.parse_edn(text)
+    finally:
+        if old is None:
+            del os.environ["LC_EDN_THREADS"]
+        else:
+            os.environ["LC_EDN_THREADS"] = old
+
+
+COLS = ("type", "f", "process", "key", "v0", "v1", "index")
+
+
+def test_parallel_parse_matches_serial(tmp_path):
+    """Texts over 2 MB are split at line starts and parsed on several threads;
+    the rows must be the serial reader's, in order."""
+    h = H.synth(n_keys=60, ops_per_key=400, concurrency=10, info_rate=0.01, interleave=True,
+                nemesis_period=3.0, seed=9)
+    path = str(tmp_path / "history.edn")
+    H.write_edn(path, h)
+    text = open(path).read()
+    assert len(text) > 2 << 20
+    a, b = _parse_with_threads(text, 1), _parse_with_threads(text, 8)
+    for col in COLS:
+        np.testing.assert_array_equal(getattr(a, col), getattr(b, col), err_msg=col)
+        np.testing.assert_array_equal(getattr(b, col), getattr(h, col), err_msg=col)
+
+
+def test_parallel_parse_multiline_strings_fall_back(tmp_path):
+    """Op maps whose :error strings span lines that start with '{': a split
+    inside one fails its chunk and the text is re-read serially."""
+    h = H.synth(n_keys=40, ops_per_key=400, concurrency=10, seed=10)
+    path = str(tmp_path / "history.edn")
+    H.write_edn(path, h)
+    lines = open(path).read().splitlines()
+    lines = [ln[:-1] + ', :error "boom\n{:type :ok, :f :read}\n"}' if i % 3 == 0 else ln
+             for i, ln in enumerate(lines)]
+    text = "\n".join(lines) + "\n"
+    assert len(text) > 2 << 20
+    a, b = _parse_with_threads(text, 1), _parse_with_threads(text, 8)
+    for col in COLS:
+        np.testing.assert_array_equal(getattr(a, col), getattr(b, col), err_msg=col)
+        np.testing.assert_array_equal(getattr(b, col), getattr(h, col), err_msg=col)
+
+
+def test_non_independent_values():
+    """Plain (non-tuple) values: the reader takes them as they are."""
+    text = ("{:type :invoke, :f :write, :value 3, :process 0, :index 0}\n"
+            "{:type :ok, :f :write, :value 3, :process 0, :index 1}\n"
+            "{:type :invoke, :f :cas, :value [3 4], :process 1, :index 2}\n")
+    h = H.parse_edn(text)
+    assert list(h.key) == [N.LC_NO_KEY] * 3
+    assert (h.v0[2], h.v1[2]) == (3, 4) and h.v0[0] == 3
