@@ -245,7 +245,8 @@ typedef struct lc_stats {
                                  0 unless lc_opts.flags has LC_OPT_COUNT_PROBES */
     uint64_t lds_keys;        /* keys finished in the LDS tier                  */
     uint64_t deep_keys;       /* keys (re)searched in the HBM tier              */
-    uint64_t events;          /* events processed                               */
+    uint64_t events;          /* events processed (0, like lds_keys, when the
+                                 step was T0 alone: no counter readback)     */
     double   tier0_ms;        /* device time of the register-lattice tier alone */
     double   tier3_ms;        /* device time of the HBM tier launches (0 if none) */
     uint64_t probes_t3;       /* the part of `probes` made by the HBM tier      */

@@ -59,6 +59,7 @@ struct lc_dev_batch {
     uint8_t *key_width = nullptr;
     uint16_t *key_states = nullptr;
     int32_t *order = nullptr;  // LPT: keys by event count, descending
+    bool t0_only = false;      // every key fits the register lattice: T0 never spills
     size_t input_bytes = 0;    // bytes the search reads per pass (events + offsets + tables)
     ~lc_dev_batch() {
         dfree(ev_off); dfree(events); dfree(trans); dfree(trans_off);
@@ -361,6 +362,19 @@ extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
     };
     rc = up();
     if (rc) { delete d; return rc; }
+    // T0 spills a key only for its width (ops pending at once), its state
+    // count or the initial state; all three are known here.
+    {
+        bool ok = K > 0 && b->key_width && b->init_state < lcd::t0_max_states();
+        for (int64_t k = 0; ok && k < K; ++k) ok = b->key_width[k] <= lcd::t0_max_width();
+        if (ok && b->trans_off) {
+            ok = b->key_states != nullptr;
+            for (int64_t k = 0; ok && k < K; ++k) ok = b->key_states[k] <= lcd::t0_max_states();
+        } else if (ok) {
+            ok = d->shared_states <= lcd::t0_max_states();
+        }
+        d->t0_only = ok;
+    }
     d->input_bytes = (size_t)d->n_events * 4 + ((size_t)K + 1) * 8;
     *out = d;
     return LC_OK;
@@ -428,6 +442,11 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     if (K > 0) {
         HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream));
         HIPCHK(hipEventRecord(c->et0, c->stream));
+    }
+    // Verdicts left on the device, nothing counted, and no key can leave T0:
+    // no T1/T2 launches and no counter readback -- the step ends with T0.
+    const bool t0_step = K > 0 && d->t0_only && dev_result && !(c->o.flags & LC_OPT_COUNT_PROBES);
+    if (K > 0 && !t0_step) {
         // T1: LDS hash sets
         lcd::Args a1 = a;
         a1.order = spill0; a1.n_order = 0; a1.n_in = n_spill0; a1.ticket = c->counters + 9;
@@ -463,8 +482,14 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         HIPCHK(hipStreamSynchronize(c->stream));
         return LC_OK;
     };
-    rc = readback();
-    if (rc) return rc;
+    if (t0_step) {
+        HIPCHK(hipEventRecord(c->e1, c->stream));
+        HIPCHK(hipEventSynchronize(c->e1));
+        std::memset(c->hctl, 0, CTL_BYTES);  // counters not read back on this path
+    } else {
+        rc = readback();
+        if (rc) return rc;
+    }
     bool t3 = false;
     const unsigned long long probes_pre_t3 = acc[0];
     if (K > 0 && (cnt[2] > 0 || cnt[3] > 0)) {

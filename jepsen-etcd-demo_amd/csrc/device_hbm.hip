@@ -63,10 +63,10 @@ struct Narrow {
     __device__ static void rec(T c, uint64_t &w0, uint64_t &w1) { w0 = c & LMASK; w1 = (c >> 56) << 48; }
     __device__ static void erase(T *tab, uint32_t pos) { tab[pos] = EMPTY; }
     static constexpr int U = LC_T3_U;  // inserts in flight per lane
-    // Small :oks keep both hash sets in LDS (LDS_E slots each, at most
-    // LDS_LIM configs per set); larger ones use the HBM tables.
+    // Small :oks keep both hash sets in LDS (S': LDS_ES slots, I: LDS_EI,
+    // each at most half full); larger ones use the HBM tables.
     static constexpr bool LDS_MODE = true;
-    static constexpr uint32_t LDS_E = 4096, LDS_LIM = 2048;
+    static constexpr uint32_t LDS_ES = 4096, LDS_EI = 8192, LIM_S = LDS_ES / 2, LIM_I = LDS_EI / 2;
     __device__ static bool insert(T *tab, uint32_t mask, T key, uint32_t &pos, uint32_t *err) {
         return insert_at(tab, mask, key, hash64(key) & mask, pos);
     }
@@ -141,7 +141,7 @@ struct Wide {
     __device__ static uint32_t hash(T c) { return hash64(c.lo ^ (c.hi * 0x9E3779B97F4A7C15ull)); }
     static constexpr int U = 2;
     static constexpr bool LDS_MODE = false;  // the publish protocol is HBM-only
-    static constexpr uint32_t LDS_E = 1, LDS_LIM = 0;
+    static constexpr uint32_t LDS_ES = 1, LDS_EI = 1, LIM_S = 0, LIM_I = 0;
     // Wide inserts keep their publish protocol: one at a time.
     __device__ static void insert_n(T *tab, uint32_t mask, const T (&key)[U], const bool (&act)[U],
                                     uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err) {
@@ -194,7 +194,8 @@ struct HbmShared {
     unsigned long long probes;
     // closure successors staged per wave until 64 x U are ready to insert
     typename C::T stage[WG / 64][64 * C::U + 64];
-    uint64_t lt[2][C::LDS_E];  // LDS-mode hash sets: [0] S', [1] I
+    uint64_t ltS[C::LDS_ES];  // LDS-mode hash sets: S'
+    uint64_t ltI[C::LDS_EI];  //                     I
 };
 
 // Sum of one value over the workgroup (every thread gets it).
@@ -270,21 +271,21 @@ __device__ void erase_all(const HbmWs &w, Slot<C> &sl, const uint32_t *posI, uin
 }
 
 // Insert into an LDS-mode hash set (narrow configs).  The probe sequence is
-// bounded: a table that fills up (sets past LDS_LIM, plus other waves'
+// bounded: a table that fills up (a set past its limit, plus other waves'
 // in-flight batches) raises `redo` and the :ok is run again on HBM tables.
-template <class C>
+template <uint32_t E>
 __device__ __forceinline__ bool lds_set_insert(uint64_t *tab, uint64_t key, bool active, uint32_t &pos,
                                                uint32_t *redo) {
     bool isnew = false;
-    uint32_t h = hash64(key) & (C::LDS_E - 1);
+    uint32_t h = hash64(key) & (E - 1);
     bool done = !active;
     for (uint32_t n = 0; !done; ++n) {
-        if (n == C::LDS_E) { *redo = 1; break; }
+        if (n == E) { *redo = 1; break; }
         const unsigned long long old = atomicCAS((unsigned long long *)&tab[h], (unsigned long long)EMPTY,
                                                  (unsigned long long)key);
         if (old == EMPTY) { isnew = true; done = true; }
         else if (old == key) { done = true; }
-        else { h = (h + 1) & (C::LDS_E - 1); }
+        else { h = (h + 1) & (E - 1); }
     }
     pos = h;
     return isnew;
@@ -296,17 +297,20 @@ __device__ __forceinline__ void set_insert_n(HbmShared<C, WG> &sh, typename C::T
                                              uint32_t (&pos)[C::U], bool (&nw)[C::U]) {
     if constexpr (LDS) {
 #pragma unroll
-        for (int u = 0; u < C::U; ++u) nw[u] = lds_set_insert<C>(sh.lt[which], key[u], act[u], pos[u], &sh.redo);
+        for (int u = 0; u < C::U; ++u)
+            nw[u] = which == 0 ? lds_set_insert<C::LDS_ES>(sh.ltS, key[u], act[u], pos[u], &sh.redo)
+                               : lds_set_insert<C::LDS_EI>(sh.ltI, key[u], act[u], pos[u], &sh.redo);
     } else {
         C::insert_n(htab, hmask, key, act, pos, nw, &sh.err);
     }
 }
 
-// Position r of a new config: past the set's limit it is an error in HBM
-// mode (cap covers every overshoot) and a redo in LDS mode.
+// Position r of a new config in set `which` (0 S', 1 I): past the cap it is
+// an error in HBM mode (cap covers every overshoot), past the LDS set's
+// limit a redo in LDS mode.
 template <class C, int WG, bool LDS>
-__device__ __forceinline__ bool take_pos(HbmShared<C, WG> &sh, uint32_t r, uint32_t cap) {
-    if (LDS && r >= C::LDS_LIM) { sh.redo = 1; sh.stop = 1; }
+__device__ __forceinline__ bool take_pos(HbmShared<C, WG> &sh, uint32_t r, uint32_t cap, int which) {
+    if (LDS && r >= (which == 0 ? C::LIM_S : C::LIM_I)) { sh.redo = 1; sh.stop = 1; }
     if (r < cap) return true;
     sh.err = 1;
     return false;
@@ -333,7 +337,7 @@ __device__ void flush_stage(typename C::T *stg, uint32_t n, Slot<C> &sl, HbmShar
     for (int u = 0; u < U; ++u) {
         const uint32_t r = block_append<WG>(&sh.nI, nw[u]);
         if (nw[u]) {
-            if (take_pos<C, WG, LDS>(sh, r, cap)) { sl.I[r] = key[u]; sl.posI[r] = pos[u]; }
+            if (take_pos<C, WG, LDS>(sh, r, cap, 1)) { sl.I[r] = key[u]; sl.posI[r] = pos[u]; }
             if (r + 1 > budget) sh.stop = 1;
         }
     }
@@ -352,7 +356,8 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
     constexpr int U = C::U;
     const uint32_t tid = threadIdx.x;
     if constexpr (LDS) {
-        for (uint32_t j = tid; j < 2 * C::LDS_E; j += WG) (&sh.lt[0][0])[j] = EMPTY;
+        for (uint32_t j = tid; j < C::LDS_ES; j += WG) sh.ltS[j] = EMPTY;
+        for (uint32_t j = tid; j < C::LDS_EI; j += WG) sh.ltI[j] = EMPTY;
         __syncthreads();
     }
     // -- partition S (U configs per thread, their inserts in flight together)
@@ -376,8 +381,8 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
         for (int u = 0; u < U; ++u) {
             const uint32_t rs = block_append<WG>(&sh.nSn, ns[u]);
             const uint32_t ri = block_append<WG>(&sh.nI, ni[u]);
-            if (ns[u] && take_pos<C, WG, LDS>(sh, rs, cap)) { Sn[rs] = kS[u]; posSn[rs] = pS[u]; }
-            if (ni[u] && take_pos<C, WG, LDS>(sh, ri, cap)) { sl.I[ri] = kI[u]; sl.posI[ri] = pI[u]; }
+            if (ns[u] && take_pos<C, WG, LDS>(sh, rs, cap, 0)) { Sn[rs] = kS[u]; posSn[rs] = pS[u]; }
+            if (ni[u] && take_pos<C, WG, LDS>(sh, ri, cap, 1)) { sl.I[ri] = kI[u]; sl.posI[ri] = pI[u]; }
         }
     }
     if (tid == 0) probes += nS;
@@ -443,7 +448,7 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
         for (int u = 0; u < U; ++u) {
             const uint32_t r = block_append<WG>(&sh.nSn, nw[u]);
             if (nw[u]) {
-                if (take_pos<C, WG, LDS>(sh, r, cap)) { Sn[r] = k2[u]; posSn[r] = pos[u]; }
+                if (take_pos<C, WG, LDS>(sh, r, cap, 0)) { Sn[r] = k2[u]; posSn[r] = pos[u]; }
                 if (r + 1 > a.budget) sh.stop = 1;
             }
         }
@@ -525,7 +530,7 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
             // Small sets run with both hash sets in LDS; a pass that outgrows
             // them is discarded (S is untouched) and run again on the HBM
             // tables, which the erasure above has left clean.
-            bool lds = C::LDS_MODE && nS <= C::LDS_LIM && nIbig <= C::LDS_LIM;
+            bool lds = C::LDS_MODE && nS <= C::LIM_S && nIbig <= C::LIM_I;
             const uint64_t probes0 = probes;
             int pr;
             for (;;) {

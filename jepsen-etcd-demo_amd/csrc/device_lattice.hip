@@ -60,6 +60,8 @@ constexpr int T0_RMEM = 16;            // workspace lattice (global memory): n <
 #endif
 constexpr uint32_t T0_MAX_WIDTH = LC_T0_MAX_WIDTH;  // <= 6 + log2(T0_RMEM)
 constexpr uint32_t T0_MAX_STATES = 32;
+uint32_t t0_max_width() { return T0_MAX_WIDTH; }
+uint32_t t0_max_states() { return T0_MAX_STATES; }
 
 struct Xfer { uint32_t k, cap, b; };
 

@@ -186,3 +186,69 @@ def test_verdicts_only_fast_path(shape):
                                        anomaly_rate=0.2, seed=21),
     }[shape]()
     device_vs_oracle(h, dev, verdicts_only=True)
+
+
+class _HipBuf:
+    """Device memory from the HIP runtime liblincheck itself links (a second
+    runtime -- torch's -- must not initialise the GPU after this one)."""
+    _rt = None
+
+    def __init__(self, nbytes: int):
+        import ctypes as C
+        if _HipBuf._rt is None:
+            _HipBuf._rt = C.CDLL("libamdhip64.so.7")
+        self.C, self.n = C, nbytes
+        self.ptr = C.c_void_p()
+        assert self._rt.hipMalloc(C.byref(self.ptr), C.c_size_t(nbytes)) == 0
+
+    def fill(self, byte: int):
+        assert self._rt.hipMemset(self.ptr, self.C.c_int(byte), self.C.c_size_t(self.n)) == 0
+
+    def get(self, dtype) -> np.ndarray:
+        out = np.empty(self.n // np.dtype(dtype).itemsize, dtype)
+        assert self._rt.hipMemcpy(out.ctypes.data_as(self.C.c_void_p), self.ptr, self.C.c_size_t(self.n), 2) == 0
+        return out
+
+    def __del__(self):
+        if self._rt is not None and self.ptr:
+            self._rt.hipFree(self.ptr)
+
+
+@pytest.mark.parametrize("shape", ["c5", "high_concurrency", "many_values", "crashed"])
+def test_resident_device_results(device, shape):
+    """The bench's path: a batch resident in HBM, verdicts written to caller
+    device arrays (lc_check_device with dev_result).  When no key can leave
+    T0 the step is T0 alone (no T1/T2 launches, no counter readback); the
+    other shapes take the full tier chain.  Repeated steps on one batch must
+    keep giving the oracle's verdicts and failing events."""
+    import ctypes as C
+
+    import cref
+    from lincheck import _native as N
+    from lincheck.checker import Packed
+
+    h = {
+        "c5": lambda: H.synth(n_keys=400, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=5),
+        "high_concurrency": lambda: H.synth(n_keys=64, ops_per_key=600, concurrency=16, seed=17),
+        "many_values": lambda: H.synth(n_keys=32, ops_per_key=600, concurrency=8, n_values=5000,
+                                       anomaly_rate=0.2, seed=21),
+        "crashed": lambda: H.synth(n_keys=32, ops_per_key=600, concurrency=16, info_rate=0.01, anomaly_rate=0.1,
+                                   seed=31),
+    }[shape]()
+    packed = Packed(h)
+    dev = Device(0)
+    db = dev.upload(packed)
+    K = packed.n_keys
+    valid, fev, cause = _HipBuf(K), _HipBuf(4 * K), _HipBuf(K)
+    r = N.LcResult(C.cast(valid.ptr, N.P(C.c_int8)), C.cast(fev.ptr, N.P(C.c_int32)),
+                   C.cast(cause.ptr, N.P(C.c_uint8)), None, None, None)
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    for _ in range(3):
+        for b in (valid, fev, cause):
+            b.fill(0x5A)
+        st = db.check_into(r)
+        np.testing.assert_array_equal(valid.get(np.int8), orc["valid"])
+        np.testing.assert_array_equal(fev.get(np.int32), orc["fail_event"])
+        np.testing.assert_array_equal(cause.get(np.uint8), orc["cause"])
+    if shape == "c5":
+        assert st.deep_keys == 0
