@@ -96,6 +96,10 @@ struct lc_ctx {
     lcd::Args *dargs = nullptr;    // device copy of T0's Args (read once per key)
     lcd::Args *hargs = nullptr;    // its pinned host staging copy (copied only when it changes)
     bool hargs_valid = false;
+    // T0-only steps (lc_check_device) skip re-zeroing the control block: the
+    // ticket continues from where the previous such step left it.
+    bool ticket_live = false;
+    uint32_t ticket_next = 0;
     int lat_ws_blocks = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
     struct Ws {
@@ -417,7 +421,14 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     int32_t *n_spill0 = c->counters + 0, *n_spill1 = c->counters + 1, *n_spill2 = c->counters + 2;
     int32_t *n_wide = c->counters + 3;
 
-    HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_BYTES, c->stream));
+    // Verdicts left on the device, nothing counted, and no key can leave T0:
+    // no T1/T2 launches, no counter readback and no control-block memset --
+    // the step is T0 alone.
+    const bool t0_step = K > 0 && d->t0_only && dev_result && !(c->o.flags & LC_OPT_COUNT_PROBES);
+    uint32_t ticket_base = 0;
+    if (t0_step && c->ticket_live) ticket_base = c->ticket_next;
+    else HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_BYTES, c->stream));
+    c->ticket_live = false;
     if (a.n_final && K > 0) HIPCHK(hipMemsetAsync(a.n_final, 0, (size_t)K * 4, c->stream));
     // T0: every key, LPT order; keys outside the register lattice spill to T1
     lcd::Args a0 = a;
@@ -440,12 +451,9 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     }
     HIPCHK(hipEventRecord(c->e0, c->stream));
     if (K > 0) {
-        HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream));
+        HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
     }
-    // Verdicts left on the device, nothing counted, and no key can leave T0:
-    // no T1/T2 launches and no counter readback -- the step ends with T0.
-    const bool t0_step = K > 0 && d->t0_only && dev_result && !(c->o.flags & LC_OPT_COUNT_PROBES);
     if (K > 0 && !t0_step) {
         // T1: LDS hash sets
         lcd::Args a1 = a;
@@ -486,6 +494,8 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         HIPCHK(hipEventRecord(c->e1, c->stream));
         HIPCHK(hipEventSynchronize(c->e1));
         std::memset(c->hctl, 0, CTL_BYTES);  // counters not read back on this path
+        c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
+        c->ticket_live = true;
     } else {
         rc = readback();
         if (rc) return rc;

@@ -189,7 +189,7 @@ struct T0Args {
     uint64_t budget;
     int32_t n_order;
     uint32_t init_state, shared_states, flags;
-    uint32_t one;                // 1 (unused)
+    uint32_t ticket_base;        // ticket value this launch starts from (see launch_t0)
 };
 
 // Transfer masks of one event: vk[q] = op q's accept mask on lanes with bit
@@ -923,9 +923,9 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
     const bool fast = !(a.flags & (T0_COUNT | T0_WANT_PEAK | T0_WANT_FINAL)) && a.budget >= 16ull * 64u * 32u;
     for (int32_t guard = 0; guard <= a.n_order; ++guard) {  // every wave takes at most n_order keys
         int32_t w = 0;
-        if (lane_id() == 0) w = atomicAdd(a.ticket, 1);
+        if (lane_id() == 0) w = (int32_t)((uint32_t)atomicAdd(a.ticket, 1) - a.ticket_base);
         w = __builtin_amdgcn_readfirstlane(w);
-        if (w >= a.n_order) break;
+        if ((uint32_t)w >= (uint32_t)a.n_order) break;
         const int32_t key = a.order[w];
         const int kr = fast ? lattice_key<RM, true>(a, key, ws) : lattice_key<RM, false>(a, key, ws);
         if (kr == K_SPILL) {
@@ -959,12 +959,15 @@ extern "C" int lc_debug_t0_stamps(unsigned long long *host, int n_blocks) {
 
 size_t lat_ws_words() { return 3 * T0_RMEM * 64; }
 
-hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s) {
+// Every block ends with exactly one ticket past the work list, so a launch
+// leaves the ticket at ticket_base + n_order + grid: back-to-back launches
+// can start from there instead of re-zeroing it.
+hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s, uint32_t ticket_base) {
     T0Args t{};
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
     t.key_width = a.key_width; t.key_states = a.key_states; t.order = a.order; t.ticket = a.ticket;
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
-    t.init_state = a.init_state; t.shared_states = a.shared_states; t.one = 1u;
+    t.init_state = a.init_state; t.shared_states = a.shared_states; t.ticket_base = ticket_base;
     t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) | (a.final_cfg ? T0_WANT_FINAL : 0u) |
               (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u);
     if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(grid), dim3(64), 0, s, t);

@@ -58,7 +58,7 @@ struct HbmWs {
 
 size_t lds_bytes_t1();
 size_t lds_bytes_t2();
-hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s);
+hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s, uint32_t ticket_base);
 size_t lat_ws_words();
 uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
