@@ -252,3 +252,18 @@ def test_resident_device_results(device, shape):
         np.testing.assert_array_equal(cause.get(np.uint8), orc["cause"])
     if shape == "c5":
         assert st.deep_keys == 0
+
+
+def test_c3_shard_scale(device):
+    """One GPU's C3 shard at 8 GPUs (12,500 keys x 2,000 ops = 25 M ops, the
+    compact T0 build with many keys per SIMD), with 0.5 % of keys corrupted:
+    bit-exact against the oracle on every key, plus the generator's
+    size-independent property -- a key that was not corrupted is
+    linearizable by construction, so every invalid key is a corrupted one."""
+    h = H.synth(n_keys=12_500, ops_per_key=2000, concurrency=10, anomaly_rate=0.005, seed=3)
+    packed, res, orc = device_vs_oracle(h, Device(0), verdicts_only=True)
+    bad = set(h.anomalous_keys)
+    keys = np.array(packed.keys)
+    assert set(keys[res.valid == 0]) <= bad
+    assert (res.valid[~np.isin(keys, list(bad))] == 1).all()
+    assert (res.valid == 0).sum() > 0
