@@ -434,6 +434,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     lcd::Args a0 = a;
     a0.order = d->order; a0.n_order = (int32_t)K; a0.n_in = nullptr; a0.ticket = c->counters + 8;
     a0.spill = spill0; a0.n_spill = n_spill0; a0.wide = wide; a0.n_wide = n_wide;
+    a0.deep = spill2; a0.n_deep = n_spill2;  // very wide keys: straight to T3
     // T0 has two builds: 16 lattice registers (n <= 10 pending in VGPRs, 2
     // waves per SIMD) when every key can be resident at once -- each key's
     // events are serial, so there per-key latency is the whole story -- and

@@ -930,7 +930,8 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
         const int kr = fast ? lattice_key<RM, true>(a, key, ws) : lattice_key<RM, false>(a, key, ws);
         if (kr == K_SPILL) {
             const Args &f = *a.full;
-            push_list(f.spill, f.n_spill, key);
+            const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
+            push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key);
         }
 #ifdef LC_T0_STAMPS
         ++nkeys;

@@ -45,7 +45,15 @@ struct Args {
     int32_t *n_spill;
     int32_t *wide;
     int32_t *n_wide;
+    // T0 only: keys wider than LC_DIRECT_T3_WIDTH skip the LDS tiers (their
+    // sets outgrow them; every tier computes the same sets, so this is
+    // routing, not semantics) and go straight to the HBM tier's list
+    int32_t *deep;
+    int32_t *n_deep;
 };
+
+// Ops pending at once above which a key leaving T0 goes straight to T3.
+constexpr uint32_t LC_DIRECT_T3_WIDTH = 28;
 
 // Per-block HBM workspace of the T3 tier (one slot per resident block).
 struct HbmWs {
