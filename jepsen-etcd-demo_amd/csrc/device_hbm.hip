@@ -36,7 +36,7 @@ namespace lcd {
 #define T3P_DECL uint64_t t3p[6] = {0, 0, 0, 0, 0, 0}, t3last = 0, t3lev = 0, t3gen = 0, t3nok = 0;
 #define T3P_MARK(i) do { if (tid == 0) { const uint64_t t_ = __builtin_readcyclecounter(); if ((i) >= 0) t3p[(i) < 0 ? 0 : (i)] += t_ - t3last; t3last = t_; } } while (0)
 #define T3P_ADD(v, x) do { if (tid == 0) v += (x); } while (0)
-#define T3P_PRINT() do { if (tid == 0) printf("T3KEY blk %d key %d ok %llu setup %llu pass %llu nS %u t1 %llu\n", (int)blockIdx.x, key, (unsigned long long)t3nok, (unsigned long long)t3p[0], (unsigned long long)t3p[2], nS, (unsigned long long)__builtin_readcyclecounter()); } while (0)
+#define T3P_PRINT() do { if (tid == 0) printf("T3KEY blk %d key %d ok %llu between %llu setup %llu hbm %llu lds %llu n_lds %llu n_redo %llu nS %u\n", (int)blockIdx.x, key, (unsigned long long)t3nok, (unsigned long long)t3p[1], (unsigned long long)t3p[0], (unsigned long long)t3p[2], (unsigned long long)t3p[3], (unsigned long long)t3p[4], (unsigned long long)t3p[5], nS); } while (0)
 #else
 #define T3P_DECL
 #define T3P_MARK(i) do {} while (0)
@@ -66,6 +66,7 @@ struct Narrow {
     // Small :oks keep both hash sets in LDS (S': LDS_ES slots, I: LDS_EI,
     // each at most half full); larger ones use the HBM tables.
     static constexpr bool LDS_MODE = true;
+    static constexpr bool NARROW = true;
     static constexpr uint32_t LDS_ES = 4096, LDS_EI = 8192, LIM_S = LDS_ES / 2, LIM_I = LDS_EI / 2;
     __device__ static bool insert(T *tab, uint32_t mask, T key, uint32_t &pos, uint32_t *err) {
         return insert_at(tab, mask, key, hash64(key) & mask, pos);
@@ -88,17 +89,20 @@ struct Narrow {
     // key is a duplicate and costs no atomic.  A stale EMPTY only means one
     // CAS more; a key cannot read stale, since its slot was erased by this
     // workgroup's own earlier stores.
+    // probe_first: only for full batches.  The read costs a round trip, which
+    // a small (latency-bound) closure level cannot hide; a large level is
+    // bound by memory-side traffic, where the saved atomics pay.
     __device__ static void insert_n(T *tab, uint32_t mask, const T (&key)[U], const bool (&act)[U],
-                                    uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err) {
+                                    uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err, bool probe_first) {
         uint32_t h[U];
         unsigned long long old[U];
         bool need[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             h[u] = hash64(key[u]) & mask;
-            old[u] = act[u] ? __hip_atomic_load((unsigned long long *)&tab[h[u]], __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT)
-                            : (unsigned long long)key[u];
+            old[u] = act[u] && probe_first ? __hip_atomic_load((unsigned long long *)&tab[h[u]], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)
+                                           : (act[u] ? EMPTY : (unsigned long long)key[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -141,10 +145,11 @@ struct Wide {
     __device__ static uint32_t hash(T c) { return hash64(c.lo ^ (c.hi * 0x9E3779B97F4A7C15ull)); }
     static constexpr int U = 2;
     static constexpr bool LDS_MODE = false;  // the publish protocol is HBM-only
+    static constexpr bool NARROW = false;
     static constexpr uint32_t LDS_ES = 1, LDS_EI = 1, LIM_S = 0, LIM_I = 0;
     // Wide inserts keep their publish protocol: one at a time.
     __device__ static void insert_n(T *tab, uint32_t mask, const T (&key)[U], const bool (&act)[U],
-                                    uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err) {
+                                    uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err, bool) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             pos[u] = NOPOS;
@@ -189,6 +194,7 @@ struct HbmShared {
     uint32_t slot_desc[128];
     uint32_t cand_slot[128];
     uint32_t cand_desc[128];
+    uint64_t legal[C::NARROW ? 256 : 1];  // narrow: candidate slots legal from each state
     uint32_t nSn, nI, stop, err, redo;
     int32_t work;
     unsigned long long probes;
@@ -292,7 +298,7 @@ __device__ __forceinline__ bool lds_set_insert(uint64_t *tab, uint64_t key, bool
 }
 
 template <class C, int WG, bool LDS>
-__device__ __forceinline__ void set_insert_n(HbmShared<C, WG> &sh, typename C::T *htab, int which, uint32_t hmask,
+__device__ __forceinline__ void set_insert_n(HbmShared<C, WG> &sh, typename C::T *htab, int which, uint32_t hmask, bool big,
                                              const typename C::T (&key)[C::U], const bool (&act)[C::U],
                                              uint32_t (&pos)[C::U], bool (&nw)[C::U]) {
     if constexpr (LDS) {
@@ -301,7 +307,7 @@ __device__ __forceinline__ void set_insert_n(HbmShared<C, WG> &sh, typename C::T
             nw[u] = which == 0 ? lds_set_insert<C::LDS_ES>(sh.ltS, key[u], act[u], pos[u], &sh.redo)
                                : lds_set_insert<C::LDS_EI>(sh.ltI, key[u], act[u], pos[u], &sh.redo);
     } else {
-        C::insert_n(htab, hmask, key, act, pos, nw, &sh.err);
+        C::insert_n(htab, hmask, key, act, pos, nw, &sh.err, big);
     }
 }
 
@@ -332,7 +338,7 @@ __device__ void flush_stage(typename C::T *stg, uint32_t n, Slot<C> &sl, HbmShar
         act[u] = i < n;
         key[u] = act[u] ? stg[i] : C::init(0);
     }
-    set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, key, act, pos, nw);
+    set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, n == 64u * U, key, act, pos, nw);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t r = block_append<WG>(&sh.nI, nw[u]);
@@ -351,15 +357,25 @@ enum { PASS_OK = 0, PASS_CLOSURE_STOP = 1, PASS_REDO = 2 };
 template <class C, int WG, bool LDS>
 __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typename C::T *S, uint32_t nS,
                        typename C::T *Sn, uint32_t *posSn, uint32_t p, uint32_t dp, uint32_t nc, uint32_t cap,
-                       uint32_t hmask, uint64_t &probes) {
+                       uint32_t hmask, uint32_t nstates, uint64_t &probes) {
     using T = typename C::T;
     constexpr int U = C::U;
     const uint32_t tid = threadIdx.x;
     if constexpr (LDS) {
         for (uint32_t j = tid; j < C::LDS_ES; j += WG) sh.ltS[j] = EMPTY;
         for (uint32_t j = tid; j < C::LDS_EI; j += WG) sh.ltI[j] = EMPTY;
-        __syncthreads();
     }
+    if constexpr (C::NARROW) {  // per state, the candidates whose step is legal there
+        for (uint32_t st = tid; st < nstates; st += WG) {
+            uint64_t m = 0;
+            for (uint32_t k = 0; k < nc; ++k) {
+                uint32_t s2;
+                if (step(st, sh.cand_desc[k], s2)) m |= 1ull << sh.cand_slot[k];
+            }
+            sh.legal[st] = m;
+        }
+    }
+    if constexpr (LDS || C::NARROW) __syncthreads();
     // -- partition S (U configs per thread, their inserts in flight together)
     for (uint32_t j0 = 0; j0 < nS; j0 += WG * U) {
         T kS[U], kI[U];
@@ -375,8 +391,8 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             kS[u] = C::drop(c, p);
             kI[u] = c;
         }
-        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, kS, hasp, pS, ns);
-        set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, kI, toI, pI, ni);
+        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, nS >= WG * U, kS, hasp, pS, ns);
+        set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, nS >= WG * U, kI, toI, pI, ni);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t rs = block_append<WG>(&sh.nSn, ns[u]);
@@ -403,6 +419,30 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             const bool in = j < end;
             const T c = in ? sl.I[j] : C::init(0);
             const uint32_t st = C::state(c);
+            if constexpr (C::NARROW) {
+                // each lane walks only its config's legal, unlinearized
+                // candidates: the wave loops max-over-lanes times, not nc
+                uint64_t m = in ? (sh.legal[st] & ~(c & LMASK)) : 0ull;
+                for (;;) {
+                    const bool act = m != 0;
+                    const uint64_t bm = __ballot(act);
+                    if (bm == 0) break;
+                    const uint32_t q = act ? (uint32_t)__builtin_ctzll(m) : 0u;
+                    m &= m - 1;
+                    uint32_t s2 = st;
+                    (void)step(st, sh.slot_desc[q], s2);
+                    probes += act;
+                    if (act) stg[nst + rank_of(bm)] = C::lin(c, q, s2);
+                    nst += (uint32_t)__popcll(bm);
+                    if (nst >= 64u * U) {
+                        flush_stage<C, WG, LDS>(stg, 64u * U, sl, sh, hmask, cap, a.budget);
+                        nst -= 64u * U;
+                        if (lane_id() < nst) stg[lane_id()] = stg[64u * U + lane_id()];
+                        if (*(volatile uint32_t *)&sh.stop) { halt = true; break; }
+                    }
+                }
+                continue;
+            }
             for (uint32_t k = 0; k < nc; ++k) {
                 const uint32_t q = sh.cand_slot[k];
                 uint32_t s2 = 0;
@@ -443,7 +483,7 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             probes += act[u];
             k2[u] = C::restate(c, s2);
         }
-        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, k2, act, pos, nw);
+        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, nI >= WG * U, k2, act, pos, nw);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t r = block_append<WG>(&sh.nSn, nw[u]);
@@ -465,6 +505,8 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     const uint32_t cap = w.cap, hmask = w.hmask;
+    uint32_t nstates = a.trans_off ? (a.key_states ? (uint32_t)a.key_states[key] : 256u) : a.shared_states;
+    nstates = nstates < 256u ? nstates : 256u;  // narrow configs hold 8-bit states
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
         if (tid == 0) finish_key(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
@@ -507,7 +549,7 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
             typename C::T *Sn = sl.S[cur ^ 1];
             uint32_t *posSn = sl.posS[cur ^ 1];
             __syncthreads();  // slot_desc of earlier invokes visible
-            T3P_MARK(-1);
+            T3P_MARK(1);
             T3P_ADD(t3nok, 1);
             const uint32_t dp = sh.slot_desc[p];
             for (uint32_t j = tid; j < nIlast; j += WG) C::erase(sl.hI, sl.posI[j]);
@@ -533,6 +575,7 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
             bool lds = C::LDS_MODE && nS <= C::LIM_S && nIbig <= C::LIM_I;
             const uint64_t probes0 = probes;
             int pr;
+            uint32_t pr_redos = 0;
             for (;;) {
                 if (tid == 0) { sh.nSn = 0; sh.nI = 0; sh.stop = 0; sh.redo = 0; }
                 __threadfence_block();
@@ -540,17 +583,21 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
                 T3P_MARK(0);
                 if constexpr (C::LDS_MODE) {
                     if (lds)
-                        pr = ok_pass<C, WG, true>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, probes);
+                        pr = ok_pass<C, WG, true>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, nstates, probes);
                     else
-                        pr = ok_pass<C, WG, false>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, probes);
+                        pr = ok_pass<C, WG, false>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, nstates, probes);
                 } else {
-                    pr = ok_pass<C, WG, false>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, probes);
+                    pr = ok_pass<C, WG, false>(a, sl, sh, S, nS, Sn, posSn, p, dp, nc, cap, hmask, nstates, probes);
                 }
                 if (pr != PASS_REDO) break;
                 lds = false;
+                ++pr_redos;
                 probes = probes0;
             }
-            T3P_MARK(2);
+            (void)pr_redos;
+            T3P_MARK(lds ? 3 : 2);
+            T3P_ADD(t3p[4], lds ? 1 : 0);
+            T3P_ADD(t3p[5], pr_redos);
             const uint32_t nI = sh.nI < cap ? sh.nI : cap;
             nIbig = sh.nI;
             if (pr == PASS_CLOSURE_STOP) {
@@ -566,7 +613,7 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
 #ifdef LC_T3_PROF
             if (tid == 0 && blockIdx.x == 0)
                 printf("T3OK key %d ev %d nS %u nI %u nSn %u nc %u lds %d setup %llu pass %llu\n", key, evno, nS, nI, sh.nSn, nc,
-                       (int)lds, (unsigned long long)t3p[0], (unsigned long long)t3p[2]);
+                       (int)lds, (unsigned long long)t3p[0], (unsigned long long)(t3p[2] + t3p[3]));
 #endif
             const uint32_t nSn_all = sh.nSn;
             const uint32_t nSn = nSn_all < cap ? nSn_all : cap;
