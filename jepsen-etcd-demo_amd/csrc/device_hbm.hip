@@ -62,7 +62,8 @@ struct Narrow {
     __device__ static T drop(T c, uint32_t p) { return c & ~(1ull << p); }
     __device__ static void rec(T c, uint64_t &w0, uint64_t &w1) { w0 = c & LMASK; w1 = (c >> 56) << 48; }
     __device__ static void erase(T *tab, uint32_t pos) { tab[pos] = EMPTY; }
-    static constexpr int U = LC_T3_U;  // inserts in flight per lane
+    static constexpr int U = LC_T3_U;  // closure inserts in flight per lane
+    static constexpr int UA = 2;       // partition / apply (4 measured no better on C4)
     // Small :oks keep both hash sets in LDS (S': LDS_ES slots, I: LDS_EI,
     // each at most half full); larger ones use the HBM tables.
     static constexpr bool LDS_MODE = true;
@@ -92,6 +93,7 @@ struct Narrow {
     // probe_first: only for full batches.  The read costs a round trip, which
     // a small (latency-bound) closure level cannot hide; a large level is
     // bound by memory-side traffic, where the saved atomics pay.
+    template <int U>
     __device__ static void insert_n(T *tab, uint32_t mask, const T (&key)[U], const bool (&act)[U],
                                     uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err, bool probe_first) {
         uint32_t h[U];
@@ -144,10 +146,12 @@ struct Wide {
     __device__ static void erase(T *tab, uint32_t pos) { tab[pos].hi = EMPTY; }
     __device__ static uint32_t hash(T c) { return hash64(c.lo ^ (c.hi * 0x9E3779B97F4A7C15ull)); }
     static constexpr int U = 2;
+    static constexpr int UA = 2;
     static constexpr bool LDS_MODE = false;  // the publish protocol is HBM-only
     static constexpr bool NARROW = false;
     static constexpr uint32_t LDS_ES = 1, LDS_EI = 1, LIM_S = 0, LIM_I = 0;
     // Wide inserts keep their publish protocol: one at a time.
+    template <int U>
     __device__ static void insert_n(T *tab, uint32_t mask, const T (&key)[U], const bool (&act)[U],
                                     uint32_t (&pos)[U], bool (&isnew)[U], uint32_t *err, bool) {
 #pragma unroll
@@ -297,17 +301,17 @@ __device__ __forceinline__ bool lds_set_insert(uint64_t *tab, uint64_t key, bool
     return isnew;
 }
 
-template <class C, int WG, bool LDS>
+template <class C, int WG, bool LDS, int N>
 __device__ __forceinline__ void set_insert_n(HbmShared<C, WG> &sh, typename C::T *htab, int which, uint32_t hmask, bool big,
-                                             const typename C::T (&key)[C::U], const bool (&act)[C::U],
-                                             uint32_t (&pos)[C::U], bool (&nw)[C::U]) {
+                                             const typename C::T (&key)[N], const bool (&act)[N],
+                                             uint32_t (&pos)[N], bool (&nw)[N]) {
     if constexpr (LDS) {
 #pragma unroll
-        for (int u = 0; u < C::U; ++u)
+        for (int u = 0; u < N; ++u)
             nw[u] = which == 0 ? lds_set_insert<C::LDS_ES>(sh.ltS, key[u], act[u], pos[u], &sh.redo)
                                : lds_set_insert<C::LDS_EI>(sh.ltI, key[u], act[u], pos[u], &sh.redo);
     } else {
-        C::insert_n(htab, hmask, key, act, pos, nw, &sh.err, big);
+        C::template insert_n<N>(htab, hmask, key, act, pos, nw, &sh.err, big);
     }
 }
 
@@ -338,7 +342,7 @@ __device__ void flush_stage(typename C::T *stg, uint32_t n, Slot<C> &sl, HbmShar
         act[u] = i < n;
         key[u] = act[u] ? stg[i] : C::init(0);
     }
-    set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, n == 64u * U, key, act, pos, nw);
+    set_insert_n<C, WG, LDS, U>(sh, sl.hI, 1, hmask, n == 64u * U, key, act, pos, nw);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t r = block_append<WG>(&sh.nI, nw[u]);
@@ -359,7 +363,7 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
                        typename C::T *Sn, uint32_t *posSn, uint32_t p, uint32_t dp, uint32_t nc, uint32_t cap,
                        uint32_t hmask, uint32_t nstates, uint64_t &probes) {
     using T = typename C::T;
-    constexpr int U = C::U;
+    constexpr int U = C::U, UA = C::UA;
     const uint32_t tid = threadIdx.x;
     if constexpr (LDS) {
         for (uint32_t j = tid; j < C::LDS_ES; j += WG) sh.ltS[j] = EMPTY;
@@ -376,13 +380,13 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
         }
     }
     if constexpr (LDS || C::NARROW) __syncthreads();
-    // -- partition S (U configs per thread, their inserts in flight together)
-    for (uint32_t j0 = 0; j0 < nS; j0 += WG * U) {
-        T kS[U], kI[U];
-        bool hasp[U], toI[U], ns[U], ni[U];
-        uint32_t pS[U], pI[U];
+    // -- partition S (UA configs per thread, their inserts in flight together)
+    for (uint32_t j0 = 0; j0 < nS; j0 += WG * UA) {
+        T kS[UA], kI[UA];
+        bool hasp[UA], toI[UA], ns[UA], ni[UA];
+        uint32_t pS[UA], pI[UA];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UA; ++u) {
             const uint32_t j = j0 + u * WG + tid;
             const bool act = j < nS;
             const T c = act ? S[j] : C::init(0);
@@ -391,10 +395,10 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             kS[u] = C::drop(c, p);
             kI[u] = c;
         }
-        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, nS >= WG * U, kS, hasp, pS, ns);
-        set_insert_n<C, WG, LDS>(sh, sl.hI, 1, hmask, nS >= WG * U, kI, toI, pI, ni);
+        set_insert_n<C, WG, LDS, UA>(sh, sl.hS, 0, hmask, nS >= WG * UA, kS, hasp, pS, ns);
+        set_insert_n<C, WG, LDS, UA>(sh, sl.hI, 1, hmask, nS >= WG * UA, kI, toI, pI, ni);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UA; ++u) {
             const uint32_t rs = block_append<WG>(&sh.nSn, ns[u]);
             const uint32_t ri = block_append<WG>(&sh.nI, ni[u]);
             if (ns[u] && take_pos<C, WG, LDS>(sh, rs, cap, 0)) { Sn[rs] = kS[u]; posSn[rs] = pS[u]; }
@@ -469,13 +473,13 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
     if (sh.nI > a.budget || sh.err) return PASS_CLOSURE_STOP;
     // -- apply p
     const uint32_t nI = sh.nI;
-    for (uint32_t j0 = 0; j0 < nI; j0 += WG * U) {
+    for (uint32_t j0 = 0; j0 < nI; j0 += WG * UA) {
         if (*(volatile uint32_t *)&sh.stop) break;
-        T k2[U];
-        bool act[U], nw[U];
-        uint32_t pos[U];
+        T k2[UA];
+        bool act[UA], nw[UA];
+        uint32_t pos[UA];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UA; ++u) {
             const uint32_t j = j0 + u * WG + tid;
             const T c = j < nI ? sl.I[j] : C::init(0);
             uint32_t s2 = 0;
@@ -483,9 +487,9 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             probes += act[u];
             k2[u] = C::restate(c, s2);
         }
-        set_insert_n<C, WG, LDS>(sh, sl.hS, 0, hmask, nI >= WG * U, k2, act, pos, nw);
+        set_insert_n<C, WG, LDS, UA>(sh, sl.hS, 0, hmask, nI >= WG * UA, k2, act, pos, nw);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UA; ++u) {
             const uint32_t r = block_append<WG>(&sh.nSn, nw[u]);
             if (nw[u]) {
                 if (take_pos<C, WG, LDS>(sh, r, cap, 0)) { Sn[r] = k2[u]; posSn[r] = pos[u]; }
@@ -678,7 +682,10 @@ hipError_t launch_t3_wide(const Args &a, const HbmWs &w, int grid, hipStream_t s
 }
 // Configs a set can pass the budget by before every wave sees the stop flag:
 // each wave has at most one batch of U inserts per lane in flight.
-int t3_block() { return T3_WG * (Narrow::U > Wide::U ? Narrow::U : Wide::U); }
+int t3_block() {
+    constexpr int u = Narrow::U > Narrow::UA ? Narrow::U : Narrow::UA, w = Wide::U > Wide::UA ? Wide::U : Wide::UA;
+    return T3_WG * (u > w ? u : w);
+}
 size_t cfg_bytes_narrow() { return sizeof(Narrow::T); }
 size_t cfg_bytes_wide() { return sizeof(Wide::T); }
 
