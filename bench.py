@@ -178,14 +178,18 @@ def main():
     # verdict records only: no peak sizes, no counterexample configs in the step
     res = N.LcResult(C.cast(valid.data_ptr(), N.P(C.c_int8)), C.cast(fail_event.data_ptr(), N.P(C.c_int32)),
                      C.cast(cause.data_ptr(), N.P(C.c_uint8)), None, None, None)
-    gathered = torch.empty(K * world, dtype=torch.int64, device=tdev) if world > 1 else None
+    # equal-sized all-gather blocks: a strong-scaling shard may be one key short
+    K_blk = -(-cfg["keys"] // world) if strong else K
+    gathered = torch.empty(K_blk * world, dtype=torch.int64, device=tdev) if world > 1 else None
+    rec = torch.zeros(K_blk, dtype=torch.int64, device=tdev) if world > 1 else None
 
     from lincheck import parallel as P
 
     def step():
         st = db.check_into(res)
         if world > 1:  # the path's one exchange step: verdict records over RCCL
-            dist.all_gather_into_tensor(gathered, P.pack_records(valid, cause, fail_event))
+            rec[:K] = P.pack_records(valid, cause, fail_event)
+            dist.all_gather_into_tensor(gathered, rec)
         return st
 
     for _ in range(args.warmup):
