@@ -3,14 +3,18 @@
 // Same set computation as the LDS tiers (device_search.hip; semantics in
 // oracle/linear_ref.py), for keys whose config sets outgrow LDS or whose
 // window needs more than 56 slots / 255 register states.  One workgroup of
-// WG threads searches one key; its S / S' / I arrays and the two
+// WG (1,024) threads searches one key; its S / S' / I arrays and the two
 // open-addressed hash sets live in a per-block HBM workspace slot sized from
-// the search budget (a key can never hold more than budget + WG configs:
-// insertion stops as soon as a count passes the budget, which is exactly
-// the LC_CAUSE_BUDGET verdict).
+// the search budget (a key can never hold more than budget + t3_block()
+// configs: insertion stops as soon as a count passes the budget, which is
+// exactly the LC_CAUSE_BUDGET verdict).  Per :ok, sets of up to 2,048 / 4,096
+// configs (narrow) use hash tables in LDS instead; a pass that outgrows them
+// is discarded and redone on the HBM tables (ok_pass, PASS_REDO).
 //
 // Hash sets, open addressing with linear probing:
-//   narrow (u64 configs): one 64-bit atomicCAS on EMPTY per probe.
+//   narrow (u64 configs): one 64-bit atomicCAS on EMPTY per probe, U per
+//     lane in flight, with an L1-bypassing read first in full batches so
+//     that duplicates cost no memory-side atomic.
 //   wide (2 x u64: lo = slots 0..63, hi = slots 64..111 | state << 48):
 //     CAS hi from EMPTY to hi|BUSY, store lo, release-store hi; a prober
 //     that meets its own hi still BUSY waits (bounded) for the publisher,
