@@ -169,15 +169,22 @@ def main():
     db = dev.upload(packed)
     print(f"[rank {rank}] packed + uploaded; setup {t_gen:.1f} s", file=sys.stderr, flush=True)
 
-    # device-resident result arrays (torch tensors) -> no D2H inside the step
+    # device-resident result arrays (torch tensors) -> no D2H inside the step.
+    # Two sets, alternating per step: step k's records are packed and
+    # all-gathered on torch's stream while step k+1's search (the library's
+    # own stream) writes the other set; before a set is reused, the event
+    # recorded after its packing is waited on.
     tdev = torch.device("cuda", local)
-    valid = torch.empty(K, dtype=torch.int8, device=tdev)
-    fail_event = torch.empty(K, dtype=torch.int32, device=tdev)
-    cause = torch.empty(K, dtype=torch.uint8, device=tdev)
     import ctypes as C
-    # verdict records only: no peak sizes, no counterexample configs in the step
-    res = N.LcResult(C.cast(valid.data_ptr(), N.P(C.c_int8)), C.cast(fail_event.data_ptr(), N.P(C.c_int32)),
-                     C.cast(cause.data_ptr(), N.P(C.c_uint8)), None, None, None)
+    bufs = []
+    for _ in range(2 if world > 1 else 1):
+        valid = torch.empty(K, dtype=torch.int8, device=tdev)
+        fail_event = torch.empty(K, dtype=torch.int32, device=tdev)
+        cause = torch.empty(K, dtype=torch.uint8, device=tdev)
+        # verdict records only: no peak sizes, no counterexample configs in the step
+        res = N.LcResult(C.cast(valid.data_ptr(), N.P(C.c_int8)), C.cast(fail_event.data_ptr(), N.P(C.c_int32)),
+                         C.cast(cause.data_ptr(), N.P(C.c_uint8)), None, None, None)
+        bufs.append({"valid": valid, "fail_event": fail_event, "cause": cause, "res": res, "packed": None})
     # equal-sized all-gather blocks: a strong-scaling shard may be one key short
     K_blk = -(-cfg["keys"] // world) if strong else K
     gathered = torch.empty(K_blk * world, dtype=torch.int64, device=tdev) if world > 1 else None
@@ -185,10 +192,18 @@ def main():
 
     from lincheck import parallel as P
 
+    n_step = [0]
+
     def step():
-        st = db.check_into(res)
+        b = bufs[n_step[0] % len(bufs)]
+        n_step[0] += 1
+        if b["packed"] is not None:
+            b["packed"].synchronize()  # this set's previous records are packed
+        st = db.check_into(b["res"])
         if world > 1:  # the path's one exchange step: verdict records over RCCL
-            rec[:K] = P.pack_records(valid, cause, fail_event)
+            rec[:K] = P.pack_records(b["valid"], b["cause"], b["fail_event"])
+            b["packed"] = torch.cuda.Event()
+            b["packed"].record()
             dist.all_gather_into_tensor(gathered, rec)
         return st
 
@@ -217,8 +232,9 @@ def main():
         elapsed = float(t.item())
 
     # results of the last step (host copy, outside the timed region)
-    v_host = valid.cpu().numpy()
-    fe_host = fail_event.cpu().numpy()
+    last = bufs[(n_step[0] - 1) % len(bufs)]
+    v_host = last["valid"].cpu().numpy()
+    fe_host = last["fail_event"].cpu().numpy()
     if rank == 0:
         # probe count from one extra, untimed pass with
         # LC_OPT_COUNT_PROBES: the timed steps skip the per-event popcounts
