@@ -7,6 +7,7 @@ failing event, the peak config-set size, and the total probe count.
 import numpy as np
 import pytest
 
+import cref
 from helpers import device_vs_oracle
 from lincheck import history as H
 from lincheck.checker import Device
@@ -267,3 +268,41 @@ def test_c3_shard_scale(device):
     assert set(keys[res.valid == 0]) <= bad
     assert (res.valid[~np.isin(keys, list(bad))] == 1).all()
     assert (res.valid == 0).sum() > 0
+
+
+def test_degenerate_histories(device):
+    """Edge cases of the demo's check, end to end through
+    independent/checker(linearizable): an empty history, nemesis ops only,
+    an op that never returns, a failed op only (its pair is dropped, so the
+    key has no events), and a crashed write that must be linearized for a
+    later read.  Each result map must agree with the oracle's verdicts."""
+    from lincheck import checker as ck
+    from lincheck import independent, model
+    from lincheck.independent import Tuple
+
+    def op(t, f, v, p):
+        return {"type": t, "f": f, "value": v, "process": p}
+
+    nem = op("info", "start", None, "nemesis")
+    cases = {
+        "empty": ([], True, []),
+        "nemesis_only": ([nem, op("info", "stop", None, "nemesis")], True, []),
+        "never_returns": ([op("invoke", "read", Tuple(0, None), 0)], True, []),
+        "failed_only": ([op("invoke", "write", Tuple(0, 1), 0), op("fail", "write", Tuple(0, 1), 0)], True, []),
+        "crashed_write_read_later": ([op("invoke", "write", Tuple(0, 3), 0), op("info", "write", Tuple(0, 3), 0),
+                                      op("invoke", "read", Tuple(0, None), 1), op("ok", "read", Tuple(0, 3), 1)],
+                                     True, []),
+        "stale_read_two_keys": ([op("invoke", "write", Tuple(0, 3), 0), op("ok", "write", Tuple(0, 3), 0),
+                                 op("invoke", "read", Tuple(0, None), 1), op("ok", "read", Tuple(0, 4), 1),
+                                 op("invoke", "write", Tuple(1, 2), 2), op("ok", "write", Tuple(1, 2), 2), nem],
+                                False, [0]),
+    }
+    chk = independent.checker(ck.linearizable({"model": model.cas_register(), "algorithm": "linear"}))
+    for name, (ops, valid, failures) in cases.items():
+        out = chk.check({}, ops, {})
+        assert out["valid?"] is valid, name
+        assert sorted(out["failures"]) == failures, name
+        if ops:
+            h = H.History.from_ops(ops)
+            keys, orc = cref.check_history(h.as_c(), budget=1 << 20)
+            assert sorted(k for k, r in zip(keys, orc) if r["valid"] == 0) == failures, name
