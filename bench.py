@@ -137,10 +137,19 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # Rehearsal of the N > 1 path on a one-GPU box: LC_BENCH_BACKEND=gloo and
+    # LC_BENCH_DEVICE=0 put every rank on cuda:0 (RCCL refuses two ranks on one
+    # device).  The driver's multi-GPU runs use neither: RCCL, one GPU per rank.
+    backend = os.environ.get("LC_BENCH_BACKEND", "nccl")
+    if os.environ.get("LC_BENCH_DEVICE"):
+        local = int(os.environ["LC_BENCH_DEVICE"])
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(local)
 
@@ -235,7 +244,33 @@ def main():
     last = bufs[(n_step[0] - 1) % len(bufs)]
     v_host = last["valid"].cpu().numpy()
     fe_host = last["fail_event"].cpu().numpy()
+    node = None
+    if world > 1:
+        # whole-node verdicts from the last step's all-gather (the rank blocks
+        # are K_blk records each; a short strong-scaling shard leaves padding)
+        torch.cuda.synchronize()
+        g = gathered.cpu().numpy().reshape(world, K_blk)
+        parts = []
+        for r in range(world):
+            kr = ((r + 1) * cfg["keys"] // world - r * cfg["keys"] // world) if strong else K
+            parts.append(g[r, :kr])
+        gv, _, gfe = P.unpack_records(np.concatenate(parts))
+        # rank 0's block of the gather must be exactly its local records
+        own_ok = bool(np.array_equal(gv[:K], v_host) and np.array_equal(gfe[:K], fe_host))
+        node = {"keys": int(gv.size), "valid": int((gv == 1).sum()), "invalid": int((gv == 0).sum()),
+                "unknown": int((gv == -1).sum()), "rank0_block_matches_local": own_ok}
+    h2h_ms = None
     if rank == 0:
+        # SURVEY.md 8(d) D-1's end-to-end rate, outside the timed region: one
+        # lc_check_batch from the packed SoA in host memory to host verdict
+        # arrays (upload over PCIe + search + download), best of 3.  Never `value`.
+        h2h = []
+        for _ in range(3):
+            th = time.perf_counter()
+            hr = dev.check(packed, verdicts_only=True)
+            h2h.append(time.perf_counter() - th)
+        h2h_ms = min(h2h) * 1e3
+        h2h_same = bool(np.array_equal(hr.valid, v_host) and np.array_equal(hr.fail_event, fe_host))
         # probe count from one extra, untimed pass with
         # LC_OPT_COUNT_PROBES: the timed steps skip the per-event popcounts
         dev_c = Device(local, budget=args.budget, count_probes=True)
@@ -349,6 +384,10 @@ def main():
             "verdicts": {"valid": int((v_host == 1).sum()), "invalid": int((v_host == 0).sum()),
                          "unknown": int((v_host == -1).sum())},
             "parity_vs_oracle": parity,
+            "node_verdicts": node,
+            "host_to_host": {"ms": h2h_ms, "ops_per_s_one_gpu": K * ops / (h2h_ms * 1e-3),
+                             "same_verdicts_as_resident": h2h_same,
+                             "what": "rank 0: lc_check_batch from packed host SoA to host verdicts (PCIe incl.)"},
             "setup_s": round(t_gen, 2),
         }
         print(json.dumps(line), flush=True)

@@ -61,11 +61,35 @@ struct lc_dev_batch {
     int32_t *order = nullptr;  // LPT: keys by event count, descending
     bool t0_only = false;      // every key fits the register lattice: T0 never spills
     size_t input_bytes = 0;    // bytes the search reads per pass (events + offsets + tables)
+    // Device storage behind the arrays above, grown on demand: a batch that is
+    // re-uploaded (the ctx's staging batch for lc_check_batch) keeps it, so a
+    // host-to-host check allocates nothing once its sizes have been seen.
+    struct Mem {
+        void *p = nullptr;
+        size_t cap = 0;
+    } mem[7];
     ~lc_dev_batch() {
-        dfree(ev_off); dfree(events); dfree(trans); dfree(trans_off);
-        dfree(key_width); dfree(key_states); dfree(order);
+        for (Mem &m : mem)
+            if (m.p) (void)hipFree(m.p);
     }
 };
+
+// Point p at m's storage, growing it to hold n elements of T.
+template <class T>
+static hipError_t grow(lc_dev_batch::Mem &m, T *&p, size_t n) {
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    if (bytes > m.cap) {
+        if (m.p) (void)hipFree(m.p);
+        m.p = nullptr;
+        m.cap = 0;
+        p = nullptr;
+        hipError_t e = hipMalloc(&m.p, bytes);
+        if (e != hipSuccess) return e;
+        m.cap = bytes;
+    }
+    p = (T *)m.p;
+    return hipSuccess;
+}
 
 constexpr size_t CTL_BYTES = 4 * sizeof(unsigned long long) + 16 * sizeof(int32_t);
 
@@ -96,6 +120,10 @@ struct lc_ctx {
     lcd::Args *dargs = nullptr;    // device copy of T0's Args (read once per key)
     lcd::Args *hargs = nullptr;    // its pinned host staging copy (copied only when it changes)
     bool hargs_valid = false;
+    // lc_check_batch's staging batch (device arrays reused across calls) and
+    // the lock that keeps one lc_check_batch at a time on it
+    lc_dev_batch *staged = nullptr;
+    std::mutex batch_mu;
     // T0-only steps (lc_check_device) skip re-zeroing the control block: the
     // ticket continues from where the previous such step left it.
     bool ticket_live = false;
@@ -114,6 +142,7 @@ struct lc_ctx {
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(lat_ws); dfree(dargs);
         if (hargs) (void)hipHostFree(hargs);
+        delete staged;
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (et0) (void)hipEventDestroy(et0);
@@ -306,14 +335,8 @@ static int validate_batch(const lc_batch *b) {
     return LC_OK;
 }
 
-extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
-    if (!c || !b || !out) return lc::fail(LC_E_INVALID, "lc_upload: null argument");
-    std::lock_guard<std::mutex> g(c->mu);
-    int rc = validate_batch(b);
-    if (rc) return rc;
-    HIPCHK(hipSetDevice(c->device));
-    lc_dev_batch *d = new (std::nothrow) lc_dev_batch();
-    if (!d) return lc::fail(LC_E_NOMEM, "lc_upload: out of memory");
+// Copy a validated batch into d's device arrays (grown as needed); c->mu held.
+static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d) {
     const int64_t K = b->n_keys;
     d->device = c->device;
     d->n_keys = K;
@@ -336,11 +359,14 @@ extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
     std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
         return b->ev_off[x + 1] - b->ev_off[x] > b->ev_off[y + 1] - b->ev_off[y];
     });
+    d->trans_off = nullptr;
+    d->key_width = nullptr;
+    d->key_states = nullptr;
     auto up = [&]() -> int {
-        HIPCHK(dalloc(&d->ev_off, (size_t)K + 1));
-        HIPCHK(dalloc(&d->events, (size_t)d->n_events));
-        HIPCHK(dalloc(&d->trans, (size_t)d->n_trans));
-        HIPCHK(dalloc(&d->order, (size_t)K));
+        HIPCHK(grow(d->mem[0], d->ev_off, (size_t)K + 1));
+        HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
+        HIPCHK(grow(d->mem[2], d->trans, (size_t)d->n_trans));
+        HIPCHK(grow(d->mem[3], d->order, (size_t)K));
         if (K) {
             HIPCHK(hipMemcpyAsync(d->ev_off, b->ev_off, ((size_t)K + 1) * 8, hipMemcpyHostToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(d->order, order.data(), (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
@@ -350,22 +376,22 @@ extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
         if (b->n_trans > 0)
             HIPCHK(hipMemcpyAsync(d->trans, b->trans, (size_t)b->n_trans * 4, hipMemcpyHostToDevice, c->stream));
         if (b->trans_off && K) {
-            HIPCHK(dalloc(&d->trans_off, (size_t)K));
+            HIPCHK(grow(d->mem[4], d->trans_off, (size_t)K));
             HIPCHK(hipMemcpyAsync(d->trans_off, b->trans_off, (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
         }
         if (b->key_width && K) {
-            HIPCHK(dalloc(&d->key_width, (size_t)K));
+            HIPCHK(grow(d->mem[5], d->key_width, (size_t)K));
             HIPCHK(hipMemcpyAsync(d->key_width, b->key_width, (size_t)K, hipMemcpyHostToDevice, c->stream));
         }
         if (b->key_states && K) {
-            HIPCHK(dalloc(&d->key_states, (size_t)K));
+            HIPCHK(grow(d->mem[6], d->key_states, (size_t)K));
             HIPCHK(hipMemcpyAsync(d->key_states, b->key_states, (size_t)K * 2, hipMemcpyHostToDevice, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
         return LC_OK;
     };
-    rc = up();
-    if (rc) { delete d; return rc; }
+    int rc = up();
+    if (rc) return rc;
     // T0 spills a key only for its width (ops pending at once), its state
     // count or the initial state; all three are known here.
     {
@@ -380,6 +406,19 @@ extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
         d->t0_only = ok;
     }
     d->input_bytes = (size_t)d->n_events * 4 + ((size_t)K + 1) * 8;
+    return LC_OK;
+}
+
+extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
+    if (!c || !b || !out) return lc::fail(LC_E_INVALID, "lc_upload: null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = validate_batch(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    lc_dev_batch *d = new (std::nothrow) lc_dev_batch();
+    if (!d) return lc::fail(LC_E_NOMEM, "lc_upload: out of memory");
+    rc = upload_into(c, b, d);
+    if (rc) { delete d; return rc; }
     *out = d;
     return LC_OK;
 }
@@ -549,11 +588,23 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
 
 extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_stats *st) {
     auto t0 = std::chrono::steady_clock::now();
-    lc_dev_batch *d = nullptr;
-    int rc = lc_upload(c, b, &d);
-    if (rc) return rc;
-    rc = lc_check_device(c, d, r, 0, st);
-    lc_dev_batch_free(d);
+    if (!c || !b) return lc::fail(LC_E_INVALID, "lc_check_batch: null argument");
+    std::lock_guard<std::mutex> gb(c->batch_mu);
+    int rc;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        rc = validate_batch(b);
+        if (rc) return rc;
+        HIPCHK(hipSetDevice(c->device));
+        if (!c->staged) {
+            c->staged = new (std::nothrow) lc_dev_batch();
+            if (!c->staged) return lc::fail(LC_E_NOMEM, "lc_check_batch: out of memory");
+            c->staged->device = c->device;
+        }
+        rc = upload_into(c, b, c->staged);
+        if (rc) return rc;
+    }
+    rc = lc_check_device(c, c->staged, r, 0, st);
     if (st && rc == LC_OK)
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return rc;

@@ -306,3 +306,33 @@ def test_degenerate_histories(device):
             h = H.History.from_ops(ops)
             keys, orc = cref.check_history(h.as_c(), budget=1 << 20)
             assert sorted(k for k, r in zip(keys, orc) if r["valid"] == 0) == failures, name
+
+
+def test_check_batch_staging_reuse():
+    """lc_check_batch keeps its device arrays across calls (grown on demand):
+    batches that shrink, grow and switch models on ONE context stay bit-exact
+    with the oracle, and a batch re-checked after others gives the same answer."""
+    from histgen import mutex_history
+    from lincheck import model
+    from lincheck.checker import Packed
+    dev = Device(0)
+    seq = [H.synth(n_keys=200, ops_per_key=800, concurrency=10, anomaly_rate=0.05, seed=31),
+           H.synth(n_keys=7, ops_per_key=30, concurrency=4, anomaly_rate=0.3, seed=32),
+           None,  # mutex batch (per-model transition table) in between
+           H.synth(n_keys=500, ops_per_key=1200, concurrency=12, anomaly_rate=0.05, seed=33)]
+    first = None
+    for h in seq:
+        if h is None:
+            hm = H.History.from_ops(mutex_history(5, n_keys=50, rounds=30, procs=6))
+            pk = Packed(hm, model.mutex())
+            res = dev.check(pk)
+            _, orc = cref.check_history(hm.as_c(), model="mutex", threads=8)
+            np.testing.assert_array_equal(res.valid, orc["valid"])
+            np.testing.assert_array_equal(res.fail_event, orc["fail_event"])
+            continue
+        _, res, _ = device_vs_oracle(h, dev)
+        if first is None:
+            first = res
+    again = dev.check(Packed(seq[0]))
+    np.testing.assert_array_equal(again.valid, first.valid)
+    np.testing.assert_array_equal(again.fail_event, first.fail_event)
