@@ -274,21 +274,14 @@ extern "C" void lc_destroy(lc_ctx *c) {
     delete c;
 }
 
-// Host validation of a packed batch: every index a kernel will follow is in
-// range, every :ok names a slot that is pending.
-static int validate_batch(const lc_batch *b) {
-    if (!b || b->n_keys < 0) return lc::fail(LC_E_INVALID, "batch: bad n_keys");
-    if (b->n_keys == 0) return LC_OK;
-    if (!b->ev_off || !b->trans || b->n_trans <= 0) return lc::fail(LC_E_INVALID, "batch: missing arrays");
-    if (b->ev_off[0] != 0) return lc::fail(LC_E_INVALID, "batch: ev_off[0] != 0");
-    for (int64_t k = 0; k < b->n_keys; ++k) {
-        if (b->ev_off[k + 1] < b->ev_off[k]) return lc::fail(LC_E_INVALID, "batch: ev_off not monotone at key %lld", (long long)k);
-        if (b->ev_off[k + 1] - b->ev_off[k] > 0x7FFFFFFFull) return lc::fail(LC_E_INVALID, "batch: key %lld has > 2^31 events", (long long)k);
-    }
-    if (b->ev_off[b->n_keys] && !b->events) return lc::fail(LC_E_INVALID, "batch: events missing");
-    if (b->init_state >= LC_STATE_NONE) return lc::fail(LC_E_INVALID, "batch: bad init_state");
+// Per-event validation of a packed batch (every :ok names a pending slot,
+// every invoke's transition id is in range), over nt threads of its own.
+// Returns 0 or a reason code (1..3) with the first bad key in *badkey; sets
+// no error text, so it may run beside the caller's uploads.
+static int validate_events(const lc_batch *b, int64_t *badkey_out) {
     const int64_t K = b->n_keys;
     unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (K < 256) nt = 1;
     std::vector<int> bad((size_t)nt, 0);
     std::vector<int64_t> badkey((size_t)nt, -1);
     auto work = [&](unsigned t) {
@@ -314,16 +307,36 @@ static int validate_batch(const lc_batch *b) {
         }
     };
     std::vector<std::thread> pool;
-    if (K >= 256)
-        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
-    else
-        nt = 1, bad.resize(1), badkey.resize(1);
-    work(0);
+    for (unsigned t = 0; t < nt; ++t) pool.emplace_back(work, t);
     for (auto &th : pool) th.join();
-    for (size_t t = 0; t < bad.size(); ++t) {
-        static const char *why[] = {"", ":ok of a slot with no pending op", "transition id out of range",
-                                    ":invoke into an occupied slot"};
-        if (bad[t]) return lc::fail(LC_E_INVALID, "batch: key %lld: %s", (long long)badkey[t], why[bad[t]]);
+    for (size_t t = 0; t < bad.size(); ++t)
+        if (bad[t]) { *badkey_out = badkey[t]; return bad[t]; }
+    return 0;
+}
+
+static int events_error(int why, int64_t key) {
+    static const char *text[] = {"", ":ok of a slot with no pending op", "transition id out of range",
+                                 ":invoke into an occupied slot"};
+    return lc::fail(LC_E_INVALID, "batch: key %lld: %s", (long long)key, text[why]);
+}
+
+// Host validation of a packed batch: every index a kernel will follow is in
+// range, every :ok names a slot that is pending.  events = false leaves the
+// per-event pass to the caller (validate_events).
+static int validate_batch(const lc_batch *b, bool events = true) {
+    if (!b || b->n_keys < 0) return lc::fail(LC_E_INVALID, "batch: bad n_keys");
+    if (b->n_keys == 0) return LC_OK;
+    if (!b->ev_off || !b->trans || b->n_trans <= 0) return lc::fail(LC_E_INVALID, "batch: missing arrays");
+    if (b->ev_off[0] != 0) return lc::fail(LC_E_INVALID, "batch: ev_off[0] != 0");
+    for (int64_t k = 0; k < b->n_keys; ++k) {
+        if (b->ev_off[k + 1] < b->ev_off[k]) return lc::fail(LC_E_INVALID, "batch: ev_off not monotone at key %lld", (long long)k);
+        if (b->ev_off[k + 1] - b->ev_off[k] > 0x7FFFFFFFull) return lc::fail(LC_E_INVALID, "batch: key %lld has > 2^31 events", (long long)k);
+    }
+    if (b->ev_off[b->n_keys] && !b->events) return lc::fail(LC_E_INVALID, "batch: events missing");
+    if (b->init_state >= LC_STATE_NONE) return lc::fail(LC_E_INVALID, "batch: bad init_state");
+    if (events) {
+        int64_t bk = -1;
+        if (int why = validate_events(b, &bk)) return events_error(why, bk);
     }
     for (int64_t i = 0; i < b->n_trans; ++i) {
         uint32_t d = b->trans[i];
@@ -593,7 +606,7 @@ extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_sta
     int rc;
     {
         std::lock_guard<std::mutex> g(c->mu);
-        rc = validate_batch(b);
+        rc = validate_batch(b, false);
         if (rc) return rc;
         HIPCHK(hipSetDevice(c->device));
         if (!c->staged) {
@@ -601,7 +614,15 @@ extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_sta
             if (!c->staged) return lc::fail(LC_E_NOMEM, "lc_check_batch: out of memory");
             c->staged->device = c->device;
         }
+        // the per-event pass runs beside the uploads (nothing is launched
+        // before it has passed); upload_into reads only validated headers
+        int why = 0;
+        int64_t bk = -1;
+        std::thread vt;
+        if (b->n_keys) vt = std::thread([&] { why = validate_events(b, &bk); });
         rc = upload_into(c, b, c->staged);
+        if (vt.joinable()) vt.join();
+        if (why) return events_error(why, bk);
         if (rc) return rc;
     }
     rc = lc_check_device(c, c->staged, r, 0, st);

@@ -336,3 +336,29 @@ def test_check_batch_staging_reuse():
     again = dev.check(Packed(seq[0]))
     np.testing.assert_array_equal(again.valid, first.valid)
     np.testing.assert_array_equal(again.fail_event, first.fail_event)
+
+
+def test_malformed_batch_rejected_then_context_reusable():
+    """A batch whose event stream breaks the pairing invariants is refused with
+    LC_E_INVALID and a message naming the key -- lc_check_batch validates the
+    events beside its uploads and launches nothing -- and the same context
+    then checks a good batch bit-exactly."""
+    import ctypes as C
+    from lincheck import _native as N
+    from lincheck.checker import Packed
+    dev = Device(0)
+    h = H.synth(n_keys=400, ops_per_key=200, concurrency=6, seed=41)
+    pk = Packed(h)
+    n_ev = int(pk.ev_off[-1])
+    ev = np.ctypeslib.as_array(pk.view.events, shape=(n_ev,))
+    j = int(pk.ev_off[317])  # key 317's first event is an invoke: make it an :ok
+    assert not ev[j] & N.LC_EV_OK_BIT
+    saved = int(ev[j])
+    ev[j] = saved | N.LC_EV_OK_BIT
+    with pytest.raises(N.LincheckError) as ei:
+        dev.check(pk)
+    assert ei.value.code == -1 and "key 317" in str(ei.value)
+    with pytest.raises(N.LincheckError):
+        dev.upload(pk)
+    ev[j] = saved
+    device_vs_oracle(h, dev)
