@@ -11,6 +11,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -43,6 +45,66 @@ void dfree(T *&p) {
 }
 
 }  // namespace
+
+// Host worker threads kept for the life of a context, so the per-event
+// validation pass of every lc_check_batch does not pay thread creation.
+// run(n, fn) calls fn(0..n-1) on the workers and the caller, and returns when
+// all have finished.
+class HostPool {
+  public:
+    explicit HostPool(unsigned n) {
+        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+    void run(unsigned n, const std::function<void(unsigned)> &fn) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &fn;
+            n_ = n;
+            pending_ = n > 1 ? n - 1 : 0;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)> *fn;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (id >= n_) continue;
+                fn = fn_;
+            }
+            (*fn)(id);
+            std::lock_guard<std::mutex> g(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)> *fn_ = nullptr;
+    unsigned n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 struct lc_dev_batch {
     int device = 0;
@@ -123,6 +185,9 @@ struct lc_ctx {
     // lc_check_batch's staging batch (device arrays reused across calls) and
     // the lock that keeps one lc_check_batch at a time on it
     lc_dev_batch *staged = nullptr;
+    uint32_t *hstage = nullptr;  // pinned copy of its event words
+    HostPool *pool = nullptr;    // validation workers, created on first use
+    size_t hstage_cap = 0;
     std::mutex batch_mu;
     // T0-only steps (lc_check_device) skip re-zeroing the control block: the
     // ticket continues from where the previous such step left it.
@@ -143,6 +208,8 @@ struct lc_ctx {
         dfree(ws[0].base); dfree(ws[1].base); dfree(lat_ws); dfree(dargs);
         if (hargs) (void)hipHostFree(hargs);
         delete staged;
+        delete pool;
+        if (hstage) (void)hipHostFree(hstage);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (et0) (void)hipEventDestroy(et0);
@@ -278,14 +345,27 @@ extern "C" void lc_destroy(lc_ctx *c) {
 // every invoke's transition id is in range), over nt threads of its own.
 // Returns 0 or a reason code (1..3) with the first bad key in *badkey; sets
 // no error text, so it may run beside the caller's uploads.
-static int validate_events(const lc_batch *b, int64_t *badkey_out) {
+// stage (optional): pinned host buffer that receives a copy of the event
+// words; each thread copies the contiguous run of keys it validates, so the
+// events are read once, in cache, on their way to the DMA engine.
+static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *stage = nullptr,
+                           HostPool *hp = nullptr) {
     const int64_t K = b->n_keys;
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    unsigned nt = hp ? hp->size() : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     if (K < 256) nt = 1;
     std::vector<int> bad((size_t)nt, 0);
     std::vector<int64_t> badkey((size_t)nt, -1);
+    // contiguous key runs of about equal event counts
+    const uint64_t n_ev = b->ev_off[K];
+    std::vector<int64_t> cut((size_t)nt + 1, K);
+    cut[0] = 0;
+    for (unsigned t = 1; t < nt; ++t)
+        cut[t] = std::upper_bound(b->ev_off, b->ev_off + K, n_ev * t / nt) - b->ev_off - 1;
     auto work = [&](unsigned t) {
-        for (int64_t k = t; k < K && !bad[t]; k += nt) {
+        const int64_t k0 = std::max<int64_t>(cut[t], 0), k1 = std::max<int64_t>(cut[t + 1], k0);
+        if (stage && k1 > k0)
+            std::memcpy(stage + b->ev_off[k0], b->events + b->ev_off[k0], (b->ev_off[k1] - b->ev_off[k0]) * 4);
+        for (int64_t k = k0; k < k1 && !bad[t]; ++k) {
             uint64_t tb = b->trans_off ? b->trans_off[k] : 0;
             uint64_t pend[2] = {0, 0};
             for (uint64_t j = b->ev_off[k]; j < b->ev_off[k + 1]; ++j) {
@@ -306,9 +386,13 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out) {
             }
         }
     };
-    std::vector<std::thread> pool;
-    for (unsigned t = 0; t < nt; ++t) pool.emplace_back(work, t);
-    for (auto &th : pool) th.join();
+    if (hp) {
+        hp->run(nt, work);
+    } else {
+        std::vector<std::thread> pool;
+        for (unsigned t = 0; t < nt; ++t) pool.emplace_back(work, t);
+        for (auto &th : pool) th.join();
+    }
     for (size_t t = 0; t < bad.size(); ++t)
         if (bad[t]) { *badkey_out = badkey[t]; return bad[t]; }
     return 0;
@@ -349,7 +433,9 @@ static int validate_batch(const lc_batch *b, bool events = true) {
 }
 
 // Copy a validated batch into d's device arrays (grown as needed); c->mu held.
-static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d) {
+// events_src: where the event words are copied from (b->events by default;
+// lc_check_batch passes its pinned staging copy).
+static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d, const uint32_t *events_src = nullptr) {
     const int64_t K = b->n_keys;
     d->device = c->device;
     d->n_keys = K;
@@ -385,7 +471,8 @@ static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d) {
             HIPCHK(hipMemcpyAsync(d->order, order.data(), (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
         }
         if (d->n_events)
-            HIPCHK(hipMemcpyAsync(d->events, b->events, (size_t)d->n_events * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
+                                  hipMemcpyHostToDevice, c->stream));
         if (b->n_trans > 0)
             HIPCHK(hipMemcpyAsync(d->trans, b->trans, (size_t)b->n_trans * 4, hipMemcpyHostToDevice, c->stream));
         if (b->trans_off && K) {
@@ -473,10 +560,10 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     int32_t *n_spill0 = c->counters + 0, *n_spill1 = c->counters + 1, *n_spill2 = c->counters + 2;
     int32_t *n_wide = c->counters + 3;
 
-    // Verdicts left on the device, nothing counted, and no key can leave T0:
-    // no T1/T2 launches, no counter readback and no control-block memset --
-    // the step is T0 alone.
-    const bool t0_step = K > 0 && d->t0_only && dev_result && !(c->o.flags & LC_OPT_COUNT_PROBES);
+    // Nothing counted and no key can leave T0: no T1/T2 launches, no counter
+    // readback and no control-block memset -- the step is T0 alone (plus the
+    // result download when the results go to host memory).
+    const bool t0_step = K > 0 && d->t0_only && !(c->o.flags & LC_OPT_COUNT_PROBES);
     uint32_t ticket_base = 0;
     if (t0_step && c->ticket_live) ticket_base = c->ticket_next;
     else HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_BYTES, c->stream));
@@ -544,9 +631,14 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         return LC_OK;
     };
     if (t0_step) {
-        HIPCHK(hipEventRecord(c->e1, c->stream));
-        HIPCHK(hipEventSynchronize(c->e1));
-        std::memset(c->hctl, 0, CTL_BYTES);  // counters not read back on this path
+        if (dev_result) {
+            HIPCHK(hipEventRecord(c->e1, c->stream));
+            HIPCHK(hipEventSynchronize(c->e1));
+        } else {
+            rc = readback();
+            if (rc) return rc;
+        }
+        std::memset(c->hctl, 0, CTL_BYTES);  // counters not kept on this path
         c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
     } else {
@@ -603,6 +695,7 @@ extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_sta
     auto t0 = std::chrono::steady_clock::now();
     if (!c || !b) return lc::fail(LC_E_INVALID, "lc_check_batch: null argument");
     std::lock_guard<std::mutex> gb(c->batch_mu);
+    auto t_val = t0;
     int rc;
     {
         std::lock_guard<std::mutex> g(c->mu);
@@ -614,18 +707,38 @@ extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_sta
             if (!c->staged) return lc::fail(LC_E_NOMEM, "lc_check_batch: out of memory");
             c->staged->device = c->device;
         }
-        // the per-event pass runs beside the uploads (nothing is launched
-        // before it has passed); upload_into reads only validated headers
-        int why = 0;
+        // The per-event pass copies the event words into pinned staging as it
+        // validates them (one parallel read of the caller's array); the DMA
+        // then runs from pinned memory instead of the driver's pageable path.
+        // Batches above 256 MB of events keep the pageable path (no pinned
+        // allocation that large).
+        const size_t n_ev = b->n_keys ? (size_t)b->ev_off[b->n_keys] : 0;
+        const bool stage = n_ev > 0 && n_ev <= (256u << 20) / 4;
+        if (stage && n_ev > c->hstage_cap) {
+            if (c->hstage) (void)hipHostFree(c->hstage);
+            c->hstage = nullptr;
+            c->hstage_cap = 0;
+            HIPCHK(hipHostMalloc((void **)&c->hstage, n_ev * 4, hipHostMallocDefault));
+            c->hstage_cap = n_ev;
+        }
         int64_t bk = -1;
-        std::thread vt;
-        if (b->n_keys) vt = std::thread([&] { why = validate_events(b, &bk); });
-        rc = upload_into(c, b, c->staged);
-        if (vt.joinable()) vt.join();
-        if (why) return events_error(why, bk);
+        if (b->n_keys >= 256 && !c->pool)
+            c->pool = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+        if (b->n_keys)
+            if (int why = validate_events(b, &bk, stage ? c->hstage : nullptr, b->n_keys >= 256 ? c->pool : nullptr))
+                return events_error(why, bk);
+        t_val = std::chrono::steady_clock::now();
+        rc = upload_into(c, b, c->staged, stage ? c->hstage : nullptr);
         if (rc) return rc;
     }
+    const auto t_up = std::chrono::steady_clock::now();
     rc = lc_check_device(c, c->staged, r, 0, st);
+    if (std::getenv("LC_TIMING")) {
+        using ms = std::chrono::duration<double, std::milli>;
+        const auto t_end = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "lc_check_batch: validate %.3f ms, upload %.3f ms, check %.3f ms\n",
+                     ms(t_val - t0).count(), ms(t_up - t_val).count(), ms(t_end - t_up).count());
+    }
     if (st && rc == LC_OK)
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return rc;
