@@ -55,7 +55,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--budget", type=int, default=1 << 20)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-cpu", action="store_true",
+                    help="skip the CPU baseline and the host-to-host pass (profiling runs: only the timed steps "
+                         "and the probe-count pass launch the search)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU (exploration only)")
     ap.add_argument("--ops", type=int, default=0, help="override ops per key (exploration only)")
@@ -259,8 +261,8 @@ def main():
         own_ok = bool(np.array_equal(gv[:K], v_host) and np.array_equal(gfe[:K], fe_host))
         node = {"keys": int(gv.size), "valid": int((gv == 1).sum()), "invalid": int((gv == 0).sum()),
                 "unknown": int((gv == -1).sum()), "rank0_block_matches_local": own_ok}
-    h2h_ms = None
-    if rank == 0:
+    h2h_ms, h2h_same = None, None
+    if rank == 0 and not args.no_cpu:
         # SURVEY.md 8(d) D-1's end-to-end rate, outside the timed region: one
         # lc_check_batch from the packed SoA in host memory to host verdict
         # arrays (upload over PCIe + search + download), best of 3.  Never `value`.
@@ -271,6 +273,7 @@ def main():
             h2h.append(time.perf_counter() - th)
         h2h_ms = min(h2h) * 1e3
         h2h_same = bool(np.array_equal(hr.valid, v_host) and np.array_equal(hr.fail_event, fe_host))
+    if rank == 0:
         # probe count from one extra, untimed pass with
         # LC_OPT_COUNT_PROBES: the timed steps skip the per-event popcounts
         dev_c = Device(local, budget=args.budget, count_probes=True)
@@ -385,9 +388,9 @@ def main():
                          "unknown": int((v_host == -1).sum())},
             "parity_vs_oracle": parity,
             "node_verdicts": node,
-            "host_to_host": {"ms": h2h_ms, "ops_per_s_one_gpu": K * ops / (h2h_ms * 1e-3),
-                             "same_verdicts_as_resident": h2h_same,
-                             "what": "rank 0: lc_check_batch from packed host SoA to host verdicts (PCIe incl.)"},
+            "host_to_host": None if h2h_ms is None else {
+                "ms": h2h_ms, "ops_per_s_one_gpu": K * ops / (h2h_ms * 1e-3), "same_verdicts_as_resident": h2h_same,
+                "what": "rank 0: lc_check_batch from packed host SoA to host verdicts (PCIe incl.), best of 3"},
             "setup_s": round(t_gen, 2),
         }
         print(json.dumps(line), flush=True)
