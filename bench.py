@@ -204,13 +204,18 @@ def main():
     from lincheck import parallel as P
 
     n_step = [0]
+    # N = 1: a step whose keys all stay in the register tier is only enqueued
+    # (LC_DEV_ASYNC), so step k+1's launch is queued while step k runs; the
+    # HIP events of lc_wait give the launches' span.  N > 1 waits per step:
+    # the records are packed on torch's stream right after the search.
+    use_async = world == 1
 
     def step():
         b = bufs[n_step[0] % len(bufs)]
         n_step[0] += 1
         if b["packed"] is not None:
             b["packed"].synchronize()  # this set's previous records are packed
-        st = db.check_into(b["res"])
+        st = db.check_into(b["res"], asynchronous=use_async)
         if world > 1:  # the path's one exchange step: verdict records over RCCL
             rec[:K] = P.pack_records(b["valid"], b["cause"], b["fail_event"])
             b["packed"] = torch.cuda.Event()
@@ -221,6 +226,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    dev.wait()  # resets the asynchronous-step span
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -237,6 +243,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    n_async, span_ms = dev.wait()
+    if n_async:  # asynchronous steps: per-launch time = the span over the launches
+        assert n_async == args.steps, (n_async, args.steps)
+        kernel_ms = tier0_ms = [span_ms / n_async]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

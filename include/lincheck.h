@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 3
+#define LC_ABI_VERSION 4
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -268,11 +268,23 @@ int  lc_check_batch(lc_ctx *ctx, const lc_batch *b, lc_result *r, lc_stats *s);
 /* Device-resident batches: upload once, check many times (the bench's step). */
 int  lc_upload(lc_ctx *ctx, const lc_batch *b, lc_dev_batch **out);
 void lc_dev_batch_free(lc_dev_batch *db);
-/* Search an uploaded batch.  If dev_result != 0 the result arrays in r are
- * DEVICE pointers (e.g. torch tensors for an RCCL all-gather) and nothing is
- * copied back; otherwise they are host arrays. */
+/* Search an uploaded batch.  flags:
+ *   LC_DEV_RESULT  the result arrays in r are DEVICE pointers (e.g. torch
+ *                  tensors for an RCCL all-gather) and nothing is copied back;
+ *                  without it they are host arrays.
+ *   LC_DEV_ASYNC   (with LC_DEV_RESULT) when the step is the register tier
+ *                  alone (every key fits it, no probe counting), return once it
+ *                  is enqueued on the context's stream: s is zeroed, and results
+ *                  are ready after lc_wait.  Other steps run synchronously. */
+#define LC_DEV_RESULT 1
+#define LC_DEV_ASYNC  2
 int  lc_check_device(lc_ctx *ctx, const lc_dev_batch *db, lc_result *r,
-                     int dev_result, lc_stats *s);
+                     int flags, lc_stats *s);
+/* Wait for every step enqueued on the context.  Returns the number of
+ * LC_DEV_ASYNC steps since the previous lc_wait (or a negative LC_E_* code);
+ * s->kernel_ms = their span (HIP events, first start .. last end) and
+ * s->tier0_ms = span / count. */
+int  lc_wait(lc_ctx *ctx, lc_stats *s);
 
 /* ---- synthetic histories ------------------------------ */
 typedef struct lc_synth_opts {

@@ -161,6 +161,8 @@ struct lc_ctx {
     int cu_count = 256;
     hipStream_t stream = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr, et3a = nullptr, et3b = nullptr;
+    hipEvent_t ea0 = nullptr, ea1 = nullptr;  // span of the LC_DEV_ASYNC steps since lc_wait
+    uint32_t n_async = 0;
     std::mutex mu;
     // scratch, grown on demand
     int64_t cap_keys = 0;
@@ -215,6 +217,8 @@ struct lc_ctx {
         if (et0) (void)hipEventDestroy(et0);
         if (et3a) (void)hipEventDestroy(et3a);
         if (et3b) (void)hipEventDestroy(et3b);
+        if (ea0) (void)hipEventDestroy(ea0);
+        if (ea1) (void)hipEventDestroy(ea1);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -320,6 +324,8 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         HIPCHK(hipEventCreate(&c->et0));
         HIPCHK(hipEventCreate(&c->et3a));
         HIPCHK(hipEventCreate(&c->et3b));
+        HIPCHK(hipEventCreate(&c->ea0));
+        HIPCHK(hipEventCreate(&c->ea1));
         HIPCHK(dalloc(&c->ctl, 16));
         c->acc = c->ctl;
         c->counters = (int32_t *)(c->ctl + 4);
@@ -529,7 +535,9 @@ extern "C" void lc_dev_batch_free(lc_dev_batch *d) {
     delete d;
 }
 
-extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, int dev_result, lc_stats *st) {
+extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, int flags, lc_stats *st) {
+    if (flags & ~(LC_DEV_RESULT | LC_DEV_ASYNC)) return lc::fail(LC_E_INVALID, "lc_check_device: unknown flags 0x%x", flags);
+    const bool dev_result = (flags & LC_DEV_RESULT) != 0;
     if (!c || !d || !r || !r->valid || !r->fail_event || !r->cause)
         return lc::fail(LC_E_INVALID, "lc_check_device: null argument");
     if (d->device != c->device) return lc::fail(LC_E_INVALID, "lc_check_device: batch lives on another device");
@@ -564,6 +572,8 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     // readback and no control-block memset -- the step is T0 alone (plus the
     // result download when the results go to host memory).
     const bool t0_step = K > 0 && d->t0_only && !(c->o.flags & LC_OPT_COUNT_PROBES);
+    // LC_DEV_ASYNC: such a step is only enqueued; lc_wait ends the run
+    const bool async = t0_step && dev_result && (flags & LC_DEV_ASYNC);
     uint32_t ticket_base = 0;
     if (t0_step && c->ticket_live) ticket_base = c->ticket_next;
     else HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_BYTES, c->stream));
@@ -585,14 +595,25 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     // T0 reads the result/counter/list pointers from a device copy of its
     // Args, refreshed (outside the timed region) only when they change
     if (!c->hargs_valid || std::memcmp(c->hargs, &a0, sizeof a0) != 0) {
+        // the pinned staging copy may still feed an enqueued copy
+        if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
         std::memcpy(c->hargs, &a0, sizeof a0);
         HIPCHK(hipMemcpyAsync(c->dargs, c->hargs, sizeof(lcd::Args), hipMemcpyHostToDevice, c->stream));
         c->hargs_valid = true;
     }
     HIPCHK(hipEventRecord(c->e0, c->stream));
+    if (async && c->n_async == 0) HIPCHK(hipEventRecord(c->ea0, c->stream));
     if (K > 0) {
         HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
+    }
+    if (async) {
+        HIPCHK(hipEventRecord(c->ea1, c->stream));
+        ++c->n_async;
+        c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
+        c->ticket_live = true;
+        if (st) *st = lc_stats{};  // times come from lc_wait
+        return LC_OK;
     }
     if (K > 0 && !t0_step) {
         // T1: LDS hash sets
@@ -689,6 +710,23 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         st->deep_keys = (uint64_t)cnt[0];  // keys that left the register tier
     }
     return LC_OK;
+}
+
+extern "C" int lc_wait(lc_ctx *c, lc_stats *st) {
+    if (!c) return lc::fail(LC_E_INVALID, "lc_wait: null context");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const int n = (int)c->n_async;
+    float ms = 0;
+    if (n) HIPCHK(hipEventElapsedTime(&ms, c->ea0, c->ea1));
+    c->n_async = 0;
+    if (st) {
+        *st = lc_stats{};
+        st->kernel_ms = ms;                    // first enqueued step's start .. last one's end
+        st->tier0_ms = n ? ms / (float)n : 0;  // per step, gaps between launches included
+    }
+    return n;
 }
 
 extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_stats *st) {

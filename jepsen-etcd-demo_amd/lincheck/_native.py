@@ -17,8 +17,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 3
+LC_ABI_VERSION = 4
 LC_OPT_COUNT_PROBES = 0x1
+LC_DEV_RESULT, LC_DEV_ASYNC = 1, 2
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
 LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE = 0, 1, 2, 3, 4, 5
 LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX = 0, 1, 2
@@ -94,6 +95,7 @@ SIGNATURES = {
     "lc_upload": (C.c_int, [C.c_void_p, P(LcBatch), P(C.c_void_p)]),
     "lc_dev_batch_free": (None, [C.c_void_p]),
     "lc_check_device": (C.c_int, [C.c_void_p, C.c_void_p, P(LcResult), C.c_int, P(LcStats)]),
+    "lc_wait": (C.c_int, [C.c_void_p, P(LcStats)]),
     "lc_pack": (C.c_int, [P(LcHistory), P(LcPackOpts), P(C.c_void_p)]),
     "lc_packed_free": (None, [C.c_void_p]),
     "lc_packed_view": (C.c_int, [C.c_void_p, P(LcBatch)]),

@@ -145,6 +145,13 @@ class Device:
         N.check(N.lib().lc_check_batch(self.handle, C.byref(packed.view), C.byref(r), C.byref(st)))
         return self._results(arrs, K, st)
 
+    def wait(self):
+        """lc_wait: (number of asynchronous steps since the last wait, their
+        span in ms from the first start to the last end)."""
+        st = N.LcStats()
+        n = N.check(N.lib().lc_wait(self.handle, C.byref(st)))
+        return n, float(st.kernel_ms)
+
     def upload(self, packed: Packed) -> "DevBatch":
         return DevBatch(self, packed)
 
@@ -173,10 +180,13 @@ class DevBatch:
         N.check(N.lib().lc_check_device(self.dev.handle, self.handle, C.byref(r), 0, C.byref(st)))
         return self.dev._results({k: v.copy() for k, v in self.arrs.items()}, self.n_keys, st)
 
-    def check_into(self, r: N.LcResult) -> N.LcStats:
-        """Search with results written to caller-provided DEVICE arrays (no D2H)."""
+    def check_into(self, r: N.LcResult, asynchronous: bool = False) -> N.LcStats:
+        """Search with results written to caller-provided DEVICE arrays (no D2H).
+        asynchronous: a register-tier-only step is only enqueued (LC_DEV_ASYNC);
+        its stats are zero and the results are ready after Device.wait()."""
         st = N.LcStats()
-        N.check(N.lib().lc_check_device(self.dev.handle, self.handle, C.byref(r), 1, C.byref(st)))
+        flags = N.LC_DEV_RESULT | (N.LC_DEV_ASYNC if asynchronous else 0)
+        N.check(N.lib().lc_check_device(self.dev.handle, self.handle, C.byref(r), flags, C.byref(st)))
         return st
 
 

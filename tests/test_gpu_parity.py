@@ -362,3 +362,39 @@ def test_malformed_batch_rejected_then_context_reusable():
         dev.upload(pk)
     ev[j] = saved
     device_vs_oracle(h, dev)
+
+
+def test_async_resident_steps():
+    """LC_DEV_ASYNC: register-tier-only steps are only enqueued, lc_wait
+    returns their count and span, and the verdicts equal a synchronous check's
+    (and the oracle's).  A batch with keys beyond the register tier ignores
+    the flag and runs synchronously (lc_wait then counts 0)."""
+    import ctypes as C
+    from lincheck import _native as N
+    from lincheck.checker import Packed
+    dev = Device(0)
+    for h, t0_only in ((H.synth(n_keys=600, ops_per_key=700, concurrency=10, anomaly_rate=0.05, seed=51), True),
+                       (H.synth(n_keys=16, ops_per_key=600, concurrency=16, seed=17), False)):
+        pk = Packed(h)
+        db = dev.upload(pk)
+        K = pk.n_keys
+        valid, fe, cause = _HipBuf(K), _HipBuf(4 * K), _HipBuf(K)
+        for b in (valid, fe, cause):
+            b.fill(0x5A)
+        r = N.LcResult(C.cast(valid.ptr, N.P(C.c_int8)), C.cast(fe.ptr, N.P(C.c_int32)),
+                       C.cast(cause.ptr, N.P(C.c_uint8)), None, None, None)
+        dev.wait()
+        for _ in range(4):
+            st = db.check_into(r, asynchronous=True)
+        n, span = dev.wait()
+        if t0_only:
+            assert n == 4 and span > 0 and st.kernel_ms == 0
+        else:
+            assert n == 0 and st.kernel_ms > 0
+        ref = db.check(peak=False)
+        np.testing.assert_array_equal(valid.get(np.int8), ref.valid)
+        np.testing.assert_array_equal(fe.get(np.int32), ref.fail_event)
+        np.testing.assert_array_equal(cause.get(np.uint8), ref.cause)
+        _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+        np.testing.assert_array_equal(ref.valid, orc["valid"])
+        np.testing.assert_array_equal(ref.fail_event, orc["fail_event"])
