@@ -398,3 +398,35 @@ def test_async_resident_steps():
         _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
         np.testing.assert_array_equal(ref.valid, orc["valid"])
         np.testing.assert_array_equal(ref.fail_event, orc["fail_event"])
+
+
+def test_concurrent_calls_on_one_context():
+    """independent/checker calls its inner checker from a
+    bounded pmap, so one context may be entered from several threads at once.
+    Calls are serialised inside the library; every thread's verdicts must be
+    its own batch's (bit-exact with the oracle)."""
+    import threading
+    from lincheck.checker import Packed
+    dev = Device(0)
+    hs = [H.synth(n_keys=n, ops_per_key=300, concurrency=8, anomaly_rate=0.1, seed=60 + i)
+          for i, n in enumerate((300, 50, 700, 5, 260, 1000))]
+    pks = [Packed(h) for h in hs]
+    out, errs = [None] * len(hs), []
+
+    def run(i):
+        try:
+            for _ in range(3):
+                out[i] = dev.check(pks[i], verdicts_only=(i % 2 == 0))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(hs))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    for h, res in zip(hs, out):
+        _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+        np.testing.assert_array_equal(res.valid, orc["valid"])
+        np.testing.assert_array_equal(res.fail_event, orc["fail_event"])
