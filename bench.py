@@ -204,27 +204,41 @@ def main():
     from lincheck import parallel as P
 
     n_step = [0]
-    # N = 1: a step whose keys all stay in the register tier is only enqueued
+    # A step whose keys all stay in the register tier is only enqueued
     # (LC_DEV_ASYNC), so step k+1's launch is queued while step k runs; the
-    # HIP events of lc_wait give the launches' span.  N > 1 waits per step:
-    # the records are packed on torch's stream right after the search.
-    use_async = world == 1
+    # HIP events of lc_wait give the launches' span.  N > 1: step k's records
+    # are packed and all-gathered during step k+1, once lc_wait_step has seen
+    # step k's search finish (step k+1's search keeps running); the last
+    # step's exchange is flushed inside the timed region.
+    pending = [None]  # result set whose search is enqueued, records not yet exchanged
+
+    def exchange(b, back):  # the path's one exchange step: verdict records over RCCL
+        dev.wait_step(back)
+        rec[:K] = P.pack_records(b["valid"], b["cause"], b["fail_event"])
+        b["packed"] = torch.cuda.Event()
+        b["packed"].record()
+        dist.all_gather_into_tensor(gathered, rec)
 
     def step():
         b = bufs[n_step[0] % len(bufs)]
         n_step[0] += 1
         if b["packed"] is not None:
             b["packed"].synchronize()  # this set's previous records are packed
-        st = db.check_into(b["res"], asynchronous=use_async)
-        if world > 1:  # the path's one exchange step: verdict records over RCCL
-            rec[:K] = P.pack_records(b["valid"], b["cause"], b["fail_event"])
-            b["packed"] = torch.cuda.Event()
-            b["packed"].record()
-            dist.all_gather_into_tensor(gathered, rec)
+        st = db.check_into(b["res"], asynchronous=True)
+        if world > 1:
+            if pending[0] is not None:
+                exchange(pending[0], 1)  # the previous step's search
+            pending[0] = b
         return st
+
+    def flush():
+        if world > 1 and pending[0] is not None:
+            exchange(pending[0], 0)
+            pending[0] = None
 
     for _ in range(args.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
     dev.wait()  # resets the asynchronous-step span
     if world > 1:
@@ -238,6 +252,7 @@ def main():
         tier0_ms.append(st.tier0_ms)
         tier3_ms.append(st.tier3_ms)
         deep = st.deep_keys
+    flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

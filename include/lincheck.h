@@ -285,6 +285,10 @@ int  lc_check_device(lc_ctx *ctx, const lc_dev_batch *db, lc_result *r,
  * s->kernel_ms = their span (HIP events, first start .. last end) and
  * s->tier0_ms = span / count. */
 int  lc_wait(lc_ctx *ctx, lc_stats *s);
+/* Wait until the LC_DEV_ASYNC step `back` steps before the latest (0 = the
+ * latest, at most 3) has finished, leaving later ones running; with no such
+ * step on record, wait for everything on the context's stream. */
+int  lc_wait_step(lc_ctx *ctx, int back);
 
 /* ---- synthetic histories ------------------------------ */
 typedef struct lc_synth_opts {

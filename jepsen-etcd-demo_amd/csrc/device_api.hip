@@ -163,6 +163,8 @@ struct lc_ctx {
     hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr, et3a = nullptr, et3b = nullptr;
     hipEvent_t ea0 = nullptr, ea1 = nullptr;  // span of the LC_DEV_ASYNC steps since lc_wait
     uint32_t n_async = 0;
+    hipEvent_t ring[4] = {};  // end of each of the last 4 LC_DEV_ASYNC steps (lc_wait_step)
+    uint64_t async_seq = 0;
     std::mutex mu;
     // scratch, grown on demand
     int64_t cap_keys = 0;
@@ -219,6 +221,8 @@ struct lc_ctx {
         if (et3b) (void)hipEventDestroy(et3b);
         if (ea0) (void)hipEventDestroy(ea0);
         if (ea1) (void)hipEventDestroy(ea1);
+        for (hipEvent_t &e : ring)
+            if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -326,6 +330,7 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         HIPCHK(hipEventCreate(&c->et3b));
         HIPCHK(hipEventCreate(&c->ea0));
         HIPCHK(hipEventCreate(&c->ea1));
+        for (hipEvent_t &e : c->ring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(dalloc(&c->ctl, 16));
         c->acc = c->ctl;
         c->counters = (int32_t *)(c->ctl + 4);
@@ -609,6 +614,8 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     }
     if (async) {
         HIPCHK(hipEventRecord(c->ea1, c->stream));
+        HIPCHK(hipEventRecord(c->ring[c->async_seq % 4], c->stream));
+        ++c->async_seq;
         ++c->n_async;
         c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
@@ -727,6 +734,18 @@ extern "C" int lc_wait(lc_ctx *c, lc_stats *st) {
         st->tier0_ms = n ? ms / (float)n : 0;  // per step, gaps between launches included
     }
     return n;
+}
+
+extern "C" int lc_wait_step(lc_ctx *c, int back) {
+    if (!c) return lc::fail(LC_E_INVALID, "lc_wait_step: null context");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    if (back < 0 || back >= 4 || (uint64_t)back >= c->async_seq) {
+        HIPCHK(hipStreamSynchronize(c->stream));  // no such step on record: everything
+    } else {
+        HIPCHK(hipEventSynchronize(c->ring[(c->async_seq - 1 - (uint64_t)back) % 4]));
+    }
+    return LC_OK;
 }
 
 extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_stats *st) {

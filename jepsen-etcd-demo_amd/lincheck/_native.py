@@ -96,6 +96,7 @@ SIGNATURES = {
     "lc_dev_batch_free": (None, [C.c_void_p]),
     "lc_check_device": (C.c_int, [C.c_void_p, C.c_void_p, P(LcResult), C.c_int, P(LcStats)]),
     "lc_wait": (C.c_int, [C.c_void_p, P(LcStats)]),
+    "lc_wait_step": (C.c_int, [C.c_void_p, C.c_int]),
     "lc_pack": (C.c_int, [P(LcHistory), P(LcPackOpts), P(C.c_void_p)]),
     "lc_packed_free": (None, [C.c_void_p]),
     "lc_packed_view": (C.c_int, [C.c_void_p, P(LcBatch)]),

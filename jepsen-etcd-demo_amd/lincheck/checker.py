@@ -152,6 +152,11 @@ class Device:
         n = N.check(N.lib().lc_wait(self.handle, C.byref(st)))
         return n, float(st.kernel_ms)
 
+    def wait_step(self, back: int = 0):
+        """lc_wait_step: wait for the asynchronous step `back` steps before the
+        latest (later ones keep running)."""
+        N.check(N.lib().lc_wait_step(self.handle, back))
+
     def upload(self, packed: Packed) -> "DevBatch":
         return DevBatch(self, packed)
 

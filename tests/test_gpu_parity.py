@@ -386,6 +386,8 @@ def test_async_resident_steps():
         dev.wait()
         for _ in range(4):
             st = db.check_into(r, asynchronous=True)
+        dev.wait_step(1)  # lc_wait_step: the step before the latest (or everything)
+        dev.wait_step(0)
         n, span = dev.wait()
         if t0_only:
             assert n == 4 and span > 0 and st.kernel_ms == 0
