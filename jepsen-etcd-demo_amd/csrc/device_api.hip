@@ -399,6 +399,8 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
     };
     if (hp) {
         hp->run(nt, work);
+    } else if (nt == 1) {
+        work(0);
     } else {
         std::vector<std::thread> pool;
         for (unsigned t = 0; t < nt; ++t) pool.emplace_back(work, t);
