@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 4
+#define LC_ABI_VERSION 5
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -146,6 +146,13 @@ typedef struct lc_batch {
     const uint8_t  *key_width;  /* [n_keys] max slots used (1 + max slot), or NULL */
     const uint16_t *key_states; /* [n_keys] state ids used, or NULL           */
     uint32_t        init_state; /* state id of the initial value (0 = nil)    */
+    const uint8_t  *key_error;  /* [n_keys] nonzero: the key's sub-history could
+                                   not be prepared (lc_pack: knossos.history/
+                                   complete's assertion, an op the model cannot
+                                   step); the key is :unknown with cause
+                                   LC_CAUSE_ERROR and its events are ignored --
+                                   jepsen.checker/check-safe around that one key
+                                   (etcdemo.clj:115).  NULL = no such key.       */
 } lc_batch;
 
 /* The Knossos model a batch is checked against (knossos.model, SURVEY.md
@@ -168,8 +175,17 @@ typedef struct lc_packed lc_packed;  /* library-owned */
 /* jepsen.independent/checker's split (history-keys + subhistory, per
  * etcdemo.clj:115) followed by knossos.history/complete + without-failures
  * and model memoisation, for the cas-register model.  Keys appear in order
- * of first appearance.  Non-tuple ops (nemesis) belong to every key's
- * sub-history and, being :info, are no-ops for the search. */
+ * of first appearance.  Non-tuple ops belong to every key's sub-history
+ * (jepsen.independent/subhistory keeps them): the nemesis's :info ops are
+ * no-ops there, and any other op is paired and stepped in every key.
+ *
+ * Errors are per key, as independent/checker runs check-safe per key: a key
+ * whose sub-history fails complete's assertion (a completion with no
+ * outstanding invocation of its process) or holds an op the model cannot
+ * step keeps its place with no events and key_error set (lc_batch), and the
+ * other keys are packed as usual; lc_packed_key_error names the cause.
+ * Only malformed arrays (bad :type / :f codes, missing pointers) fail the
+ * whole call. */
 int  lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed **out);
 void lc_packed_free(lc_packed *p);
 /* Borrowed view of the packed arrays (valid until lc_packed_free). */
@@ -181,6 +197,9 @@ int64_t lc_packed_event_row(const lc_packed *p, int64_t i, int64_t j);
 /* Number of history rows in key i's sub-history (incl. nemesis rows) and the
  * rows themselves (out may be NULL to query the count). */
 int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows);
+/* Why key i could not be prepared (NULL when it was; borrowed, valid until
+ * lc_packed_free). */
+const char *lc_packed_key_error(const lc_packed *p, int64_t i);
 /* Register value of state id s of key i (state 0 = nil -> *is_nil = 1). */
 int lc_packed_state_value(const lc_packed *p, int64_t i, uint32_t s, int64_t *value, int *is_nil);
 
@@ -224,7 +243,8 @@ typedef struct lc_opts {
 #define LC_CAUSE_BUDGET  2  /* unknown: > max_configs configs                 */
 #define LC_CAUSE_WINDOW  3  /* unknown: > LC_WIDE_MAX_SLOTS ops pending       */
 #define LC_CAUSE_STATES  4  /* unknown: > LC_WIDE_MAX_STATES register values  */
-#define LC_CAUSE_ERROR   5  /* unknown: device-side fault detected            */
+#define LC_CAUSE_ERROR   5  /* unknown: the key's sub-history could not be
+                                   prepared (lc_batch.key_error; check-safe)   */
 
 typedef struct lc_result {
     int8_t   *valid;         /* [n_keys] LC_VALID / LC_INVALID / LC_UNKNOWN         */

@@ -120,6 +120,7 @@ struct lc_dev_batch {
     uint32_t *trans_off = nullptr;
     uint8_t *key_width = nullptr;
     uint16_t *key_states = nullptr;
+    uint8_t *key_error = nullptr;
     int32_t *order = nullptr;  // LPT: keys by event count, descending
     bool t0_only = false;      // every key fits the register lattice: T0 never spills
     size_t input_bytes = 0;    // bytes the search reads per pass (events + offsets + tables)
@@ -129,7 +130,7 @@ struct lc_dev_batch {
     struct Mem {
         void *p = nullptr;
         size_t cap = 0;
-    } mem[7];
+    } mem[8];
     ~lc_dev_batch() {
         for (Mem &m : mem)
             if (m.p) (void)hipFree(m.p);
@@ -377,6 +378,7 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
         if (stage && k1 > k0)
             std::memcpy(stage + b->ev_off[k0], b->events + b->ev_off[k0], (b->ev_off[k1] - b->ev_off[k0]) * 4);
         for (int64_t k = k0; k < k1 && !bad[t]; ++k) {
+            if (b->key_error && b->key_error[k]) continue;  // not searched
             uint64_t tb = b->trans_off ? b->trans_off[k] : 0;
             uint64_t pend[2] = {0, 0};
             for (uint64_t j = b->ev_off[k]; j < b->ev_off[k + 1]; ++j) {
@@ -474,6 +476,7 @@ static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d, const uint
     d->trans_off = nullptr;
     d->key_width = nullptr;
     d->key_states = nullptr;
+    d->key_error = nullptr;
     auto up = [&]() -> int {
         HIPCHK(grow(d->mem[0], d->ev_off, (size_t)K + 1));
         HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
@@ -499,6 +502,10 @@ static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d, const uint
         if (b->key_states && K) {
             HIPCHK(grow(d->mem[6], d->key_states, (size_t)K));
             HIPCHK(hipMemcpyAsync(d->key_states, b->key_states, (size_t)K * 2, hipMemcpyHostToDevice, c->stream));
+        }
+        if (b->key_error && K) {
+            HIPCHK(grow(d->mem[7], d->key_error, (size_t)K));
+            HIPCHK(hipMemcpyAsync(d->key_error, b->key_error, (size_t)K, hipMemcpyHostToDevice, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
         return LC_OK;
@@ -558,7 +565,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
 
     lcd::Args a{};
     a.ev_off = d->ev_off; a.events = d->events; a.trans = d->trans; a.trans_off = d->trans_off;
-    a.key_width = d->key_width; a.key_states = d->key_states;
+    a.key_width = d->key_width; a.key_states = d->key_states; a.key_error = d->key_error;
     a.init_state = d->init_state; a.shared_states = d->shared_states;
     a.budget = c->o.max_configs; a.max_final = c->o.max_final; a.debug_mode = c->o.debug_mode;
     a.count_probes = (c->o.flags & LC_OPT_COUNT_PROBES) ? 1 : 0;
@@ -716,7 +723,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         st->probes = acc[0];
         st->events = acc[1];
         st->lds_keys = acc[2];
-        st->deep_keys = (uint64_t)cnt[0];  // keys that left the register tier
+        st->deep_keys = (uint64_t)(cnt[2] + cnt[3]);  // keys the HBM tier (re)searched
     }
     return LC_OK;
 }

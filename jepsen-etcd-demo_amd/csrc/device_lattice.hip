@@ -182,6 +182,7 @@ struct T0Args {
     const uint32_t *trans_off;   // may be null
     const uint8_t *key_width;    // may be null
     const uint16_t *key_states;  // may be null
+    const uint8_t *key_error;    // may be null
     const int32_t *order;
     int32_t *ticket;
     uint32_t *lat_ws;            // unused (the 9-10-pending workspace is in LDS)
@@ -649,6 +650,10 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
     const uint64_t eb = a.ev_off[key], ee = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
+    if (a.key_error && a.key_error[key]) {  // lc_pack could not prepare it (check-safe)
+        finish_key(*a.full, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+        return K_DONE;
+    }
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
         finish_key(*a.full, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
@@ -966,7 +971,8 @@ size_t lat_ws_words() { return 3 * T0_RMEM * 64; }
 hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s, uint32_t ticket_base) {
     T0Args t{};
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
-    t.key_width = a.key_width; t.key_states = a.key_states; t.order = a.order; t.ticket = a.ticket;
+    t.key_width = a.key_width; t.key_states = a.key_states; t.key_error = a.key_error; t.order = a.order;
+    t.ticket = a.ticket;
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
     t.init_state = a.init_state; t.shared_states = a.shared_states; t.ticket_base = ticket_base;
     t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) | (a.final_cfg ? T0_WANT_FINAL : 0u) |

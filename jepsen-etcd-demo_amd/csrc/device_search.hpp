@@ -17,6 +17,7 @@ struct Args {
     const uint32_t *trans_off;   // may be null
     const uint8_t *key_width;    // may be null
     const uint16_t *key_states;  // may be null
+    const uint8_t *key_error;    // may be null: nonzero = :unknown (LC_CAUSE_ERROR), not searched
     uint32_t init_state;
     uint32_t shared_states;      // state ids used by the shared table (trans_off == null)
     uint64_t budget;

@@ -15,6 +15,11 @@
 //      process with an op outstanding leaves the first pending forever (the
 //      pending index is overwritten, as complete's assoc! does).  A completion
 //      with no outstanding invocation is an error (complete asserts).
+//   A9 errors are per key: independent/checker wraps each key's check in
+//      check-safe (etcdemo.clj:115), so a key whose sub-history fails
+//      complete's assertion or holds an op the model cannot step is reported
+//      :unknown with the error while every other key is checked.  Such a key
+//      keeps its place in the batch with no events and key_error set.
 //   A4/A5 knossos.model/cas-register + knossos.model.memo: every surviving op
 //      becomes a transition descriptor over interned register states (state 0
 //      = nil, the initial value of (model/cas-register), etcdemo.clj:117).
@@ -97,6 +102,7 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
                 static const char *names[] = {"cas-register", "register", "mutex"};
                 out.err = LC_E_UNSUPPORTED;
                 out.msg = "row " + std::to_string(r) + ": " + names[model] + " cannot step this :f";
+                out.ops.clear();
                 return;
             }
             int32_t id = (int32_t)out.ops.size();
@@ -108,6 +114,7 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
             if (!pid) {
                 out.err = LC_E_INVALID;
                 out.msg = "row " + std::to_string(r) + ": process completed an operation without a prior invocation";
+                out.ops.clear();
                 return;
             }
             KOp &op = out.ops[(size_t)*pid];
@@ -182,6 +189,9 @@ struct lc_packed {
     // state id -> register value: shared table, or per key (state_off[k] ..)
     std::vector<int64_t> state_vals;  // index 0 unused (nil)
     std::vector<uint64_t> state_off;  // empty = shared
+    // keys that could not be prepared (A9): empty = none
+    std::vector<uint8_t> key_error;
+    std::vector<std::string> key_msg;
 };
 
 extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed **out) {
@@ -208,14 +218,9 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             int64_t k = h->key[r];
             if (k == LC_NO_KEY) {
                 row_key[(size_t)r] = -1;
-                // Non-tuple ops are shared by every sub-history.  Only :info ops
-                // (the nemesis) are no-ops for the search; anything else would be
-                // stepped by the model with a non-register :f or value.
-                if (h->type[r] != LC_INFO) {
-                    delete P;
-                    return lc::fail(LC_E_UNSUPPORTED,
-                                    "lc_pack: row %lld: non-tuple op of :type other than :info", (long long)r);
-                }
+                // Non-tuple ops are shared by every sub-history (subhistory keeps
+                // them): the nemesis's :info ops are no-ops there, and any other
+                // op is paired and stepped in every key as it stands.
                 P->shared_rows.push_back(r);
                 continue;
             }
@@ -249,23 +254,40 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         if (K < 64) nt = 1;
         {
             auto work = [&](unsigned t) {
-                for (int64_t k = t; k < K; k += nt)
-                    pack_key(*h, P->krows.data() + P->krow_off[(size_t)k],
-                             (int64_t)(P->krow_off[(size_t)k + 1] - P->krow_off[(size_t)k]), model, ko[(size_t)k]);
+                std::vector<int64_t> merged;  // key rows + shared rows, in history order
+                for (int64_t k = t; k < K; k += nt) {
+                    const int64_t *kr = P->krows.data() + P->krow_off[(size_t)k];
+                    const int64_t nk = (int64_t)(P->krow_off[(size_t)k + 1] - P->krow_off[(size_t)k]);
+                    if (P->shared_rows.empty()) {
+                        pack_key(*h, kr, nk, model, ko[(size_t)k]);
+                        continue;
+                    }
+                    merged.resize((size_t)nk + P->shared_rows.size());
+                    std::merge(kr, kr + nk, P->shared_rows.begin(), P->shared_rows.end(), merged.begin());
+                    pack_key(*h, merged.data(), (int64_t)merged.size(), model, ko[(size_t)k]);
+                }
             };
             std::vector<std::thread> pool;
             for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
             work(0);
             for (auto &th : pool) th.join();
         }
-        for (int64_t k = 0; k < K; ++k)
-            if (ko[(size_t)k].err) {
-                int code = ko[(size_t)k].err;
-                std::string msg = ko[(size_t)k].msg;
-                long long key = (long long)P->keys[(size_t)k];
-                delete P;
-                return lc::fail(code, "lc_pack: key %lld: %s", key, msg.c_str());
+        for (int64_t k = 0; k < K; ++k) {
+            KeyOut &o = ko[(size_t)k];
+            if (!o.err) continue;
+            if (P->key_error.empty()) {
+                P->key_error.assign((size_t)K, 0);
+                P->key_msg.assign((size_t)K, std::string());
             }
+            P->key_error[(size_t)k] = 1;
+            P->key_msg[(size_t)k] = o.msg;
+            // no events: the search never looks at this key
+            std::vector<uint32_t>().swap(o.ev);
+            std::vector<int64_t>().swap(o.ev_row);
+            std::vector<int32_t>().swap(o.ev_op);
+            std::vector<KOp>().swap(o.ops);
+            o.width = 0;
+        }
 
         // ---- A4/A5: register states + transition descriptors ----
         // A state is a value some surviving write / cas could install.
@@ -398,7 +420,14 @@ extern "C" int lc_packed_view(const lc_packed *p, lc_batch *b) {
     b->key_width = p->key_width.data();
     b->key_states = p->key_states.data();
     b->init_state = 0;
+    b->key_error = p->key_error.empty() ? nullptr : p->key_error.data();
     return LC_OK;
+}
+
+extern "C" const char *lc_packed_key_error(const lc_packed *p, int64_t i) {
+    if (!p || i < 0 || i >= (int64_t)p->keys.size() || p->key_error.empty() || !p->key_error[(size_t)i])
+        return nullptr;
+    return p->key_msg[(size_t)i].c_str();
 }
 
 extern "C" int64_t lc_packed_key(const lc_packed *p, int64_t i) {

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 4
+LC_ABI_VERSION = 5
 LC_OPT_COUNT_PROBES = 0x1
 LC_DEV_RESULT, LC_DEV_ASYNC = 1, 2
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
@@ -33,6 +33,7 @@ LC_STATE_NONE = 0x7FFF
 LC_NARROW_MAX_SLOTS, LC_WIDE_MAX_SLOTS = 56, 112
 LC_WIDE_MAX_STATES = 32767
 LC_VALID, LC_INVALID, LC_UNKNOWN = 1, 0, -1
+LC_CAUSE_ERROR = 5
 CAUSES = {0: "none", 1: "nonlin", 2: "budget", 3: "window", 4: "states", 5: "error"}
 ERRORS = {-1: "invalid", -2: "nomem", -3: "device", -4: "parse", -5: "unsupported", -6: "io"}
 
@@ -49,7 +50,7 @@ class LcBatch(C.Structure):
     _fields_ = [("n_keys", C.c_int64), ("ev_off", P(C.c_uint64)), ("events", P(C.c_uint32)),
                 ("trans", P(C.c_uint32)), ("n_trans", C.c_int64), ("trans_off", P(C.c_uint32)),
                 ("key_width", P(C.c_uint8)), ("key_states", P(C.c_uint16)),
-                ("init_state", C.c_uint32)]
+                ("init_state", C.c_uint32), ("key_error", P(C.c_uint8))]
 
 
 class LcPackOpts(C.Structure):
@@ -103,6 +104,7 @@ SIGNATURES = {
     "lc_packed_key": (C.c_int64, [C.c_void_p, C.c_int64]),
     "lc_packed_event_row": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int64]),
     "lc_packed_subhistory": (C.c_int64, [C.c_void_p, C.c_int64, P(C.c_int64)]),
+    "lc_packed_key_error": (C.c_char_p, [C.c_void_p, C.c_int64]),
     "lc_packed_state_value": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint32, P(C.c_int64), P(C.c_int)]),
     "lc_synth_generate": (C.c_int, [P(LcSynthOpts), P(C.c_void_p)]),
     "lc_hist_view": (C.c_int, [C.c_void_p, P(LcHistory)]),

@@ -78,6 +78,11 @@ class Packed:
         base = int(self._trans_off[i]) if len(self._trans_off) else 0
         return int(self._trans[base + t])
 
+    def key_error(self, i: int) -> Optional[str]:
+        """Why key i could not be prepared (lc_packed_key_error), or None."""
+        msg = N.lib().lc_packed_key_error(self.handle, i)
+        return None if msg is None else msg.decode(errors="replace")
+
     def state_value(self, i: int, s: int):
         v = C.c_int64(); nil = C.c_int()
         N.check(N.lib().lc_packed_state_value(self.handle, i, s, C.byref(v), C.byref(nil)))
@@ -355,6 +360,10 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
     """Knossos-shaped result for key i."""
     v = int(res.valid[i])
     cause = N.CAUSES.get(int(res.cause[i]), "error")
+    if v == N.LC_UNKNOWN and int(res.cause[i]) == N.LC_CAUSE_ERROR:
+        # the key's sub-history could not be prepared: what check-safe makes
+        # of the exception knossos would throw (etcdemo.clj:115)
+        return {"valid?": "unknown", "error": packed.key_error(i) or "error"}
     fe = int(res.fail_event[i])
     upto = fe if fe >= 0 else packed.n_events(i)
     kv = _KeyView(packed, i, upto)

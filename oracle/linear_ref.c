@@ -13,6 +13,10 @@
  *   complete + without-failures, cas-register step (etcdemo.clj:117), the JIT
  *   config-set search of knossos.linear (:algorithm :linear, etcdemo.clj:118)
  *   with a deterministic config budget in place of knossos.search's abort.
+ *   A key whose sub-history complete rejects (a completion with no
+ *   outstanding invocation) or that holds an op the model cannot step is
+ *   :unknown with cause LC_CAUSE_ERROR, and the other keys are checked:
+ *   independent/checker's check-safe per key (etcdemo.clj:115).
  * Written independently of the device code: plain sequential search, one
  * growable open-addressed hash set per set, a pthread pool over keys standing
  * in for independent/checker's bounded-pmap.
@@ -327,7 +331,12 @@ static void *worker(void *arg) {
         if (k >= j->nkeys) break;
         int rc = check_key(j->h, j->rows + j->off[k], (int64_t)(j->off[k + 1] - j->off[k]), j->budget, j->model,
                            &j->out[k]);
-        if (rc) { pthread_mutex_lock(&j->mu); j->rc = rc; pthread_mutex_unlock(&j->mu); }
+        if (rc == LC_E_INVALID || rc == LC_E_UNSUPPORTED) {  /* check-safe: this key alone */
+            memset(&j->out[k], 0, sizeof j->out[k]);
+            j->out[k].valid = -1; j->out[k].cause = LC_CAUSE_ERROR; j->out[k].fail_event = -1;
+        } else if (rc) {
+            pthread_mutex_lock(&j->mu); j->rc = rc; pthread_mutex_unlock(&j->mu);
+        }
     }
     return NULL;
 }
@@ -347,12 +356,12 @@ int64_t oracle_check_history_model(const lc_history *h, int model, uint64_t budg
     int64_t *rk = (int64_t *)malloc((size_t)(n + 1) * sizeof(int64_t));
     int64_t *keys = (int64_t *)malloc((size_t)(n + 1) * sizeof(int64_t));
     if (!kt || !rk || !keys) { free(kt); free(rk); free(keys); return LC_E_NOMEM; }
-    int64_t nk = 0;
+    int64_t nk = 0, nshared = 0;
     for (int64_t r = 0; r < n; ++r) {
         int64_t k = h->key[r];
-        if (k == LC_NO_KEY) {
+        if (k == LC_NO_KEY) {  /* not a tuple: in every key's sub-history */
             rk[r] = -1;
-            if (h->type[r] != LC_INFO) { free(kt); free(rk); free(keys); return LC_E_UNSUPPORTED; }
+            nshared++;
             continue;
         }
         uint64_t s = (uint64_t)((uint64_t)k * 0x9E3779B97F4A7C15ull) & (cap - 1);
@@ -364,15 +373,20 @@ int64_t oracle_check_history_model(const lc_history *h, int model, uint64_t budg
     if (max_keys == 0) { free(rk); free(keys); return nk; }
     if (max_keys < nk) { free(rk); free(keys); return LC_E_INVALID; }
     uint64_t *off = (uint64_t *)calloc((size_t)nk + 1, sizeof(uint64_t));
-    int64_t *rows = (int64_t *)malloc((size_t)(n + 1) * sizeof(int64_t));
+    int64_t *rows = (int64_t *)malloc((size_t)(n - nshared + nk * nshared + 1) * sizeof(int64_t));
     if (!off || !rows) { free(rk); free(keys); free(off); free(rows); return LC_E_NOMEM; }
     for (int64_t r = 0; r < n; ++r) if (rk[r] >= 0) off[rk[r] + 1]++;
-    for (int64_t k = 0; k < nk; ++k) off[k + 1] += off[k];
+    for (int64_t k = 0; k < nk; ++k) off[k + 1] += off[k] + (uint64_t)nshared;
     {
         uint64_t *cur = (uint64_t *)malloc((size_t)(nk + 1) * sizeof(uint64_t));
         if (!cur) { free(rk); free(keys); free(off); free(rows); return LC_E_NOMEM; }
         memcpy(cur, off, (size_t)nk * sizeof(uint64_t));
-        for (int64_t r = 0; r < n; ++r) if (rk[r] >= 0) rows[cur[rk[r]]++] = r;
+        /* jepsen.independent/subhistory: the key's own rows and every
+         * non-tuple row, in history order */
+        for (int64_t r = 0; r < n; ++r) {
+            if (rk[r] >= 0) rows[cur[rk[r]]++] = r;
+            else for (int64_t k = 0; k < nk; ++k) rows[cur[k]++] = r;
+        }
         free(cur);
     }
     free(rk);

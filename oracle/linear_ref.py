@@ -40,6 +40,10 @@ What is restated, from the published knossos 0.3.7 / jepsen 0.2.x sources
       { (s, L) in S : p not in L } by linearizing pending, not-yet-linearized
       ops other than p.  The history is invalid at the first :ok whose S' is
       empty (that event is the reported :op).
+  jepsen.checker/check-safe around each key (independent/checker,
+      etcdemo.clj:115): a key whose sub-history complete rejects, or that
+      holds an op the model cannot step, is :unknown with cause "error"
+      (check_independent / analysis_safe); the other keys are still checked.
   knossos.search (abort -> :unknown) is replaced by a deterministic budget:
       a key whose closure I or config set S' exceeds `budget` configs is
       :unknown with cause "budget".  Two representation limits are applied in
@@ -353,7 +357,18 @@ def config_sort_key(c: Config):
     return (-1 if st is None else int(st), sorted(L))
 
 
+def analysis_safe(history: Sequence[dict], budget: int = DEFAULT_BUDGET, model: str = "cas-register") -> Analysis:
+    """check-safe around analysis: a HistoryError makes the key :unknown
+    (cause "error") instead of aborting the whole check."""
+    try:
+        return analysis(history, budget, model=model)
+    except HistoryError as e:
+        a = Analysis(valid="unknown", cause="error", peak_configs=0)
+        a.error = str(e)
+        return a
+
+
 def check_independent(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
                       model: str = "cas-register") -> Dict[Any, Analysis]:
     """independent/checker over linearizable(model): per-key analyses."""
-    return {k: analysis(subhistory(history, k), budget, model=model) for k in history_keys(history)}
+    return {k: analysis_safe(subhistory(history, k), budget, model=model) for k in history_keys(history)}

@@ -30,13 +30,31 @@ def test_abi_version():
     assert N.lib().lc_abi_version() == N.LC_ABI_VERSION
 
 
-def test_struct_sizes_match_header():
-    # offsets the JNA / ctypes bindings rely on (x86-64 LP64)
-    assert C.sizeof(N.LcHistory) == 8 * 8
-    assert C.sizeof(N.LcBatch) == 8 * 9
-    assert C.sizeof(N.LcResult) == 8 * 6
-    assert C.sizeof(N.LcOpts) == 4 + 4 + 8 + 4 * 3 + 4 * 6 + 4
-    assert C.sizeof(N.LcStats) == 8 * 9
+STRUCTS = {"lc_history": N.LcHistory, "lc_batch": N.LcBatch, "lc_result": N.LcResult, "lc_opts": N.LcOpts,
+           "lc_stats": N.LcStats, "lc_pack_opts": N.LcPackOpts, "lc_synth_opts": N.LcSynthOpts}
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Every field offset and struct size the ctypes (and JNA) bindings use
+    equals the C compiler's for include/lincheck.h (x86-64 LP64)."""
+    import subprocess
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{os.path.abspath(HEADER)}"',
+             "int main(void) {"]
+    for cname, py in STRUCTS.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines += ["return 0; }"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l}
+    for cname, py in STRUCTS.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
 
 
 @pytest.mark.skipif(N.lib().lc_device_count() > 0, reason="a GPU is visible")

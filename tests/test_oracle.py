@@ -17,7 +17,7 @@ from lincheck import history as H
 from lincheck.independent import Tuple
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kat.json")
-CAUSE = {"none": 0, "nonlin": 1, "budget": 2, "window": 3, "states": 4}
+CAUSE = {"none": 0, "nonlin": 1, "budget": 2, "window": 3, "states": 4, "error": 5}
 
 
 def load_kats():
@@ -39,8 +39,11 @@ def test_known_answers(case):
     for k in LR.history_keys(ops):
         sub = LR.subhistory(ops, k)
         exp = case["expect"][str(k)]
-        a = LR.analysis(sub, model=model)
+        a = LR.analysis_safe(sub, model=model)
         assert a.valid == exp["valid?"]
+        if exp["valid?"] == "unknown":  # check-safe around one key
+            assert a.cause == "error"
+            continue
         assert brute.brute_check(sub, model=model)[0] == exp["valid?"]
         if not exp["valid?"]:
             assert sub[a.fail_pos]["index"] == exp["op"]
@@ -50,7 +53,9 @@ def test_known_answers(case):
     keys, r = cref.check_history(h.as_c(), model=model)
     for k, rr in zip(keys, r):
         exp = case["expect"][str(k)]
-        assert bool(rr["valid"] == 1) == (exp["valid?"] is True)
+        assert rr["valid"] == {True: 1, False: 0, "unknown": -1}[exp["valid?"]]
+        if exp["valid?"] == "unknown":
+            assert rr["cause"] == 5 and rr["fail_event"] == -1
 
 
 @settings(max_examples=300, deadline=None)

@@ -93,22 +93,48 @@ def test_many_values_use_per_key_tables():
     assert (states > 100).all()
 
 
-def test_completion_without_invocation_is_an_error():
-    ops = [{"type": "ok", "f": "write", "value": Tuple(0, 1), "process": 0}]
-    with pytest.raises(N.LincheckError, match="without a prior invocation"):
-        Packed(H.History.from_ops(ops))
+def test_completion_without_invocation_is_a_key_error():
+    """complete's assertion fails for key 1 only: that key keeps its place with
+    no events and an error (check-safe per key, etcdemo.clj:115); key 0 packs
+    as usual."""
+    ops = [{"type": "invoke", "f": "write", "value": Tuple(0, 1), "process": 0},
+           {"type": "ok", "f": "write", "value": Tuple(1, 1), "process": 1},
+           {"type": "ok", "f": "write", "value": Tuple(0, 1), "process": 0}]
+    pk = Packed(H.History.from_ops(ops))
+    assert pk.keys == [0, 1]
+    assert pk.key_error(0) is None
+    assert "without a prior invocation" in pk.key_error(1)
+    assert pk.n_events(0) == 2 and pk.n_events(1) == 0
+    err = np.ctypeslib.as_array(pk.view.key_error, shape=(2,))
+    assert list(err) == [0, 1]
 
 
-def test_non_tuple_client_op_is_unsupported():
-    ops = [{"type": "invoke", "f": "write", "value": 1, "process": 0}]
-    with pytest.raises(N.LincheckError, match="unsupported"):
-        Packed(H.History.from_ops(ops))
+def test_no_key_errors_no_array():
+    pk = Packed(H.synth(n_keys=3, ops_per_key=20, concurrency=3, seed=1))
+    assert not pk.view.key_error
 
 
-def test_unknown_f_is_unsupported():
-    ops = [{"type": "invoke", "f": "append", "value": Tuple(0, 1), "process": 0}]
-    with pytest.raises(N.LincheckError, match="unsupported"):
-        Packed(H.History.from_ops(ops))
+def test_non_tuple_client_op_in_every_key():
+    """jepsen.independent/subhistory keeps non-tuple ops: an un-keyed write is
+    an op of every key's sub-history."""
+    ops = [{"type": "invoke", "f": "write", "value": Tuple(0, 1), "process": 0},
+           {"type": "ok", "f": "write", "value": Tuple(0, 1), "process": 0},
+           {"type": "invoke", "f": "write", "value": 3, "process": 9},
+           {"type": "ok", "f": "write", "value": 3, "process": 9},
+           {"type": "invoke", "f": "read", "value": Tuple(1, None), "process": 1},
+           {"type": "ok", "f": "read", "value": Tuple(1, 3), "process": 1}]
+    pk = Packed(H.History.from_ops(ops))
+    assert pk.keys == [0, 1]
+    assert [pk.n_events(i) for i in range(2)] == [4, 4]
+    assert [pk.event_row(1, j) for j in range(4)] == [2, 3, 4, 5]
+    check_packed_against_oracle(ops)
+
+
+def test_unknown_f_is_a_key_error():
+    ops = [{"type": "invoke", "f": "append", "value": Tuple(0, 1), "process": 0},
+           {"type": "invoke", "f": "write", "value": Tuple(1, 1), "process": 1}]
+    pk = Packed(H.History.from_ops(ops))
+    assert "cannot step" in pk.key_error(0) and pk.key_error(1) is None
 
 
 def test_non_integer_values_rejected_on_host():
@@ -145,7 +171,5 @@ def test_models_pack():
     trans = np.ctypeslib.as_array(pk.view.trans, shape=(int(pk.view.n_trans),))
     assert sorted(int(t) for t in trans) == sorted([N.LC_T_CAS | (0 << 2) | (1 << 17), N.LC_T_CAS | (1 << 2) | (0 << 17)])
     cas = [{"type": "invoke", "f": "cas", "value": Tuple(0, [1, 2]), "process": 0}]
-    with pytest.raises(N.LincheckError):
-        Packed(H.History.from_ops(cas), model.register())
-    with pytest.raises(N.LincheckError):
-        Packed(H.History.from_ops(ops), model.cas_register())
+    assert "cannot step" in Packed(H.History.from_ops(cas), model.register()).key_error(0)
+    assert "cannot step" in Packed(H.History.from_ops(ops), model.cas_register()).key_error(0)
