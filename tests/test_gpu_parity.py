@@ -64,7 +64,10 @@ def test_hbm_tier_narrow_lds_and_hbm_passes(device, conc, info, budget):
     dev = Device(0, budget=budget, count_probes=True)
     h = H.synth(n_keys=32, ops_per_key=600, concurrency=conc, info_rate=info, anomaly_rate=0.1, seed=31)
     _, res, orc = device_vs_oracle(h, dev, budget=budget)
-    assert res.stats["deep_keys"] > 0
+    if budget >= 8192:
+        assert res.stats["deep_keys"] > 0  # keys the HBM tier searched
+    else:  # the budget ends keys before they outgrow the LDS tiers
+        assert (orc["cause"] == 2).any()
     if budget == 1 << 20:
         assert (orc["cause"] != 2).all() and orc["peak"].max() > 2048
 
