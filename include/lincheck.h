@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 5
+#define LC_ABI_VERSION 6
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -211,8 +211,11 @@ int lc_packed_state_value(const lc_packed *p, int64_t i, uint32_t s, int64_t *va
  * be linearized are properties of the history, not of the algorithm.  Only
  * the host-side result shaping (:analyzer) differs. */
 
+#define LC_MAX_DEVICES   8    /* devices one context drives (one node)        */
+#define LC_COMM_ID_BYTES 128  /* an RCCL unique id (ncclUniqueId)             */
+
 typedef struct lc_opts {
-    int32_t  device;        /* HIP device ordinal                               */
+    int32_t  device;        /* HIP device ordinal (n_devices <= 1)              */
     int32_t  algorithm;     /* LC_ALGO_*                                        */
     uint64_t max_configs;   /* search budget B (0 = default 1<<20): a key whose
                                config set or JIT closure exceeds B configs is
@@ -224,6 +227,22 @@ typedef struct lc_opts {
     int32_t  deep_slots;    /* concurrently searched HBM-tier keys (0 = auto)    */
     int32_t  flags;         /* LC_OPT_*                                          */
     int32_t  debug_mode;    /* 0 (ablation builds only)                          */
+    /* One process, several GPUs (independent/checker's pmap over the node's
+     * devices): n_devices in 2..LC_MAX_DEVICES checks every
+     * batch as contiguous key shards of about equal event counts, one per
+     * devices[g] (a device may repeat: shards then share it), all at once.
+     * 0 or 1: `device` alone. */
+    int32_t  n_devices;
+    int32_t  devices[LC_MAX_DEVICES];
+    /* One process per GPU (the launcher's ranks): comm_size > 1 makes this
+     * context rank comm_rank of an RCCL communicator over comm_size ranks,
+     * created here (ncclCommInitRank; it waits for every rank) from comm_id,
+     * which rank 0 takes from lc_comm_id and hands to every rank (comm_size
+     * 1 with a nonzero comm_id: a one-rank communicator).  lc_check_node
+     * all-gathers the verdict records over it. */
+    int32_t  comm_rank;
+    int32_t  comm_size;
+    uint8_t  comm_id[LC_COMM_ID_BYTES];
     int32_t  reserved[4];   /* must be 0                                         */
 } lc_opts;
 
@@ -282,7 +301,17 @@ int         lc_device_count(void);
 int  lc_create(const lc_opts *opts, lc_ctx **out);
 void lc_destroy(lc_ctx *ctx);
 
-/* One call per batch: H2D, search, D2H into caller-owned result arrays. */
+/* One call per batch: H2D, search, D2H into caller-owned result arrays.
+ * Validation: every array index is checked before a kernel follows it.  The
+ * per-event checks (an :ok names a pending slot, transition ids in range,
+ * key_width / key_states honest) run on the host, except for a batch whose
+ * keys are all declared to fit the register tier (key_width <= 10, <= 32
+ * states): its register-tier launch carries validation waves that walk every
+ * key's events beside the search (the search itself stays in bounds on any
+ * input), and a malformed key ends the call with LC_E_INVALID naming it.
+ * The result arrays of a refused call are unspecified.  Event words in
+ * page-locked memory (lc_pack's output on a GPU host) are uploaded directly;
+ * others through a pinned staging copy. */
 int  lc_check_batch(lc_ctx *ctx, const lc_batch *b, lc_result *r, lc_stats *s);
 
 /* Device-resident batches: upload once, check many times (the bench's step). */
@@ -309,6 +338,31 @@ int  lc_wait(lc_ctx *ctx, lc_stats *s);
  * latest, at most 3) has finished, leaving later ones running; with no such
  * step on record, wait for everything on the context's stream. */
 int  lc_wait_step(lc_ctx *ctx, int back);
+
+/* ---- one process per GPU: node-wide verdict records ------- */
+/* A key's verdict record: (valid + 1) | cause << 8 | (fail_event + 1) << 16
+ * (8 bytes; 0 = padding).  Each rank checks its shard of the keys and the
+ * records of every rank are all-gathered over RCCL (xGMI) -- the one
+ * exchange step of the path; the shards share no state. */
+#define LC_REC_VALID(r)      ((int)((r) & 0xFFu) - 1)
+#define LC_REC_CAUSE(r)      ((int)(((r) >> 8) & 0xFFu))
+#define LC_REC_FAIL_EVENT(r) ((int32_t)((int64_t)((r) >> 16) - 1))
+
+/* A fresh RCCL unique id (LC_COMM_ID_BYTES) for lc_opts.comm_id; rank 0
+ * calls it and the launcher distributes the bytes. */
+int  lc_comm_id(uint8_t *out);
+/* This rank's shard, from host SoA: upload, search, pack the shard's
+ * records into a block of `block` (>= shard keys; padded with 0), all-gather
+ * the blocks of every rank (comm_size of them, rank order), and copy the
+ * node's block * comm_size records to `node` (host).  One rank: node = the
+ * shard's block. */
+int  lc_check_node(lc_ctx *ctx, const lc_batch *shard, int64_t block, uint64_t *node, lc_stats *s);
+/* The same from a resident shard (lc_upload), records left in HBM until
+ * lc_node_records; flags LC_DEV_ASYNC: a step that is the register tier
+ * alone is only enqueued (lc_wait ends the run). */
+int  lc_check_node_device(lc_ctx *ctx, const lc_dev_batch *shard, int64_t block, int flags, lc_stats *s);
+/* The first n records of the last gather (waits for it). */
+int  lc_node_records(lc_ctx *ctx, uint64_t *node, int64_t n);
 
 /* ---- synthetic histories ------------------------------ */
 typedef struct lc_synth_opts {

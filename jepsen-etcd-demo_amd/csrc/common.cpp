@@ -1,5 +1,10 @@
 // Error reporting shared by every entry point of liblincheck.
+#include <hip/hip_runtime_api.h>
+
 #include <cstdarg>
+#include <cstdlib>
+#include <mutex>
+#include <unordered_set>
 
 #include "common.hpp"
 
@@ -17,6 +22,45 @@ int fail(int code, const char *fmt, ...) {
     va_end(ap);
     g_last_error = buf;
     return code;
+}
+
+// Page-locked host memory for arrays the device reads whole (lc_pack's event
+// words): the DMA engine reads them directly instead of through a bounce
+// buffer.  Without a visible GPU (or for small arrays) plain malloc.
+static std::mutex g_pin_mu;
+static std::unordered_set<void *> g_pinned;
+
+void *pinned_alloc(size_t bytes) {
+    static const bool gpu = [] {
+        int n = 0;
+        const bool ok = hipGetDeviceCount(&n) == hipSuccess && n > 0;
+        (void)hipGetLastError();
+        return ok;
+    }();
+    if (gpu && bytes >= (64u << 10) && bytes <= (2ull << 30)) {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess && p) {
+            std::lock_guard<std::mutex> g(g_pin_mu);
+            g_pinned.insert(p);
+            return p;
+        }
+        (void)hipGetLastError();
+    }
+    return std::malloc(bytes ? bytes : 1);
+}
+
+void pinned_free(void *p) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        auto it = g_pinned.find(p);
+        if (it != g_pinned.end()) {
+            g_pinned.erase(it);
+            (void)hipHostFree(p);
+            return;
+        }
+    }
+    std::free(p);
 }
 
 }  // namespace lc

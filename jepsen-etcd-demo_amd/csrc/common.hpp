@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -14,6 +15,30 @@ namespace lc {
 // Thread-local last error (lc_last_error).  Every failing entry point sets it.
 void set_error(const std::string &msg);
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+
+// Page-locked when a GPU is visible (a direct DMA source), else malloc.
+void *pinned_alloc(size_t bytes);
+void pinned_free(void *p);
+
+template <class T>
+struct PinnedAlloc {
+    using value_type = T;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U> &) {}
+    T *allocate(size_t n) {
+        void *p = pinned_alloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return (T *)p;
+    }
+    void deallocate(T *p, size_t) { pinned_free(p); }
+    template <class U>
+    bool operator==(const PinnedAlloc<U> &) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U> &) const { return false; }
+};
+template <class T>
+using pinned_vector = std::vector<T, PinnedAlloc<T>>;
 
 }  // namespace lc
 

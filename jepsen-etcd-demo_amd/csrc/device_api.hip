@@ -1,21 +1,30 @@
 // device_api.hip -- host orchestration of the device search (C ABI: lc_create,
-// lc_upload, lc_check_device, lc_check_batch; include/lincheck.h).
+// lc_upload, lc_check_device, lc_check_batch, lc_check_node; include/lincheck.h).
 //
 // This is the native side of the drop-in at etcdemo.clj:115-119: one call
-// checks every key of a batch (independent/checker's per-key pmap becomes a
-// work list walked by persistent kernels).  Inputs are validated on the host
-// before any launch, so a malformed batch can never drive a kernel out of
-// bounds.
+// checks every key of a batch.  independent/checker's per-key pmap becomes
+//   * across GPUs: contiguous key shards balanced by event count, one per
+//     device of the context (one host driver thread per device), or one
+//     shard per process with the verdict records all-gathered over RCCL
+//     (lc_check_node);
+//   * within a GPU: a work list walked by persistent kernels.
+// Nothing a kernel follows is trusted unchecked: the host validates every
+// index of a batch, except the per-event ones of a batch whose keys all fit
+// the register tier, which T0 checks itself as it walks the events (a
+// malformed event stops its key and the call returns LC_E_INVALID).
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
-#include <functional>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <numeric>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -29,7 +38,16 @@
             return lc::fail(LC_E_DEVICE, "%s failed: %s", #expr, hipGetErrorString(_e));  \
     } while (0)
 
+#define RCCLCHK(expr)                                                                      \
+    do {                                                                                   \
+        ncclResult_t _r = (expr);                                                          \
+        if (_r != ncclSuccess)                                                             \
+            return lc::fail(LC_E_DEVICE, "%s failed: %s", #expr, R->error(_r));            \
+    } while (0)
+
 namespace {
+
+constexpr int MAX_DEV = LC_MAX_DEVICES;
 
 template <class T>
 hipError_t dalloc(T **p, size_t n) {
@@ -44,12 +62,60 @@ void dfree(T *&p) {
     p = nullptr;
 }
 
+// RCCL, loaded on first use from the directory of the HIP runtime this
+// library is bound to (a process may hold two: torch bundles its own), so
+// the communicator and our streams belong to one runtime.
+struct Rccl {
+    void *h = nullptr;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    const char *error(ncclResult_t r) const { return error_string ? error_string(r) : "rccl error"; }
+};
+
+const Rccl *rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        Dl_info info;
+        if (dladdr((void *)&hipStreamCreateWithFlags, &info) && info.dli_fname) {
+            std::string dir = info.dli_fname;
+            dir = dir.substr(0, dir.find_last_of('/') + 1);
+            for (const char *name : {"librccl.so.1", "librccl.so"})
+                if (!h) h = dlopen((dir + name).c_str(), RTLD_NOW | RTLD_LOCAL);
+        }
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+        r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+        r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        if (r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather) r.h = h;
+    });
+    return r.h ? &r : nullptr;
+}
+
+// Verdict record of one key (include/lincheck.h LC_REC_*), 0 for padding.
+__global__ void k_pack_records(const int8_t *valid, const uint8_t *cause, const int32_t *fail_event, int64_t n,
+                               int64_t block, uint64_t *out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < block; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t r = 0;
+        if (i < n)
+            r = (uint64_t)(uint8_t)(valid[i] + 1) | (uint64_t)cause[i] << 8 | (uint64_t)(uint32_t)(fail_event[i] + 1) << 16;
+        out[i] = r;
+    }
+}
+
 }  // namespace
 
-// Host worker threads kept for the life of a context, so the per-event
-// validation pass of every lc_check_batch does not pay thread creation.
-// run(n, fn) calls fn(0..n-1) on the workers and the caller, and returns when
-// all have finished.
+// Host worker threads kept for the life of a context (per-event validation
+// and staging copies; one driver per extra device).  run(n, fn) calls
+// fn(0..n-1) on the workers and the caller, and returns when all have
+// finished.  Not reentrant: one run at a time.
 class HostPool {
   public:
     explicit HostPool(unsigned n) {
@@ -65,6 +131,7 @@ class HostPool {
     }
     unsigned size() const { return (unsigned)th_.size() + 1; }
     void run(unsigned n, const std::function<void(unsigned)> &fn) {
+        n = std::min(n, size());
         {
             std::lock_guard<std::mutex> g(m_);
             fn_ = &fn;
@@ -106,7 +173,8 @@ class HostPool {
     bool stop_ = false;
 };
 
-struct lc_dev_batch {
+// One device's part of a batch in HBM.
+struct DevBatch {
     int device = 0;
     int64_t n_keys = 0;
     uint64_t n_events = 0;
@@ -122,24 +190,38 @@ struct lc_dev_batch {
     uint16_t *key_states = nullptr;
     uint8_t *key_error = nullptr;
     int32_t *order = nullptr;  // LPT: keys by event count, descending
-    bool t0_only = false;      // every key fits the register lattice: T0 never spills
-    size_t input_bytes = 0;    // bytes the search reads per pass (events + offsets + tables)
+    bool t0_only = false;      // every key declared to fit the register lattice
+    bool validated = false;    // the host checked every event (else T0 does: T0_STRICT)
     // Device storage behind the arrays above, grown on demand: a batch that is
-    // re-uploaded (the ctx's staging batch for lc_check_batch) keeps it, so a
-    // host-to-host check allocates nothing once its sizes have been seen.
+    // re-uploaded (a context's staging batch for lc_check_batch) keeps it, so
+    // a host-to-host check allocates nothing once its sizes have been seen.
     struct Mem {
         void *p = nullptr;
         size_t cap = 0;
     } mem[8];
-    ~lc_dev_batch() {
+    ~DevBatch() {
         for (Mem &m : mem)
             if (m.p) (void)hipFree(m.p);
     }
 };
 
+struct lc_dev_batch {
+    int n_parts = 0;
+    int64_t n_keys = 0;
+    int64_t key0[MAX_DEV + 1] = {};  // part g holds keys [key0[g], key0[g + 1])
+    DevBatch *part[MAX_DEV] = {};
+    ~lc_dev_batch() {
+        for (DevBatch *p : part)
+            if (p) {
+                (void)hipSetDevice(p->device);
+                delete p;
+            }
+    }
+};
+
 // Point p at m's storage, growing it to hold n elements of T.
 template <class T>
-static hipError_t grow(lc_dev_batch::Mem &m, T *&p, size_t n) {
+static hipError_t grow(DevBatch::Mem &m, T *&p, size_t n) {
     const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
     if (bytes > m.cap) {
         if (m.p) (void)hipFree(m.p);
@@ -156,8 +238,9 @@ static hipError_t grow(lc_dev_batch::Mem &m, T *&p, size_t n) {
 
 constexpr size_t CTL_BYTES = 4 * sizeof(unsigned long long) + 16 * sizeof(int32_t);
 
-struct lc_ctx {
-    lc_opts o{};
+// One device of a context: its stream, scratch and result arrays.
+struct Dev {
+    const lc_opts *o = nullptr;  // the context's options
     int device = 0;
     int cu_count = 256;
     hipStream_t stream = nullptr;
@@ -166,13 +249,13 @@ struct lc_ctx {
     uint32_t n_async = 0;
     hipEvent_t ring[4] = {};  // end of each of the last 4 LC_DEV_ASYNC steps (lc_wait_step)
     uint64_t async_seq = 0;
-    std::mutex mu;
     // scratch, grown on demand
     int64_t cap_keys = 0;
     int32_t *lists = nullptr;      // 4 x cap_keys: spill0, spill1, spill2, wide
     // one 96-byte control block, zeroed and read back in one operation each:
     // acc (4 x u64: probes, events, keys_done) then counters (16 x i32:
-    // n_spill0, n_spill1, n_spill2, n_wide, -, tickets[8..15])
+    // n_spill0, n_spill1, n_spill2, n_wide, err bits, 1 + bad key, -, -,
+    // tickets[8..15])
     unsigned long long *ctl = nullptr;
     unsigned long long *acc = nullptr;
     int32_t *counters = nullptr;
@@ -183,22 +266,17 @@ struct lc_ctx {
     uint32_t *peak = nullptr;
     uint64_t *final_cfg = nullptr;
     uint32_t *n_final = nullptr;
-    uint32_t *lat_ws = nullptr;    // T0 workspace (lattices of 9-10 pending ops)
     lcd::Args *dargs = nullptr;    // device copy of T0's Args (read once per key)
     lcd::Args *hargs = nullptr;    // its pinned host staging copy (copied only when it changes)
     bool hargs_valid = false;
-    // lc_check_batch's staging batch (device arrays reused across calls) and
-    // the lock that keeps one lc_check_batch at a time on it
-    lc_dev_batch *staged = nullptr;
-    uint32_t *hstage = nullptr;  // pinned copy of its event words
-    HostPool *pool = nullptr;    // validation workers, created on first use
-    size_t hstage_cap = 0;
-    std::mutex batch_mu;
-    // T0-only steps (lc_check_device) skip re-zeroing the control block: the
-    // ticket continues from where the previous such step left it.
+    DevBatch *staged = nullptr;    // lc_check_batch's staging batch (device arrays reused)
+    // T0-only steps skip re-zeroing the control block: the ticket continues
+    // from where the previous such step left it.
     bool ticket_live = false;
     uint32_t ticket_next = 0;
-    int lat_ws_blocks = 0;
+    // node records (lc_check_node): this rank's block and the gathered node
+    uint64_t *send = nullptr, *node = nullptr;
+    int64_t node_cap = 0, node_n = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
     struct Ws {
         char *base = nullptr;
@@ -206,29 +284,49 @@ struct lc_ctx {
         int slots = 0;
         lcd::HbmWs w{};
     } ws[2];
-    ~lc_ctx() {
+    ~Dev() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
         dfree(lists); dfree(ctl); dfree(valid); dfree(fail_event);
         if (hctl) (void)hipHostFree(hctl);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
-        dfree(ws[0].base); dfree(ws[1].base); dfree(lat_ws); dfree(dargs);
+        dfree(ws[0].base); dfree(ws[1].base); dfree(dargs); dfree(send); dfree(node);
         if (hargs) (void)hipHostFree(hargs);
         delete staged;
-        delete pool;
-        if (hstage) (void)hipHostFree(hstage);
-        if (e0) (void)hipEventDestroy(e0);
-        if (e1) (void)hipEventDestroy(e1);
-        if (et0) (void)hipEventDestroy(et0);
-        if (et3a) (void)hipEventDestroy(et3a);
-        if (et3b) (void)hipEventDestroy(et3b);
-        if (ea0) (void)hipEventDestroy(ea0);
-        if (ea1) (void)hipEventDestroy(ea1);
+        for (hipEvent_t e : {e0, e1, et0, et3a, et3b, ea0, ea1})
+            if (e) (void)hipEventDestroy(e);
         for (hipEvent_t &e : ring)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
 
-static int ensure_capacity(lc_ctx *c, int64_t n_keys) {
+struct lc_ctx {
+    lc_opts o{};
+    int n_dev = 0;
+    Dev *dev[MAX_DEV] = {};
+    std::mutex mu;                 // one call at a time (include/lincheck.h)
+    HostPool *pool = nullptr;      // validation / staging workers, created on first use
+    HostPool *drivers = nullptr;   // one thread per device beyond the first
+    uint32_t *hstage = nullptr;    // pinned copy of a batch's event words
+    size_t hstage_cap = 0;
+    // one process per GPU: RCCL communicator over the node's ranks
+    ncclComm_t comm = nullptr;
+    int rank = 0, size = 1;
+    ~lc_ctx() {
+        if (comm) {
+            (void)hipSetDevice(dev[0]->device);
+            (void)hipStreamSynchronize(dev[0]->stream);
+            if (const Rccl *R = rccl()) (void)R->comm_destroy(comm);
+        }
+        for (Dev *d : dev) delete d;
+        delete pool;
+        delete drivers;
+        if (hstage) (void)hipHostFree(hstage);
+    }
+};
+
+static int ensure_capacity(Dev *c, int64_t n_keys) {
     if (n_keys <= c->cap_keys) return LC_OK;
     int64_t cap = std::max<int64_t>(n_keys, 1024);
     dfree(c->lists); dfree(c->valid); dfree(c->fail_event); dfree(c->cause);
@@ -238,17 +336,18 @@ static int ensure_capacity(lc_ctx *c, int64_t n_keys) {
     HIPCHK(dalloc(&c->fail_event, (size_t)cap));
     HIPCHK(dalloc(&c->cause, (size_t)cap));
     HIPCHK(dalloc(&c->peak, (size_t)cap));
-    HIPCHK(dalloc(&c->final_cfg, (size_t)cap * (size_t)c->o.max_final * 2));
+    HIPCHK(dalloc(&c->final_cfg, (size_t)cap * (size_t)c->o->max_final * 2));
     HIPCHK(dalloc(&c->n_final, (size_t)cap));
     c->cap_keys = cap;
+    c->hargs_valid = false;
     return LC_OK;
 }
 
 // Lay out (and if needed allocate) a T3 workspace for `want` blocks.
-static int ensure_ws(lc_ctx *c, int wide, int want, int *slots_out) {
-    lc_ctx::Ws &W = c->ws[wide];
+static int ensure_ws(Dev *c, int wide, int want, int *slots_out) {
+    Dev::Ws &W = c->ws[wide];
     const size_t cfg = wide ? lcd::cfg_bytes_wide() : lcd::cfg_bytes_narrow();
-    const uint64_t cap = c->o.max_configs + (uint64_t)lcd::t3_block() + 64;
+    const uint64_t cap = c->o->max_configs + (uint64_t)lcd::t3_block() + 64;
     uint64_t H = 1;
     while (H < 2 * cap) H <<= 1;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -267,13 +366,13 @@ static int ensure_ws(lc_ctx *c, int wide, int want, int *slots_out) {
     w.hmask = (uint32_t)(H - 1);
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    const int max_slots = c->o.deep_slots > 0 ? c->o.deep_slots : 2 * c->cu_count;
+    const int max_slots = c->o->deep_slots > 0 ? c->o->deep_slots : 2 * c->cu_count;
     int slots = std::min(want, max_slots);
     const size_t limit = (W.bytes ? W.bytes : 0) + free_b / 2;
     while (slots > 1 && (size_t)slots * w.slot_bytes > limit) slots /= 2;
     if ((size_t)slots * w.slot_bytes > limit)
         return lc::fail(LC_E_NOMEM, "T3 workspace: one slot needs %zu bytes (budget %llu)", w.slot_bytes,
-                        (unsigned long long)c->o.max_configs);
+                        (unsigned long long)c->o->max_configs);
     if (!W.base || W.w.slot_bytes != w.slot_bytes || W.slots < slots) {
         dfree(W.base);
         W.bytes = 0; W.slots = 0;
@@ -294,6 +393,38 @@ extern "C" int lc_device_count(void) {
     return n;
 }
 
+static int dev_init(Dev *c, int device) {
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return lc::fail(LC_E_DEVICE, "lc_create: device %d is %s, this build targets gfx950", device, prop.gcnArchName);
+    c->device = device;
+    c->cu_count = prop.multiProcessorCount;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (hipEvent_t *e : {&c->e0, &c->e1, &c->et0, &c->et3a, &c->et3b, &c->ea0, &c->ea1}) HIPCHK(hipEventCreate(e));
+    for (hipEvent_t &e : c->ring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(dalloc(&c->ctl, 16));
+    c->acc = c->ctl;
+    c->counters = (int32_t *)(c->ctl + 4);
+    HIPCHK(hipMemset(c->ctl, 0, CTL_BYTES));
+    HIPCHK(hipHostMalloc((void **)&c->hctl, 16 * sizeof(unsigned long long), hipHostMallocDefault));
+    std::memset(c->hctl, 0, 16 * sizeof(unsigned long long));
+    HIPCHK(dalloc(&c->dargs, 1));
+    HIPCHK(hipHostMalloc((void **)&c->hargs, sizeof(lcd::Args), hipHostMallocDefault));
+    return LC_OK;
+}
+
+extern "C" int lc_comm_id(uint8_t *out) {
+    if (!out) return lc::fail(LC_E_INVALID, "lc_comm_id: null out");
+    const Rccl *R = rccl();
+    if (!R) return lc::fail(LC_E_DEVICE, "lc_comm_id: librccl.so.1 could not be loaded");
+    ncclUniqueId id;
+    RCCLCHK(R->get_unique_id(&id));
+    std::memcpy(out, id.internal, LC_COMM_ID_BYTES);
+    return LC_OK;
+}
+
 extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
     if (!out) return lc::fail(LC_E_INVALID, "lc_create: null out");
     lc_opts o{};
@@ -307,63 +438,73 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
     if (o.flags & ~LC_OPT_COUNT_PROBES) return lc::fail(LC_E_INVALID, "lc_create: unknown flags 0x%x", o.flags);
     for (int32_t r : o.reserved)
         if (r) return lc::fail(LC_E_INVALID, "lc_create: reserved fields must be 0");
+    if (o.n_devices < 0 || o.n_devices > MAX_DEV)
+        return lc::fail(LC_E_INVALID, "lc_create: n_devices must be 0..%d", MAX_DEV);
+    if (o.comm_size < 0 || o.comm_size > 4096 || (o.comm_size > 1 && (o.comm_rank < 0 || o.comm_rank >= o.comm_size)))
+        return lc::fail(LC_E_INVALID, "lc_create: comm_rank %d of comm_size %d", o.comm_rank, o.comm_size);
+    if (o.comm_size > 1 && o.n_devices > 1)
+        return lc::fail(LC_E_INVALID, "lc_create: a rank of a multi-process node drives one device");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return lc::fail(LC_E_DEVICE, "lc_create: no HIP device visible");
-    if (o.device < 0 || o.device >= ndev) return lc::fail(LC_E_DEVICE, "lc_create: device %d of %d", o.device, ndev);
-    hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, o.device));
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return lc::fail(LC_E_DEVICE, "lc_create: device %d is %s, this build targets gfx950", o.device, prop.gcnArchName);
+    const int n = o.n_devices > 1 ? o.n_devices : 1;
+    int list[MAX_DEV];
+    for (int g = 0; g < n; ++g) {
+        list[g] = o.n_devices > 1 ? o.devices[g] : o.device;
+        if (list[g] < 0 || list[g] >= ndev) return lc::fail(LC_E_DEVICE, "lc_create: device %d of %d", list[g], ndev);
+    }
     lc_ctx *c = new (std::nothrow) lc_ctx();
     if (!c) return lc::fail(LC_E_NOMEM, "lc_create: out of memory");
     c->o = o;
-    c->device = o.device;
-    c->cu_count = prop.multiProcessorCount;
-    int rc = LC_OK;
-    auto init = [&]() -> int {
-        HIPCHK(hipSetDevice(o.device));
-        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        HIPCHK(hipEventCreate(&c->e0));
-        HIPCHK(hipEventCreate(&c->e1));
-        HIPCHK(hipEventCreate(&c->et0));
-        HIPCHK(hipEventCreate(&c->et3a));
-        HIPCHK(hipEventCreate(&c->et3b));
-        HIPCHK(hipEventCreate(&c->ea0));
-        HIPCHK(hipEventCreate(&c->ea1));
-        for (hipEvent_t &e : c->ring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIPCHK(dalloc(&c->ctl, 16));
-        c->acc = c->ctl;
-        c->counters = (int32_t *)(c->ctl + 4);
-        HIPCHK(hipHostMalloc((void **)&c->hctl, 16 * sizeof(unsigned long long), hipHostMallocDefault));
-        HIPCHK(dalloc(&c->dargs, 1));
-        HIPCHK(hipHostMalloc((void **)&c->hargs, sizeof(lcd::Args), hipHostMallocDefault));
-        return LC_OK;
-    };
-    rc = init();
-    if (rc) { delete c; return rc; }
+    for (int g = 0; g < n; ++g) {
+        c->dev[g] = new (std::nothrow) Dev();
+        if (!c->dev[g]) { delete c; return lc::fail(LC_E_NOMEM, "lc_create: out of memory"); }
+        c->dev[g]->o = &c->o;
+        c->n_dev = g + 1;
+        int rc = dev_init(c->dev[g], list[g]);
+        if (rc) { delete c; return rc; }
+    }
+    if (n > 1) c->drivers = new HostPool((unsigned)n - 1);
+    // comm_size 1 with an id: a one-rank communicator (the exchange runs
+    // through RCCL all the same)
+    bool want_comm = o.comm_size > 1;
+    for (uint8_t byte : o.comm_id) want_comm |= o.comm_size == 1 && byte != 0;
+    if (want_comm) {
+        const Rccl *R = rccl();
+        if (!R) { delete c; return lc::fail(LC_E_DEVICE, "lc_create: librccl.so.1 could not be loaded"); }
+        ncclUniqueId id;
+        std::memcpy(id.internal, o.comm_id, LC_COMM_ID_BYTES);
+        (void)hipSetDevice(list[0]);
+        ncclResult_t r = R->comm_init_rank(&c->comm, o.comm_size, id, o.comm_rank);
+        if (r != ncclSuccess) {
+            c->comm = nullptr;
+            delete c;
+            return lc::fail(LC_E_DEVICE, "lc_create: ncclCommInitRank (rank %d of %d) failed: %s", o.comm_rank,
+                            o.comm_size, R->error(r));
+        }
+        c->rank = o.comm_rank;
+        c->size = o.comm_size;
+    }
     *out = c;
     return LC_OK;
 }
 
-extern "C" void lc_destroy(lc_ctx *c) {
-    if (!c) return;
-    (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    delete c;
-}
+extern "C" void lc_destroy(lc_ctx *c) { delete c; }
 
-// Per-event validation of a packed batch (every :ok names a pending slot,
-// every invoke's transition id is in range), over nt threads of its own.
-// Returns 0 or a reason code (1..3) with the first bad key in *badkey; sets
-// no error text, so it may run beside the caller's uploads.
+// ---- validation -------------------------------------------------------------
+
+// Per-event validation of a packed batch over the worker pool: every :ok
+// names a pending slot, no :invoke lands in an occupied slot, every
+// transition id is in range, no key uses more slots than its key_width says
+// or (per-key tables) installs a state beyond its key_states.  Returns 0 or
+// a reason code with the first bad key in *badkey; sets no error text.
 // stage (optional): pinned host buffer that receives a copy of the event
 // words; each thread copies the contiguous run of keys it validates, so the
 // events are read once, in cache, on their way to the DMA engine.
-static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *stage = nullptr,
-                           HostPool *hp = nullptr) {
+// check = false: the copy alone (a batch T0 validates itself).
+static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *stage, HostPool *hp, bool check = true) {
     const int64_t K = b->n_keys;
-    unsigned nt = hp ? hp->size() : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    unsigned nt = hp ? hp->size() : 1;
     if (K < 256) nt = 1;
     std::vector<int> bad((size_t)nt, 0);
     std::vector<int64_t> badkey((size_t)nt, -1);
@@ -377,37 +518,39 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
         const int64_t k0 = std::max<int64_t>(cut[t], 0), k1 = std::max<int64_t>(cut[t + 1], k0);
         if (stage && k1 > k0)
             std::memcpy(stage + b->ev_off[k0], b->events + b->ev_off[k0], (b->ev_off[k1] - b->ev_off[k0]) * 4);
+        if (!check) return;
         for (int64_t k = k0; k < k1 && !bad[t]; ++k) {
             if (b->key_error && b->key_error[k]) continue;  // not searched
-            uint64_t tb = b->trans_off ? b->trans_off[k] : 0;
+            const uint64_t tb = b->trans_off ? b->trans_off[k] : 0;
+            const uint32_t ns = (b->trans_off && b->key_states) ? b->key_states[k] : 0xFFFFFFFFu;
             uint64_t pend[2] = {0, 0};
+            uint32_t width = 0;
             for (uint64_t j = b->ev_off[k]; j < b->ev_off[k + 1]; ++j) {
-                uint32_t ev = b->events[j];
-                uint32_t s = LC_EV_SLOT(ev);
+                const uint32_t ev = b->events[j];
+                const uint32_t s = LC_EV_SLOT(ev);
                 // slot 127 marks ops beyond the encodable window: the search
                 // stops (LC_CAUSE_WINDOW) before it could follow one.
                 if (ev & LC_EV_OK_BIT) {
                     if (s == 127) continue;
-                    if (!((pend[s >> 6] >> (s & 63)) & 1)) { bad[t] = 1; badkey[t] = k; break; }
+                    if (!((pend[s >> 6] >> (s & 63)) & 1)) { bad[t] = 1; break; }
                     pend[s >> 6] &= ~(1ull << (s & 63));
                 } else {
-                    if (tb + LC_EV_TRANS(ev) >= (uint64_t)b->n_trans) { bad[t] = 2; badkey[t] = k; break; }
+                    const uint64_t ti = tb + LC_EV_TRANS(ev);
+                    if (ti >= (uint64_t)b->n_trans) { bad[t] = 2; break; }
+                    const uint32_t d = b->trans[ti], f = d & 3u;
+                    if ((f == LC_T_WRITE || f == LC_T_CAS) && (d >> 17) >= ns) { bad[t] = 5; break; }
                     if (s == 127) continue;
-                    if ((pend[s >> 6] >> (s & 63)) & 1) { bad[t] = 3; badkey[t] = k; break; }
+                    if ((pend[s >> 6] >> (s & 63)) & 1) { bad[t] = 3; break; }
                     pend[s >> 6] |= 1ull << (s & 63);
+                    width = std::max(width, s + 1);
                 }
             }
+            if (!bad[t] && b->key_width && width > b->key_width[k]) bad[t] = 4;
+            if (bad[t]) badkey[t] = k;
         }
     };
-    if (hp) {
-        hp->run(nt, work);
-    } else if (nt == 1) {
-        work(0);
-    } else {
-        std::vector<std::thread> pool;
-        for (unsigned t = 0; t < nt; ++t) pool.emplace_back(work, t);
-        for (auto &th : pool) th.join();
-    }
+    if (hp && nt > 1) hp->run(nt, work);
+    else work(0);
     for (size_t t = 0; t < bad.size(); ++t)
         if (bad[t]) { *badkey_out = badkey[t]; return bad[t]; }
     return 0;
@@ -415,17 +558,18 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
 
 static int events_error(int why, int64_t key) {
     static const char *text[] = {"", ":ok of a slot with no pending op", "transition id out of range",
-                                 ":invoke into an occupied slot"};
+                                 ":invoke into an occupied slot", "uses more window slots than key_width says",
+                                 "installs a state beyond key_states"};
     return lc::fail(LC_E_INVALID, "batch: key %lld: %s", (long long)key, text[why]);
 }
 
-// Host validation of a packed batch: every index a kernel will follow is in
-// range, every :ok names a slot that is pending.  events = false leaves the
-// per-event pass to the caller (validate_events).
-static int validate_batch(const lc_batch *b, bool events = true) {
+// Host validation of everything but the events: offsets, the transition
+// table, init_state.  O(keys + transitions).
+static int validate_batch(const lc_batch *b) {
     if (!b || b->n_keys < 0) return lc::fail(LC_E_INVALID, "batch: bad n_keys");
     if (b->n_keys == 0) return LC_OK;
     if (!b->ev_off || !b->trans || b->n_trans <= 0) return lc::fail(LC_E_INVALID, "batch: missing arrays");
+    if (b->n_trans > 0xFFFFFFFFll) return lc::fail(LC_E_INVALID, "batch: more than 2^32 transitions");
     if (b->ev_off[0] != 0) return lc::fail(LC_E_INVALID, "batch: ev_off[0] != 0");
     for (int64_t k = 0; k < b->n_keys; ++k) {
         if (b->ev_off[k + 1] < b->ev_off[k]) return lc::fail(LC_E_INVALID, "batch: ev_off not monotone at key %lld", (long long)k);
@@ -433,24 +577,91 @@ static int validate_batch(const lc_batch *b, bool events = true) {
     }
     if (b->ev_off[b->n_keys] && !b->events) return lc::fail(LC_E_INVALID, "batch: events missing");
     if (b->init_state >= LC_STATE_NONE) return lc::fail(LC_E_INVALID, "batch: bad init_state");
-    if (events) {
-        int64_t bk = -1;
-        if (int why = validate_events(b, &bk)) return events_error(why, bk);
-    }
     for (int64_t i = 0; i < b->n_trans; ++i) {
         uint32_t d = b->trans[i];
-        uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, bb = d >> 17;
+        uint32_t f = d & 3u, bb = d >> 17;
         if ((f == LC_T_WRITE || f == LC_T_CAS) && bb >= LC_STATE_NONE)
             return lc::fail(LC_E_INVALID, "batch: transition %lld installs an invalid state", (long long)i);
-        (void)a;
     }
     return LC_OK;
 }
 
-// Copy a validated batch into d's device arrays (grown as needed); c->mu held.
+// What the register tier needs to know of a batch before any upload: the
+// state count of a shared table and whether every key is declared to fit T0
+// (width, states, initial state).  A batch that does is validated by T0
+// itself (T0_STRICT), so the host skips its per-event pass.
+struct Shape {
+    uint32_t shared_states = 0;
+    bool t0_only = false;
+};
+
+static Shape batch_shape(const lc_batch *b) {
+    Shape s;
+    uint32_t mx = b->init_state;
+    for (int64_t i = 0; i < b->n_trans; ++i) {
+        const uint32_t t = b->trans[i], f = t & 3u, a = (t >> 2) & 0x7FFFu, bb = t >> 17;
+        if ((f == LC_T_READ || f == LC_T_CAS) && a != LC_STATE_NONE) mx = std::max(mx, a);
+        if (f == LC_T_WRITE || f == LC_T_CAS) mx = std::max(mx, bb);
+    }
+    s.shared_states = mx + 1;
+    const int64_t K = b->n_keys;
+    bool ok = K > 0 && b->key_width && b->init_state < lcd::t0_max_states();
+    for (int64_t k = 0; ok && k < K; ++k) ok = b->key_width[k] <= lcd::t0_max_width();
+    if (ok && b->trans_off) {
+        ok = b->key_states != nullptr;
+        for (int64_t k = 0; ok && k < K; ++k) ok = b->key_states[k] <= lcd::t0_max_states() && b->key_states[k] > 0;
+    } else if (ok) {
+        ok = s.shared_states <= lcd::t0_max_states();
+    }
+    s.t0_only = ok;
+    return s;
+}
+
+// Is p page-locked host memory (a DMA source without a bounce)?
+static bool pinned(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+// Keys [k0, k1) of b as a batch of their own (ev_off rebased into `off`).
+static lc_batch sub_batch(const lc_batch *b, int64_t k0, int64_t k1, std::vector<uint64_t> &off) {
+    lc_batch s = *b;
+    s.n_keys = k1 - k0;
+    off.resize((size_t)(k1 - k0) + 1);
+    const uint64_t base = b->ev_off[k0];
+    for (int64_t k = k0; k <= k1; ++k) off[(size_t)(k - k0)] = b->ev_off[k] - base;
+    s.ev_off = off.data();
+    s.events = b->events ? b->events + base : nullptr;
+    if (b->trans_off) s.trans_off = b->trans_off + k0;
+    if (b->key_width) s.key_width = b->key_width + k0;
+    if (b->key_states) s.key_states = b->key_states + k0;
+    if (b->key_error) s.key_error = b->key_error + k0;
+    return s;
+}
+
+// Contiguous key shards of about equal event counts, one per device.
+static void shard_keys(const lc_batch *b, int n, int64_t *key0) {
+    const int64_t K = b->n_keys;
+    const uint64_t tot = K ? b->ev_off[K] : 0;
+    key0[0] = 0;
+    for (int g = 1; g < n; ++g) {
+        int64_t k = tot ? std::upper_bound(b->ev_off, b->ev_off + K + 1, tot * (uint64_t)g / (uint64_t)n) - b->ev_off - 1
+                        : K * g / n;
+        key0[g] = std::min(std::max(k, key0[g - 1]), K);
+    }
+    key0[n] = K;
+}
+
+// Copy a validated batch into d's device arrays (grown as needed).
 // events_src: where the event words are copied from (b->events by default;
 // lc_check_batch passes its pinned staging copy).
-static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d, const uint32_t *events_src = nullptr) {
+static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, bool validated,
+                       const uint32_t *events_src = nullptr) {
     const int64_t K = b->n_keys;
     d->device = c->device;
     d->n_keys = K;
@@ -458,15 +669,9 @@ static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d, const uint
     d->n_trans = b->n_trans > 0 ? b->n_trans : 1;
     d->init_state = b->init_state;
     d->has_trans_off = b->trans_off != nullptr;
-    {
-        uint32_t mx = b->init_state;
-        for (int64_t i = 0; i < b->n_trans; ++i) {
-            const uint32_t t = b->trans[i], f = t & 3u, a = (t >> 2) & 0x7FFFu, bb = t >> 17;
-            if ((f == LC_T_READ || f == LC_T_CAS) && a != LC_STATE_NONE) mx = std::max(mx, a);
-            if (f == LC_T_WRITE || f == LC_T_CAS) mx = std::max(mx, bb);
-        }
-        d->shared_states = mx + 1;
-    }
+    d->shared_states = sh.shared_states;
+    d->t0_only = sh.t0_only;
+    d->validated = validated;
     // LPT order: longest keys first
     std::vector<int32_t> order((size_t)K);
     std::iota(order.begin(), order.end(), 0);
@@ -477,106 +682,95 @@ static int upload_into(lc_ctx *c, const lc_batch *b, lc_dev_batch *d, const uint
     d->key_width = nullptr;
     d->key_states = nullptr;
     d->key_error = nullptr;
-    auto up = [&]() -> int {
-        HIPCHK(grow(d->mem[0], d->ev_off, (size_t)K + 1));
-        HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
-        HIPCHK(grow(d->mem[2], d->trans, (size_t)d->n_trans));
-        HIPCHK(grow(d->mem[3], d->order, (size_t)K));
-        if (K) {
-            HIPCHK(hipMemcpyAsync(d->ev_off, b->ev_off, ((size_t)K + 1) * 8, hipMemcpyHostToDevice, c->stream));
-            HIPCHK(hipMemcpyAsync(d->order, order.data(), (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
-        }
-        if (d->n_events)
-            HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
-                                  hipMemcpyHostToDevice, c->stream));
-        if (b->n_trans > 0)
-            HIPCHK(hipMemcpyAsync(d->trans, b->trans, (size_t)b->n_trans * 4, hipMemcpyHostToDevice, c->stream));
-        if (b->trans_off && K) {
-            HIPCHK(grow(d->mem[4], d->trans_off, (size_t)K));
-            HIPCHK(hipMemcpyAsync(d->trans_off, b->trans_off, (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
-        }
-        if (b->key_width && K) {
-            HIPCHK(grow(d->mem[5], d->key_width, (size_t)K));
-            HIPCHK(hipMemcpyAsync(d->key_width, b->key_width, (size_t)K, hipMemcpyHostToDevice, c->stream));
-        }
-        if (b->key_states && K) {
-            HIPCHK(grow(d->mem[6], d->key_states, (size_t)K));
-            HIPCHK(hipMemcpyAsync(d->key_states, b->key_states, (size_t)K * 2, hipMemcpyHostToDevice, c->stream));
-        }
-        if (b->key_error && K) {
-            HIPCHK(grow(d->mem[7], d->key_error, (size_t)K));
-            HIPCHK(hipMemcpyAsync(d->key_error, b->key_error, (size_t)K, hipMemcpyHostToDevice, c->stream));
-        }
-        HIPCHK(hipStreamSynchronize(c->stream));
-        return LC_OK;
-    };
-    int rc = up();
-    if (rc) return rc;
-    // T0 spills a key only for its width (ops pending at once), its state
-    // count or the initial state; all three are known here.
-    {
-        bool ok = K > 0 && b->key_width && b->init_state < lcd::t0_max_states();
-        for (int64_t k = 0; ok && k < K; ++k) ok = b->key_width[k] <= lcd::t0_max_width();
-        if (ok && b->trans_off) {
-            ok = b->key_states != nullptr;
-            for (int64_t k = 0; ok && k < K; ++k) ok = b->key_states[k] <= lcd::t0_max_states();
-        } else if (ok) {
-            ok = d->shared_states <= lcd::t0_max_states();
-        }
-        d->t0_only = ok;
-    }
-    d->input_bytes = (size_t)d->n_events * 4 + ((size_t)K + 1) * 8;
-    return LC_OK;
-}
-
-extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
-    if (!c || !b || !out) return lc::fail(LC_E_INVALID, "lc_upload: null argument");
-    std::lock_guard<std::mutex> g(c->mu);
-    int rc = validate_batch(b);
-    if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
-    lc_dev_batch *d = new (std::nothrow) lc_dev_batch();
-    if (!d) return lc::fail(LC_E_NOMEM, "lc_upload: out of memory");
-    rc = upload_into(c, b, d);
-    if (rc) { delete d; return rc; }
-    *out = d;
+    HIPCHK(grow(d->mem[0], d->ev_off, (size_t)K + 1));
+    HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
+    HIPCHK(grow(d->mem[2], d->trans, (size_t)d->n_trans));
+    HIPCHK(grow(d->mem[3], d->order, (size_t)K));
+    if (K) {
+        HIPCHK(hipMemcpyAsync(d->ev_off, b->ev_off, ((size_t)K + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->order, order.data(), (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    if (d->n_events)
+        HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
+                              hipMemcpyHostToDevice, c->stream));
+    if (b->n_trans > 0)
+        HIPCHK(hipMemcpyAsync(d->trans, b->trans, (size_t)b->n_trans * 4, hipMemcpyHostToDevice, c->stream));
+    if (b->trans_off && K) {
+        HIPCHK(grow(d->mem[4], d->trans_off, (size_t)K));
+        HIPCHK(hipMemcpyAsync(d->trans_off, b->trans_off, (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    if (b->key_width && K) {
+        HIPCHK(grow(d->mem[5], d->key_width, (size_t)K));
+        HIPCHK(hipMemcpyAsync(d->key_width, b->key_width, (size_t)K, hipMemcpyHostToDevice, c->stream));
+    }
+    if (b->key_states && K) {
+        HIPCHK(grow(d->mem[6], d->key_states, (size_t)K));
+        HIPCHK(hipMemcpyAsync(d->key_states, b->key_states, (size_t)K * 2, hipMemcpyHostToDevice, c->stream));
+    }
+    if (b->key_error && K) {
+        HIPCHK(grow(d->mem[7], d->key_error, (size_t)K));
+        HIPCHK(hipMemcpyAsync(d->key_error, b->key_error, (size_t)K, hipMemcpyHostToDevice, c->stream));
+    }
+    // the host arrays (order above, the caller's) must outlive the copies
+    HIPCHK(hipStreamSynchronize(c->stream));
     return LC_OK;
 }
 
-extern "C" void lc_dev_batch_free(lc_dev_batch *d) {
-    if (!d) return;
-    (void)hipSetDevice(d->device);
-    delete d;
+// ---- one device's search ----------------------------------------------------
+
+// After a readback of the control block: a malformed batch T0 found.
+static int take_error(Dev *c, int64_t key0) {
+    int32_t *cnt = (int32_t *)(c->hctl + 4);
+    if (!cnt[4]) return LC_OK;
+    const int why = cnt[4];
+    const int64_t key = key0 + (int64_t)cnt[5] - 1;
+    cnt[4] = cnt[5] = 0;
+    HIPCHK(hipMemsetAsync(c->counters + 4, 0, 2 * sizeof(int32_t), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return lc::fail(LC_E_INVALID, "batch: key %lld: %s", (long long)key,
+                    (why & lcd::LC_BATCH_E_SLOTS)   ? "an :ok of a slot with no pending op, or an :invoke into an occupied slot"
+                    : (why & lcd::LC_BATCH_E_TRANS) ? "transition id out of range, or a state beyond key_states"
+                                                    : "key_width / key_states understate the key");
 }
 
-extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, int flags, lc_stats *st) {
-    if (flags & ~(LC_DEV_RESULT | LC_DEV_ASYNC)) return lc::fail(LC_E_INVALID, "lc_check_device: unknown flags 0x%x", flags);
-    const bool dev_result = (flags & LC_DEV_RESULT) != 0;
-    if (!c || !d || !r || !r->valid || !r->fail_event || !r->cause)
-        return lc::fail(LC_E_INVALID, "lc_check_device: null argument");
-    if (d->device != c->device) return lc::fail(LC_E_INVALID, "lc_check_device: batch lives on another device");
-    std::lock_guard<std::mutex> g(c->mu);
+enum ResMode { RES_HOST = 0, RES_DEV = 1, RES_CTX = 2 };
+
+// Search d on c.  RES_HOST: r's arrays are host memory and receive the
+// results; RES_DEV: r's arrays are device memory on c; RES_CTX: results stay
+// in c's own device arrays (r unused).  allow_async: a step that is T0 alone
+// is only enqueued (*enqueued = true; errors surface at the next wait).
+static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mode, bool allow_async, int64_t key0,
+                      lc_stats *st, bool *enqueued = nullptr) {
+    if (enqueued) *enqueued = false;
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(c->device));
     const int64_t K = d->n_keys;
     if (K > 0x7FFFFFFF) return lc::fail(LC_E_INVALID, "lc_check_device: too many keys");
     int rc = ensure_capacity(c, K);
     if (rc) return rc;
+    const lc_opts &o = *c->o;
 
     lcd::Args a{};
     a.ev_off = d->ev_off; a.events = d->events; a.trans = d->trans; a.trans_off = d->trans_off;
     a.key_width = d->key_width; a.key_states = d->key_states; a.key_error = d->key_error;
     a.init_state = d->init_state; a.shared_states = d->shared_states;
-    a.budget = c->o.max_configs; a.max_final = c->o.max_final; a.debug_mode = c->o.debug_mode;
-    a.count_probes = (c->o.flags & LC_OPT_COUNT_PROBES) ? 1 : 0;
-    if (dev_result) {
+    a.n_trans = (uint32_t)d->n_trans;
+    a.strict = d->validated ? 0 : 1;
+    a.budget = o.max_configs; a.max_final = o.max_final; a.debug_mode = o.debug_mode;
+    a.count_probes = (o.flags & LC_OPT_COUNT_PROBES) ? 1 : 0;
+    if (mode == RES_DEV) {
         a.valid = r->valid; a.fail_event = r->fail_event; a.cause = r->cause;
         a.peak = r->peak_configs; a.final_cfg = r->final_configs; a.n_final = r->n_final;
     } else {
         a.valid = c->valid; a.fail_event = c->fail_event; a.cause = c->cause;
-        a.peak = c->peak; a.final_cfg = c->final_cfg; a.n_final = c->n_final;
+        a.peak = (mode == RES_HOST && r->peak_configs) ? c->peak : nullptr;
+        a.final_cfg = (mode == RES_HOST && r->final_configs) ? c->final_cfg : nullptr;
+        a.n_final = (mode == RES_HOST && r->n_final) ? c->n_final : nullptr;
     }
     a.probes = c->acc + 0; a.ev_count = c->acc + 1; a.keys_done = c->acc + 2;
+    a.err = c->counters + 4;
+    a.list_cap = (int32_t)c->cap_keys;
     int32_t *spill0 = c->lists, *spill1 = c->lists + c->cap_keys, *spill2 = c->lists + 2 * c->cap_keys;
     int32_t *wide = c->lists + 3 * c->cap_keys;
     int32_t *n_spill0 = c->counters + 0, *n_spill1 = c->counters + 1, *n_spill2 = c->counters + 2;
@@ -585,12 +779,17 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     // Nothing counted and no key can leave T0: no T1/T2 launches, no counter
     // readback and no control-block memset -- the step is T0 alone (plus the
     // result download when the results go to host memory).
-    const bool t0_step = K > 0 && d->t0_only && !(c->o.flags & LC_OPT_COUNT_PROBES);
-    // LC_DEV_ASYNC: such a step is only enqueued; lc_wait ends the run
-    const bool async = t0_step && dev_result && (flags & LC_DEV_ASYNC);
+    const bool t0_step = K > 0 && d->t0_only && !(o.flags & LC_OPT_COUNT_PROBES);
+    const bool async = t0_step && allow_async && mode != RES_HOST;
     uint32_t ticket_base = 0;
-    if (t0_step && c->ticket_live) ticket_base = c->ticket_next;
-    else HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_BYTES, c->stream));
+    if (t0_step && c->ticket_live) {
+        ticket_base = c->ticket_next;
+    } else {
+        // zero everything but the error words (a malformed batch reported at
+        // the next wait keeps them until then)
+        HIPCHK(hipMemsetAsync(c->ctl, 0, 4 * sizeof(unsigned long long) + 4 * sizeof(int32_t), c->stream));
+        HIPCHK(hipMemsetAsync(c->counters + 6, 0, 10 * sizeof(int32_t), c->stream));
+    }
     c->ticket_live = false;
     if (a.n_final && K > 0) HIPCHK(hipMemsetAsync(a.n_final, 0, (size_t)K * 4, c->stream));
     // T0: every key, LPT order; keys outside the register lattice spill to T1
@@ -607,7 +806,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     const int g0 = (int)std::max<int64_t>(1, std::min<int64_t>(K, (int64_t)c->cu_count * (t0_wide ? 8 : 16)));
     a0.lat_ws = nullptr;
     // T0 reads the result/counter/list pointers from a device copy of its
-    // Args, refreshed (outside the timed region) only when they change
+    // Args, refreshed only when they change
     if (!c->hargs_valid || std::memcmp(c->hargs, &a0, sizeof a0) != 0) {
         // the pinned staging copy may still feed an enqueued copy
         if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
@@ -629,6 +828,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
         if (st) *st = lc_stats{};  // times come from lc_wait
+        if (enqueued) *enqueued = true;
         return LC_OK;
     }
     if (K > 0 && !t0_step) {
@@ -652,47 +852,51 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
     auto readback = [&]() -> int {
         HIPCHK(hipEventRecord(c->e1, c->stream));
         HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
-        if (!dev_result && K > 0) {
+        if (mode == RES_HOST && K > 0) {
             HIPCHK(hipMemcpyAsync(r->valid, c->valid, (size_t)K, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(r->fail_event, c->fail_event, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(r->cause, c->cause, (size_t)K, hipMemcpyDeviceToHost, c->stream));
             if (r->peak_configs)
                 HIPCHK(hipMemcpyAsync(r->peak_configs, c->peak, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
             if (r->final_configs)
-                HIPCHK(hipMemcpyAsync(r->final_configs, c->final_cfg, (size_t)K * c->o.max_final * 16,
+                HIPCHK(hipMemcpyAsync(r->final_configs, c->final_cfg, (size_t)K * o.max_final * 16,
                                       hipMemcpyDeviceToHost, c->stream));
             if (r->n_final)
                 HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
-        return LC_OK;
+        return take_error(c, key0);
     };
     if (t0_step) {
-        if (dev_result) {
+        if (mode != RES_HOST) {
+            // only the error words come back
             HIPCHK(hipEventRecord(c->e1, c->stream));
-            HIPCHK(hipEventSynchronize(c->e1));
+            HIPCHK(hipMemcpyAsync(c->hctl + 6, c->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            rc = take_error(c, key0);
         } else {
             rc = readback();
-            if (rc) return rc;
         }
         std::memset(c->hctl, 0, CTL_BYTES);  // counters not kept on this path
         c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
+        if (rc) return rc;
     } else {
         rc = readback();
         if (rc) return rc;
     }
     bool t3 = false;
     const unsigned long long probes_pre_t3 = acc[0];
-    if (K > 0 && (cnt[2] > 0 || cnt[3] > 0)) {
+    const int32_t n_deep = cnt[2], n_widek = cnt[3];
+    if (K > 0 && (n_deep > 0 || n_widek > 0)) {
         // T3 (HBM tier): keys beyond T2, then keys needing wide configs
         t3 = true;
         HIPCHK(hipEventRecord(c->et3a, c->stream));
         lcd::Args a3 = a;
         a3.wide = wide; a3.n_wide = n_wide;
-        if (cnt[2] > 0) {
+        if (n_deep > 0) {
             int slots = 0;
-            rc = ensure_ws(c, 0, cnt[2], &slots);
+            rc = ensure_ws(c, 0, n_deep, &slots);
             if (rc) return rc;
             a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 11;
             HIPCHK(lcd::launch_t3_narrow(a3, c->ws[0].w, slots, c->stream));
@@ -723,7 +927,146 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
         st->probes = acc[0];
         st->events = acc[1];
         st->lds_keys = acc[2];
-        st->deep_keys = (uint64_t)(cnt[2] + cnt[3]);  // keys the HBM tier (re)searched
+        st->deep_keys = (uint64_t)(n_deep + n_widek);  // keys the HBM tier (re)searched
+    }
+    return LC_OK;
+}
+
+// Wait for everything enqueued on c; *n_async / *span_ms: the asynchronous
+// steps since the last wait and their HIP-event span.
+static int dev_wait(Dev *c, int *n_async, float *span_ms) {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->hctl + 6, c->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *n_async = (int)c->n_async;
+    *span_ms = 0;
+    if (c->n_async) HIPCHK(hipEventElapsedTime(span_ms, c->ea0, c->ea1));
+    c->n_async = 0;
+    return take_error(c, 0);
+}
+
+static void merge_stats(lc_stats &t, const lc_stats &s) {
+    t.kernel_ms = std::max(t.kernel_ms, s.kernel_ms);
+    t.tier0_ms = std::max(t.tier0_ms, s.tier0_ms);
+    t.tier3_ms = std::max(t.tier3_ms, s.tier3_ms);
+    t.probes += s.probes;
+    t.probes_t3 += s.probes_t3;
+    t.lds_keys += s.lds_keys;
+    t.deep_keys += s.deep_keys;
+    t.events += s.events;
+}
+
+// Run fn(g) for every device g of c at once (one driver thread per device
+// beyond the first); returns the first nonzero code.
+static int each_device(lc_ctx *c, const std::function<int(int)> &fn) {
+    if (c->n_dev == 1) return fn(0);
+    std::vector<int> rc((size_t)c->n_dev, 0);
+    std::vector<std::string> err((size_t)c->n_dev);
+    c->drivers->run((unsigned)c->n_dev, [&](unsigned g) {
+        rc[g] = fn((int)g);
+        if (rc[g]) err[g] = lc_last_error();
+    });
+    for (int g = 0; g < c->n_dev; ++g)
+        if (rc[g]) return lc::fail(rc[g], "%s", err[g].c_str());
+    return LC_OK;
+}
+
+// Validate b (events too unless T0 will) and, when its event words are not
+// page-locked, copy them into the context's pinned staging buffer.  *src:
+// where the uploads read the events from (b->events or the staging copy).
+static int prepare_batch(lc_ctx *c, const lc_batch *b, Shape *sh, const uint32_t **src) {
+    int rc = validate_batch(b);
+    if (rc) return rc;
+    *sh = batch_shape(b);
+    *src = b->events;
+    const int64_t K = b->n_keys;
+    if (!K) return LC_OK;
+    const size_t n_ev = (size_t)b->ev_off[K];
+    // Batches above 256 MB of events keep the pageable path (no pinned
+    // allocation that large); page-locked caller memory is used as it is.
+    const bool stage = n_ev > 0 && n_ev <= (256u << 20) / 4 && !pinned(b->events);
+    if (stage && n_ev > c->hstage_cap) {
+        if (c->hstage) (void)hipHostFree(c->hstage);
+        c->hstage = nullptr;
+        c->hstage_cap = 0;
+        HIPCHK(hipHostMalloc((void **)&c->hstage, n_ev * 4, hipHostMallocDefault));
+        c->hstage_cap = n_ev;
+    }
+    if (!stage && sh->t0_only) return LC_OK;  // nothing to copy, T0 validates
+    if (K >= 256 && !c->pool)
+        c->pool = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+    int64_t bk = -1;
+    if (int why = validate_events(b, &bk, stage ? c->hstage : nullptr, K >= 256 ? c->pool : nullptr, !sh->t0_only))
+        return events_error(why, bk);
+    if (stage) *src = c->hstage;
+    return LC_OK;
+}
+
+// ---- C ABI ------------------------------------------------------------------
+
+extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
+    if (!c || !b || !out) return lc::fail(LC_E_INVALID, "lc_upload: null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    Shape sh;
+    const uint32_t *src = nullptr;
+    int rc = prepare_batch(c, b, &sh, &src);
+    if (rc) return rc;
+    lc_dev_batch *d = new (std::nothrow) lc_dev_batch();
+    if (!d) return lc::fail(LC_E_NOMEM, "lc_upload: out of memory");
+    d->n_parts = c->n_dev;
+    d->n_keys = b->n_keys;
+    shard_keys(b, c->n_dev, d->key0);
+    for (int p = 0; p < c->n_dev; ++p) {
+        d->part[p] = new (std::nothrow) DevBatch();
+        if (!d->part[p]) { delete d; return lc::fail(LC_E_NOMEM, "lc_upload: out of memory"); }
+        d->part[p]->device = c->dev[p]->device;
+    }
+    rc = each_device(c, [&](int p) {
+        std::vector<uint64_t> off;
+        const lc_batch s = c->n_dev > 1 ? sub_batch(b, d->key0[p], d->key0[p + 1], off) : *b;
+        const uint32_t *es = src ? src + (b->n_keys ? b->ev_off[d->key0[p]] : 0) : nullptr;
+        return upload_into(c->dev[p], &s, d->part[p], sh, !sh.t0_only, es);
+    });
+    if (rc) { delete d; return rc; }
+    *out = d;
+    return LC_OK;
+}
+
+extern "C" void lc_dev_batch_free(lc_dev_batch *d) { delete d; }
+
+extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, int flags, lc_stats *st) {
+    if (flags & ~(LC_DEV_RESULT | LC_DEV_ASYNC)) return lc::fail(LC_E_INVALID, "lc_check_device: unknown flags 0x%x", flags);
+    const bool dev_result = (flags & LC_DEV_RESULT) != 0;
+    if (!c || !d || !r || !r->valid || !r->fail_event || !r->cause)
+        return lc::fail(LC_E_INVALID, "lc_check_device: null argument");
+    if (d->n_parts != c->n_dev) return lc::fail(LC_E_INVALID, "lc_check_device: batch uploaded by another context shape");
+    for (int p = 0; p < d->n_parts; ++p)
+        if (d->part[p]->device != c->dev[p]->device)
+            return lc::fail(LC_E_INVALID, "lc_check_device: batch lives on another device");
+    if (dev_result && c->n_dev > 1)
+        return lc::fail(LC_E_INVALID, "lc_check_device: LC_DEV_RESULT needs a one-device context");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->n_dev == 1)
+        return dev_search(c->dev[0], d->part[0], r, dev_result ? RES_DEV : RES_HOST, (flags & LC_DEV_ASYNC) != 0, 0, st);
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<lc_stats> ps((size_t)c->n_dev);
+    const int mf = c->o.max_final;
+    int rc = each_device(c, [&](int p) {
+        const int64_t k0 = d->key0[p];
+        lc_result rp = *r;
+        rp.valid = r->valid + k0;
+        rp.fail_event = r->fail_event + k0;
+        rp.cause = r->cause + k0;
+        if (r->peak_configs) rp.peak_configs = r->peak_configs + k0;
+        if (r->final_configs) rp.final_configs = r->final_configs + (size_t)k0 * mf * 2;
+        if (r->n_final) rp.n_final = r->n_final + k0;
+        return dev_search(c->dev[p], d->part[p], &rp, RES_HOST, false, k0, &ps[(size_t)p]);
+    });
+    if (rc) return rc;
+    if (st) {
+        *st = lc_stats{};
+        for (const lc_stats &s : ps) merge_stats(*st, s);
+        st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return LC_OK;
 }
@@ -731,12 +1074,18 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
 extern "C" int lc_wait(lc_ctx *c, lc_stats *st) {
     if (!c) return lc::fail(LC_E_INVALID, "lc_wait: null context");
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const int n = (int)c->n_async;
+    int n = 0;
     float ms = 0;
-    if (n) HIPCHK(hipEventElapsedTime(&ms, c->ea0, c->ea1));
-    c->n_async = 0;
+    int rc = LC_OK;
+    for (int p = 0; p < c->n_dev; ++p) {
+        int np = 0;
+        float mp = 0;
+        int r = dev_wait(c->dev[p], &np, &mp);
+        if (r && !rc) rc = r;
+        n = std::max(n, np);
+        ms = std::max(ms, mp);
+    }
+    if (rc) return rc;
     if (st) {
         *st = lc_stats{};
         st->kernel_ms = ms;                    // first enqueued step's start .. last one's end
@@ -748,64 +1097,167 @@ extern "C" int lc_wait(lc_ctx *c, lc_stats *st) {
 extern "C" int lc_wait_step(lc_ctx *c, int back) {
     if (!c) return lc::fail(LC_E_INVALID, "lc_wait_step: null context");
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->device));
-    if (back < 0 || back >= 4 || (uint64_t)back >= c->async_seq) {
-        HIPCHK(hipStreamSynchronize(c->stream));  // no such step on record: everything
-    } else {
-        HIPCHK(hipEventSynchronize(c->ring[(c->async_seq - 1 - (uint64_t)back) % 4]));
+    for (int p = 0; p < c->n_dev; ++p) {
+        Dev *d = c->dev[p];
+        HIPCHK(hipSetDevice(d->device));
+        if (back < 0 || back >= 4 || (uint64_t)back >= d->async_seq) {
+            HIPCHK(hipStreamSynchronize(d->stream));  // no such step on record: everything
+        } else {
+            HIPCHK(hipEventSynchronize(d->ring[(d->async_seq - 1 - (uint64_t)back) % 4]));
+        }
     }
     return LC_OK;
 }
 
 extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_stats *st) {
     auto t0 = std::chrono::steady_clock::now();
-    if (!c || !b) return lc::fail(LC_E_INVALID, "lc_check_batch: null argument");
-    std::lock_guard<std::mutex> gb(c->batch_mu);
-    auto t_val = t0;
-    int rc;
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        rc = validate_batch(b, false);
-        if (rc) return rc;
-        HIPCHK(hipSetDevice(c->device));
-        if (!c->staged) {
-            c->staged = new (std::nothrow) lc_dev_batch();
-            if (!c->staged) return lc::fail(LC_E_NOMEM, "lc_check_batch: out of memory");
-            c->staged->device = c->device;
+    if (!c || !b || !r || !r->valid || !r->fail_event || !r->cause)
+        return lc::fail(LC_E_INVALID, "lc_check_batch: null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    Shape sh;
+    const uint32_t *src = nullptr;
+    int rc = prepare_batch(c, b, &sh, &src);
+    if (rc) return rc;
+    const auto t_val = std::chrono::steady_clock::now();
+    int64_t key0[MAX_DEV + 1];
+    shard_keys(b, c->n_dev, key0);
+    std::vector<lc_stats> ps((size_t)c->n_dev);
+    const int mf = c->o.max_final;
+    rc = each_device(c, [&](int p) {
+        Dev *d = c->dev[p];
+        if (!d->staged) {
+            d->staged = new (std::nothrow) DevBatch();
+            if (!d->staged) return lc::fail(LC_E_NOMEM, "lc_check_batch: out of memory");
         }
-        // The per-event pass copies the event words into pinned staging as it
-        // validates them (one parallel read of the caller's array); the DMA
-        // then runs from pinned memory instead of the driver's pageable path.
-        // Batches above 256 MB of events keep the pageable path (no pinned
-        // allocation that large).
-        const size_t n_ev = b->n_keys ? (size_t)b->ev_off[b->n_keys] : 0;
-        const bool stage = n_ev > 0 && n_ev <= (256u << 20) / 4;
-        if (stage && n_ev > c->hstage_cap) {
-            if (c->hstage) (void)hipHostFree(c->hstage);
-            c->hstage = nullptr;
-            c->hstage_cap = 0;
-            HIPCHK(hipHostMalloc((void **)&c->hstage, n_ev * 4, hipHostMallocDefault));
-            c->hstage_cap = n_ev;
-        }
-        int64_t bk = -1;
-        if (b->n_keys >= 256 && !c->pool)
-            c->pool = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
-        if (b->n_keys)
-            if (int why = validate_events(b, &bk, stage ? c->hstage : nullptr, b->n_keys >= 256 ? c->pool : nullptr))
-                return events_error(why, bk);
-        t_val = std::chrono::steady_clock::now();
-        rc = upload_into(c, b, c->staged, stage ? c->hstage : nullptr);
-        if (rc) return rc;
-    }
-    const auto t_up = std::chrono::steady_clock::now();
-    rc = lc_check_device(c, c->staged, r, 0, st);
+        std::vector<uint64_t> off;
+        const lc_batch s = c->n_dev > 1 ? sub_batch(b, key0[p], key0[p + 1], off) : *b;
+        const uint32_t *es = src ? src + (b->n_keys ? b->ev_off[key0[p]] : 0) : nullptr;
+        int e = upload_into(d, &s, d->staged, sh, !sh.t0_only, es);
+        if (e) return e;
+        const int64_t k0 = key0[p];
+        lc_result rp = *r;
+        rp.valid = r->valid + k0;
+        rp.fail_event = r->fail_event + k0;
+        rp.cause = r->cause + k0;
+        if (r->peak_configs) rp.peak_configs = r->peak_configs + k0;
+        if (r->final_configs) rp.final_configs = r->final_configs + (size_t)k0 * mf * 2;
+        if (r->n_final) rp.n_final = r->n_final + k0;
+        return dev_search(d, d->staged, &rp, RES_HOST, false, k0, &ps[(size_t)p]);
+    });
     if (std::getenv("LC_TIMING")) {
         using ms = std::chrono::duration<double, std::milli>;
-        const auto t_end = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "lc_check_batch: validate %.3f ms, upload %.3f ms, check %.3f ms\n",
-                     ms(t_val - t0).count(), ms(t_up - t_val).count(), ms(t_end - t_up).count());
+        std::fprintf(stderr, "lc_check_batch: validate/stage %.3f ms, upload + check %.3f ms\n",
+                     ms(t_val - t0).count(), ms(std::chrono::steady_clock::now() - t_val).count());
     }
-    if (st && rc == LC_OK)
+    if (rc) return rc;
+    if (st) {
+        *st = lc_stats{};
+        for (const lc_stats &s : ps) merge_stats(*st, s);
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return rc;
+    }
+    return LC_OK;
+}
+
+// ---- one process per GPU: node-wide verdict records ---------------------------
+
+// Pack this rank's verdicts (c's device arrays) into its block and all-gather
+// the blocks of every rank over RCCL (one rank: the block is the node), on
+// c's stream.
+static int gather_node(lc_ctx *x, Dev *c, int64_t n, int64_t block) {
+    const int64_t total = block * x->size;
+    if (block > c->node_cap || !c->send) {
+        dfree(c->send);
+        dfree(c->node);
+        HIPCHK(dalloc(&c->send, (size_t)std::max<int64_t>(block, 1)));
+        HIPCHK(dalloc(&c->node, (size_t)std::max<int64_t>(block, 1) * x->size));
+        c->node_cap = block;
+    }
+    if (block > 0) {
+        const int threads = 256;
+        const int blocks = (int)std::min<int64_t>((block + threads - 1) / threads, 4096);
+        hipLaunchKernelGGL(k_pack_records, dim3(blocks), dim3(threads), 0, c->stream, c->valid, c->cause, c->fail_event,
+                           n, block, x->comm ? c->send : c->node);
+        HIPCHK(hipGetLastError());
+    }
+    if (x->comm) {
+        const Rccl *R = rccl();
+        RCCLCHK(R->all_gather(c->send, c->node, (size_t)block, ncclUint64, x->comm, c->stream));
+    }
+    c->node_n = total;
+    return LC_OK;
+}
+
+static int node_check_args(lc_ctx *c, int64_t n_keys, int64_t block) {
+    if (c->n_dev != 1) return lc::fail(LC_E_INVALID, "lc_check_node: needs a one-device context");
+    if (block < n_keys) return lc::fail(LC_E_INVALID, "lc_check_node: block %lld < the shard's %lld keys",
+                                        (long long)block, (long long)n_keys);
+    return LC_OK;
+}
+
+extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64_t *node, lc_stats *st) {
+    auto t0 = std::chrono::steady_clock::now();
+    if (!c || !b || !node) return lc::fail(LC_E_INVALID, "lc_check_node: null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = node_check_args(c, b->n_keys, block);
+    if (rc) return rc;
+    Shape sh;
+    const uint32_t *src = nullptr;
+    rc = prepare_batch(c, b, &sh, &src);
+    if (rc) return rc;
+    Dev *d = c->dev[0];
+    if (!d->staged) {
+        d->staged = new (std::nothrow) DevBatch();
+        if (!d->staged) return lc::fail(LC_E_NOMEM, "lc_check_node: out of memory");
+    }
+    rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src);
+    if (rc) return rc;
+    lc_result none{};
+    bool enq = false;
+    rc = dev_search(d, d->staged, &none, RES_CTX, true, 0, st, &enq);
+    if (rc) return rc;
+    rc = gather_node(c, d, b->n_keys, block);
+    if (rc) return rc;
+    if (d->node_n) HIPCHK(hipMemcpyAsync(node, d->node, (size_t)d->node_n * 8, hipMemcpyDeviceToHost, d->stream));
+    if (enq) {  // a T0-only step: one wait for the search, the exchange and the download
+        int n_async = 0;
+        float span = 0;
+        rc = dev_wait(d, &n_async, &span);
+        if (rc) return rc;
+        if (st) st->kernel_ms = st->tier0_ms = span;
+    } else {
+        HIPCHK(hipStreamSynchronize(d->stream));
+    }
+    if (st) st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return LC_OK;
+}
+
+extern "C" int lc_check_node_device(lc_ctx *c, const lc_dev_batch *db, int64_t block, int flags, lc_stats *st) {
+    if (!c || !db) return lc::fail(LC_E_INVALID, "lc_check_node_device: null argument");
+    if (flags & ~LC_DEV_ASYNC) return lc::fail(LC_E_INVALID, "lc_check_node_device: unknown flags 0x%x", flags);
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = node_check_args(c, db->n_keys, block);
+    if (rc) return rc;
+    if (db->n_parts != 1 || db->part[0]->device != c->dev[0]->device)
+        return lc::fail(LC_E_INVALID, "lc_check_node_device: batch lives on another device");
+    Dev *d = c->dev[0];
+    lc_result none{};
+    bool enq = false;
+    rc = dev_search(d, db->part[0], &none, RES_CTX, (flags & LC_DEV_ASYNC) != 0, 0, st, &enq);
+    if (rc) return rc;
+    rc = gather_node(c, d, db->n_keys, block);
+    if (rc) return rc;
+    if (!enq) HIPCHK(hipStreamSynchronize(d->stream));
+    return LC_OK;
+}
+
+extern "C" int lc_node_records(lc_ctx *c, uint64_t *node, int64_t n) {
+    if (!c || (!node && n)) return lc::fail(LC_E_INVALID, "lc_node_records: null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    Dev *d = c->dev[0];
+    if (n > d->node_n) return lc::fail(LC_E_INVALID, "lc_node_records: %lld records asked, %lld gathered",
+                                       (long long)n, (long long)d->node_n);
+    HIPCHK(hipSetDevice(d->device));
+    if (n) HIPCHK(hipMemcpyAsync(node, d->node, (size_t)n * 8, hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    return LC_OK;
 }

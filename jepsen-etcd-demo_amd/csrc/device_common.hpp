@@ -68,10 +68,12 @@ __device__ __forceinline__ void write_final_narrow(const Args &a, int32_t key, c
     if (lane_id() == 0 && a.n_final) a.n_final[key] = nf;
 }
 
-__device__ __forceinline__ void push_list(int32_t *list, int32_t *count, int32_t key) {
+// Append key to a work list of `cap` entries (a list holds each key of a
+// step at most once, and cap >= the step's keys; the bound is a guard).
+__device__ __forceinline__ void push_list(int32_t *list, int32_t *count, int32_t key, int32_t cap) {
     if (lane_id() == 0) {
         int32_t i = atomicAdd(count, 1);
-        list[i] = key;
+        if (i < cap) list[i] = key;
     }
 }
 

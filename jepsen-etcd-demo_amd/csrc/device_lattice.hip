@@ -39,6 +39,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "../../include/lincheck.h"
@@ -175,6 +176,11 @@ using Lat = uint32_t[T0_RBIG];
 // T0's kernel arguments: only what the event loop reads, so the loop keeps
 // its scalar registers (the full Args would spill SGPRs into VGPR lanes).
 constexpr uint32_t T0_COUNT = 1, T0_WANT_PEAK = 2, T0_DBG_NOEVENTS = 4, T0_DBG_NOFINAL = 8, T0_WANT_FINAL = 16;
+// T0_STRICT: the host skipped its per-event validation (a T0-only step: every
+// key declared to fit the lattice).  T0 then checks the event stream itself
+// as it walks it, and a key that would leave T0 is an error, not a spill (no
+// later tier is launched to take it).
+constexpr uint32_t T0_STRICT = 32;
 struct T0Args {
     const uint64_t *ev_off;
     const uint32_t *events;
@@ -185,13 +191,23 @@ struct T0Args {
     const uint8_t *key_error;    // may be null
     const int32_t *order;
     int32_t *ticket;
+    int32_t *err;                // [0] LC_BATCH_E_* bits, [1] 1 + largest malformed key
     uint32_t *lat_ws;            // unused (the 9-10-pending workspace is in LDS)
     const Args *full;            // device copy: results, counters, spill list
     uint64_t budget;
     int32_t n_order;
     uint32_t init_state, shared_states, flags;
+    uint32_t n_trans;            // entries of trans[]
+    uint32_t n_val;              // validation blocks at the front of the grid (T0_STRICT), else 0
     uint32_t ticket_base;        // ticket value this launch starts from (see launch_t0)
 };
+
+__device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint32_t why) {
+    if (lane_id() == 0) {
+        atomicOr(&a.err[0], (int32_t)why);
+        atomicMax(&a.err[1], key + 1);
+    }
+}
 
 // Transfer masks of one event: vk[q] = op q's accept mask on lanes with bit
 // q (0 elsewhere and for q = p); sc[q] / sb[q] = op q's cap / shift.
@@ -665,8 +681,20 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     const bool want_peak = !FAST && (a.flags & T0_WANT_PEAK) != 0;
     const bool count = !FAST && (a.flags & T0_COUNT) != 0;
     const uint32_t *const evp = a.events + eb;
-    const uint32_t *const trp = a.trans + tb;
+    // The key may name transitions trans[tb + t], t < ntr.  A batch the host
+    // did not validate may hold larger ids: they load nothing (the event is
+    // then a read of nil), and the batch's validation waves report them.
+    // Every other malformation (an :ok of a slot that is not pending, an
+    // :invoke into an occupied one) leaves T0 in bounds -- indices stay below
+    // T0_MAX_WIDTH and lanes below 64 -- with a verdict the failed call
+    // does not return.
+    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
+    const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
     const uint32_t nev = (a.flags & T0_DBG_NOEVENTS) ? 0u : (uint32_t)(ee - eb);
+    auto ldesc = [&](uint32_t w, bool have) -> uint32_t {
+        const uint32_t t = LC_EV_TRANS(w);
+        return (have && !(w & LC_EV_OK_BIT) && t < ntr) ? trp[t] : 0u;
+    };
 
     uint32_t W[RM];
 #pragma unroll
@@ -688,9 +716,9 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     // Event cursor: events arrive 64 at a time, one per lane; the next
     // chunk's words and descriptors are in flight while this one is searched.
     uint32_t ev = lane < nev ? evp[lane] : 0u;
-    uint32_t dsc = (lane < nev && !(ev & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev)] : 0u;
+    uint32_t dsc = ldesc(ev, lane < nev);
     uint32_t ev_n = 64 + lane < nev ? evp[64 + lane] : 0u;
-    uint32_t dsc_n = (64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
+    uint32_t dsc_n = ldesc(ev_n, 64 + lane < nev);
     uint32_t ev_nn = 128 + lane < nev ? evp[128 + lane] : 0u;
     // each lane decodes its event's transition once per chunk (VALU, all 64
     // at a time), so an invoke only reads three lanes
@@ -703,7 +731,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
             i = 0; base += 64;
             ev = ev_n; dsc = dsc_n; ev_n = ev_nn;
             xc = xfer_of(dsc);
-            dsc_n = (base + 64 + lane < nev && !(ev_n & LC_EV_OK_BIT)) ? trp[LC_EV_TRANS(ev_n)] : 0u;
+            dsc_n = ldesc(ev_n, base + 64 + lane < nev);
             ev_nn = base + 128 + lane < nev ? evp[base + 128 + lane] : 0u;
         }
     };
@@ -754,7 +782,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                     dirty = true;
                 }
             } else {
-                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
                 uint32_t nSn = 0;
 #if defined(LC_ABL_NOOK) || defined(LC_ABL_NOOKALL)
                 const int r = 0;  // ablation build: bookkeeping only
@@ -836,7 +864,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                     ++n;
                 }
             } else {
-                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot);
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
                 uint32_t nSn = 0;
                 int r;
 #ifdef LC_ABL_NOOKALL
@@ -893,6 +921,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     // per-key epilogue (results through `full`); on a failure W / live still
     // hold the set before the failing event, which is what is reported
     const Args &f = *a.full;
+
     if (!in_mem) {
 #pragma unroll
         for (int k = 0; k < RM; ++k) m.W[k * 64 + lane] = W[k];
@@ -915,9 +944,65 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 __device__ unsigned long long lc_t0_stamps[8192 * 6];
 #endif
 
+// Validation waves (T0_STRICT launches: the host skipped its per-event pass).
+// The first n_val blocks of the launch check every key of the batch, one key
+// per lane, each walking its key's events in order: an :ok must name a
+// pending slot, an :invoke a free slot below 64, a transition id must be in
+// range and install only states the key has.  Violations set the batch's
+// error words (the call then returns LC_E_INVALID).  Eight event words, then
+// their descriptors, are loaded at a time, so a lane keeps loads in flight;
+// the whole pass is a small fraction of the search's time and runs beside it.
+__device__ void validate_keys(const T0Args &a, uint32_t vb, uint32_t n_val) {
+    const uint32_t lane = lane_id();
+    constexpr int G = 8;
+    for (int64_t k = (int64_t)vb * 64 + lane; k < a.n_order; k += (int64_t)n_val * 64) {
+        if (a.key_error && a.key_error[k]) continue;
+        const uint64_t eb = a.ev_off[k], ee = a.ev_off[k + 1];
+        const uint32_t tb = a.trans_off ? a.trans_off[k] : 0u;
+        const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
+        const uint32_t ns = a.trans_off ? (a.key_states ? a.key_states[k] : 0u) : a.shared_states;
+        uint64_t pend = 0;
+        int32_t why = 0;
+        for (uint64_t j = eb; j < ee && !why; j += G) {
+            uint32_t w[G], d[G];
+#pragma unroll
+            for (int i = 0; i < G; ++i) w[i] = j + i < ee ? a.events[j + i] : LC_EV_OK_BIT | (127u << 24);
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                const uint32_t t = LC_EV_TRANS(w[i]);
+                d[i] = (!(w[i] & LC_EV_OK_BIT) && t < ntr) ? a.trans[tb + t] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                if (why || j + i >= ee) break;
+                const uint32_t s = LC_EV_SLOT(w[i]);
+                if (s >= 64) { why = LC_BATCH_E_FIT; break; }
+                const uint64_t bit = 1ull << s;
+                if (w[i] & LC_EV_OK_BIT) {
+                    if (!(pend & bit)) why = LC_BATCH_E_SLOTS;
+                    pend &= ~bit;
+                } else {
+                    if (LC_EV_TRANS(w[i]) >= ntr || ((d[i] & 3u) >= LC_T_WRITE && (d[i] >> 17) >= ns))
+                        why = LC_BATCH_E_TRANS;
+                    else if (pend & bit) why = LC_BATCH_E_SLOTS;
+                    pend |= bit;
+                }
+            }
+        }
+        if (why) {
+            atomicOr(&a.err[0], why);
+            atomicMax(&a.err[1], (int32_t)k + 1);
+        }
+    }
+}
+
 template <int RM>
 __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
     __shared__ uint32_t ws[3 * T0_RMEM * 64];  // lattices of 9-10 pending ops (12 KB)
+    if (blockIdx.x < a.n_val) {  // T0_STRICT launches: the validation waves come first
+        validate_keys(a, blockIdx.x, a.n_val);
+        return;
+    }
 #ifdef LC_T0_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     uint32_t nkeys = 0, lastkey = 0;
@@ -935,8 +1020,13 @@ __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
         const int kr = fast ? lattice_key<RM, true>(a, key, ws) : lattice_key<RM, false>(a, key, ws);
         if (kr == K_SPILL) {
             const Args &f = *a.full;
-            const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
-            push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key);
+            if (a.flags & T0_STRICT) {  // declared to fit T0, and it does not: no later tier runs
+                t0_malformed(a, key, LC_BATCH_E_FIT);
+                finish_key(f, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+            } else {
+                const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
+                push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key, f.list_cap);
+            }
         }
 #ifdef LC_T0_STAMPS
         ++nkeys;
@@ -973,12 +1063,22 @@ hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipS
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
     t.key_width = a.key_width; t.key_states = a.key_states; t.key_error = a.key_error; t.order = a.order;
     t.ticket = a.ticket;
+    t.err = a.err;
+    t.n_trans = a.n_trans;
+    // a batch the host did not validate: validation waves first (one lane per
+    // key, at most 4 per CU's worth), search blocks after
+    t.n_val = a.strict ? (uint32_t)std::min<int64_t>((a.n_order + 63) / 64, 1024) : 0u;
+#ifdef LC_T0_NO_VALIDATE  // A/B diagnostic build only: no validation waves
+    t.n_val = 0;
+#endif
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
     t.init_state = a.init_state; t.shared_states = a.shared_states; t.ticket_base = ticket_base;
     t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) | (a.final_cfg ? T0_WANT_FINAL : 0u) |
-              (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u);
-    if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(grid), dim3(64), 0, s, t);
-    else hipLaunchKernelGGL(k_search_lattice<T0_RSMALL>, dim3(grid), dim3(64), 0, s, t);
+              (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u) |
+              (a.strict ? T0_STRICT : 0u);
+    const int g = grid + (int)t.n_val;
+    if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(g), dim3(64), 0, s, t);
+    else hipLaunchKernelGGL(k_search_lattice<T0_RSMALL>, dim3(g), dim3(64), 0, s, t);
     return hipGetLastError();
 }
 

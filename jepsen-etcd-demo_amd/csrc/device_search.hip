@@ -231,13 +231,13 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
 template <int CAP_S, int CAP_I>
 __global__ __launch_bounds__(64) void k_search_lds(Args a) {
     __shared__ LdsTier<CAP_S, CAP_I> t;
-    const int32_t n = a.n_in ? *a.n_in : a.n_order;
+    const int32_t n = a.n_in ? min(*a.n_in, a.list_cap) : a.n_order;
     if (n == 0) return;  // empty work list: no ticket traffic
     for (int32_t w = next_work(a); w < n; w = next_work(a)) {
         const int32_t key = a.order[w];
         const int r = search_key_lds<CAP_S, CAP_I>(a, key, t);
-        if (r == K_SPILL) push_list(a.spill, a.n_spill, key);
-        else if (r == K_WIDE) push_list(a.wide, a.n_wide, key);
+        if (r == K_SPILL) push_list(a.spill, a.n_spill, key, a.list_cap);
+        else if (r == K_WIDE) push_list(a.wide, a.n_wide, key, a.list_cap);
         __syncthreads();
     }
 }

@@ -29,6 +29,9 @@ struct Args {
     int32_t n_order;
     const int32_t *n_in;
     int32_t *ticket;         // zeroed before the launch
+    int32_t *err;            // T0: [0] LC_BATCH_E_* bits, [1] 1 + largest malformed key
+    uint32_t n_trans;        // entries of trans[]
+    int32_t strict;          // T0: the host did not validate the events (T0_STRICT)
     // per-key results (device pointers)
     int8_t *valid;
     int32_t *fail_event;
@@ -51,7 +54,13 @@ struct Args {
     // routing, not semantics) and go straight to the HBM tier's list
     int32_t *deep;
     int32_t *n_deep;
+    int32_t list_cap;        // entries of each work list above
 };
+
+// Malformed-batch reasons T0 reports when it validates a batch itself.
+constexpr int32_t LC_BATCH_E_SLOTS = 1;  // :ok of a slot with no pending op / :invoke into an occupied slot
+constexpr int32_t LC_BATCH_E_TRANS = 2;  // transition id out of range / installs a state the key lacks
+constexpr int32_t LC_BATCH_E_FIT = 4;    // a key declared to fit T0 (width, states) does not
 
 // Ops pending at once above which a key leaving T0 goes straight to T3.
 constexpr uint32_t LC_DIRECT_T3_WIDTH = 28;

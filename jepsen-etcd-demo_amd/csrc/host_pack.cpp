@@ -175,8 +175,8 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
 
 struct lc_packed {
     std::vector<int64_t> keys;
-    std::vector<uint64_t> ev_off;
-    std::vector<uint32_t> events;
+    lc::pinned_vector<uint64_t> ev_off;  // page-locked on a GPU host: lc_check_* DMA it directly
+    lc::pinned_vector<uint32_t> events;
     std::vector<int64_t> ev_row;
     std::vector<uint32_t> trans;
     std::vector<uint32_t> trans_off;  // empty = shared table

@@ -17,7 +17,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 5
+LC_ABI_VERSION = 6
+LC_MAX_DEVICES = 8
+LC_COMM_ID_BYTES = 128
 LC_OPT_COUNT_PROBES = 0x1
 LC_DEV_RESULT, LC_DEV_ASYNC = 1, 2
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
@@ -60,7 +62,10 @@ class LcPackOpts(C.Structure):
 class LcOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("algorithm", C.c_int32), ("max_configs", C.c_uint64),
                 ("max_final", C.c_int32), ("lds_configs", C.c_int32), ("deep_slots", C.c_int32),
-                ("flags", C.c_int32), ("debug_mode", C.c_int32), ("reserved", C.c_int32 * 4)]
+                ("flags", C.c_int32), ("debug_mode", C.c_int32),
+                ("n_devices", C.c_int32), ("devices", C.c_int32 * LC_MAX_DEVICES),
+                ("comm_rank", C.c_int32), ("comm_size", C.c_int32), ("comm_id", C.c_uint8 * LC_COMM_ID_BYTES),
+                ("reserved", C.c_int32 * 4)]
 
 
 class LcResult(C.Structure):
@@ -98,6 +103,10 @@ SIGNATURES = {
     "lc_check_device": (C.c_int, [C.c_void_p, C.c_void_p, P(LcResult), C.c_int, P(LcStats)]),
     "lc_wait": (C.c_int, [C.c_void_p, P(LcStats)]),
     "lc_wait_step": (C.c_int, [C.c_void_p, C.c_int]),
+    "lc_comm_id": (C.c_int, [P(C.c_uint8)]),
+    "lc_check_node": (C.c_int, [C.c_void_p, P(LcBatch), C.c_int64, P(C.c_uint64), P(LcStats)]),
+    "lc_check_node_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, P(LcStats)]),
+    "lc_node_records": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int64]),
     "lc_pack": (C.c_int, [P(LcHistory), P(LcPackOpts), P(C.c_void_p)]),
     "lc_packed_free": (None, [C.c_void_p]),
     "lc_packed_view": (C.c_int, [C.c_void_p, P(LcBatch)]),

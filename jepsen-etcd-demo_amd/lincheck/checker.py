@@ -101,19 +101,38 @@ class KeyResults:
     stats: Dict[str, float]
 
 
+def comm_id() -> bytes:
+    """lc_comm_id: a fresh RCCL unique id (rank 0 hands it to every rank)."""
+    buf = (C.c_uint8 * N.LC_COMM_ID_BYTES)()
+    N.check(N.lib().lc_comm_id(buf))
+    return bytes(buf)
+
+
 class Device:
-    """An lc_ctx on one GPU (lc_create)."""
+    """An lc_ctx (lc_create) on one GPU, on several (devices=[...]: one
+    contiguous key shard per entry, checked at once), or as one rank of a
+    multi-process node (comm=(rank, size, comm_id bytes): lc_check_node
+    all-gathers the verdict records over RCCL)."""
 
     def __init__(self, device: int = 0, budget: int = DEFAULT_BUDGET, max_final: int = TRUNCATE,
-                 debug_mode: int = 0, count_probes: bool = False, algorithm: int = N.LC_ALGO_LINEAR):
+                 debug_mode: int = 0, count_probes: bool = False, algorithm: int = N.LC_ALGO_LINEAR,
+                 devices: Optional[Sequence[int]] = None, comm: Optional[tuple] = None):
         o = N.LcOpts()
         o.device, o.algorithm, o.max_configs, o.max_final = device, algorithm, budget, max_final
         o.flags = N.LC_OPT_COUNT_PROBES if count_probes else 0
         o.debug_mode = debug_mode  # ablation builds only; 0 = the real search
+        if devices is not None and len(devices) > 1:
+            o.n_devices = len(devices)
+            for g, d in enumerate(devices):
+                o.devices[g] = d
+        if comm is not None:
+            o.comm_rank, o.comm_size = comm[0], comm[1]
+            C.memmove(o.comm_id, comm[2], N.LC_COMM_ID_BYTES)
         h = C.c_void_p()
         N.check(N.lib().lc_create(C.byref(o), C.byref(h)))
         self.handle, self.device, self.budget, self.max_final = h, device, budget, max_final
         self.count_probes = count_probes
+        self.world = comm[1] if comm is not None and comm[1] > 1 else 1
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -149,6 +168,22 @@ class Device:
         st = N.LcStats()
         N.check(N.lib().lc_check_batch(self.handle, C.byref(packed.view), C.byref(r), C.byref(st)))
         return self._results(arrs, K, st)
+
+    def check_node(self, packed: Packed, block: int, out: Optional[np.ndarray] = None):
+        """lc_check_node: this rank's shard from host SoA to the node's verdict
+        records (block per rank, all-gathered).  Returns (records, stats)."""
+        n = block * self.world
+        if out is None or out.size < n:
+            out = np.zeros(max(n, 1), np.uint64)
+        st = N.LcStats()
+        N.check(N.lib().lc_check_node(self.handle, C.byref(packed.view), block, N.ptr(out, C.c_uint64), C.byref(st)))
+        return out[:n], st
+
+    def node_records(self, n: int) -> np.ndarray:
+        """lc_node_records: the first n records of the last gather."""
+        out = np.zeros(max(n, 1), np.uint64)
+        N.check(N.lib().lc_node_records(self.handle, N.ptr(out, C.c_uint64), n))
+        return out[:n]
 
     def wait(self):
         """lc_wait: (number of asynchronous steps since the last wait, their
@@ -189,6 +224,14 @@ class DevBatch:
             r = N.LcResult(r.valid, r.fail_event, r.cause, None, r.final_configs, r.n_final)
         N.check(N.lib().lc_check_device(self.dev.handle, self.handle, C.byref(r), 0, C.byref(st)))
         return self.dev._results({k: v.copy() for k, v in self.arrs.items()}, self.n_keys, st)
+
+    def check_node(self, block: int, asynchronous: bool = False) -> N.LcStats:
+        """lc_check_node_device: search the resident shard and all-gather the
+        node's verdict records (left in HBM; Device.node_records reads them)."""
+        st = N.LcStats()
+        N.check(N.lib().lc_check_node_device(self.dev.handle, self.handle, block,
+                                             N.LC_DEV_ASYNC if asynchronous else 0, C.byref(st)))
+        return st
 
     def check_into(self, r: N.LcResult, asynchronous: bool = False) -> N.LcStats:
         """Search with results written to caller-provided DEVICE arrays (no D2H).

@@ -1,0 +1,258 @@
+"""Multi-device contexts, node-wide verdict records and batches T0 validates.
+
+* independent/checker's pmap over a node's
+  GPUs (etcdemo.clj:115).  A context over several devices checks contiguous
+  key shards at once; on this one-GPU box the shards are logical (devices
+  [0, 0] and [0, 0, 0]: one stream and scratch per shard on the same card),
+  and every result array must equal the one-shard check bit for bit.
+* lc_check_node: a rank's shard -> verdict records all-gathered over the
+  node.  One rank here, with and without a (one-rank) RCCL communicator:
+  the decoded records must equal lc_check_batch's verdicts.
+* A batch whose keys all fit the register tier is validated by T0 while it
+  walks the events: each malformation is refused (LC_E_INVALID naming the
+  key) on the host-to-host, resident and asynchronous paths, and the
+  context keeps working.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import cref
+from helpers import device_vs_oracle
+from lincheck import _native as N
+from lincheck import history as H
+from lincheck import parallel as P
+from lincheck.checker import Device, Packed, comm_id
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {
+    # register tier only (T0-validated batches)
+    "c5": dict(n_keys=300, ops_per_key=400, concurrency=10, anomaly_rate=0.1, seed=71),
+    # keys leave T0 (host-validated; T1-T3 run)
+    "crashed": dict(n_keys=24, ops_per_key=500, concurrency=14, info_rate=0.01, anomaly_rate=0.2, seed=72),
+}
+
+
+def _same(a, b, max_final=10):
+    for f in ("valid", "fail_event", "cause", "peak", "n_final"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    for i in range(len(a.valid)):
+        n = int(a.n_final[i])
+        if n < max_final:  # the whole final set: equal as a set (hash tiers append in any order)
+            sa = sorted(map(tuple, a.final[i, :n].tolist()))
+            sb = sorted(map(tuple, b.final[i, :n].tolist()))
+            assert sa == sb, f"final configs of key {i}"
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_logical_shards_bit_exact(shape, devices):
+    h = H.synth(**SHAPES[shape])
+    pk = Packed(h)
+    one = Device(0).check(pk)
+    multi = Device(0, devices=devices)
+    _same(multi.check(pk), one)
+    _same(multi.upload(pk).check(), one)  # resident shards, host results
+    _, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)
+    np.testing.assert_array_equal(one.valid, orc["valid"])
+    np.testing.assert_array_equal(one.fail_event, orc["fail_event"])
+
+
+def test_logical_shards_more_than_keys():
+    """Three shards over two keys: a shard with no keys is a no-op."""
+    h = H.synth(n_keys=2, ops_per_key=300, concurrency=8, anomaly_rate=0.5, seed=73)
+    dev = Device(0, devices=[0, 0, 0])
+    device_vs_oracle(h, dev)
+
+
+def _decode(rec, K):
+    v, c, fe = P.unpack_records(rec.astype(np.int64))
+    return v[:K], c[:K], fe[:K]
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("rccl", [False, True])
+def test_node_records_one_rank(shape, rccl):
+    h = H.synth(**SHAPES[shape])
+    pk = Packed(h)
+    K = pk.n_keys
+    ref = Device(0).check(pk)
+    dev = Device(0, comm=(0, 1, comm_id()) if rccl else None)
+    block = K + 7  # padded block: the padding records are 0
+    rec, _ = dev.check_node(pk, block)
+    assert rec.size == block and not rec[K:].any()
+    v, c, fe = _decode(rec, K)
+    np.testing.assert_array_equal(v, ref.valid)
+    np.testing.assert_array_equal(c, ref.cause)
+    np.testing.assert_array_equal(fe, ref.fail_event)
+    # resident shard: synchronous, then asynchronous steps + lc_wait
+    db = dev.upload(pk)
+    db.check_node(block)
+    np.testing.assert_array_equal(dev.node_records(block), rec)
+    for _ in range(3):
+        db.check_node(block, asynchronous=True)
+    dev.wait()
+    np.testing.assert_array_equal(dev.node_records(block), rec)
+
+
+def test_node_block_too_small():
+    pk = Packed(H.synth(n_keys=10, ops_per_key=50, concurrency=4, seed=74))
+    with pytest.raises(N.LincheckError) as ei:
+        Device(0).check_node(pk, 9)
+    assert ei.value.code == -1
+
+
+def _batch_copy(pk):
+    """Writable copies of a packed batch's arrays (the caller-built batch of
+    include/lincheck.h: events, offsets, widths) and an lc_batch over them."""
+    K = pk.n_keys
+    n_ev = int(pk.ev_off[-1])
+    arrs = dict(ev_off=pk.ev_off.copy(),
+                events=np.ctypeslib.as_array(pk.view.events, shape=(n_ev,)).copy(),
+                trans=np.ctypeslib.as_array(pk.view.trans, shape=(int(pk.view.n_trans),)).copy(),
+                width=np.ctypeslib.as_array(pk.view.key_width, shape=(K,)).copy(),
+                states=np.ctypeslib.as_array(pk.view.key_states, shape=(K,)).copy())
+    b = N.LcBatch()
+    b.n_keys = K
+    b.ev_off = N.ptr(arrs["ev_off"], C.c_uint64)
+    b.events = N.ptr(arrs["events"], C.c_uint32)
+    b.trans = N.ptr(arrs["trans"], C.c_uint32)
+    b.n_trans = int(pk.view.n_trans)
+    b.key_width = N.ptr(arrs["width"], C.c_uint8)
+    b.key_states = N.ptr(arrs["states"], C.c_uint16)
+    return arrs, b
+
+
+def _check_batch(dev, b, K):
+    arrs, r = dev._alloc(K)
+    st = N.LcStats()
+    N.check(N.lib().lc_check_batch(dev.handle, C.byref(b), C.byref(r), C.byref(st)))
+    return arrs
+
+
+def _expect_invalid(dev, b, K, key):
+    with pytest.raises(N.LincheckError) as ei:
+        _check_batch(dev, b, K)
+    assert ei.value.code == -1 and f"key {key}" in str(ei.value), str(ei.value)
+    h = C.c_void_p()
+    N.check(N.lib().lc_upload(dev.handle, C.byref(b), C.byref(h)))  # T0-validated: uploads as it is
+    try:
+        valid, fe, cause = (np.zeros(K, np.int8), np.zeros(K, np.int32), np.zeros(K, np.uint8))
+        r = N.LcResult(N.ptr(valid, C.c_int8), N.ptr(fe, C.c_int32), N.ptr(cause, C.c_uint8), None, None, None)
+        st = N.LcStats()
+        with pytest.raises(N.LincheckError) as ei:
+            N.check(N.lib().lc_check_device(dev.handle, h, C.byref(r), 0, C.byref(st)))
+        assert f"key {key}" in str(ei.value)  # (the result arrays of a refused call are unspecified)
+    finally:
+        N.lib().lc_dev_batch_free(h)
+
+
+def test_t0_validates_events():
+    """Every per-event malformation T0 checks, one at a time, on a batch of
+    register-tier keys; after each refusal the same context checks the good
+    batch bit-exactly."""
+    h = H.synth(n_keys=300, ops_per_key=200, concurrency=6, anomaly_rate=0.1, seed=75)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0)
+    arrs, b = _batch_copy(pk)
+    ev = arrs["events"]
+    good = _check_batch(dev, b, K)
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    np.testing.assert_array_equal(good["valid"][:K], orc["valid"])
+
+    def at(key, pred):
+        lo, hi = int(pk.ev_off[key]), int(pk.ev_off[key + 1])
+        return lo + int(np.flatnonzero(pred(ev[lo:hi]))[0])
+
+    cases = []
+    # an :ok of a slot with no pending op (the key's first event made an :ok)
+    cases.append((211, at(211, lambda e: np.ones(len(e), bool)), lambda w: w | N.LC_EV_OK_BIT))
+    # an :invoke into an occupied slot (the key's first :ok made an invoke)
+    cases.append((57, at(57, lambda e: (e & N.LC_EV_OK_BIT) != 0), lambda w: (w & 0x7F000000)))
+    # a transition id beyond the table
+    cases.append((123, at(123, lambda e: (e & N.LC_EV_OK_BIT) == 0), lambda w: (w & 0xFF000000) | 0xFFFFF))
+    # an :invoke in a slot >= 64 (a key declared to fit T0 cannot hold it)
+    cases.append((290, at(290, lambda e: (e & N.LC_EV_OK_BIT) == 0), lambda w: (w & 0x80FFFFFF) | (70 << 24)))
+    for key, j, mutate in cases:
+        saved = int(ev[j])
+        ev[j] = mutate(saved)
+        _expect_invalid(dev, b, K, key)
+        ev[j] = saved
+        again = _check_batch(dev, b, K)
+        np.testing.assert_array_equal(again["valid"][:K], good["valid"][:K])
+        np.testing.assert_array_equal(again["fail_event"][:K], good["fail_event"][:K])
+
+
+def test_t0_refuses_understated_width():
+    """key_width claims fewer ops pending at once than a key has: the batch is
+    declared register-tier-only, T0 meets the 11th pending op, and the key is
+    refused instead of being spilled to a tier that is never launched."""
+    h = H.synth(n_keys=40, ops_per_key=400, concurrency=14, seed=76)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0)
+    arrs, b = _batch_copy(pk)
+    wide = np.flatnonzero(arrs["width"] > 10)
+    assert wide.size > 0
+    arrs["width"][:] = np.minimum(arrs["width"], 10)
+    with pytest.raises(N.LincheckError) as ei:
+        _check_batch(dev, b, K)
+    assert ei.value.code == -1 and "understate" in str(ei.value)
+    device_vs_oracle(h, dev)
+
+
+def test_async_errors_surface_at_wait():
+    """An asynchronous resident step over a malformed T0-validated batch:
+    the refusal comes from lc_wait."""
+    h = H.synth(n_keys=300, ops_per_key=200, concurrency=6, seed=77)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0)
+    arrs, b = _batch_copy(pk)
+    j = int(pk.ev_off[99])
+    arrs["events"][j] |= N.LC_EV_OK_BIT
+    h_db = C.c_void_p()
+    N.check(N.lib().lc_upload(dev.handle, C.byref(b), C.byref(h_db)))
+    try:
+        st = N.LcStats()
+        N.check(N.lib().lc_check_node_device(dev.handle, h_db, K, N.LC_DEV_ASYNC, C.byref(st)))
+        with pytest.raises(N.LincheckError) as ei:
+            dev.wait()
+        assert "key 99" in str(ei.value)
+    finally:
+        N.lib().lc_dev_batch_free(h_db)
+    device_vs_oracle(h, dev)
+
+
+def test_wait_step_waits_for_the_step_asked():
+    """lc_wait_step(1) returns once the step before the latest is done: step
+    A's records (one node buffer per step would be overwritten, so A and B
+    write different result arrays) are final while B may still run."""
+    from test_gpu_parity import _HipBuf
+    dev = Device(0)
+    hA = H.synth(n_keys=500, ops_per_key=600, concurrency=10, anomaly_rate=0.1, seed=78)
+    hB = H.synth(n_keys=500, ops_per_key=600, concurrency=10, anomaly_rate=0.1, seed=79)
+    outs = []
+    for h in (hA, hB):
+        pk = Packed(h)
+        K = pk.n_keys
+        bufs = (_HipBuf(K), _HipBuf(4 * K), _HipBuf(K))
+        for x in bufs:
+            x.fill(0x5A)
+        r = N.LcResult(C.cast(bufs[0].ptr, N.P(C.c_int8)), C.cast(bufs[1].ptr, N.P(C.c_int32)),
+                       C.cast(bufs[2].ptr, N.P(C.c_uint8)), None, None, None)
+        outs.append((h, dev.upload(pk), bufs, r))
+    dev.wait()
+    for _, db, _, r in outs:
+        db.check_into(r, asynchronous=True)
+    dev.wait_step(1)
+    _, orcA = cref.check_history(hA.as_c(), budget=dev.budget, threads=8)
+    np.testing.assert_array_equal(outs[0][2][0].get(np.int8), orcA["valid"])
+    np.testing.assert_array_equal(outs[0][2][1].get(np.int32), orcA["fail_event"])
+    n, _ = dev.wait()
+    assert n == 2
+    _, orcB = cref.check_history(hB.as_c(), budget=dev.budget, threads=8)
+    np.testing.assert_array_equal(outs[1][2][0].get(np.int8), orcB["valid"])

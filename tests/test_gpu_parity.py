@@ -343,9 +343,10 @@ def test_check_batch_staging_reuse():
 
 def test_malformed_batch_rejected_then_context_reusable():
     """A batch whose event stream breaks the pairing invariants is refused with
-    LC_E_INVALID and a message naming the key -- lc_check_batch validates the
-    events beside its uploads and launches nothing -- and the same context
-    then checks a good batch bit-exactly."""
+    LC_E_INVALID and a message naming the key, and the same context then checks
+    a good batch bit-exactly.  Every key of this batch fits the register tier,
+    so the events are checked by T0 as it walks them (T0_STRICT), on both the
+    host-to-host and the resident path."""
     import ctypes as C
     from lincheck import _native as N
     from lincheck.checker import Packed
@@ -361,8 +362,10 @@ def test_malformed_batch_rejected_then_context_reusable():
     with pytest.raises(N.LincheckError) as ei:
         dev.check(pk)
     assert ei.value.code == -1 and "key 317" in str(ei.value)
-    with pytest.raises(N.LincheckError):
-        dev.upload(pk)
+    db = dev.upload(pk)  # T0 validates this batch: the upload takes it as it is
+    with pytest.raises(N.LincheckError) as ei:
+        db.check(peak=False)
+    assert ei.value.code == -1 and "key 317" in str(ei.value)
     ev[j] = saved
     device_vs_oracle(h, dev)
 
