@@ -374,8 +374,9 @@ def main():
         for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
             try:
                 d = json.load(open(fpath))
+                tag = "lattice" if "T0" in dominant else "hbm"
                 if (d.get("workload") == args.config and d.get("bytes_per_launch")
-                        and d.get("budget", args.budget) == args.budget and d.get("kernel", dominant) == dominant):
+                        and d.get("budget", args.budget) == args.budget and tag in d.get("kernel", tag)):
                     traffic = d["bytes_per_launch"]
             except (OSError, ValueError):
                 pass

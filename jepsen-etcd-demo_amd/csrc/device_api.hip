@@ -244,6 +244,8 @@ struct Dev {
     int device = 0;
     int cu_count = 256;
     hipStream_t stream = nullptr;
+    hipStream_t vstream = nullptr;  // validation of host-unchecked batches, beside T0
+    hipEvent_t vin = nullptr, vdone = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr, et3a = nullptr, et3b = nullptr;
     hipEvent_t ea0 = nullptr, ea1 = nullptr;  // span of the LC_DEV_ASYNC steps since lc_wait
     uint32_t n_async = 0;
@@ -293,8 +295,10 @@ struct Dev {
         dfree(ws[0].base); dfree(ws[1].base); dfree(dargs); dfree(send); dfree(node);
         if (hargs) (void)hipHostFree(hargs);
         delete staged;
-        for (hipEvent_t e : {e0, e1, et0, et3a, et3b, ea0, ea1})
+        if (vstream) (void)hipStreamSynchronize(vstream);
+        for (hipEvent_t e : {e0, e1, et0, et3a, et3b, ea0, ea1, vin, vdone})
             if (e) (void)hipEventDestroy(e);
+        if (vstream) (void)hipStreamDestroy(vstream);
         for (hipEvent_t &e : ring)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -402,6 +406,9 @@ static int dev_init(Dev *c, int device) {
     c->cu_count = prop.multiProcessorCount;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->vstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->vin, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->vdone, hipEventDisableTiming));
     for (hipEvent_t *e : {&c->e0, &c->e1, &c->et0, &c->et3a, &c->et3b, &c->ea0, &c->ea1}) HIPCHK(hipEventCreate(e));
     for (hipEvent_t &e : c->ring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(dalloc(&c->ctl, 16));
@@ -816,10 +823,21 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     }
     HIPCHK(hipEventRecord(c->e0, c->stream));
     if (async && c->n_async == 0) HIPCHK(hipEventRecord(c->ea0, c->stream));
+    if (K > 0 && a.strict) {
+        // the event-by-event validation the host skipped: on the second
+        // stream, beside T0, joined before the step's results are read
+        HIPCHK(hipEventRecord(c->vin, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->vstream, c->vin, 0));
+        lcd::Args av = a;
+        av.n_order = (int32_t)K;
+        HIPCHK(lcd::launch_validate(av, c->vstream));
+        HIPCHK(hipEventRecord(c->vdone, c->vstream));
+    }
     if (K > 0) {
         HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
     }
+    if (K > 0 && a.strict) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));
     if (async) {
         HIPCHK(hipEventRecord(c->ea1, c->stream));
         HIPCHK(hipEventRecord(c->ring[c->async_seq % 4], c->stream));

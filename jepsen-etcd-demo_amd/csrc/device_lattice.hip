@@ -198,7 +198,6 @@ struct T0Args {
     int32_t n_order;
     uint32_t init_state, shared_states, flags;
     uint32_t n_trans;            // entries of trans[]
-    uint32_t n_val;              // validation blocks at the front of the grid (T0_STRICT), else 0
     uint32_t ticket_base;        // ticket value this launch starts from (see launch_t0)
 };
 
@@ -944,18 +943,18 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 __device__ unsigned long long lc_t0_stamps[8192 * 6];
 #endif
 
-// Validation waves (T0_STRICT launches: the host skipped its per-event pass).
-// The first n_val blocks of the launch check every key of the batch, one key
-// per lane, each walking its key's events in order: an :ok must name a
-// pending slot, an :invoke a free slot below 64, a transition id must be in
-// range and install only states the key has.  Violations set the batch's
-// error words (the call then returns LC_E_INVALID).  Eight event words, then
-// their descriptors, are loaded at a time, so a lane keeps loads in flight;
-// the whole pass is a small fraction of the search's time and runs beside it.
-__device__ void validate_keys(const T0Args &a, uint32_t vb, uint32_t n_val) {
+// Validation of a batch the host did not check event by event (T0_STRICT
+// steps): a kernel of its own on a second stream, running beside T0 (which
+// stays in bounds on any input).  One key per lane, each walking its key's
+// events in order: an :ok must name a pending slot, an :invoke a free slot
+// below 64, a transition id must be in range and install only states the
+// key has.  Violations set the batch's error words (the call then returns
+// LC_E_INVALID).  Eight event words, then their descriptors, are loaded at a
+// time, so a lane keeps loads in flight.
+__global__ __launch_bounds__(64) void k_validate(T0Args a) {
     const uint32_t lane = lane_id();
     constexpr int G = 8;
-    for (int64_t k = (int64_t)vb * 64 + lane; k < a.n_order; k += (int64_t)n_val * 64) {
+    for (int64_t k = (int64_t)blockIdx.x * 64 + lane; k < a.n_order; k += (int64_t)gridDim.x * 64) {
         if (a.key_error && a.key_error[k]) continue;
         const uint64_t eb = a.ev_off[k], ee = a.ev_off[k + 1];
         const uint32_t tb = a.trans_off ? a.trans_off[k] : 0u;
@@ -966,7 +965,7 @@ __device__ void validate_keys(const T0Args &a, uint32_t vb, uint32_t n_val) {
         for (uint64_t j = eb; j < ee && !why; j += G) {
             uint32_t w[G], d[G];
 #pragma unroll
-            for (int i = 0; i < G; ++i) w[i] = j + i < ee ? a.events[j + i] : LC_EV_OK_BIT | (127u << 24);
+            for (int i = 0; i < G; ++i) w[i] = j + i < ee ? a.events[j + i] : LC_EV_OK_BIT;  // past the end: no-op
 #pragma unroll
             for (int i = 0; i < G; ++i) {
                 const uint32_t t = LC_EV_TRANS(w[i]);
@@ -974,19 +973,18 @@ __device__ void validate_keys(const T0Args &a, uint32_t vb, uint32_t n_val) {
             }
 #pragma unroll
             for (int i = 0; i < G; ++i) {
-                if (why || j + i >= ee) break;
+                const bool real = j + i < ee;
                 const uint32_t s = LC_EV_SLOT(w[i]);
-                if (s >= 64) { why = LC_BATCH_E_FIT; break; }
-                const uint64_t bit = 1ull << s;
-                if (w[i] & LC_EV_OK_BIT) {
-                    if (!(pend & bit)) why = LC_BATCH_E_SLOTS;
-                    pend &= ~bit;
-                } else {
-                    if (LC_EV_TRANS(w[i]) >= ntr || ((d[i] & 3u) >= LC_T_WRITE && (d[i] >> 17) >= ns))
-                        why = LC_BATCH_E_TRANS;
-                    else if (pend & bit) why = LC_BATCH_E_SLOTS;
-                    pend |= bit;
-                }
+                const uint64_t bit = 1ull << (s & 63u);
+                const bool ok = (w[i] & LC_EV_OK_BIT) != 0;
+                int32_t e = 0;
+                if (s >= 64) e = LC_BATCH_E_FIT;
+                else if (ok) e = (pend & bit) ? 0 : LC_BATCH_E_SLOTS;
+                else if (LC_EV_TRANS(w[i]) >= ntr || ((d[i] & 3u) >= LC_T_WRITE && (d[i] >> 17) >= ns))
+                    e = LC_BATCH_E_TRANS;
+                else e = (pend & bit) ? LC_BATCH_E_SLOTS : 0;
+                why = (real && !why) ? e : why;
+                pend = (real && !ok) ? (pend | bit) : (real ? (pend & ~bit) : pend);
             }
         }
         if (why) {
@@ -999,10 +997,7 @@ __device__ void validate_keys(const T0Args &a, uint32_t vb, uint32_t n_val) {
 template <int RM>
 __global__ __launch_bounds__(64) void k_search_lattice(T0Args a) {
     __shared__ uint32_t ws[3 * T0_RMEM * 64];  // lattices of 9-10 pending ops (12 KB)
-    if (blockIdx.x < a.n_val) {  // T0_STRICT launches: the validation waves come first
-        validate_keys(a, blockIdx.x, a.n_val);
-        return;
-    }
+
 #ifdef LC_T0_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     uint32_t nkeys = 0, lastkey = 0;
@@ -1065,20 +1060,24 @@ hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipS
     t.ticket = a.ticket;
     t.err = a.err;
     t.n_trans = a.n_trans;
-    // a batch the host did not validate: validation waves first (one lane per
-    // key, at most 4 per CU's worth), search blocks after
-    t.n_val = a.strict ? (uint32_t)std::min<int64_t>((a.n_order + 63) / 64, 1024) : 0u;
-#ifdef LC_T0_NO_VALIDATE  // A/B diagnostic build only: no validation waves
-    t.n_val = 0;
-#endif
+
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
     t.init_state = a.init_state; t.shared_states = a.shared_states; t.ticket_base = ticket_base;
     t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) | (a.final_cfg ? T0_WANT_FINAL : 0u) |
               (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u) |
               (a.strict ? T0_STRICT : 0u);
-    const int g = grid + (int)t.n_val;
-    if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(g), dim3(64), 0, s, t);
-    else hipLaunchKernelGGL(k_search_lattice<T0_RSMALL>, dim3(g), dim3(64), 0, s, t);
+    if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(grid), dim3(64), 0, s, t);
+    else hipLaunchKernelGGL(k_search_lattice<T0_RSMALL>, dim3(grid), dim3(64), 0, s, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_validate(const Args &a, hipStream_t s) {
+    T0Args t{};
+    t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
+    t.key_states = a.key_states; t.key_error = a.key_error; t.err = a.err;
+    t.n_order = a.n_order; t.shared_states = a.shared_states; t.n_trans = a.n_trans;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n_order + 63) / 64, 1024));
+    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64), 0, s, t);
     return hipGetLastError();
 }
 

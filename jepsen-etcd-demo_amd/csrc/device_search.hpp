@@ -78,6 +78,9 @@ size_t lds_bytes_t1();
 size_t lds_bytes_t2();
 hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s, uint32_t ticket_base);
 size_t lat_ws_words();
+// T0_STRICT steps: the batch's event-by-event validation (err words), a
+// kernel of its own for a second stream
+hipError_t launch_validate(const Args &a, hipStream_t s);
 uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
