@@ -202,6 +202,33 @@ int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows);
 const char *lc_packed_key_error(const lc_packed *p, int64_t i);
 /* Register value of state id s of key i (state 0 = nil -> *is_nil = 1). */
 int lc_packed_state_value(const lc_packed *p, int64_t i, uint32_t s, int64_t *value, int *is_nil);
+/* Every key at once (n_keys entries), in packed order. */
+int lc_packed_keys(const lc_packed *p, int64_t *out);
+
+/* ---- Knossos-shaped result of one key -------- */
+/* jepsen.checker/linearizable's result map (etcdemo.clj:117-118) for packed
+ * key i, from its verdict record (valid, fail_event) and the final configs
+ * the device returned for it (lc_result.final_configs + i * max_final * 2,
+ * n_final[i]).  Ops are named by history rows (positions in the lc_history
+ * given to lc_pack); an op is (invoke row, completion row or -1), from which
+ * a binding builds the op map knossos.history/complete would (the
+ * invocation, taking the completion's :value when it has none).  Model
+ * states are register values (LC_NIL for nil).  Writes int64 words:
+ *   [0] :op row (the :ok that could not be linearized) or -1
+ *   [1] :previous-ok row (= :last-op: the last :ok before it) or -1
+ *   [2] n_configs (<= max_paths)   [3] n_paths (<= max_paths)
+ *   per config: state, n_pending, n_pending x op, n_linearized, n_linearized x op
+ *   per path:   start state (the :previous-ok step's model), n_steps,
+ *               n_steps x (op, state after it), and the state in which the
+ *               failing op is inconsistent (its "can't ..." message)
+ * Paths (invalid keys only): from each final config, every sequence of
+ * further pending ops the model allows, then the failing op; depth-first,
+ * shortest first, in device config order, at most max_paths distinct ones
+ * (Knossos iterates a hash set there: only the SET is comparable).  Returns
+ * the number of words; nothing is written when that exceeds cap (call again
+ * with a larger buffer). */
+int64_t lc_report(const lc_packed *p, int64_t i, int32_t valid, int32_t fail_event, const uint64_t *final_configs,
+                  uint32_t n_final, int32_t max_paths, int64_t *out, int64_t cap);
 
 /* ---- device checking (rows A6-A9) ------------------------------------------ */
 #define LC_ALGO_LINEAR      0  /* :algorithm :linear (etcdemo.clj:118)              */

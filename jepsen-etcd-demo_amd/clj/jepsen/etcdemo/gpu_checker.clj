@@ -10,31 +10,30 @@
 
   at src/jepsen/etcdemo.clj:115-119.  The whole history goes to liblincheck.so
   in one native call (lc_pack + lc_check_batch, include/lincheck.h) through
-  JNA, which is already on the demo's classpath (jepsen.etcdemo.iml:61-62,
-  net.java.dev.jna/jna 4.1.0).  The result has independent/checker's shape:
-  {:valid? .. :results {k {:valid? .. :linear {...} :timeline {...}}}
-   :failures [k ..]}.
+  JNA direct mapping (jepsen.etcdemo.LincheckNative; JNA 4.1.0 is already on
+  the demo's classpath, jepsen.etcdemo.iml:61-62).  The result has
+  independent/checker's shape:
+    {:valid? .. :results {k {:valid? .. :linear {...} :timeline {...}}}
+     :failures [k ..]}
+  with each :linear map shaped as jepsen.checker/linearizable's: :valid?,
+  :analyzer, and for a key that is not valid :op, :previous-ok, :last-op,
+  :configs and :final-paths (truncated to 10), rendered natively by
+  lc_report -- the same rendering the Python mirror decodes.
 
   NOT EXERCISED IN THIS REPOSITORY: the build container has no JVM, no
-  Clojure and no Leiningen.  The same ABI is exercised from Python
-  (jepsen-etcd-demo_amd/lincheck/_native.py, tests/)."
+  Clojure and no Leiningen.  The same ABI and the same report decoding are
+  exercised from Python (jepsen-etcd-demo_amd/lincheck/, tests/)."
   (:require [jepsen [checker :as checker]
                     [independent :as independent]]
-            [jepsen.checker.timeline :as timeline])
-  (:import (com.sun.jna Function Memory NativeLibrary Pointer)
-           (com.sun.jna.ptr PointerByReference)))
+            [jepsen.checker.timeline :as timeline]
+            [knossos.model :as model])
+  (:import (com.sun.jna Memory Pointer)
+           (jepsen.etcdemo LincheckNative)))
 
-(def ^:private lib (delay (NativeLibrary/getInstance "lincheck")))
-
-(defn- f ^Function [name] (.getFunction ^NativeLibrary @lib name))
-
-(defn- call-int [name & args]
-  (let [rc (.invokeInt (f name) (object-array args))]
-    (when (neg? rc)
-      (throw (ex-info (str name " failed: "
-                           (.invokeString (f "lc_last_error") (object-array []) false))
-                      {:rc rc})))
-    rc))
+(defn- check-rc [rc what]
+  (when (neg? rc)
+    (throw (ex-info (str what " failed: " (LincheckNative/lc_last_error)) {:rc rc})))
+  rc)
 
 (def ^:private nil-long Long/MIN_VALUE)  ; LC_NIL / LC_NO_KEY / LC_NO_PROCESS
 
@@ -43,6 +42,12 @@
 
 ;; LC_MODEL_*: which knossos.model the device checks against
 (def ^:private model-code {:cas-register 0 :register 1 :mutex 2})
+
+;; LC_ALGO_*: jepsen.checker/linearizable's :algorithm (:linear, :wgl, else
+;; competition).  All three run the same device search; only :analyzer differs.
+(defn- algo-code [algorithm] (case algorithm :linear 0 :wgl 1 2))
+
+(def ^:private max-final 10)  ; jepsen.checker/linearizable truncates to 10
 
 (defn- long-or-nil [x] (if (nil? x) nil-long (long x)))
 
@@ -59,95 +64,199 @@
         v1     (Memory. bytes)
         index  (Memory. bytes)
         hist   (Memory. 64)]
-    (doseq [[i op] (map-indexed vector history)]
-      (let [value         (:value op)
-            [k v]         (if (independent/tuple? value) [(key value) (val value)] [nil value])
-            fc            (f-code (:f op) 3)
-            [a b]         (cond (= fc 2) (if (nil? v) [nil nil] v)
-                                (<= 4 fc) [nil nil]      ; mutex ops carry no value
-                                :else     [v nil])]
-        (.setByte type i (byte (type-code (:type op))))
-        (.setByte fn i (byte fc))
-        (.setLong proc (* 8 i) (if (integer? (:process op)) (long (:process op)) nil-long))
-        (.setLong key (* 8 i) (long-or-nil k))
-        (.setLong v0 (* 8 i) (if (= fc 3) nil-long (long-or-nil a)))
-        (.setLong v1 (* 8 i) (if (= fc 3) nil-long (long-or-nil b)))
-        (.setLong index (* 8 i) (long (or (:index op) -1)))))
+    (loop [i 0, ops (seq history)]
+      (when ops
+        (let [op    (first ops)
+              value (:value op)
+              [k v] (if (independent/tuple? value) [(key value) (val value)] [nil value])
+              fc    (f-code (:f op) 3)
+              [a b] (cond (= fc 2) (if (nil? v) [nil nil] v)
+                          (<= 4 fc) [nil nil]      ; mutex ops carry no value
+                          :else     [v nil])]
+          (.setByte type i (byte (type-code (:type op))))
+          (.setByte fn i (byte fc))
+          (.setLong proc (* 8 i) (if (integer? (:process op)) (long (:process op)) nil-long))
+          (.setLong key (* 8 i) (long-or-nil k))
+          (.setLong v0 (* 8 i) (if (= fc 3) nil-long (long-or-nil a)))
+          (.setLong v1 (* 8 i) (if (= fc 3) nil-long (long-or-nil b)))
+          (.setLong index (* 8 i) (long (or (:index op) -1)))
+          (recur (inc i) (next ops)))))
     (.setLong hist 0 n)
     (doseq [[off m] [[8 type] [16 fn] [24 proc] [32 key] [40 v0] [48 v1] [56 index]]]
       (.setPointer hist off m))
     {:hist hist :keep [type fn proc key v0 v1 index]}))
 
-;; LC_ALGO_*: jepsen.checker/linearizable's :algorithm (:linear, :wgl, else
-;; competition).  All three run the same device search; only :analyzer differs.
-(defn- algo-code [algorithm] (case algorithm :linear 0 :wgl 1 2))
+;; One lc_ctx per (device(s), budget, algorithm), created on first use and
+;; kept: a context owns its streams, scratch and staging buffers, so repeated
+;; checks allocate nothing once their sizes have been seen.  Calls on one
+;; context are serialised inside the library.
+(defonce ^:private contexts (atom {}))
 
-(defn- lc-create [device budget algorithm]
-  (let [opts (Memory. 56)
-        out  (PointerByReference.)]
+(defn- lc-create ^Pointer [devices budget algorithm]
+  (let [opts (Memory. 224)      ; sizeof(lc_opts), ABI 6
+        out  (Memory. 8)
+        devs (vec devices)]
     (.clear opts)
-    (.setInt opts 0 (int device))
-    (.setInt opts 4 (int (algo-code algorithm)))
-    (.setLong opts 8 (long budget))
-    (.setInt opts 16 (int 10))          ; max_final: jepsen truncates to 10
-    (call-int "lc_create" opts out)
-    (.getValue out)))
+    (.setInt opts 0 (int (first devs)))             ; device
+    (.setInt opts 4 (int (algo-code algorithm)))    ; algorithm
+    (.setLong opts 8 (long budget))                 ; max_configs
+    (.setInt opts 16 (int max-final))               ; max_final
+    (when (< 1 (count devs))                        ; one key shard per device
+      (.setInt opts 36 (int (count devs)))          ; n_devices
+      (doseq [[g d] (map-indexed vector devs)]
+        (.setInt opts (+ 40 (* 4 g)) (int d))))     ; devices[g]
+    (check-rc (LincheckNative/lc_create opts out) "lc_create")
+    (.getPointer out 0)))
+
+(defn- context ^Pointer [devices budget algorithm]
+  (let [k [(vec devices) budget algorithm]]
+    (or (get @contexts k)
+        (locking contexts
+          (or (get @contexts k)
+              (let [ctx (lc-create devices budget algorithm)]
+                (swap! contexts assoc k ctx)
+                ctx))))))
+
+(defn close!
+  "Destroys every cached device context (e.g. at the end of a test run)."
+  []
+  (locking contexts
+    (doseq [ctx (vals @contexts)] (LincheckNative/lc_destroy ctx))
+    (reset! contexts {})))
+
+(defn- unwrap
+  "An op as it appears in its key's sub-history (independent/subhistory
+  unwraps the tuple value)."
+  [op]
+  (let [v (:value op)]
+    (if (independent/tuple? v) (assoc op :value (val v)) op)))
+
+(defn- model-of
+  "The knossos model record holding register value x (LC_NIL = nil)."
+  [model x]
+  (let [v (when-not (= x nil-long) x)]
+    (case model
+      :cas-register (model/cas-register v)
+      :register     (model/register v)
+      :mutex        (assoc (model/mutex) :locked (= 1 v)))))
+
+(defn- report
+  "Decodes lc_report's words for packed key i into the :linear map."
+  [history model algorithm packed i valid fail-ev cause ^Memory finals n-final]
+  (let [words (long-array 256)
+        fin   (.share finals (* i max-final 16))
+        need  (check-rc (LincheckNative/lc_report packed i valid fail-ev fin n-final max-final words 256)
+                        "lc_report")
+        words (if (<= need 256)
+                words
+                (let [w (long-array need)]
+                  (check-rc (LincheckNative/lc_report packed i valid fail-ev fin n-final max-final w need)
+                            "lc_report")
+                  w))
+        row   (fn [r] (when (<= 0 r) (unwrap (nth history r))))
+        op    (fn [inv done]               ; knossos.history/complete's invocation
+                (let [o (row inv)]
+                  (if (and (nil? (:value o)) (<= 0 done)) (assoc o :value (:value (row done))) o)))
+        fail-op (row (aget words 0))
+        prev    (row (aget words 1))
+        n-cfg   (aget words 2)
+        n-paths (aget words 3)
+        pos     (volatile! 4)
+        take!   (fn [] (let [x (aget words @pos)] (vswap! pos inc) x))
+        ops!    (fn [] (vec (repeatedly (take!) #(op (take!) (take!)))))
+        configs (vec (repeatedly n-cfg
+                                 (fn [] (let [m (model-of model (take!))
+                                              pending (ops!)
+                                              linear  (ops!)]
+                                          {:model m :last-op prev :pending pending :linearized linear}))))
+        paths   (vec (repeatedly n-paths
+                                 (fn []
+                                   (let [m0    (model-of model (take!))
+                                         steps (vec (repeatedly (take!)
+                                                                (fn [] (let [o (op (take!) (take!))]
+                                                                         {:op o :model (model-of model (take!))}))))
+                                         bad   (model/step (model-of model (take!)) fail-op)]
+                                     (into [{:op prev :model m0}]
+                                           (conj steps {:op fail-op :model {:msg (:msg bad)}}))))))
+        base    {:analyzer (if (= algorithm :wgl) :wgl :linear)
+                 :configs  configs}]
+    (case (int valid)
+      1 (assoc base :valid? true :final-paths [])
+      0 (assoc base :valid? false :op fail-op :previous-ok prev :last-op prev :final-paths paths)
+      (cond-> (assoc base :valid? :unknown :final-paths []
+                     :cause (nth [:none :nonlin :budget :window :states :error] (long cause) :error))
+        fail-op (assoc :op fail-op)))))
 
 (defn check-history
-  "Runs the device search over every key; returns per-key verdict maps."
-  [history {:keys [device budget model algorithm]
+  "Runs the device search over every key; returns {k :linear-map}."
+  [history {:keys [device devices budget model algorithm]
             :or {device 0 budget (bit-shift-left 1 20) model :cas-register
                  algorithm :linear}}]
-  (let [{:keys [hist]} (marshal history)
-        pack-opts      (doto (Memory. 4) (.setInt 0 (int (model-code model))))
-        packed-ref     (PointerByReference.)
-        _              (call-int "lc_pack" hist pack-opts packed-ref)
-        packed         (.getValue packed-ref)
-        batch          (Memory. 72)
-        _              (call-int "lc_packed_view" packed batch)
-        n-keys         (.getLong batch 0)
-        ctx            (lc-create device budget algorithm)
-        valid          (Memory. (max 1 n-keys))
-        fail-ev        (Memory. (* 4 (max 1 n-keys)))
-        cause          (Memory. (max 1 n-keys))
-        result         (Memory. 48)]
+  (let [history    (vec history)
+        {:keys [hist keep]} (marshal history)
+        pack-opts  (doto (Memory. 4) (.setInt 0 (int (model-code model))))
+        out        (Memory. 8)
+        _          (check-rc (LincheckNative/lc_pack hist pack-opts out) "lc_pack")
+        packed     (.getPointer out 0)]
     (try
-      (.clear result)
-      (.setPointer result 0 valid)
-      (.setPointer result 8 fail-ev)
-      (.setPointer result 16 cause)
-      (call-int "lc_check_batch" ctx batch result nil)
-      (into {}
-            (for [i (range n-keys)]
-              (let [k  (.invokeLong (f "lc_packed_key") (object-array [packed (long i)]))
+      (let [batch    (Memory. 80)                ; sizeof(lc_batch)
+            _        (check-rc (LincheckNative/lc_packed_view packed batch) "lc_packed_view")
+            n-keys   (.getLong batch 0)
+            keys     (long-array (max 1 n-keys))
+            _        (check-rc (LincheckNative/lc_packed_keys packed keys) "lc_packed_keys")
+            ctx      (context (or devices [device]) budget algorithm)
+            n1       (max 1 n-keys)
+            valid    (Memory. n1)
+            fail-ev  (Memory. (* 4 n1))
+            cause    (Memory. n1)
+            finals   (Memory. (* 16 max-final n1))
+            n-final  (Memory. (* 4 n1))
+            result   (Memory. 48)]               ; sizeof(lc_result)
+        (.clear result)
+        (.setPointer result 0 valid)
+        (.setPointer result 8 fail-ev)
+        (.setPointer result 16 cause)
+        (.setPointer result 32 finals)
+        (.setPointer result 40 n-final)
+        (check-rc (LincheckNative/lc_check_batch ctx batch result nil) "lc_check_batch")
+        (persistent!
+          (reduce
+            (fn [m i]
+              (let [k  (aget keys i)
                     v  (.getByte valid i)
-                    fe (.getInt fail-ev (* 4 i))
-                    op (when (<= 0 fe)
-                         (history (.invokeLong (f "lc_packed_event_row")
-                                               (object-array [packed (long i) (long fe)]))))]
-                [k (cond-> {:valid?   (case v 1 true 0 false :unknown)
-                            :analyzer (if (= algorithm :wgl) :wgl :linear)
-                            :configs  []
-                            :final-paths []}
-                     (zero? v) (assoc :op op)
-                     (neg? v)  (assoc :cause ([:none :nonlin :budget :window :states :error]
-                                              (.getByte cause i))))])))
+                    c  (.getByte cause i)]
+                (assoc! m k
+                        (cond
+                          ;; the key's sub-history could not be prepared:
+                          ;; what check-safe makes of knossos's exception
+                          (and (neg? v) (= 5 c))
+                          {:valid? :unknown :error (LincheckNative/lc_packed_key_error packed i)}
+                          ;; valid keys: no counterexample to render
+                          (= 1 v)
+                          {:valid? true :analyzer (if (= algorithm :wgl) :wgl :linear)
+                           :configs [] :final-paths []}
+                          :else
+                          (report history model algorithm packed i v (.getInt fail-ev (* 4 i)) c
+                                  finals (.getInt n-final (* 4 i)))))))
+            (transient {})
+            (range n-keys))))
       (finally
-        (.invokeVoid (f "lc_destroy") (object-array [ctx]))
-        (.invokeVoid (f "lc_packed_free") (object-array [packed]))))))
+        (LincheckNative/lc_packed_free packed)
+        (identity keep)))))
 
 (defn checker
   "independent/checker over compose{:linear linearizable(cas-register),
   :timeline html}, with the :linear part batched on the GPU.  opts:
-  :device, :budget, :model (:cas-register, the default and the demo's;
-  :register or :mutex for the other Knossos models, SURVEY.md 8(f) F-4) and
-  :algorithm (:linear, the demo's; :wgl; anything else = competition)."
+  :device (or :devices, a vector: one key shard per entry, checked at once),
+  :budget, :model (:cas-register, the default and the demo's; :register or
+  :mutex for the other Knossos models, SURVEY.md 8(f) F-4) and :algorithm
+  (:linear, the demo's; :wgl; anything else = competition)."
   ([] (checker {}))
   ([opts]
    (reify checker/Checker
      (check [_ test history check-opts]
-       (let [linear (check-history history opts)
-             tl     (timeline/html)
+       (let [linear  (check-history history opts)
+             tl      (timeline/html)
              results (into {}
                            (for [[k lin] linear]
                              (let [sub (independent/subhistory k history)
@@ -160,4 +269,5 @@
                                    :timeline t}])))]
          {:valid?   (checker/merge-valid (map :valid? (vals results)))
           :results  results
+          ;; :unknown is truthy: such keys are not failures (independent/checker)
           :failures (->> results (remove (comp :valid? val)) (map key) vec)})))))

@@ -413,9 +413,16 @@ extern "C" int lc_edn_parse(const char *text, int64_t len, lc_hist **out) {
         const size_t n = cut.size() - 1;
         std::vector<Chunk> ch(n);
         std::vector<std::thread> th;
-        for (size_t i = 0; i < n; ++i)
-            th.emplace_back([&, i] { parse_range(text, cut[i], cut[i + 1], true, false, ch[i]); });
+        th.reserve(n);
+        bool spawned = true;
+        try {
+            for (size_t i = 0; i < n; ++i)
+                th.emplace_back([&, i] { parse_range(text, cut[i], cut[i + 1], true, false, ch[i]); });
+        } catch (const std::system_error &) {
+            spawned = false;  // joined below, then the serial read
+        }
         for (auto &t : th) t.join();
+        if (!spawned) return finish_serial(text, len, out);
         bool any_client = false;
         for (auto &c : ch) {
             if (!c.err.empty() || c.not_indep || c.conv_err != CONV_OK) return finish_serial(text, len, out);

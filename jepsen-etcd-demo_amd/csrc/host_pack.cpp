@@ -34,6 +34,7 @@
 #include <unordered_map>
 
 #include "common.hpp"
+#include "packed.hpp"
 
 namespace {
 
@@ -173,26 +174,6 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
 
 }  // namespace
 
-struct lc_packed {
-    std::vector<int64_t> keys;
-    lc::pinned_vector<uint64_t> ev_off;  // page-locked on a GPU host: lc_check_* DMA it directly
-    lc::pinned_vector<uint32_t> events;
-    std::vector<int64_t> ev_row;
-    std::vector<uint32_t> trans;
-    std::vector<uint32_t> trans_off;  // empty = shared table
-    std::vector<uint8_t> key_width;
-    std::vector<uint16_t> key_states;
-    // sub-history rows: per-key rows + rows shared by every key
-    std::vector<uint64_t> krow_off;
-    std::vector<int64_t> krows;
-    std::vector<int64_t> shared_rows;
-    // state id -> register value: shared table, or per key (state_off[k] ..)
-    std::vector<int64_t> state_vals;  // index 0 unused (nil)
-    std::vector<uint64_t> state_off;  // empty = shared
-    // keys that could not be prepared (A9): empty = none
-    std::vector<uint8_t> key_error;
-    std::vector<std::string> key_msg;
-};
 
 extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed **out) {
     if (!h || !out) return lc::fail(LC_E_INVALID, "lc_pack: null argument");

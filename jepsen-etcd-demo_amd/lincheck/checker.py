@@ -50,7 +50,9 @@ class Packed:
         self.view = v
         self.n_keys = int(v.n_keys)
         self.ev_off = N.carray(v.ev_off, self.n_keys + 1, np.uint64)
-        self.keys = [int(N.lib().lc_packed_key(self.handle, i)) for i in range(self.n_keys)]
+        keys = np.zeros(max(self.n_keys, 1), np.int64)
+        N.check(N.lib().lc_packed_keys(self.handle, N.ptr(keys, C.c_int64)))
+        self.keys = [int(k) for k in keys[:self.n_keys]]
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -266,19 +268,6 @@ def merge_valid(vals: Sequence[Any]) -> Any:
     return True
 
 
-def desc_step(d: int, st: int) -> Optional[int]:
-    """One interned transition (include/lincheck.h LC_DESC) from state id st:
-    the next state id, or None when the model step is inconsistent."""
-    t, a, b = d & 3, (d >> 2) & 0x7FFF, d >> 17
-    if t == N.LC_T_READ_ANY:
-        return st
-    if t == N.LC_T_READ:
-        return st if st == a else None
-    if t == N.LC_T_WRITE:
-        return b
-    return b if st == a else None
-
-
 def _sub_op(packed: Packed, row: int) -> Dict:
     """Row as it appears in the key's sub-history (independent/subhistory
     unwraps the tuple value)."""
@@ -289,153 +278,86 @@ def _sub_op(packed: Packed, row: int) -> Dict:
     return op
 
 
-class _KeyView:
-    """Key i's event stream around the failing (or last) event, for result
-    shaping: which invoke holds each window slot, its completed op map and
-    its transition descriptor."""
-
-    def __init__(self, packed: Packed, i: int, upto: int):
-        self.packed, self.i = packed, i
-        self.ev = packed.events(i)
-        e = self.ev[:upto]
-        slots = (e >> 24) & 0x7F
-        # each slot's last event before `upto`: an invoke means the slot is held
-        rev_slots = slots[::-1]
-        u, first_rev = np.unique(rev_slots, return_index=True)
-        last = upto - 1 - first_rev
-        held = (e[last] & N.LC_EV_OK_BIT) == 0
-        self.slot_ev: Dict[int, int] = {int(s): int(j) for s, j in zip(u[held], last[held])}
-        oks = np.flatnonzero(e & N.LC_EV_OK_BIT)
-        self.last_ok: Optional[int] = int(oks[-1]) if len(oks) else None
-        self._ops: Dict[int, Dict] = {}
-
-    def op(self, j: int) -> Dict:
-        """Event j's op map; an invocation carries its completion's value
-        when it has none (knossos.history/complete)."""
-        if j not in self._ops:
-            op = _sub_op(self.packed, self.packed.event_row(self.i, j))
-            w = int(self.ev[j])
-            if not (w & N.LC_EV_OK_BIT) and op.get("value") is None:
-                s = (w >> 24) & 0x7F
-                for k in range(j + 1, len(self.ev)):
-                    wk = int(self.ev[k])
-                    if (wk >> 24) & 0x7F == s:   # the slot's next event is its :ok
-                        if wk & N.LC_EV_OK_BIT:
-                            op["value"] = _sub_op(self.packed, self.packed.event_row(self.i, k)).get("value")
-                        break
-            self._ops[j] = op
-        return self._ops[j]
-
-    def desc(self, j: int) -> int:
-        return self.packed.desc(self.i, int(self.ev[j]) & 0x00FFFFFF)
-
-
-def _final_paths(kv: _KeyView, fe: int, finals: List, prev_op, limit: int = TRUNCATE,
-                 max_visits: int = 1 << 16) -> List[List[Dict]]:
-    """knossos.linear's :final-paths for an invalid key.
-
-    From each final config (model state, linearized pending ops), every
-    sequence of further pending ops that the model allows, followed by the
-    failing op, whose step is inconsistent in every state so reached (that is
-    what made the config set empty).  A path is [{"op": previous-ok, "model":
-    config state}, {"op": op, "model": state after it} ..., {"op": failing op,
-    "model": {"msg": "can't ..."}}].  Paths are generated depth-first, shortest
-    first, from the configs in device order; at most `limit` distinct ones are
-    kept (jepsen.checker/linearizable truncates to 10).  Knossos iterates a
-    hash set here, so only the SET of paths is comparable (SURVEY.md 8(a) A8);
-    its exact element shape is unpinned (knossos is absent)."""
-    packed, i = kv.packed, kv.i
-    fw = int(kv.ev[fe])
-    p_slot = (fw >> 24) & 0x7F
-    p_desc = kv.desc(kv.slot_ev[p_slot])
-    fail_op = _sub_op(packed, packed.event_row(i, fe))
-    others = [(s, kv.slot_ev[s], kv.desc(kv.slot_ev[s])) for s in sorted(kv.slot_ev) if s != p_slot]
-    out: List[List[Dict]] = []
-    seen = set()
-    visits = 0
-    state_cache: Dict[int, Any] = {}
-
-    def model_of(st):
-        if st not in state_cache:
-            state_cache[st] = packed.model.of_state(packed.state_value(i, st))
-        return state_cache[st]
-
-    def emit(st0, steps, st):
-        key = (st0, tuple(steps))
-        if key in seen:
-            return
-        seen.add(key)
-        f, v = fail_op["f"], fail_op.get("value")
-        bad = model_of(st).step(f, v)
-        msg = getattr(bad, "msg", None) or f"can't {f} {fmt(v)}"
-        path = [{"op": prev_op, "model": model_of(st0).render()}]
-        path += [{"op": kv.op(j), "model": model_of(s2).render()} for j, s2 in steps]
-        path.append({"op": fail_op, "model": {"msg": msg}})
-        out.append(path)
-
-    def dfs(st0, st, used, steps):
-        nonlocal visits
-        visits += 1
-        if len(out) >= limit or visits > max_visits:
-            return
-        if desc_step(p_desc, st) is None:
-            emit(st0, steps, st)
-        for s, j, d in others:
-            if (used >> s) & 1:
-                continue
-            st2 = desc_step(d, st)
-            if st2 is not None:
-                steps.append((j, st2))
-                dfs(st0, st2, used | (1 << s), steps)
-                steps.pop()
-                if len(out) >= limit or visits > max_visits:
-                    return
-
-    for st, mask in finals:
-        if len(out) >= limit:
-            break
-        dfs(st, st, mask, [])
-    return out
+def _report(packed: Packed, i: int, res: "KeyResults") -> np.ndarray:
+    """lc_report: the key's Knossos-shaped counterexample as int64 words
+    (include/lincheck.h), rendered natively -- the same rendering the JVM
+    binding decodes."""
+    fin = np.ascontiguousarray(res.final[i], dtype=np.uint64) if len(res.final) else np.zeros((1, 2), np.uint64)
+    nf = int(res.n_final[i]) if len(res.n_final) else 0
+    cap = 256
+    while True:
+        buf = np.zeros(cap, np.int64)
+        n = N.check(N.lib().lc_report(packed.handle, i, int(res.valid[i]), int(res.fail_event[i]),
+                                      N.ptr(fin, C.c_uint64), nf, TRUNCATE, N.ptr(buf, C.c_int64), cap))
+        if n <= cap:
+            return buf[:n]
+        cap = n
 
 
 def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.ndarray],
                 analyzer: str = "linear") -> Dict:
-    """Knossos-shaped result for key i."""
+    """Knossos-shaped result for key i,
+    decoded from lc_report."""
     v = int(res.valid[i])
     cause = N.CAUSES.get(int(res.cause[i]), "error")
     if v == N.LC_UNKNOWN and int(res.cause[i]) == N.LC_CAUSE_ERROR:
         # the key's sub-history could not be prepared: what check-safe makes
         # of the exception knossos would throw (etcdemo.clj:115)
         return {"valid?": "unknown", "error": packed.key_error(i) or "error"}
-    fe = int(res.fail_event[i])
-    upto = fe if fe >= 0 else packed.n_events(i)
-    kv = _KeyView(packed, i, upto)
-    prev = _sub_op(packed, packed.event_row(i, kv.last_ok)) if kv.last_ok is not None else None
-    finals = []
-    for c in range(int(res.n_final[i])):
-        lo, hi = int(res.final[i, c, 0]), int(res.final[i, c, 1])
-        finals.append(((hi >> 48) & 0x7FFF, lo | ((hi & ((1 << 48) - 1)) << 64)))
+    w = _report(packed, i, res)
+    ops: Dict[tuple, Dict] = {}
+
+    def op(inv: int, done: int) -> Dict:
+        """The invocation as knossos.history/complete leaves it: it takes its
+        completion's :value when it has none."""
+        if (inv, done) not in ops:
+            o = _sub_op(packed, inv)
+            if o.get("value") is None and done >= 0:
+                o["value"] = _sub_op(packed, done).get("value")
+            ops[(inv, done)] = o
+        return ops[(inv, done)]
+
+    def state(x: int):
+        return packed.model.of_state(None if x == N.LC_NIL else int(x))
+
+    op_row, prev_row, n_cfg, n_paths = (int(x) for x in w[:4])
+    prev = _sub_op(packed, prev_row) if prev_row >= 0 else None
+    at = 4
     configs = []
-    for st, mask in finals[:TRUNCATE]:
-        slots = sorted(kv.slot_ev)
-        configs.append({"model": packed.model.of_state(packed.state_value(i, st)).render(),
-                        "last-op": prev,
-                        "pending": [kv.op(kv.slot_ev[s]) for s in slots if not (mask >> s) & 1],
-                        "linearized": [kv.op(kv.slot_ev[s]) for s in slots if (mask >> s) & 1]})
+    for _ in range(n_cfg):
+        st = state(w[at]); at += 1
+        lists = []
+        for _ in range(2):
+            n = int(w[at]); at += 1
+            lists.append([op(int(w[at + 2 * j]), int(w[at + 2 * j + 1])) for j in range(n)])
+            at += 2 * n
+        configs.append({"model": st.render(), "last-op": prev, "pending": lists[0], "linearized": lists[1]})
+    paths = []
+    fail_op = _sub_op(packed, op_row) if op_row >= 0 else None
+    for _ in range(n_paths):
+        path = [{"op": prev, "model": state(w[at]).render()}]
+        n = int(w[at + 1]); at += 2
+        for j in range(n):
+            path.append({"op": op(int(w[at]), int(w[at + 1])), "model": state(w[at + 2]).render()})
+            at += 3
+        f, val = fail_op["f"], fail_op.get("value")
+        bad = state(w[at]).step(f, val); at += 1
+        path.append({"op": fail_op, "model": {"msg": getattr(bad, "msg", None) or f"can't {f} {fmt(val)}"}})
+        paths.append(path)
     out: Dict[str, Any] = {"analyzer": analyzer, "configs": configs, "final-paths": []}
     if v == N.LC_VALID:
         out["valid?"] = True
     elif v == N.LC_INVALID:
         out["valid?"] = False
-        out["op"] = _sub_op(packed, packed.event_row(i, fe))
+        out["op"] = fail_op
         out["previous-ok"] = prev
         out["last-op"] = prev
-        out["final-paths"] = _final_paths(kv, fe, finals, prev)
+        out["final-paths"] = paths
     else:
         out["valid?"] = "unknown"
         out["cause"] = cause
-        if fe >= 0:
-            out["op"] = _sub_op(packed, packed.event_row(i, fe))
+        if op_row >= 0:
+            out["op"] = fail_op
     return out
 
 
