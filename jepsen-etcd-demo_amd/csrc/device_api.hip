@@ -191,6 +191,8 @@ struct DevBatch {
     uint8_t *key_error = nullptr;
     int32_t *order = nullptr;  // LPT: keys by event count, descending
     bool t0_only = false;      // every key declared to fit the register lattice
+    bool taggable = false;     // keys may be cut into segments (shared table, states 0..5, no op installs nil)
+    bool seg_pays = false;     // sampled keys have quiescent points close enough for segments to pay
     bool validated = false;    // the host checked every event (else T0 does: T0_STRICT)
     // Device storage behind the arrays above, grown on demand: a batch that is
     // re-uploaded (a context's staging batch for lc_check_batch) keeps it, so
@@ -276,6 +278,12 @@ struct Dev {
     // from where the previous such step left it.
     bool ticket_live = false;
     uint32_t ticket_next = 0;
+    // key segments (register-tier steps of a batch of about one key per
+    // SIMD): per-key cut points, segment results, work lists
+    int64_t seg_keys = 0;
+    uint32_t *seg_cnt = nullptr, *seg_end = nullptr, *seg_out = nullptr, *seg_work = nullptr;
+    uint32_t *seg_rerun = nullptr, *seg_rerun_init = nullptr;
+    int32_t *seg0_fev = nullptr, *seg_ctl = nullptr;
     // node records (lc_check_node): this rank's block and the gathered node
     uint64_t *send = nullptr, *node = nullptr;
     int64_t node_cap = 0, node_n = 0;
@@ -293,6 +301,8 @@ struct Dev {
         if (hctl) (void)hipHostFree(hctl);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(dargs); dfree(send); dfree(node);
+        dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
+        dfree(seg0_fev); dfree(seg_ctl);
         if (hargs) (void)hipHostFree(hargs);
         delete staged;
         if (vstream) (void)hipStreamSynchronize(vstream);
@@ -600,7 +610,36 @@ static int validate_batch(const lc_batch *b) {
 struct Shape {
     uint32_t shared_states = 0;
     bool t0_only = false;
+    bool taggable = false;  // segments (lcd::SegArgs): shared table, states 0..5 from nil, nothing installs nil
+    bool seg_pays = false;  // sampled keys: the longest stretch without a quiescent point is short
 };
+
+// Would key segments pay?  A segment ends only at a quiescent point, so the
+// longest stretch without one bounds the segmented search, as the whole key
+// bounds the unsegmented one.  Up to 4 keys spread over the batch are
+// scanned on the host (a few thousand events); segments pay when their
+// longest stretch is at most a quarter of their length.
+static bool segments_pay(const lc_batch *b) {
+    const int64_t K = b->n_keys;
+    if (K <= 0 || !b->events) return false;
+    uint64_t len = 0, gap = 0;
+    for (int s = 0; s < 4; ++s) {
+        const int64_t k = K * s / 4;
+        const uint64_t e0 = b->ev_off[k], e1 = b->ev_off[k + 1];
+        int64_t pend = 0;
+        uint64_t last = e0;
+        for (uint64_t j = e0; j < e1; ++j) {
+            pend += (b->events[j] & LC_EV_OK_BIT) ? -1 : 1;
+            if (pend == 0) {
+                gap = std::max(gap, j + 1 - last);
+                last = j + 1;
+            }
+        }
+        gap = std::max(gap, e1 - last);
+        len += e1 - e0;
+    }
+    return len >= 4 * 512 && gap * 4 * 4 <= len;
+}
 
 static Shape batch_shape(const lc_batch *b) {
     Shape s;
@@ -611,6 +650,13 @@ static Shape batch_shape(const lc_batch *b) {
         if (f == LC_T_WRITE || f == LC_T_CAS) mx = std::max(mx, bb);
     }
     s.shared_states = mx + 1;
+    bool installs_nil = false;
+    for (int64_t i = 0; i < b->n_trans; ++i) {
+        const uint32_t t = b->trans[i], f = t & 3u;
+        installs_nil |= (f == LC_T_WRITE || f == LC_T_CAS) && (t >> 17) == 0;
+    }
+    s.taggable = !b->trans_off && s.shared_states <= 6 && b->init_state == 0 && !installs_nil;
+    s.seg_pays = s.taggable && segments_pay(b);
     const int64_t K = b->n_keys;
     bool ok = K > 0 && b->key_width && b->init_state < lcd::t0_max_states();
     for (int64_t k = 0; ok && k < K; ++k) ok = b->key_width[k] <= lcd::t0_max_width();
@@ -678,6 +724,8 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     d->has_trans_off = b->trans_off != nullptr;
     d->shared_states = sh.shared_states;
     d->t0_only = sh.t0_only;
+    d->taggable = sh.taggable;
+    d->seg_pays = sh.seg_pays;
     d->validated = validated;
     // LPT order: longest keys first
     std::vector<int32_t> order((size_t)K);
@@ -741,6 +789,25 @@ static int take_error(Dev *c, int64_t key0) {
                                                     : "key_width / key_states understate the key");
 }
 
+// Segment arrays for n_keys keys (grown on demand).
+static int ensure_segments(Dev *c, int64_t n_keys) {
+    if (n_keys <= c->seg_keys && c->seg_ctl) return LC_OK;
+    const int64_t cap = std::max<int64_t>(n_keys, 1024);
+    const size_t per = (size_t)cap * lcd::SEG_MAX;
+    dfree(c->seg_cnt); dfree(c->seg_end); dfree(c->seg_out); dfree(c->seg_work); dfree(c->seg_rerun);
+    dfree(c->seg_rerun_init); dfree(c->seg0_fev); dfree(c->seg_ctl);
+    HIPCHK(dalloc(&c->seg_cnt, (size_t)cap));
+    HIPCHK(dalloc(&c->seg_end, per));
+    HIPCHK(dalloc(&c->seg_out, per));
+    HIPCHK(dalloc(&c->seg_work, per));
+    HIPCHK(dalloc(&c->seg_rerun, (size_t)cap));
+    HIPCHK(dalloc(&c->seg_rerun_init, (size_t)cap));
+    HIPCHK(dalloc(&c->seg0_fev, (size_t)cap));
+    HIPCHK(dalloc(&c->seg_ctl, 4));
+    c->seg_keys = cap;
+    return LC_OK;
+}
+
 enum ResMode { RES_HOST = 0, RES_DEV = 1, RES_CTX = 2 };
 
 // Search d on c.  RES_HOST: r's arrays are host memory and receive the
@@ -788,6 +855,20 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // result download when the results go to host memory).
     const bool t0_step = K > 0 && d->t0_only && !(o.flags & LC_OPT_COUNT_PROBES);
     const bool async = t0_step && allow_async && mode != RES_HOST;
+    // Key segments (device_lattice.hip): verdicts only, a batch of about one
+    // key per SIMD or fewer (where each key's serial chain is exposed), and
+    // quiescent points close enough for the cuts to pay (segments_pay: on
+    // C2, whose clients think about as long as an op takes, the longest
+    // stretch without one is most of a key, so its keys stay whole).
+    // LC_SPLIT=0/1 forces the choice (A/B and tests).
+    const char *force = std::getenv("LC_SPLIT");
+    const bool fast = !a.peak && !a.final_cfg && o.max_configs >= 16ull * 64 * 32;
+    const bool want = force ? force[0] == '1' : d->seg_pays;
+    const bool split = t0_step && fast && d->taggable && want && K <= (int64_t)c->cu_count * 8;
+    if (split) {
+        rc = ensure_segments(c, K);
+        if (rc) return rc;
+    }
     uint32_t ticket_base = 0;
     if (t0_step && c->ticket_live) {
         ticket_base = c->ticket_next;
@@ -833,7 +914,24 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         HIPCHK(lcd::launch_validate(av, c->vstream));
         HIPCHK(hipEventRecord(c->vdone, c->vstream));
     }
-    if (K > 0) {
+    if (split) {
+        lcd::SegArgs sa{};
+        sa.ev_off = d->ev_off; sa.events = d->events; sa.trans = d->trans; sa.key_error = d->key_error;
+        sa.n_trans = (uint32_t)d->n_trans; sa.n_keys = (int32_t)K; sa.max_seg = lcd::SEG_MAX;
+        // segments of about fill x (resident waves / keys) per key
+        const double fill = std::getenv("LC_SEG_FILL") ? std::atof(std::getenv("LC_SEG_FILL")) : 2.0;
+        const int grid = c->cu_count * 12;
+        const double per_key = std::max(1.0, fill * grid / (double)K);
+        sa.seg_len = (uint32_t)std::max<double>(64.0, (double)d->n_events / (double)K / per_key);
+        if (const char *e = std::getenv("LC_SEG_LEN")) sa.seg_len = (uint32_t)std::max(1, std::atoi(e));
+        sa.seg_cnt = c->seg_cnt; sa.seg_end = c->seg_end; sa.seg_out = c->seg_out; sa.seg0_fev = c->seg0_fev;
+        sa.work = c->seg_work; sa.rerun = c->seg_rerun; sa.rerun_init = c->seg_rerun_init; sa.ctl = c->seg_ctl;
+        sa.err = c->counters + 4; sa.valid = a.valid; sa.fail_event = a.fail_event; sa.cause = a.cause;
+        sa.strict = a.strict;
+        HIPCHK(hipMemsetAsync(c->seg_ctl, 0, 4 * sizeof(int32_t), c->stream));
+        HIPCHK(lcd::launch_segments(sa, grid, c->stream));
+        HIPCHK(hipEventRecord(c->et0, c->stream));
+    } else if (K > 0) {
         HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
     }
@@ -843,7 +941,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         HIPCHK(hipEventRecord(c->ring[c->async_seq % 4], c->stream));
         ++c->async_seq;
         ++c->n_async;
-        c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
+        c->ticket_next = split ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
         if (st) *st = lc_stats{};  // times come from lc_wait
         if (enqueued) *enqueued = true;
@@ -896,7 +994,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             rc = readback();
         }
         std::memset(c->hctl, 0, CTL_BYTES);  // counters not kept on this path
-        c->ticket_next = ticket_base + (uint32_t)K + (uint32_t)g0;
+        c->ticket_next = split ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
         if (rc) return rc;
     } else {

@@ -64,7 +64,7 @@ constexpr uint32_t T0_MAX_STATES = 32;
 uint32_t t0_max_width() { return T0_MAX_WIDTH; }
 uint32_t t0_max_states() { return T0_MAX_STATES; }
 
-struct Xfer { uint32_t k, cap, b; };
+struct Xfer { uint32_t k, cap, b, m; };
 
 __device__ __forceinline__ Xfer xfer_of(uint32_t d) {
     const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
@@ -73,6 +73,33 @@ __device__ __forceinline__ Xfer xfer_of(uint32_t d) {
     x.k = (f == LC_T_READ || f == LC_T_CAS) ? abit : 0xFFFFFFFFu;
     x.cap = f >= LC_T_WRITE ? 1u : 0xFFFFFFFFu;
     x.b = f >= LC_T_WRITE ? (b & 31u) : 0u;
+    x.m = ~0u;
+    return x;
+}
+
+// Tagged transfers (key segments, see k_search_segments): the lattice word
+// holds 5 groups of 6 bits, group t = the states reachable from initial
+// state t + 1 (register states 1..5, bit s - 1 of a group; bit 5 spare, 0).
+// An op's transfer on a word is
+//   T(M) = (((M & K) + C) >> s) & Mb
+// with K = the accepted states in every group, and for a write / cas of
+// state b: C = 31 in every group (a nonempty group carries into its bit 5),
+// s = 6 - b (that bit lands on bit b - 1), Mb = bit b - 1 in every group;
+// for a read C = 0, s = 0, Mb = ~0 (T(M) = M & K).  K = 0 gives 0 in every
+// case (31 >> s never reaches bit b - 1), as the untagged form's does.
+constexpr uint32_t TAG_REP = 0x1041041u;  // 1 in each 6-bit group
+constexpr uint32_t TAG_ID = 0x10204081u;  // group t holds state t + 1: the identity start
+
+__device__ __forceinline__ Xfer xfer_tag(uint32_t d) {
+    const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
+    const uint32_t abit = (a >= 1u && a <= 5u) ? 1u << (a - 1u) : 0u;
+    Xfer x;
+    x.k = (f == LC_T_READ || f == LC_T_CAS) ? abit * TAG_REP : 0x1Fu * TAG_REP;
+    const bool inst = f >= LC_T_WRITE && b >= 1u && b <= 5u;
+    x.cap = inst ? 31u * TAG_REP : 0u;            // C
+    x.b = inst ? 6u - b : 0u;                     // s
+    x.m = inst ? (1u << (b - 1u)) * TAG_REP : ~0u;  // Mb
+    if (f >= LC_T_WRITE && !inst) x.k = 0u;       // installs a state outside the tags: never taken
     return x;
 }
 
@@ -85,8 +112,12 @@ __device__ __forceinline__ uint32_t vand(uint32_t s, uint32_t v) {
 }
 
 // acc | T(x) = acc | (min(x & k, cap) << b): v_and_b32, v_min_u32, v_lshl_or_b32
-__device__ __forceinline__ uint32_t xacc(uint32_t acc, uint32_t x, uint32_t k, uint32_t cap, uint32_t b) {
-    return (__builtin_elementwise_min(x & k, cap) << b) | acc;
+// (tagged: acc | ((((x & K) + C) >> s) & Mb): v_and, v_add, v_lshrrev, v_and_or)
+template <bool TAG = false>
+__device__ __forceinline__ uint32_t xacc(uint32_t acc, uint32_t x, uint32_t k, uint32_t cap, uint32_t b,
+                                         uint32_t mb = ~0u) {
+    if constexpr (TAG) return ((((x & k) + cap) >> b) & mb) | acc;
+    else return (__builtin_elementwise_min(x & k, cap) << b) | acc;
 }
 
 // One-directional gathers along subset bit q < 6 (a lane-index bit):
@@ -160,8 +191,10 @@ __device__ __forceinline__ uint32_t xv(uint32_t x, uint32_t lane) {
     return ((lane >> Q) & 1u) ? d : u;
 }
 
-__device__ __forceinline__ uint32_t xapply(uint32_t M, uint32_t k, uint32_t cap, uint32_t b) {
-    return __builtin_elementwise_min(M & k, cap) << b;
+template <bool TAG = false>
+__device__ __forceinline__ uint32_t xapply(uint32_t M, uint32_t k, uint32_t cap, uint32_t b, uint32_t mb = ~0u) {
+    if constexpr (TAG) return (((M & k) + cap) >> b) & mb;
+    else return __builtin_elementwise_min(M & k, cap) << b;
 }
 
 __device__ __forceinline__ bool idx_has(uint32_t lane, int k, uint32_t q) {
@@ -211,12 +244,12 @@ __device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint3
 // Transfer masks of one event: vk[q] = op q's accept mask on lanes with bit
 // q (0 elsewhere and for q = p); sc[q] / sb[q] = op q's cap / shift.
 struct LaneMasks {
-    uint32_t vk[6], sc[10], sb[10];
+    uint32_t vk[6], sc[10], sb[10], sm[10];
 };
 
-template <int N>
+template <int N, bool TAG = false>
 __device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t k_v, uint32_t cap_v, uint32_t b_v,
-                                           uint32_t lane) {
+                                           uint32_t lane, uint32_t m_v = 0) {
 #pragma unroll
     for (int q = 0; q < 6; ++q) m.vk[q] = 0u;
 #pragma unroll
@@ -231,6 +264,7 @@ __device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t k_
     for (int q = 0; q < (N < 10 ? N : 10); ++q) {
         m.sc[q] = __builtin_amdgcn_readlane(cap_v, q);
         m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
+        if constexpr (TAG) m.sm[q] = __builtin_amdgcn_readlane(m_v, q);
     }
 }
 
@@ -240,10 +274,14 @@ __device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t k_
 // v_and_b32 (v_and_b32_dpp); the permlane swaps (Q = 4, 5) clobber both
 // operands, so their other operand is `prev`, the previous position's min()
 // result, dead once it has been shifted into cur -- one copy of cur per swap.
-template <int Q, int N>
+template <int Q, int N, bool TAG = false>
 __device__ __forceinline__ uint32_t sweep_lanes(uint32_t cur, const LaneMasks &m, uint32_t prev = 0) {
     if constexpr (Q >= N || Q >= 6) {
         return cur;
+    } else if constexpr (TAG) {
+        const uint32_t x = gdown_j<Q>(cur, prev);
+        const uint32_t t = (x & m.vk[Q]) + m.sc[Q];
+        return sweep_lanes<Q + 1, N, TAG>(((t >> m.sb[Q]) & m.sm[Q]) | cur, m, t);
     } else {
         const uint32_t x = gdown_j<Q>(cur, prev);
         const uint32_t t = __builtin_elementwise_min(x & m.vk[Q], m.sc[Q]);
@@ -359,9 +397,10 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 // supersets of Knossos's, so this path is used only when no set size, probe
 // count or config list is asked for (FAST in lattice_key).
 // Returns 0 normal, 1 invalid (W unchanged).
-template <int T>
+template <int T, bool TAG = false>
 __device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t live, uint32_t k_v, uint32_t cap_v,
-                                              uint32_t b_v, uint32_t lane, const uint32_t (&lm)[6], bool dirty) {
+                                              uint32_t b_v, uint32_t lane, const uint32_t (&lm)[6], bool dirty,
+                                              uint32_t m_v = 0) {
     uint32_t C = W;
     if (dirty) {
         LaneMasks m;
@@ -370,11 +409,12 @@ __device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t 
             m.vk[q] = vand(__builtin_amdgcn_readlane(k_v, q), lm[q]);
             m.sc[q] = __builtin_amdgcn_readlane(cap_v, q);
             m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
+            if constexpr (TAG) m.sm[q] = __builtin_amdgcn_readlane(m_v, q);
         }
         const uint32_t nc = (uint32_t)__popc(live);  // a path has at most nc steps
 #pragma unroll 1
         for (uint32_t s = 0; s < nc; ++s) {
-            const uint32_t nv = sweep_lanes<0, T>(C, m);
+            const uint32_t nv = sweep_lanes<0, T, TAG>(C, m);
             const bool ch = nv != C;
             C = nv;
             if (!__any(ch)) break;
@@ -389,14 +429,14 @@ __device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t 
 
 // One :ok(p) event on a lattice of RL registers (N = 7 or 8 ops pending):
 // lane bits 0..5 as in ok_lane, register bits 6.. through register pairs.
-template <int RL, int RM>
+template <int RL, int RM, bool TAG = false>
 __device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t k_v, uint32_t cap_v, uint32_t b_v,
                                       uint32_t lane, uint64_t budget, bool count, uint32_t &probes,
-                                      uint32_t &nSn_out, bool want_size) {
+                                      uint32_t &nSn_out, bool want_size, uint32_t m_v = 0) {
     constexpr int NB = lat_bits<RL>();  // = ops pending
     constexpr int NR = NB - 6;          // register bits
     LaneMasks m;
-    lane_masks<NB>(m, p, k_v, cap_v, b_v, lane);
+    lane_masks<NB, TAG>(m, p, k_v, cap_v, b_v, lane, m_v);
     uint32_t rk[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -406,6 +446,7 @@ __device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t k_
     }
     const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
                    pb = __builtin_amdgcn_readlane(b_v, p);
+    const uint32_t pm = TAG ? __builtin_amdgcn_readlane(m_v, p) : ~0u;
     uint32_t Ret[RL], I[RL];
     if (count) {
 #pragma unroll
@@ -436,12 +477,13 @@ __device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t k_
     for (int s = 1; s < NB; ++s) {
         uint32_t nv[RL];
 #pragma unroll
-        for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6>(I[k], m);
+        for (int k = 0; k < RL; ++k) nv[k] = sweep_lanes<0, 6, TAG>(I[k], m);
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
             for (int k = 0; k < RL; ++k)
-                if ((k >> r) & 1) nv[k] = xacc(nv[k], nv[k ^ (1 << r)], rk[r], m.sc[6 + r], m.sb[6 + r]);
+                if ((k >> r) & 1)
+                    nv[k] = xacc<TAG>(nv[k], nv[k ^ (1 << r)], rk[r], m.sc[6 + r], m.sb[6 + r], TAG ? m.sm[6 + r] : ~0u);
         bool ch = false;
 #pragma unroll
         for (int k = 0; k < RL; ++k) { ch |= nv[k] != I[k]; I[k] = nv[k]; }
@@ -452,7 +494,7 @@ __device__ __forceinline__ int ok_reg(uint32_t (&W)[RM], uint32_t p, uint32_t k_
     uint32_t cI = 0, cS = 0;
 #pragma unroll
     for (int k = 0; k < RL; ++k) {
-        Ret[k] = xacc(Ret[k], I[k], pk, pc, pb);
+        Ret[k] = xacc<TAG>(Ret[k], I[k], pk, pc, pb, pm);
         cI += (uint32_t)__popc(I[k]);
         cS += (uint32_t)__popc(Ret[k]);
     }
@@ -505,10 +547,11 @@ struct LatMem {
     uint32_t *W, *R, *I;
 };
 
-template <int RL>
+template <int RL, bool TAG = false>
 __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_t n, uint32_t k_v,
                                             uint32_t cap_v, uint32_t b_v, uint32_t lane, uint64_t budget,
-                                            bool count, uint32_t &probes, uint32_t &nSn_out, bool want_size) {
+                                            bool count, uint32_t &probes, uint32_t &nSn_out, bool want_size,
+                                            uint32_t m_v = 0) {
     constexpr int NB = lat_bits<RL>();
     const uint32_t cand = ((1u << n) - 1u) & ~(1u << p);
     // transfer of candidate q: lane q of k_v/cap_v/b_v, read at use
@@ -517,8 +560,9 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 #define KK(Q) __builtin_amdgcn_readlane(ck, Q)
 #define CP(Q) __builtin_amdgcn_readlane(cap_v, Q)
 #define SB(Q) __builtin_amdgcn_readlane(b_v, Q)
+#define SM(Q) (TAG ? __builtin_amdgcn_readlane(m_v, Q) : ~0u)
     const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
-                   pb = __builtin_amdgcn_readlane(b_v, p);
+                   pb = __builtin_amdgcn_readlane(b_v, p), pm = SM(p);
     const uint32_t plm = p < 6 ? 1u << p : 0u, prm = p >= 6 ? 1u << (p - 6) : 0u;
 #pragma unroll 1
     for (int k = 0; k < RL; ++k) {
@@ -538,13 +582,14 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 #define LC_LANEBIT(Q)                                                                  \
             {                                                                          \
                 const uint32_t y = xv<Q>(x, lane);                                     \
-                acc |= ((lane >> Q) & 1u) ? xapply(y, KK(Q), CP(Q), SB(Q)) : 0u;      \
+                acc |= ((lane >> Q) & 1u) ? xapply<TAG>(y, KK(Q), CP(Q), SB(Q), SM(Q)) : 0u; \
             }
             LC_LANEBIT(0) LC_LANEBIT(1) LC_LANEBIT(2) LC_LANEBIT(3) LC_LANEBIT(4) LC_LANEBIT(5)
 #undef LC_LANEBIT
 #pragma unroll
             for (int q = 6; q < NB; ++q)
-                if ((k >> (q - 6)) & 1) acc |= xapply(m.I[(k ^ (1 << (q - 6))) * 64 + lane], KK(q), CP(q), SB(q));
+                if ((k >> (q - 6)) & 1)
+                    acc |= xapply<TAG>(m.I[(k ^ (1 << (q - 6))) * 64 + lane], KK(q), CP(q), SB(q), SM(q));
             if (acc != x) { m.I[k * 64 + lane] = acc; ch = true; }
         }
         if (!__any(ch)) break;
@@ -559,7 +604,7 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
                 if (!idx_has(lane, k, (uint32_t)q)) probes += (uint32_t)__popc(x & KK(q));
             probes += (uint32_t)__popc(x & pk);
         }
-        const uint32_t r = m.R[k * 64 + lane] | xapply(x, pk, pc, pb);
+        const uint32_t r = m.R[k * 64 + lane] | xapply<TAG>(x, pk, pc, pb, pm);
         m.R[k * 64 + lane] = r;
         cI += (uint32_t)__popc(x);
         cS += (uint32_t)__popc(r);
@@ -577,6 +622,7 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 #undef KK
 #undef CP
 #undef SB
+#undef SM
     // relocation: the op at index `last` moves to index p
     const uint32_t last = n - 1;
     const uint32_t llm = last < 6 ? 1u << last : 0u, lrm = last >= 6 ? 1u << (last - 6) : 0u;
@@ -944,17 +990,18 @@ __device__ unsigned long long lc_t0_stamps[8192 * 6];
 #endif
 
 // Validation of a batch the host did not check event by event (T0_STRICT
-// steps): a kernel of its own on a second stream, running beside T0 (which
-// stays in bounds on any input).  One key per lane, each walking its key's
-// events in order: an :ok must name a pending slot, an :invoke a free slot
-// below 64, a transition id must be in range and install only states the
-// key has.  Violations set the batch's error words (the call then returns
-// LC_E_INVALID).  Eight event words, then their descriptors, are loaded at a
-// time, so a lane keeps loads in flight.
+// steps): a kernel of its own on a second stream, running beside the search
+// (which stays in bounds on any input).  One wave per key, 64 events per
+// pass: every transition id in range and installing only states the key
+// has, every slot below 64, and the slot protocol -- the events of one slot
+// alternate :invoke, :ok, :invoke ... -- checked per distinct slot of the
+// chunk: with b = 1 when the slot is pending at the chunk's start, the r-th
+// event of the slot in the chunk (r from 0, wave rank among the slot's lanes)
+// must be an :ok exactly when r + b is odd.  Violations set the batch's
+// error words (the call then returns LC_E_INVALID).
 __global__ __launch_bounds__(64) void k_validate(T0Args a) {
     const uint32_t lane = lane_id();
-    constexpr int G = 8;
-    for (int64_t k = (int64_t)blockIdx.x * 64 + lane; k < a.n_order; k += (int64_t)gridDim.x * 64) {
+    for (int64_t k = blockIdx.x; k < a.n_order; k += gridDim.x) {
         if (a.key_error && a.key_error[k]) continue;
         const uint64_t eb = a.ev_off[k], ee = a.ev_off[k + 1];
         const uint32_t tb = a.trans_off ? a.trans_off[k] : 0u;
@@ -962,32 +1009,30 @@ __global__ __launch_bounds__(64) void k_validate(T0Args a) {
         const uint32_t ns = a.trans_off ? (a.key_states ? a.key_states[k] : 0u) : a.shared_states;
         uint64_t pend = 0;
         int32_t why = 0;
-        for (uint64_t j = eb; j < ee && !why; j += G) {
-            uint32_t w[G], d[G];
-#pragma unroll
-            for (int i = 0; i < G; ++i) w[i] = j + i < ee ? a.events[j + i] : LC_EV_OK_BIT;  // past the end: no-op
-#pragma unroll
-            for (int i = 0; i < G; ++i) {
-                const uint32_t t = LC_EV_TRANS(w[i]);
-                d[i] = (!(w[i] & LC_EV_OK_BIT) && t < ntr) ? a.trans[tb + t] : 0u;
+        for (uint64_t base = eb; base < ee && !why; base += 64) {
+            const uint64_t j = base + lane;
+            const bool in = j < ee;
+            const uint32_t w = in ? a.events[j] : 0u;
+            const bool ok = (w & LC_EV_OK_BIT) != 0;
+            const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
+            const uint32_t d = (in && !ok && t < ntr) ? a.trans[tb + t] : 0u;
+            if (__any(in && !ok && (t >= ntr || ((d & 3u) >= LC_T_WRITE && (d >> 17) >= ns)))) why |= LC_BATCH_E_TRANS;
+            if (__any(in && s >= 64)) why |= LC_BATCH_E_FIT;
+            if (why) break;
+            uint64_t todo = __ballot(in), npend = pend;
+            while (todo) {
+                const uint32_t sl = __builtin_amdgcn_readlane(s, (uint32_t)__builtin_ctzll(todo));
+                const uint64_t ms = __ballot(in && s == sl);
+                const uint32_t b0 = (uint32_t)(pend >> sl) & 1u;
+                const uint32_t r = rank_of(ms);
+                if (__any(in && s == sl && ok != (((r + b0) & 1u) != 0))) why |= LC_BATCH_E_SLOTS;
+                if (((uint32_t)__popcll(ms) + b0) & 1u) npend |= 1ull << sl;
+                else npend &= ~(1ull << sl);
+                todo &= ~ms;
             }
-#pragma unroll
-            for (int i = 0; i < G; ++i) {
-                const bool real = j + i < ee;
-                const uint32_t s = LC_EV_SLOT(w[i]);
-                const uint64_t bit = 1ull << (s & 63u);
-                const bool ok = (w[i] & LC_EV_OK_BIT) != 0;
-                int32_t e = 0;
-                if (s >= 64) e = LC_BATCH_E_FIT;
-                else if (ok) e = (pend & bit) ? 0 : LC_BATCH_E_SLOTS;
-                else if (LC_EV_TRANS(w[i]) >= ntr || ((d[i] & 3u) >= LC_T_WRITE && (d[i] >> 17) >= ns))
-                    e = LC_BATCH_E_TRANS;
-                else e = (pend & bit) ? LC_BATCH_E_SLOTS : 0;
-                why = (real && !why) ? e : why;
-                pend = (real && !ok) ? (pend | bit) : (real ? (pend & ~bit) : pend);
-            }
+            pend = npend;
         }
-        if (why) {
+        if (why && lane == 0) {
             atomicOr(&a.err[0], why);
             atomicMax(&a.err[1], (int32_t)k + 1);
         }
@@ -1076,8 +1121,372 @@ hipError_t launch_validate(const Args &a, hipStream_t s) {
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
     t.key_states = a.key_states; t.key_error = a.key_error; t.err = a.err;
     t.n_order = a.n_order; t.shared_states = a.shared_states; t.n_trans = a.n_trans;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((a.n_order + 63) / 64, 1024));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_order, 2048));
     hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64), 0, s, t);
+    return hipGetLastError();
+}
+
+// ---- Key segments ------------------------------------------------------------
+//
+// With every key's events strictly serial, a batch of about one key per SIMD
+// (C2: 1,000 keys on 1,024 SIMDs) leaves each SIMD one wave whose dependency
+// chains are all exposed.  The search distributes over initial states: the
+// set after any event, from an initial set S, is the union of the sets
+// reached from each s in S.  So a key is cut at quiescent points (no op
+// pending: the config set is a plain set of register states) and each
+// segment is searched on a wave of its own from every start state at once:
+// the lattice word holds one 6-bit group per start state (xfer_tag), valid
+// where the key's values are interned as states 1..5 and no op installs nil
+// (state 0): a cut is placed only after a write or cas has been invoked
+// (and, the point being quiescent, completed), so nil cannot be a start
+// state.  Segment 0 starts from the initial state alone and is searched
+// untagged.  A per-key composition then walks the segments: the states
+// after segment s are the union, over the states standing before it, of
+// their groups in its final word; the key dies in the first segment whose
+// union is empty, and only that segment is searched again, untagged, from
+// the states before it, for the failing event.  Verdicts only (the FAST
+// path): no set sizes, probes or final configs.
+
+// Inclusive prefix sum over the wave's lanes, by DPP: Hillis-Steele within
+// each row of 16 (row_shr 1, 2, 4, 8), then row_bcast 15 and 31 carry each
+// row's total into the rows above it.
+__device__ __forceinline__ int32_t wave_scan(int32_t x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// Cut points of one key per wave: a chunk of 64 events per pass (the next
+// chunk's words in flight), the pending count as a wave prefix sum, a cut
+// after an event that leaves nothing pending once a write / cas has been
+// invoked, at least seg_len events past the previous cut (longer for a key
+// that would otherwise need more than max_seg segments).
+__global__ __launch_bounds__(64) void k_seg_prep(SegArgs a) {
+    const uint32_t lane = lane_id();
+    for (int32_t key = blockIdx.x; key < a.n_keys; key += gridDim.x) {
+        uint32_t *ends = a.seg_end + (size_t)key * a.max_seg;
+        if (a.key_error && a.key_error[key]) {
+            if (lane == 0) a.seg_cnt[key] = 0;
+            continue;
+        }
+        const uint64_t eb = a.ev_off[key];
+        const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
+        const uint32_t seg_len = max(a.seg_len, (nev + a.max_seg - 2) / (a.max_seg - 1));
+        int32_t count = 0;   // ops pending before this chunk
+        bool wseen = false;  // a write / cas invoked before this chunk
+        uint32_t last = 0, nseg = 0;
+        uint32_t w_next = lane < nev ? a.events[eb + lane] : LC_EV_OK_BIT;
+        for (uint32_t base = 0; base < nev; base += 64) {
+            const uint32_t j = base + lane;
+            const bool in = j < nev;
+            const uint32_t w = w_next;
+            w_next = j + 64 < nev ? a.events[eb + j + 64] : LC_EV_OK_BIT;
+            const bool ok = (w & LC_EV_OK_BIT) != 0;
+            const uint32_t t = LC_EV_TRANS(w);
+            const uint32_t d = (in && !ok && t < a.n_trans) ? a.trans[t] : 0u;
+            const int32_t x = wave_scan(in ? (ok ? -1 : 1) : 0);
+            const int32_t cnt = count + x;  // ops pending after event j
+            const uint64_t wb = __ballot(in && !ok && (d & 3u) >= LC_T_WRITE);
+            const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+            const bool wsj = wseen || (wb & upto) != 0;
+            uint64_t cand = __ballot(in && cnt == 0 && wsj && j + 1 < nev);
+            while (cand && nseg + 1 < a.max_seg) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(cand);
+                cand &= cand - 1;
+                const uint32_t pos = base + l + 1;
+                if (pos - last >= seg_len) {
+                    if (lane == 0) ends[nseg] = pos;
+                    ++nseg;
+                    last = pos;
+                }
+            }
+            count = __shfl(cnt, 63);
+            wseen = wseen || wb != 0;
+        }
+        if (lane == 0) {
+            ends[nseg] = nev;
+            ++nseg;
+            a.seg_cnt[key] = nseg;
+            const int32_t at = atomicAdd(&a.ctl[0], (int32_t)nseg);
+            for (uint32_t s = 0; s < nseg; ++s) a.work[at + (int32_t)s] = ((uint32_t)key << 8) | s;
+        }
+    }
+}
+
+// One segment [sb, se) of a key from the start word `init` (untagged: a
+// state mask; tagged: TAG_ID), on the compact lattice with closed sets (the
+// register tier's FAST path).  status 0: fin = the OR of every config word
+// left (for a quiescent end, lane 0's word); 1: every start died at event
+// fev (key-relative); 3: the key does not fit the register tier.
+template <bool TAG>
+__device__ __forceinline__ void segment_search(const SegArgs &a, int32_t key, uint32_t sb, uint32_t se,
+                                               uint32_t init, uint32_t *ws, int &status_out, uint32_t &fev_out,
+                                               uint32_t &fin_out) {
+    constexpr int RM = T0_RSMALL;
+    const uint32_t lane = lane_id();
+    const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
+    const uint32_t *const evp = a.events + a.ev_off[key] + sb;
+    const uint32_t nev = se - sb;
+    const uint32_t ntr = a.n_trans;
+    auto ldesc = [&](uint32_t w, bool have) -> uint32_t {
+        const uint32_t t = LC_EV_TRANS(w);
+        return (have && !(w & LC_EV_OK_BIT) && t < ntr) ? a.trans[t] : 0u;
+    };
+    auto decode = [](uint32_t d) -> Xfer { return TAG ? xfer_tag(d) : xfer_of(d); };
+    uint32_t W[RM];
+#pragma unroll
+    for (int k = 0; k < RM; ++k) W[k] = 0;
+    if (lane == 0) W[0] = init;
+    bool in_mem = false;
+    uint32_t k_v = 0, cap_v = 0, b_v = 0, m_v = 0;
+    uint32_t slot_v = 0, dense_v = 0, n = 0, live = 0;
+    uint32_t lm[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) lm[q] = (uint32_t)__builtin_amdgcn_sbfe((int)lane, q, 1);
+    int status = 0;
+    uint32_t fev = 0;
+    uint32_t ev = lane < nev ? evp[lane] : 0u;
+    uint32_t dsc = ldesc(ev, lane < nev);
+    uint32_t ev_n = 64 + lane < nev ? evp[64 + lane] : 0u;
+    uint32_t dsc_n = ldesc(ev_n, 64 + lane < nev);
+    uint32_t ev_nn = 128 + lane < nev ? evp[128 + lane] : 0u;
+    Xfer xc = decode(dsc);
+    uint32_t e = 0, i = 0, base = 0, lim = nev;
+    auto advance = [&]() {
+        ++e;
+        if (++i == 64u) {
+            i = 0; base += 64;
+            ev = ev_n; dsc = dsc_n; ev_n = ev_nn;
+            xc = decode(dsc);
+            dsc_n = ldesc(ev_n, base + 64 + lane < nev);
+            ev_nn = base + 128 + lane < nev ? evp[base + 128 + lane] : 0u;
+        }
+    };
+    uint32_t W0 = W[0];
+    bool dirty = true;
+    for (uint32_t phase = 0; phase <= nev && e < lim; ++phase) {
+        while (e < lim) {  // lane phase: <= 6 pending
+            const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
+            const uint32_t slot = LC_EV_SLOT(evi);
+            if (!(evi & LC_EV_OK_BIT)) {
+                if (n == 6) break;
+                if (n >= T0_MAX_WIDTH || slot >= 64) {
+                    status = 3;
+                } else {
+                    const uint32_t idx = (uint32_t)__builtin_ctz(~live);
+                    const bool me = lane == idx;
+                    slot_v = me ? slot : slot_v;
+                    k_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.k, i) : k_v;
+                    cap_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.cap, i) : cap_v;
+                    b_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.b, i) : b_v;
+                    if constexpr (TAG) m_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.m, i) : m_v;
+                    dense_v = lane == slot ? idx : dense_v;
+                    live |= 1u << idx;
+                    ++n;
+                    dirty = true;
+                }
+            } else {
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
+                const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
+                int r;
+                if (top >= 6) r = ok_lane_closed<6, TAG>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty, m_v);
+                else if (top == 5) r = ok_lane_closed<5, TAG>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty, m_v);
+                else r = ok_lane_closed<4, TAG>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty, m_v);
+                dirty = false;
+                k_v = lane == p ? 0u : k_v;
+                live = r ? live : live & ~(1u << p);
+                n = r ? n : n - 1;
+                status = r;
+                fev = e;
+            }
+            lim = status ? 0u : lim;
+            advance();
+        }
+        if (e >= lim) break;
+        W[0] = W0;
+#pragma unroll
+        for (int k = 1; k < RM; ++k) W[k] = 0u;
+        while (e < lim) {  // dense phase: 7-10 pending
+            const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
+            const uint32_t slot = LC_EV_SLOT(evi);
+            if (!(evi & LC_EV_OK_BIT)) {
+                if (n >= T0_MAX_WIDTH || slot >= 64) {
+                    status = 3;
+                } else {
+                    if (n == 8) {  // 9 pending: the lattice moves to the workspace
+#pragma unroll
+                        for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < RM ? W[k < RM ? k : 0] : 0u;
+                        in_mem = true;
+                    }
+                    const uint32_t idx = n;
+                    const bool me = lane == idx;
+                    slot_v = me ? slot : slot_v;
+                    k_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.k, i) : k_v;
+                    cap_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.cap, i) : cap_v;
+                    b_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.b, i) : b_v;
+                    if constexpr (TAG) m_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.m, i) : m_v;
+                    dense_v = lane == slot ? idx : dense_v;
+                    live |= 1u << idx;
+                    ++n;
+                }
+            } else {
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
+                uint32_t nSn = 0, probes = 0;
+                int r;
+                if (n == 7) r = ok_reg<2, RM, TAG>(W, p, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false, m_v);
+                else if (n == 8) r = ok_reg<4, RM, TAG>(W, p, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false, m_v);
+                else if (n == 9)
+                    r = ok_event_mem<8, TAG>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false, m_v);
+                else
+                    r = ok_event_mem<16, TAG>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false, m_v);
+                const uint32_t last = n - 1;
+                const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
+                const uint32_t x0 = __builtin_amdgcn_readlane(k_v, last), x1 = __builtin_amdgcn_readlane(cap_v, last),
+                               x2 = __builtin_amdgcn_readlane(b_v, last);
+                const uint32_t x3 = TAG ? __builtin_amdgcn_readlane(m_v, last) : 0u;
+                const bool mp = lane == p && !r;
+                slot_v = mp ? s_last : slot_v;
+                k_v = mp ? x0 : k_v;
+                cap_v = mp ? x1 : cap_v;
+                b_v = mp ? x2 : b_v;
+                if constexpr (TAG) m_v = mp ? x3 : m_v;
+                dense_v = (lane == s_last && !r) ? p : dense_v;
+                k_v = (lane == last && !r) ? 0u : k_v;
+                live = r ? live : (1u << last) - 1u;
+                if (in_mem && n == 9 && !r) {
+#pragma unroll
+                    for (int k = 0; k < RM; ++k) W[k] = m.W[k * 64 + lane];
+                    in_mem = false;
+                }
+                n = r ? n : n - 1;
+                status = r;
+                fev = e;
+            }
+            lim = status ? 0u : lim;
+            advance();
+            if (n <= 6) break;
+        }
+        W0 = W[0];
+        dirty = true;
+    }
+    W[0] = W0;
+    uint32_t f = 0;
+    if (in_mem) {
+#pragma unroll 1
+        for (int k = 0; k < T0_RMEM; ++k) f |= m.W[k * 64 + lane];
+    } else {
+#pragma unroll
+        for (int k = 0; k < RM; ++k) f |= W[k];
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
+    status_out = status;
+    fev_out = sb + fev;
+    fin_out = status ? 0u : f;
+}
+
+// Every segment of the work list, one wave each (persistent grid, tickets).
+__global__ __launch_bounds__(64) void k_search_segments(SegArgs a) {
+    __shared__ uint32_t ws[3 * T0_RMEM * 64];
+    const int32_t nwork = a.ctl[0];
+    for (int32_t guard = 0; guard <= nwork; ++guard) {
+        int32_t w = 0;
+        if (lane_id() == 0) w = atomicAdd(&a.ctl[1], 1);
+        w = __builtin_amdgcn_readfirstlane(w);
+        if (w >= nwork) break;
+        const uint32_t item = a.work[w];
+        const int32_t key = (int32_t)(item >> 8);
+        const uint32_t s = item & 0xFFu;
+        const uint32_t *ends = a.seg_end + (size_t)key * a.max_seg;
+        const uint32_t sb = s ? ends[s - 1] : 0u, se = ends[s];
+        int status;
+        uint32_t fev, fin;
+        if (s == 0) segment_search<false>(a, key, sb, se, 1u, ws, status, fev, fin);  // from nil (state 0)
+        else segment_search<true>(a, key, sb, se, TAG_ID, ws, status, fev, fin);
+        if (lane_id() == 0) {
+            a.seg_out[(size_t)key * a.max_seg + s] = fin;
+            if (s == 0) a.seg0_fev[key] = status == 1 ? (int32_t)fev : -1;
+            if (status == 3) {  // declared to fit the register tier, and it does not
+                atomicOr(&a.err[0], LC_BATCH_E_FIT);
+                atomicMax(&a.err[1], key + 1);
+            }
+        }
+    }
+}
+
+// Per key (one thread each): compose the segments' final words.
+__global__ __launch_bounds__(256) void k_seg_compose(SegArgs a) {
+    for (int32_t key = blockIdx.x * blockDim.x + threadIdx.x; key < a.n_keys; key += gridDim.x * blockDim.x) {
+        if (a.key_error && a.key_error[key]) {
+            a.valid[key] = LC_UNKNOWN; a.cause[key] = LC_CAUSE_ERROR; a.fail_event[key] = -1;
+            continue;
+        }
+        const uint32_t n = a.seg_cnt[key];
+        const uint32_t *out = a.seg_out + (size_t)key * a.max_seg;
+        if (out[0] == 0u) {  // segment 0 is searched from the initial state itself
+            a.valid[key] = LC_INVALID; a.cause[key] = LC_CAUSE_NONLIN; a.fail_event[key] = a.seg0_fev[key];
+            continue;
+        }
+        uint32_t S = (out[0] >> 1) & 0x1Fu;  // state ids 1..5 -> start groups 0..4
+        bool dead = false;
+        for (uint32_t s = 1; s < n && !dead; ++s) {
+            const uint32_t F = out[s];
+            uint32_t S2 = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 5; ++t)
+                if ((S >> t) & 1u) S2 |= (F >> (6u * t)) & 0x1Fu;
+            if (!S2) {
+                const int32_t at = atomicAdd(&a.ctl[2], 1);
+                a.rerun[at] = ((uint32_t)key << 8) | s;
+                a.rerun_init[at] = S << 1;  // back to state ids
+                dead = true;
+            }
+            S = S2;
+        }
+        if (!dead) {
+            a.valid[key] = LC_VALID; a.cause[key] = LC_CAUSE_NONE; a.fail_event[key] = -1;
+        }
+    }
+}
+
+// The segment each dead key died in, searched again untagged from the states
+// standing before it: the failing event.
+__global__ __launch_bounds__(64) void k_seg_rerun(SegArgs a) {
+    __shared__ uint32_t ws[3 * T0_RMEM * 64];
+    const int32_t nr = a.ctl[2];
+    for (int32_t guard = 0; guard <= nr; ++guard) {
+        int32_t w = 0;
+        if (lane_id() == 0) w = atomicAdd(&a.ctl[3], 1);
+        w = __builtin_amdgcn_readfirstlane(w);
+        if (w >= nr) break;
+        const uint32_t item = a.rerun[w];
+        const int32_t key = (int32_t)(item >> 8);
+        const uint32_t s = item & 0xFFu;
+        const uint32_t *ends = a.seg_end + (size_t)key * a.max_seg;
+        int status;
+        uint32_t fev, fin;
+        segment_search<false>(a, key, ends[s - 1], ends[s], a.rerun_init[w], ws, status, fev, fin);
+        if (lane_id() == 0) {
+            if (status == 1) {
+                a.valid[key] = LC_INVALID; a.cause[key] = LC_CAUSE_NONLIN; a.fail_event[key] = (int32_t)fev;
+            } else {  // cannot happen for a consistent batch: report it as malformed
+                a.valid[key] = LC_UNKNOWN; a.cause[key] = LC_CAUSE_ERROR; a.fail_event[key] = -1;
+                atomicOr(&a.err[0], LC_BATCH_E_FIT);
+                atomicMax(&a.err[1], key + 1);
+            }
+        }
+    }
+}
+
+hipError_t launch_segments(const SegArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_seg_prep, dim3((unsigned)std::max(1, a.n_keys)), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_search_segments, dim3((unsigned)grid), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_seg_compose, dim3((unsigned)std::max(1, (a.n_keys + 255) / 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_seg_rerun, dim3(256), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

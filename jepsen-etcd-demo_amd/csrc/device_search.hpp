@@ -81,6 +81,36 @@ size_t lat_ws_words();
 // T0_STRICT steps: the batch's event-by-event validation (err words), a
 // kernel of its own for a second stream
 hipError_t launch_validate(const Args &a, hipStream_t s);
+
+// Key segments (device_lattice.hip, "Key segments"): a register-tier step
+// whose keys are cut at quiescent points and searched as independent
+// segments, then composed per key.  Device arrays of seg_cap entries each
+// (seg_cap = n_keys * max_seg), sized by the host.
+struct SegArgs {
+    const uint64_t *ev_off;
+    const uint32_t *events;
+    const uint32_t *trans;       // the shared table (segments need it)
+    const uint8_t *key_error;    // may be null
+    uint32_t n_trans;
+    int32_t n_keys;
+    uint32_t seg_len;            // cut at the first quiescent point this far past the last cut
+    uint32_t max_seg;            // segments per key at most
+    uint32_t *seg_cnt;           // [n_keys]
+    uint32_t *seg_end;           // [n_keys * max_seg] end event (exclusive) of each segment
+    uint32_t *seg_out;           // [n_keys * max_seg] final word (0: every start dead)
+    int32_t *seg0_fev;           // [n_keys] failing event of segment 0 (searched exactly)
+    uint32_t *work;              // [n_keys * max_seg] key << 8 | segment
+    uint32_t *rerun;             // [n_keys] key << 8 | segment, then its start states
+    uint32_t *rerun_init;        // [n_keys]
+    int32_t *ctl;                // [0] work items, [1] search ticket, [2] reruns, [3] rerun ticket
+    int32_t *err;                // T0_STRICT error words (a key that does not fit)
+    int8_t *valid;
+    int32_t *fail_event;
+    uint8_t *cause;
+    int32_t strict;
+};
+constexpr uint32_t SEG_MAX = 256;  // work items are key << 8 | segment
+hipError_t launch_segments(const SegArgs &a, int grid, hipStream_t s);
 uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
