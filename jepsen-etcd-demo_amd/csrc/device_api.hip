@@ -201,9 +201,18 @@ struct DevBatch {
         void *p = nullptr;
         size_t cap = 0;
     } mem[8];
+    // pinned host staging of the per-key arrays and the transition table
+    // (one copy per upload); `hmeta_done` marks the end of the last copy out
+    // of it, so it is not rewritten while that copy may still read it
+    char *hmeta = nullptr;
+    size_t hmeta_cap = 0;
+    hipEvent_t hmeta_done = nullptr;
     ~DevBatch() {
+        if (hmeta_done) (void)hipEventSynchronize(hmeta_done);
         for (Mem &m : mem)
             if (m.p) (void)hipFree(m.p);
+        if (hmeta) (void)hipHostFree(hmeta);
+        if (hmeta_done) (void)hipEventDestroy(hmeta_done);
     }
 };
 
@@ -284,6 +293,9 @@ struct Dev {
     uint32_t *seg_cnt = nullptr, *seg_end = nullptr, *seg_out = nullptr, *seg_work = nullptr;
     uint32_t *seg_rerun = nullptr, *seg_rerun_init = nullptr;
     int32_t *seg0_fev = nullptr, *seg_ctl = nullptr;
+    // speculative segments: each wave's 9-10-pending workspace
+    uint32_t *spec_ws = nullptr;
+    size_t spec_ws_words = 0;
     // node records (lc_check_node): this rank's block and the gathered node
     uint64_t *send = nullptr, *node = nullptr;
     int64_t node_cap = 0, node_n = 0;
@@ -302,7 +314,7 @@ struct Dev {
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(dargs); dfree(send); dfree(node);
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
-        dfree(seg0_fev); dfree(seg_ctl);
+        dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws);
         if (hargs) (void)hipHostFree(hargs);
         delete staged;
         if (vstream) (void)hipStreamSynchronize(vstream);
@@ -712,9 +724,13 @@ static void shard_keys(const lc_batch *b, int n, int64_t *key0) {
 
 // Copy a validated batch into d's device arrays (grown as needed).
 // events_src: where the event words are copied from (b->events by default;
-// lc_check_batch passes its pinned staging copy).
+// lc_check_batch passes its pinned staging copy).  The per-key arrays and the
+// transition table go through one pinned staging block and one copy; the
+// event words are copied straight from the caller's (page-locked) memory.
+// sync: wait for the copies (the caller may free its arrays on return);
+// otherwise the caller keeps them alive until its stream has passed them.
 static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, bool validated,
-                       const uint32_t *events_src = nullptr) {
+                       const uint32_t *events_src = nullptr, bool sync = true) {
     const int64_t K = b->n_keys;
     d->device = c->device;
     d->n_keys = K;
@@ -727,48 +743,55 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     d->taggable = sh.taggable;
     d->seg_pays = sh.seg_pays;
     d->validated = validated;
+    HIPCHK(hipSetDevice(c->device));
+    // layout of the staging block (16-byte aligned pieces)
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t Kz = (size_t)K;
+    const size_t o_off = 0, o_order = al(o_off + (Kz + 1) * 8), o_trans = al(o_order + Kz * 4);
+    const size_t o_toff = al(o_trans + (size_t)d->n_trans * 4);
+    const size_t o_width = al(o_toff + (b->trans_off ? Kz * 4 : 0));
+    const size_t o_states = al(o_width + (b->key_width ? Kz : 0));
+    const size_t o_err = al(o_states + (b->key_states ? Kz * 2 : 0));
+    const size_t bytes = al(o_err + (b->key_error ? Kz : 0));
+    if (!d->hmeta_done) HIPCHK(hipEventCreateWithFlags(&d->hmeta_done, hipEventDisableTiming));
+    HIPCHK(hipEventSynchronize(d->hmeta_done));  // the previous copy out of the block is done
+    if (bytes > d->hmeta_cap) {
+        if (d->hmeta) (void)hipHostFree(d->hmeta);
+        d->hmeta = nullptr;
+        d->hmeta_cap = 0;
+        HIPCHK(hipHostMalloc((void **)&d->hmeta, bytes, hipHostMallocDefault));
+        d->hmeta_cap = bytes;
+    }
+    char *h = d->hmeta;
+    std::memcpy(h + o_off, b->ev_off, (Kz + 1) * 8);
     // LPT order: longest keys first
-    std::vector<int32_t> order((size_t)K);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+    int32_t *order = (int32_t *)(h + o_order);
+    std::iota(order, order + K, 0);
+    std::stable_sort(order, order + K, [&](int32_t x, int32_t y) {
         return b->ev_off[x + 1] - b->ev_off[x] > b->ev_off[y + 1] - b->ev_off[y];
     });
-    d->trans_off = nullptr;
-    d->key_width = nullptr;
-    d->key_states = nullptr;
-    d->key_error = nullptr;
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(grow(d->mem[0], d->ev_off, (size_t)K + 1));
+    if (b->n_trans > 0) std::memcpy(h + o_trans, b->trans, (size_t)b->n_trans * 4);
+    else std::memset(h + o_trans, 0, 4);
+    if (b->trans_off) std::memcpy(h + o_toff, b->trans_off, Kz * 4);
+    if (b->key_width) std::memcpy(h + o_width, b->key_width, Kz);
+    if (b->key_states) std::memcpy(h + o_states, b->key_states, Kz * 2);
+    if (b->key_error) std::memcpy(h + o_err, b->key_error, Kz);
+    char *dm = nullptr;
+    HIPCHK(grow(d->mem[0], dm, bytes));
     HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
-    HIPCHK(grow(d->mem[2], d->trans, (size_t)d->n_trans));
-    HIPCHK(grow(d->mem[3], d->order, (size_t)K));
-    if (K) {
-        HIPCHK(hipMemcpyAsync(d->ev_off, b->ev_off, ((size_t)K + 1) * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(d->order, order.data(), (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
-    }
+    d->ev_off = (uint64_t *)(dm + o_off);
+    d->order = (int32_t *)(dm + o_order);
+    d->trans = (uint32_t *)(dm + o_trans);
+    d->trans_off = b->trans_off ? (uint32_t *)(dm + o_toff) : nullptr;
+    d->key_width = b->key_width ? (uint8_t *)(dm + o_width) : nullptr;
+    d->key_states = b->key_states ? (uint16_t *)(dm + o_states) : nullptr;
+    d->key_error = b->key_error ? (uint8_t *)(dm + o_err) : nullptr;
     if (d->n_events)
         HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
                               hipMemcpyHostToDevice, c->stream));
-    if (b->n_trans > 0)
-        HIPCHK(hipMemcpyAsync(d->trans, b->trans, (size_t)b->n_trans * 4, hipMemcpyHostToDevice, c->stream));
-    if (b->trans_off && K) {
-        HIPCHK(grow(d->mem[4], d->trans_off, (size_t)K));
-        HIPCHK(hipMemcpyAsync(d->trans_off, b->trans_off, (size_t)K * 4, hipMemcpyHostToDevice, c->stream));
-    }
-    if (b->key_width && K) {
-        HIPCHK(grow(d->mem[5], d->key_width, (size_t)K));
-        HIPCHK(hipMemcpyAsync(d->key_width, b->key_width, (size_t)K, hipMemcpyHostToDevice, c->stream));
-    }
-    if (b->key_states && K) {
-        HIPCHK(grow(d->mem[6], d->key_states, (size_t)K));
-        HIPCHK(hipMemcpyAsync(d->key_states, b->key_states, (size_t)K * 2, hipMemcpyHostToDevice, c->stream));
-    }
-    if (b->key_error && K) {
-        HIPCHK(grow(d->mem[7], d->key_error, (size_t)K));
-        HIPCHK(hipMemcpyAsync(d->key_error, b->key_error, (size_t)K, hipMemcpyHostToDevice, c->stream));
-    }
-    // the host arrays (order above, the caller's) must outlive the copies
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpyAsync(dm, h, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(d->hmeta_done, c->stream));
+    if (sync) HIPCHK(hipStreamSynchronize(c->stream));
     return LC_OK;
 }
 
@@ -869,6 +892,26 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         rc = ensure_segments(c, K);
         if (rc) return rc;
     }
+    // Speculative segments (device_lattice.hip): the same regime without
+    // quiescent points -- every key a workgroup of `segs` waves, about four
+    // segment waves per SIMD in all (C2: 1,000 keys x 4).  LC_SPEC=0/1 forces
+    // the choice, LC_SPEC_SEGS the segments per key.
+    const char *fspec = std::getenv("LC_SPEC");
+    int segs = K > 0 ? (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1)) : 0;
+    if (const char *e = std::getenv("LC_SPEC_SEGS")) segs = std::atoi(e);
+    segs = segs >= 8 ? 8 : segs >= 4 ? 4 : segs >= 2 ? 2 : 0;
+    const bool spec = !split && t0_step && fast && segs >= 2 && (fspec ? fspec[0] == '1' : true);
+    if (spec) {
+        const size_t need = lcd::spec_ws_words(K, segs);
+        if (need > c->spec_ws_words) {
+            if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
+            dfree(c->spec_ws);
+            c->spec_ws = nullptr;
+            c->spec_ws_words = 0;
+            HIPCHK(dalloc(&c->spec_ws, need));
+            c->spec_ws_words = need;
+        }
+    }
     uint32_t ticket_base = 0;
     if (t0_step && c->ticket_live) {
         ticket_base = c->ticket_next;
@@ -931,6 +974,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         HIPCHK(hipMemsetAsync(c->seg_ctl, 0, 4 * sizeof(int32_t), c->stream));
         HIPCHK(lcd::launch_segments(sa, grid, c->stream));
         HIPCHK(hipEventRecord(c->et0, c->stream));
+    } else if (spec) {
+        const uint32_t ck1 = std::getenv("LC_SPEC_CK1") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK1")) : 32u;
+        const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 160u;
+        HIPCHK(lcd::launch_spec(a0, c->dargs, segs, c->spec_ws, ck1, ck2, c->stream));
+        HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0) {
         HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
@@ -941,7 +989,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         HIPCHK(hipEventRecord(c->ring[c->async_seq % 4], c->stream));
         ++c->async_seq;
         ++c->n_async;
-        c->ticket_next = split ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
+        c->ticket_next = (split || spec) ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
         if (st) *st = lc_stats{};  // times come from lc_wait
         if (enqueued) *enqueued = true;
@@ -994,7 +1042,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             rc = readback();
         }
         std::memset(c->hctl, 0, CTL_BYTES);  // counters not kept on this path
-        c->ticket_next = split ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
+        c->ticket_next = (split || spec) ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
         if (rc) return rc;
     } else {
@@ -1325,23 +1373,40 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
         d->staged = new (std::nothrow) DevBatch();
         if (!d->staged) return lc::fail(LC_E_NOMEM, "lc_check_node: out of memory");
     }
-    rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src);
+    const auto t_prep = std::chrono::steady_clock::now();
+    rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false);  // this call waits before it returns
     if (rc) return rc;
+    const auto t_up = std::chrono::steady_clock::now();
     lc_result none{};
     bool enq = false;
+    // on an error below, the copies out of the caller's arrays are waited for
+    auto drained = [&](int e) {
+        (void)hipStreamSynchronize(d->stream);
+        return e;
+    };
     rc = dev_search(d, d->staged, &none, RES_CTX, true, 0, st, &enq);
-    if (rc) return rc;
+    if (rc) return drained(rc);
+    const auto t_search = std::chrono::steady_clock::now();
     rc = gather_node(c, d, b->n_keys, block);
-    if (rc) return rc;
-    if (d->node_n) HIPCHK(hipMemcpyAsync(node, d->node, (size_t)d->node_n * 8, hipMemcpyDeviceToHost, d->stream));
+    if (rc) return drained(rc);
+    if (d->node_n && hipMemcpyAsync(node, d->node, (size_t)d->node_n * 8, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
+        return drained(lc::fail(LC_E_DEVICE, "lc_check_node: record download failed"));
+    const auto t_gather = std::chrono::steady_clock::now();
     if (enq) {  // a T0-only step: one wait for the search, the exchange and the download
         int n_async = 0;
         float span = 0;
         rc = dev_wait(d, &n_async, &span);
-        if (rc) return rc;
+        if (rc) return drained(rc);
         if (st) st->kernel_ms = st->tier0_ms = span;
     } else {
         HIPCHK(hipStreamSynchronize(d->stream));
+    }
+    if (std::getenv("LC_TIMING")) {
+        using ms = std::chrono::duration<double, std::milli>;
+        std::fprintf(stderr, "lc_check_node: prepare %.3f, upload %.3f, search enqueue %.3f, gather enqueue %.3f, "
+                     "wait %.3f ms (search span %.3f)\n", ms(t_prep - t0).count(), ms(t_up - t_prep).count(),
+                     ms(t_search - t_up).count(), ms(t_gather - t_search).count(),
+                     ms(std::chrono::steady_clock::now() - t_gather).count(), st ? st->kernel_ms : 0.f);
     }
     if (st) st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return LC_OK;

@@ -232,6 +232,7 @@ struct T0Args {
     uint32_t init_state, shared_states, flags;
     uint32_t n_trans;            // entries of trans[]
     uint32_t ticket_base;        // ticket value this launch starts from (see launch_t0)
+    uint32_t spec_ck1, spec_ck2; // speculative segments: checkpoint distances past a cut
 };
 
 __device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint32_t why) {
@@ -624,6 +625,70 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 #undef SB
 #undef SM
     // relocation: the op at index `last` moves to index p
+    const uint32_t last = n - 1;
+    const uint32_t llm = last < 6 ? 1u << last : 0u, lrm = last >= 6 ? 1u << (last - 6) : 0u;
+#pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t r = m.R[k * 64 + lane];
+        const uint32_t src = (uint32_t)__shfl_xor((int)m.R[(k ^ (prm | lrm)) * 64 + lane], (int)(plm | llm));
+        const bool hp = (lane & plm) || ((uint32_t)k & prm);
+        const bool hl = (lane & llm) || ((uint32_t)k & lrm);
+        m.W[k * 64 + lane] = p == last ? r : (hl ? 0u : (hp ? src : r));
+    }
+    return 0;
+}
+
+// ok_event_mem's closure as Gauss-Seidel sweeps (verdicts only: no sizes or
+// probes): each row a one-directional lane sweep (sweep_lanes, 3 VALU per
+// position), then the register bits from the rows below it, already updated
+// in this sweep.  The bidirectional per-row form above needs about twice the
+// instructions per sweep and more sweeps.
+template <int RL>
+__device__ __forceinline__ int ok_event_mem_gs(const LatMem &m, uint32_t p, uint32_t n, uint32_t k_v, uint32_t cap_v,
+                                               uint32_t b_v, uint32_t lane) {
+    constexpr int NB = lat_bits<RL>();
+    constexpr int NR = NB - 6;
+    LaneMasks lmk;
+    lane_masks<NB>(lmk, p, k_v, cap_v, b_v, lane);
+    uint32_t rk[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) rk[r] = (uint32_t)(6 + r) != p ? __builtin_amdgcn_readlane(k_v, 6 + r) : 0u;
+    const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
+                   pb = __builtin_amdgcn_readlane(b_v, p);
+    const uint32_t plm = p < 6 ? 1u << p : 0u, prm = p >= 6 ? 1u << (p - 6) : 0u;
+#pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t w = m.W[k * 64 + lane];
+        const uint32_t src = (uint32_t)__shfl_xor((int)m.W[(k ^ prm) * 64 + lane], (int)plm);
+        const bool hp = (lane & plm) || ((uint32_t)k & prm);
+        m.R[k * 64 + lane] = hp ? 0u : src;
+        m.I[k * 64 + lane] = hp ? 0u : w;
+    }
+#pragma unroll 1
+    for (int s = 0; s < NB; ++s) {
+        bool ch = false;
+#pragma unroll 1
+        for (int k = 0; k < RL; ++k) {
+            const uint32_t x = m.I[k * 64 + lane];
+            uint32_t nv = sweep_lanes<0, 6>(x, lmk);
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+                if ((k >> r) & 1) nv = xacc(nv, m.I[(k ^ (1 << r)) * 64 + lane], rk[r], lmk.sc[6 + r], lmk.sb[6 + r]);
+            if (nv != x) {
+                m.I[k * 64 + lane] = nv;
+                ch = true;
+            }
+        }
+        if (!__any(ch)) break;
+    }
+    uint32_t cS = 0;
+#pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t r = m.R[k * 64 + lane] | xapply(m.I[k * 64 + lane], pk, pc, pb);
+        m.R[k * 64 + lane] = r;
+        cS |= r;
+    }
+    if (!__any(cS != 0u)) return 1;
     const uint32_t last = n - 1;
     const uint32_t llm = last < 6 ? 1u << last : 0u, lrm = last >= 6 ? 1u << (last - 6) : 0u;
 #pragma unroll 1
@@ -1098,19 +1163,24 @@ size_t lat_ws_words() { return 3 * T0_RMEM * 64; }
 // Every block ends with exactly one ticket past the work list, so a launch
 // leaves the ticket at ticket_base + n_order + grid: back-to-back launches
 // can start from there instead of re-zeroing it.
-hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s, uint32_t ticket_base) {
+static T0Args make_t0(const Args &a, const Args *a_dev) {
     T0Args t{};
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
     t.key_width = a.key_width; t.key_states = a.key_states; t.key_error = a.key_error; t.order = a.order;
     t.ticket = a.ticket;
     t.err = a.err;
     t.n_trans = a.n_trans;
-
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
-    t.init_state = a.init_state; t.shared_states = a.shared_states; t.ticket_base = ticket_base;
+    t.init_state = a.init_state; t.shared_states = a.shared_states;
     t.flags = (a.count_probes ? T0_COUNT : 0u) | (a.peak ? T0_WANT_PEAK : 0u) | (a.final_cfg ? T0_WANT_FINAL : 0u) |
               (a.debug_mode == 2 ? T0_DBG_NOEVENTS : 0u) | (a.debug_mode == 3 ? T0_DBG_NOFINAL : 0u) |
               (a.strict ? T0_STRICT : 0u);
+    return t;
+}
+
+hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s, uint32_t ticket_base) {
+    T0Args t = make_t0(a, a_dev);
+    t.ticket_base = ticket_base;
     if (wide) hipLaunchKernelGGL(k_search_lattice<T0_RBIG>, dim3(grid), dim3(64), 0, s, t);
     else hipLaunchKernelGGL(k_search_lattice<T0_RSMALL>, dim3(grid), dim3(64), 0, s, t);
     return hipGetLastError();
@@ -1487,6 +1557,586 @@ hipError_t launch_segments(const SegArgs &a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_search_segments, dim3((unsigned)grid), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_seg_compose, dim3((unsigned)std::max(1, (a.n_keys + 255) / 256)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_seg_rerun, dim3(256), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---- Speculative key segments -----------------------------------------------
+//
+// The other way to cut a serial key (no quiescent point needed).  The search
+// is monotone: from a larger config set every later set is at least as large.
+// So segment s of a key (s >= 1, cut where at most 6 ops are pending) is
+// searched from TOP = every register state with every subset of the ops
+// pending at the cut linearized -- a superset of the real set there, whatever
+// came before.  Runs from different start sets through the same events meet
+// quickly (a completed write collapses the register; measured on C2-shaped
+// keys with tools/spec_conv.py: within 8 events at the median, 25 at most),
+// and once two runs hold equal sets they stay equal.  One workgroup per key,
+// one wave per segment:
+//   1. every wave searches its segment from TOP (segment 0 from the initial
+//      state, exactly), recording the set after the first :ok past cut + ck1
+//      and past cut + ck2 (checkpoints), its failing event if it dies, and its
+//      set at the segment's end;
+//   2. every wave s >= 1 then searches its segment again from the set segment
+//      s - 1 ended with, until the two runs meet at a checkpoint.  Inductively
+//      every set is then exact: where they meet, the TOP run IS the real run
+//      from there on, so its death (or survival) is the segment's;
+//   3. wave 0 walks the segments in order: the key fails in the first
+//      segment whose real run dies.  A pair of runs that never met (not seen
+//      on any measured history) sends the key to the unsegmented search.
+// Compared sets are the closed sets the FAST path keeps, taken right after an
+// :ok, where they are canonical (ok_lane_closed); both runs of a segment start
+// from the same op-index assignment (slot order at the cut), so the
+// assignments stay equal event by event.  Verdicts only.
+extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
+constexpr uint32_t SPEC_NONE = 0xFFFFFFFFu;
+constexpr uint32_t SPEC_MIN_LEN = 128;  // events per segment at least
+constexpr uint32_t SPEC_MAX_PEND = 6;   // ops pending at a cut at most (the lane phase)
+
+// A wave-uniform value the compiler cannot prove uniform (a reduction's
+// result, an LDS read): into a scalar register, so control flow on it stays
+// scalar (no EXEC masking).
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni(uint64_t x) {
+    return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
+}
+
+// Segment boundaries balance the search's cost, not the event count: with
+// the compact lattice an :ok costs about 1.4 events' time with 7-8 ops
+// pending and about 20 with 9-10 (LC_SPEC_STAMPS fit on C2).  Weights in
+// 1/16 event.
+constexpr uint32_t SPEC_W_EV = 16, SPEC_W_DENSE = 6, SPEC_W_DEEP = 320;
+
+// Two passes over a key's events (64 per step, pending counts by wave scan):
+// the total weight, then for s = 1 .. eff-1 the first event position whose
+// preceding weight reaches s/eff of it -- lane s of pos_v -- and the ops
+// pending there (lane s of pend_v).
+__device__ __forceinline__ void spec_targets(const uint32_t *evp, uint32_t nev, uint32_t eff, uint32_t &pos_v,
+                                             int32_t &pend_v) {
+    const uint32_t lane = lane_id();
+    uint64_t tot = 0;
+    uint32_t next = 1;
+    uint64_t target = 0;
+    pos_v = nev;
+    pend_v = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        uint64_t cum = 0;  // weight before this chunk
+        int32_t cnt = 0;   // ops pending before this chunk
+        if (pass == 1) target = tot * next / eff;
+        for (uint32_t base = 0; base < nev && (pass == 0 || next < eff); base += 64) {
+            const uint32_t j = base + lane;
+            const bool in = j < nev;
+            const uint32_t w = in ? evp[j] : 0u;
+            const bool ok = (w >> 31) != 0;
+            const int32_t d = in ? (ok ? -1 : 1) : 0;
+            const int32_t after = cnt + wave_scan(d);  // pending after event j
+            const int32_t before = after - d;
+            const int32_t wt = !in ? 0 : (int32_t)SPEC_W_EV + (ok ? (before >= 9 ? (int32_t)SPEC_W_DEEP
+                                                                  : before >= 7 ? (int32_t)SPEC_W_DENSE : 0) : 0);
+            const int32_t incl = wave_scan(wt);
+            if (pass == 1) {
+                const uint64_t wb = cum + (uint64_t)(incl - wt);  // weight before event j
+                for (;;) {
+                    const uint64_t hit = __ballot(in && wb >= target);
+                    if (!hit || next >= eff) break;
+                    const uint32_t l = (uint32_t)__builtin_ctzll(hit);
+                    const uint32_t at = base + l;
+                    const int32_t pa = __builtin_amdgcn_readlane(before, l);
+                    pos_v = lane == next ? at : pos_v;
+                    pend_v = lane == next ? pa : pend_v;
+                    ++next;
+                    target = tot * next / eff;
+                }
+            }
+            cum += (uint64_t)uni((uint32_t)__builtin_amdgcn_readlane(incl, 63));
+            cnt = uni(__builtin_amdgcn_readlane(after, 63));
+        }
+        tot = cum;
+    }
+}
+
+// The cut for target position t (c_t ops pending there): of the boundaries t
+// .. t + 64 (t + i = before event t + i), the one with the fewest ops pending,
+// the earliest of those, if that is at most SPEC_MAX_PEND and it lies inside
+// the key; else SPEC_NONE.  n_at: ops pending at the cut.
+__device__ __forceinline__ uint32_t spec_cut_at(const uint32_t *evp, uint32_t nev, uint32_t t, int32_t c_t,
+                                                uint32_t &n_at) {
+    const uint32_t lane = lane_id();
+    const uint32_t j = t + lane;  // event j; boundary j + 1 after it
+    const int32_t d = j < nev ? 1 - 2 * (int32_t)(evp[j] >> 31) : 0;
+    const int32_t cnt = c_t + wave_scan(d);
+    uint32_t key = (j + 1u < nev && cnt >= 0 && cnt <= (int32_t)SPEC_MAX_PEND) ? ((uint32_t)cnt << 7) | (lane + 1u)
+                                                                               : ~0u;
+    if (lane == 0 && t < nev && c_t >= 0 && c_t <= (int32_t)SPEC_MAX_PEND) key = min(key, (uint32_t)c_t << 7);
+    const uint32_t best = uni(__ockl_wfred_min_u32(key));
+    if (best == ~0u) return SPEC_NONE;
+    n_at = best >> 7;
+    return t + (best & 127u);
+}
+
+// The ops pending at boundary c (n expected, n <= 6): each slot is decided by
+// its last event before c, walking back.  Returns their :invoke words in slot
+// order, word j in lane j; found = how many.
+__device__ __forceinline__ uint32_t spec_pending(const uint32_t *evp, uint32_t c, uint32_t n, uint32_t &found) {
+    const uint32_t lane = lane_id();
+    uint64_t seen = 0, pm = 0;
+    uint32_t byslot = 0;
+    found = 0;
+    n = min(n, SPEC_MAX_PEND);
+    for (uint32_t j = c; found < n && j > 0;) {
+        const uint32_t base = j > 64u ? j - 64u : 0u, cnt = j - base;
+        const uint32_t w = lane < cnt ? evp[base + lane] : 0u;
+        for (int32_t i = (int32_t)cnt - 1; i >= 0 && found < n; --i) {
+            const uint32_t wi = __builtin_amdgcn_readlane(w, i);
+            const uint32_t sl = LC_EV_SLOT(wi) & 63u;
+            if (!((seen >> sl) & 1ull)) {
+                seen |= 1ull << sl;
+                if (!(wi & LC_EV_OK_BIT)) {
+                    pm |= 1ull << sl;
+                    byslot = lane == sl ? wi : byslot;
+                    ++found;
+                }
+            }
+        }
+        j = base;
+    }
+    uint32_t words = 0;
+    for (uint32_t k = 0; k < found; ++k) {
+        const uint32_t sl = (uint32_t)__builtin_ctzll(pm);
+        pm &= pm - 1;
+        const uint32_t wi = __builtin_amdgcn_readlane(byslot, sl);
+        words = lane == k ? wi : words;
+    }
+    return words;
+}
+
+// Register-tier state of a walk (the lane phase's registers).
+struct SpecState {
+    uint32_t W0, k_v, cap_v, b_v, slot_v, dense_v, n, live;
+};
+
+// The ops pending at a cut (words in lanes 0 .. n-1, slot order) take op
+// indices 0 .. n-1.
+__device__ __forceinline__ void spec_setup(SpecState &st, uint32_t words, uint32_t n, const uint32_t *trp,
+                                           uint32_t ntr) {
+    const uint32_t lane = lane_id();
+    const bool me = lane < n;
+    const uint32_t t = LC_EV_TRANS(words);
+    const Xfer x = xfer_of((me && t < ntr) ? trp[t] : 0u);
+    st.k_v = me ? x.k : 0u;
+    st.cap_v = me ? x.cap : 0u;
+    st.b_v = me ? x.b : 0u;
+    st.slot_v = me ? (LC_EV_SLOT(words) & 63u) : 0u;
+    st.dense_v = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, j);
+        st.dense_v = lane == sl ? j : st.dense_v;
+    }
+    st.n = n;
+    st.live = (1u << n) - 1u;
+}
+
+// Events [b, e_end) of a key from st, on the compact lattice with closed sets
+// (the register tier's FAST path).  MODE 0 (TOP run): records the set after
+// the first lane-phase :ok at or past b + ck1 and past b + ck2 into ck_w /
+// ck_e.  MODE 1 (verifying run): compares with them at those events.
+// Returns 0 alive at e_end (st: the walk's state there; st.W0 the lattice if
+// st.n <= 6), 1 dead at fev, 3 the key does not fit the register tier,
+// 4 (MODE 1) met the TOP run, 5 (MODE 1) passed both checkpoints unmet.
+// The 9-10-pending workspace: one of the workgroup's NWS LDS slots while one
+// is free (busy flags in LDS), else the wave's global slot (an :ok there costs
+// ~40k cycles against ~2k in LDS).  NWS = 1, 2, 4 slots for 2, 4, 8 waves
+// keep 4 waves per SIMD within the CU's LDS.
+template <int S>
+constexpr int spec_lds_ws() { return S <= 2 ? 1 : S <= 4 ? 2 : 4; }
+template <int MODE, int NWS>
+__device__ __forceinline__ int spec_walk(const uint32_t *evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
+                                         uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
+                                         int32_t *lds_busy, uint32_t (*ck_w)[64], int32_t *ck_e, uint32_t ck1,
+                                         uint32_t ck2, uint32_t &fev_out) {
+    constexpr int RM = T0_RSMALL;
+    const uint32_t lane = lane_id();
+    LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
+    int32_t held = -1;  // LDS slot held
+    const uint32_t *const ep = evp + b;
+    const uint32_t nev = e_end - b;
+    auto ldesc = [&](uint32_t w, bool have) -> uint32_t {
+        const uint32_t t = LC_EV_TRANS(w);
+        return (have && !(w & LC_EV_OK_BIT) && t < ntr) ? trp[t] : 0u;
+    };
+    uint32_t W[RM];
+#pragma unroll
+    for (int k = 0; k < RM; ++k) W[k] = 0;
+    bool in_mem = false;
+    uint32_t k_v = st.k_v, cap_v = st.cap_v, b_v = st.b_v, slot_v = st.slot_v, dense_v = st.dense_v;
+    uint32_t n = st.n, live = st.live;
+    uint32_t lm[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) lm[q] = (uint32_t)__builtin_amdgcn_sbfe((int)lane, q, 1);
+    int status = 0;
+    uint32_t fev = 0;
+    uint32_t ev = lane < nev ? ep[lane] : 0u;
+    uint32_t dsc = ldesc(ev, lane < nev);
+    uint32_t ev_n = 64 + lane < nev ? ep[64 + lane] : 0u;
+    uint32_t dsc_n = ldesc(ev_n, 64 + lane < nev);
+    uint32_t ev_nn = 128 + lane < nev ? ep[128 + lane] : 0u;
+    Xfer xc = xfer_of(dsc);
+    uint32_t e = 0, i = 0, base = 0, lim = nev;
+    auto advance = [&]() {
+        ++e;
+        if (++i == 64u) {
+            i = 0; base += 64;
+            ev = ev_n; dsc = dsc_n; ev_n = ev_nn;
+            xc = xfer_of(dsc);
+            dsc_n = ldesc(ev_n, base + 64 + lane < nev);
+            ev_nn = base + 128 + lane < nev ? ep[base + 128 + lane] : 0u;
+        }
+    };
+    // next checkpoint (relative event; ~0u: none)
+    uint32_t ck_i = 0;
+    uint32_t ck_at = MODE == 0 ? ck1 : (uni(ck_e[0]) >= 0 ? (uint32_t)uni(ck_e[0]) - b : ~0u);
+    uint32_t W0 = st.W0;
+    bool dirty = true;
+    for (uint32_t phase = 0; phase <= nev && e < lim; ++phase) {
+        while (e < lim) {  // lane phase: <= 6 pending
+            const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
+            const uint32_t slot = LC_EV_SLOT(evi);
+            if (!(evi & LC_EV_OK_BIT)) {
+                if (n == 6) break;
+                if (n >= T0_MAX_WIDTH || slot >= 64) {
+                    status = 3;
+                } else {
+                    const uint32_t idx = (uint32_t)__builtin_ctz(~live);
+                    const bool me = lane == idx;
+                    slot_v = me ? slot : slot_v;
+                    k_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.k, i) : k_v;
+                    cap_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.cap, i) : cap_v;
+                    b_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.b, i) : b_v;
+                    dense_v = lane == slot ? idx : dense_v;
+                    live |= 1u << idx;
+                    ++n;
+                    dirty = true;
+                }
+            } else {
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
+                int r;
+                // closed sets: exact ones (ok_lane, as the wide T0 keeps
+                // them) measured 10 % slower per event here
+                const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
+                if (top >= 6) r = ok_lane_closed<6>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                dirty = false;
+                k_v = lane == p ? 0u : k_v;
+                live = r ? live : live & ~(1u << p);
+                n = r ? n : n - 1;
+                status = r;
+                fev = e;
+                if (!r && e >= ck_at) {  // a checkpoint (a lane-phase :ok: the set is canonical)
+                    if constexpr (MODE == 0) {
+                        ck_w[ck_i][lane] = W0;
+                        if (lane == 0) ck_e[ck_i] = (int32_t)(b + e);
+                        ++ck_i;
+                        ck_at = ck_i < 2 ? max(ck2, e + 1u) : ~0u;
+                    } else {
+                        if (!__any(W0 != ck_w[ck_i][lane])) {
+                            status = 4;
+                        } else {
+                            ++ck_i;
+                            const int32_t nx = ck_i < 2 ? uni(ck_e[ck_i & 1]) : -1;
+                            ck_at = nx >= 0 ? (uint32_t)nx - b : ~0u;
+                            if (ck_i == 2) status = 5;
+                        }
+                    }
+                }
+            }
+            lim = status ? 0u : lim;
+            advance();
+        }
+        if (e >= lim) break;
+        W[0] = W0;
+#pragma unroll
+        for (int k = 1; k < RM; ++k) W[k] = 0u;
+        while (e < lim) {  // dense phase: 7-10 pending
+            const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
+            const uint32_t slot = LC_EV_SLOT(evi);
+            if (!(evi & LC_EV_OK_BIT)) {
+                if (n >= T0_MAX_WIDTH || slot >= 64) {
+                    status = 3;
+                } else {
+                    if (n == 8) {  // 9 pending: the lattice moves to the workspace
+                        int32_t got = -1;
+                        if (lane == 0) {
+                            for (int q = 0; q < NWS && got < 0; ++q)
+                                if (atomicCAS(&lds_busy[q], 0, 1) == 0) got = q;
+                        }
+                        held = uni(got);
+                        uint32_t *const mb = held >= 0 ? lds_ws + (size_t)held * (3 * T0_RMEM * 64) : ws;
+                        m = LatMem{mb, mb + T0_RMEM * 64, mb + 2 * T0_RMEM * 64};
+#pragma unroll
+                        for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < RM ? W[k < RM ? k : 0] : 0u;
+                        in_mem = true;
+                    }
+                    const uint32_t idx = n;
+                    const bool me = lane == idx;
+                    slot_v = me ? slot : slot_v;
+                    k_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.k, i) : k_v;
+                    cap_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.cap, i) : cap_v;
+                    b_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.b, i) : b_v;
+                    dense_v = lane == slot ? idx : dense_v;
+                    live |= 1u << idx;
+                    ++n;
+                }
+            } else {
+                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
+                uint32_t nSn = 0, probes = 0;
+                int r;
+                if (n == 7) r = ok_reg<2, RM>(W, p, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
+                else if (n == 8) r = ok_reg<4, RM>(W, p, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
+#ifdef LC_SPEC_MEM_OLD  // A/B build: the bidirectional per-row closure
+                else if (n == 9) r = ok_event_mem<8>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
+                else r = ok_event_mem<16>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
+#else
+                else if (n == 9) r = ok_event_mem_gs<8>(m, p, n, k_v, cap_v, b_v, lane);
+                else r = ok_event_mem_gs<16>(m, p, n, k_v, cap_v, b_v, lane);
+#endif
+                const uint32_t last = n - 1;
+                const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
+                const uint32_t x0 = __builtin_amdgcn_readlane(k_v, last), x1 = __builtin_amdgcn_readlane(cap_v, last),
+                               x2 = __builtin_amdgcn_readlane(b_v, last);
+                const bool mp = lane == p && !r;
+                slot_v = mp ? s_last : slot_v;
+                k_v = mp ? x0 : k_v;
+                cap_v = mp ? x1 : cap_v;
+                b_v = mp ? x2 : b_v;
+                dense_v = (lane == s_last && !r) ? p : dense_v;
+                k_v = (lane == last && !r) ? 0u : k_v;
+                live = r ? live : (1u << last) - 1u;
+                if (in_mem && n == 9 && !r) {
+#pragma unroll
+                    for (int k = 0; k < RM; ++k) W[k] = m.W[k * 64 + lane];
+                    in_mem = false;
+                    if (held >= 0 && lane == 0) atomicExch(&lds_busy[held], 0);
+                    held = -1;
+                }
+                n = r ? n : n - 1;
+                status = r;
+                fev = e;
+            }
+            lim = status ? 0u : lim;
+            advance();
+            if (n <= 6) break;
+        }
+        W0 = W[0];
+        dirty = true;
+    }
+    if (held >= 0 && lane == 0) atomicExch(&lds_busy[held], 0);
+    st.W0 = W0;
+    st.k_v = k_v; st.cap_v = cap_v; st.b_v = b_v; st.slot_v = slot_v; st.dense_v = dense_v;
+    st.n = n; st.live = live;
+    fev_out = b + fev;
+    return status;
+}
+
+#ifdef LC_SPEC_STAMPS
+// Diagnostic build only: per (block, wave) clock stamps of the phases.
+__device__ unsigned long long lc_spec_stamps[4096 * 8 * 12];
+extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(lc_spec_stamps), (size_t)n * 8 * 12 * 8, 0, hipMemcpyDeviceToHost);
+}
+#define SPEC_STAMP(k, v) \
+    if (lane == 0 && blockIdx.x < 4096) lc_spec_stamps[((size_t)blockIdx.x * 8 + wv) * 12 + (k)] = (v);
+#else
+#define SPEC_STAMP(k, v)
+#endif
+
+// One workgroup of S waves per key (blockIdx = LPT position).  Results go
+// through a.full like T0's; a.lat_ws holds each wave's 9-10-pending
+// workspace (global memory: with LDS for it, fewer segments fit a CU).
+template <int S>
+__global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
+    __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
+    __shared__ uint32_t s_ck[S][2][64];   // TOP run's checkpoint sets
+    __shared__ uint32_t s_pend[S][8];     // ops pending at the cut ([0..5] words, [6] count)
+    __shared__ uint64_t s_map[S];         // end: byte i = 0x80 | slot of live op index i
+    __shared__ int32_t s_ck_e[S][2];      // checkpoint events (-1: none)
+    __shared__ int32_t s_cut[S], s_segend[S];  // segment [cut, end); cut -1: no segment
+    __shared__ int32_t s_top[S];          // TOP run: -1 alive, -2 does not fit, else its failing event
+    __shared__ int32_t s_ver[S], s_vfev[S];
+    constexpr int NWS = spec_lds_ws<S>();
+    __shared__ uint32_t s_ws[NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
+    __shared__ int32_t s_ws_busy[NWS];
+    const uint32_t lane = lane_id(), wv = uni((uint32_t)threadIdx.x >> 6);  // uniform per wave
+    const int32_t key = a.order[blockIdx.x];
+    uint32_t *ws = a.lat_ws + ((size_t)blockIdx.x * S + wv) * (3 * T0_RMEM * 64);
+    const uint64_t eb = a.ev_off[key];
+    const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
+    const uint32_t *const evp = a.events + eb;
+    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
+    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
+    const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
+    const uint32_t nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
+    const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;
+    // keys for the unsegmented search: errors, keys outside the tier (it
+    // reports them), and keys too short to cut
+    const bool plain = (a.key_error && a.key_error[key]) || nstates > T0_MAX_STATES || nstates == 0 ||
+                       width > T0_MAX_WIDTH || a.init_state >= T0_MAX_STATES || nev < 2 * SPEC_MIN_LEN;
+    const uint32_t eff = plain ? 1u : min((uint32_t)S, nev / SPEC_MIN_LEN);
+    const uint32_t topmask = nstates >= 32 ? ~0u : (1u << nstates) - 1u;
+
+    if (threadIdx.x < NWS) s_ws_busy[threadIdx.x] = 0;
+    __syncthreads();
+    SPEC_STAMP(0, __builtin_amdgcn_s_memtime())
+    SPEC_STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                      ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32))
+    SPEC_STAMP(9, (unsigned long long)key)
+    // 1. every segment from TOP (segment 0 exactly)
+    if (!plain && wv < eff) {
+        uint32_t pos_v;
+        int32_t pend_v;
+        spec_targets(evp, nev, eff, pos_v, pend_v);
+        // every cut (each wave computes them all, so all agree): a cut is
+        // kept if it lies past the last kept one
+        uint32_t cut = 0, end = nev, n0 = 0, last = 0;
+        for (uint32_t s2 = 1; s2 < eff; ++s2) {
+            uint32_t n2 = 0;
+            uint32_t c2 = spec_cut_at(evp, nev, uni(__builtin_amdgcn_readlane(pos_v, s2)),
+                                      uni(__builtin_amdgcn_readlane(pend_v, s2)), n2);
+            if (c2 != SPEC_NONE && c2 <= last) c2 = SPEC_NONE;
+            if (c2 != SPEC_NONE) last = c2;
+            if (s2 == wv) { cut = c2; n0 = n2; }
+            if (s2 > wv && c2 != SPEC_NONE && end == nev) end = c2;
+        }
+        if (lane == 0) {
+            s_cut[wv] = cut == SPEC_NONE ? -1 : (int32_t)cut;
+            s_segend[wv] = (int32_t)end;
+            s_ck_e[wv][0] = s_ck_e[wv][1] = -1;
+            s_top[wv] = -1;
+        }
+        SPEC_STAMP(1, __builtin_amdgcn_s_memtime())
+        SPEC_STAMP(6, ((unsigned long long)end << 32) | cut)
+        if (cut != SPEC_NONE) {
+            SpecState st{};
+            uint32_t words = 0, np = 0;
+            if (wv == 0) {
+                st.W0 = lane == 0 ? 1u << a.init_state : 0u;
+            } else {
+                words = spec_pending(evp, cut, n0, np);
+                spec_setup(st, words, np, trp, ntr);
+                st.W0 = lane < (1u << np) ? topmask : 0u;
+            }
+            if (lane < 6) s_pend[wv][lane] = words;
+            if (lane == 6) s_pend[wv][6] = np;
+            uint32_t fev = 0;
+            const int r = spec_walk<0, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[wv], s_ck_e[wv],
+                                       a.spec_ck1, a.spec_ck2, fev);
+            s_end[wv][lane] = st.W0;
+            uint64_t map = 0;
+            for (uint32_t q = 0; q < 6; ++q) {
+                const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, q);
+                if ((st.live >> q) & 1u) map |= (uint64_t)(0x80u | sl) << (8 * q);
+            }
+            SPEC_STAMP(2, __builtin_amdgcn_s_memtime())
+            if (lane == 0) {
+                s_map[wv] = map;
+                s_top[wv] = r == 1 ? (int32_t)fev : r == 3 ? -2 : -1;
+            }
+        }
+    }
+    __syncthreads();
+    SPEC_STAMP(3, __builtin_amdgcn_s_memtime())
+    // 2. every segment s >= 1 again, from the set segment s - 1 ended with,
+    // until the runs meet
+    if (!plain && wv >= 1 && wv < eff && uni(s_cut[wv]) >= 0) {
+        uint32_t pw = wv - 1;
+        while (uni(s_cut[pw]) < 0) --pw;  // s_cut[0] = 0
+        int32_t ver = 0, vfev = -1;
+        if (uni(s_top[pw]) == -1) {
+            const uint32_t cut = (uint32_t)uni(s_cut[wv]), end = (uint32_t)uni(s_segend[wv]);
+            const uint32_t np = uni(s_pend[wv][6]);
+            SpecState st{};
+            spec_setup(st, lane < 6 ? s_pend[wv][lane] : 0u, np, trp, ntr);
+            // the predecessor's end set, relabelled from its op indices to these
+            const uint64_t map = uni(s_map[pw]);
+            uint32_t src = 0;
+            for (uint32_t j = 0; j < np; ++j) {
+                const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, j);
+                uint32_t at = 31;
+                for (uint32_t q = 0; q < 6; ++q)
+                    if (((map >> (8 * q)) & 0xFFu) == (0x80u | sl)) at = q;
+                src |= ((lane >> j) & 1u) << at;
+            }
+            const uint32_t E = (uint32_t)__shfl((int)s_end[pw][lane], (int)(src & 63u));
+            st.W0 = lane < (1u << np) ? E : 0u;
+            uint32_t fev = 0;
+            const int r = spec_walk<1, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[wv], s_ck_e[wv], 0, 0,
+                                       fev);
+            bool last = true;
+            for (uint32_t q = wv + 1; q < eff; ++q) last = last && uni(s_cut[q]) < 0;
+            if (r == 4) ver = 1;                        // met the TOP run
+            else if (r == 1) { ver = 2; vfev = (int32_t)fev; }  // died before meeting it
+            else if (r == 3) ver = 6;                   // does not fit
+            else if (r == 5) ver = 3;                   // never met
+            else if (last) ver = 5;                     // the last segment, searched exactly to its end
+            else ver = (st.n <= 6 && !__any(st.W0 != s_end[wv][lane])) ? 1 : 3;
+            SPEC_STAMP(7, ((unsigned long long)ver << 32) | (fev - cut))
+        }
+        SPEC_STAMP(4, __builtin_amdgcn_s_memtime())
+        if (lane == 0) { s_ver[wv] = ver; s_vfev[wv] = vfev; }
+    }
+    __syncthreads();
+    SPEC_STAMP(5, __builtin_amdgcn_s_memtime())
+    // 3. the key's verdict: the first segment whose real run dies
+    if (wv == 0) {
+        const Args &f = *a.full;
+        bool rerun = plain, bad = false;
+        int32_t fv = -1;
+        if (!plain) {
+            for (uint32_t s = 0; s < eff && fv < 0 && !rerun && !bad; ++s) {
+                if (uni(s_cut[s]) < 0) continue;
+                const int32_t top = uni(s_top[s]);
+                if (top == -2) { bad = true; break; }
+                if (s == 0) { fv = top; continue; }
+                const int32_t ver = uni(s_ver[s]);
+                if (ver == 1) fv = top;
+                else if (ver == 2) fv = uni(s_vfev[s]);
+                else if (ver == 6) bad = true;
+                else if (ver != 5) rerun = true;  // never met (or nothing to start from): unsegmented
+            }
+        }
+        int kr = K_DONE;
+        if (rerun) kr = lattice_key<T0_RSMALL, true>(a, key, ws);
+        else if (bad) kr = K_SPILL;
+        else if (fv >= 0) finish_key(f, key, LC_INVALID, LC_CAUSE_NONLIN, fv, 0, 0, (uint64_t)fv + 1u);
+        else finish_key(f, key, LC_VALID, LC_CAUSE_NONE, -1, 0, 0, nev);
+        if (kr == K_SPILL) {
+            if (a.flags & T0_STRICT) {
+                t0_malformed(a, key, LC_BATCH_E_FIT);
+                finish_key(f, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+            } else {
+                const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
+                push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key, f.list_cap);
+            }
+        }
+    }
+}
+
+size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * lat_ws_words(); }
+
+// Keys order[0 .. n_order) in workgroups of `segs` segments (2, 4 or 8);
+// ws: spec_ws_words(n_order, segs) words.
+hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, uint32_t ck1, uint32_t ck2,
+                       hipStream_t s) {
+    T0Args t = make_t0(a, a_dev);
+    t.lat_ws = ws;
+    t.spec_ck1 = ck1;
+    t.spec_ck2 = ck2;
+    const dim3 grid((unsigned)std::max(1, a.n_order));
+    if (segs >= 8) hipLaunchKernelGGL(k_spec<8>, grid, dim3(512), 0, s, t);
+    else if (segs >= 4) hipLaunchKernelGGL(k_spec<4>, grid, dim3(256), 0, s, t);
+    else hipLaunchKernelGGL(k_spec<2>, grid, dim3(128), 0, s, t);
     return hipGetLastError();
 }
 

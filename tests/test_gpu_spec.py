@@ -1,0 +1,98 @@
+"""Speculative key segments (device_lattice.hip, "Speculative key segments"):
+verdict-only register-tier steps of about one key per SIMD or fewer search
+every key as a workgroup of segment waves -- each segment from the full
+config set, then again from its predecessor's end set until the two runs
+meet -- and walk the segments in order.  Verdicts, causes and failing events
+must equal the oracle's and the unsegmented search's, whatever the segment
+count and checkpoint distances (tiny distances make runs miss each other and
+exercise the fallback to the unsegmented search)."""
+import os
+
+import numpy as np
+import pytest
+
+import cref
+from lincheck import history as H
+from lincheck.checker import Device, Packed
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {
+    "c2": dict(n_keys=400, ops_per_key=1000, concurrency=10, seed=91),
+    "c5": dict(n_keys=400, ops_per_key=1000, concurrency=10, anomaly_rate=0.2, seed=92),
+    "late_anomalies": dict(n_keys=200, ops_per_key=2000, concurrency=8, anomaly_rate=0.5, seed=93),
+    "low_concurrency": dict(n_keys=300, ops_per_key=800, concurrency=3, anomaly_rate=0.2, seed=94),
+    "crashed": dict(n_keys=300, ops_per_key=800, concurrency=6, info_rate=0.002, anomaly_rate=0.2, seed=95),
+    "two_values": dict(n_keys=300, ops_per_key=800, concurrency=9, n_values=2, anomaly_rate=0.2, seed=96),
+    "wide": dict(n_keys=200, ops_per_key=1500, concurrency=10, mean_think=0.3, anomaly_rate=0.2, seed=97),
+    "short_keys": dict(n_keys=500, ops_per_key=150, concurrency=10, anomaly_rate=0.2, seed=98),
+    "think20": dict(n_keys=64, ops_per_key=3000, concurrency=10, mean_think=20.0, anomaly_rate=0.25, seed=99),
+}
+ENV = ("LC_SPEC", "LC_SPEC_SEGS", "LC_SPEC_CK1", "LC_SPEC_CK2", "LC_SPLIT")
+
+
+@pytest.fixture
+def spec_env():
+    saved = {k: os.environ.get(k) for k in ENV}
+    yield os.environ
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+def _check(dev, pk, orc, what):
+    r = dev.check(pk, verdicts_only=True)
+    np.testing.assert_array_equal(r.valid, orc["valid"], err_msg=f"{what}: valid")
+    np.testing.assert_array_equal(r.cause, orc["cause"], err_msg=f"{what}: cause")
+    np.testing.assert_array_equal(r.fail_event, orc["fail_event"], err_msg=f"{what}: fail_event")
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_spec_matches_oracle(shape, spec_env):
+    h = H.synth(**SHAPES[shape])
+    pk = Packed(h)
+    dev = Device(0)
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    spec_env["LC_SPLIT"] = "0"
+    spec_env["LC_SPEC"] = "0"
+    _check(dev, pk, orc, "unsegmented")
+    spec_env["LC_SPEC"] = "1"
+    for segs in ("2", "4", "8"):
+        spec_env["LC_SPEC_SEGS"] = segs
+        for ck in (("32", "160"), ("1", "2"), ("0", "0")):
+            spec_env["LC_SPEC_CK1"], spec_env["LC_SPEC_CK2"] = ck
+            _check(dev, pk, orc, f"segs {segs} ck {ck}")
+    if SHAPES[shape].get("anomaly_rate"):
+        assert (orc["valid"] == 0).any()
+
+
+def test_spec_default_on_c2_shape(spec_env):
+    """The default choice for a C2-sized verdicts-only batch is the
+    speculative path (checked through its result only: same as the oracle)."""
+    for k in ENV:
+        spec_env.pop(k, None)
+    h = H.synth(n_keys=1000, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=100)
+    pk = Packed(h)
+    dev = Device(0)
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    _check(dev, pk, orc, "default")
+
+
+def test_spec_resident_async(spec_env):
+    """The bench's resident steps (node records, asynchronous) on the speculative path."""
+    for k in ENV:
+        spec_env.pop(k, None)
+    spec_env["LC_SPEC"] = "1"
+    h = H.synth(n_keys=1000, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=101)
+    pk = Packed(h)
+    dev = Device(0)
+    db = dev.upload(pk)
+    for _ in range(5):
+        db.check_node(pk.n_keys, asynchronous=True)
+    dev.wait()
+    rec = dev.node_records(pk.n_keys).astype(np.int64)
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    np.testing.assert_array_equal((rec & 0xFF) - 1, orc["valid"])
+    np.testing.assert_array_equal((rec >> 16) - 1, orc["fail_event"])
