@@ -279,9 +279,16 @@ struct Dev {
     uint32_t *peak = nullptr;
     uint64_t *final_cfg = nullptr;
     uint32_t *n_final = nullptr;
-    lcd::Args *dargs = nullptr;    // device copy of T0's Args (read once per key)
-    lcd::Args *hargs = nullptr;    // its pinned host staging copy (copied only when it changes)
-    bool hargs_valid = false;
+    // Device copies of T0's Args (read once per key): a ring of 4, so steps
+    // alternating between result sets (the N > 1 bench) each find theirs
+    // without a copy; a slot's pinned staging copy is rewritten only after
+    // the copy out of it (args_ev) has run.
+    static constexpr int ARGS_RING = 4;
+    lcd::Args *dargs = nullptr;    // [ARGS_RING]
+    lcd::Args *hargs = nullptr;    // [ARGS_RING] pinned
+    hipEvent_t args_ev[ARGS_RING] = {};
+    bool args_ok[ARGS_RING] = {};
+    uint32_t args_next = 0;
     DevBatch *staged = nullptr;    // lc_check_batch's staging batch (device arrays reused)
     // T0-only steps skip re-zeroing the control block: the ticket continues
     // from where the previous such step left it.
@@ -316,6 +323,8 @@ struct Dev {
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
         dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws);
         if (hargs) (void)hipHostFree(hargs);
+        for (hipEvent_t &e : args_ev)
+            if (e) (void)hipEventDestroy(e);
         delete staged;
         if (vstream) (void)hipStreamSynchronize(vstream);
         for (hipEvent_t e : {e0, e1, et0, et3a, et3b, ea0, ea1, vin, vdone})
@@ -365,7 +374,7 @@ static int ensure_capacity(Dev *c, int64_t n_keys) {
     HIPCHK(dalloc(&c->final_cfg, (size_t)cap * (size_t)c->o->max_final * 2));
     HIPCHK(dalloc(&c->n_final, (size_t)cap));
     c->cap_keys = cap;
-    c->hargs_valid = false;
+    for (bool &v : c->args_ok) v = false;
     return LC_OK;
 }
 
@@ -439,8 +448,9 @@ static int dev_init(Dev *c, int device) {
     HIPCHK(hipMemset(c->ctl, 0, CTL_BYTES));
     HIPCHK(hipHostMalloc((void **)&c->hctl, 16 * sizeof(unsigned long long), hipHostMallocDefault));
     std::memset(c->hctl, 0, 16 * sizeof(unsigned long long));
-    HIPCHK(dalloc(&c->dargs, 1));
-    HIPCHK(hipHostMalloc((void **)&c->hargs, sizeof(lcd::Args), hipHostMallocDefault));
+    HIPCHK(dalloc(&c->dargs, Dev::ARGS_RING));
+    HIPCHK(hipHostMalloc((void **)&c->hargs, sizeof(lcd::Args) * Dev::ARGS_RING, hipHostMallocDefault));
+    for (hipEvent_t &e : c->args_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return LC_OK;
 }
 
@@ -937,14 +947,21 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     const int g0 = (int)std::max<int64_t>(1, std::min<int64_t>(K, (int64_t)c->cu_count * (t0_wide ? 8 : 16)));
     a0.lat_ws = nullptr;
     // T0 reads the result/counter/list pointers from a device copy of its
-    // Args, refreshed only when they change
-    if (!c->hargs_valid || std::memcmp(c->hargs, &a0, sizeof a0) != 0) {
-        // the pinned staging copy may still feed an enqueued copy
-        if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
-        std::memcpy(c->hargs, &a0, sizeof a0);
-        HIPCHK(hipMemcpyAsync(c->dargs, c->hargs, sizeof(lcd::Args), hipMemcpyHostToDevice, c->stream));
-        c->hargs_valid = true;
+    // Args: a ring slot holding these Args, else the next slot, refreshed
+    // (device copies are rewritten in stream order, after the launches that
+    // read them)
+    int aslot = -1;
+    for (int q = 0; q < Dev::ARGS_RING && aslot < 0; ++q)
+        if (c->args_ok[q] && std::memcmp(c->hargs + q, &a0, sizeof a0) == 0) aslot = q;
+    if (aslot < 0) {
+        aslot = (int)(c->args_next++ % Dev::ARGS_RING);
+        HIPCHK(hipEventSynchronize(c->args_ev[aslot]));  // its staging copy has been read
+        std::memcpy(c->hargs + aslot, &a0, sizeof a0);
+        HIPCHK(hipMemcpyAsync(c->dargs + aslot, c->hargs + aslot, sizeof(lcd::Args), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipEventRecord(c->args_ev[aslot], c->stream));
+        c->args_ok[aslot] = true;
     }
+    lcd::Args *const dargs = c->dargs + aslot;
     HIPCHK(hipEventRecord(c->e0, c->stream));
     if (async && c->n_async == 0) HIPCHK(hipEventRecord(c->ea0, c->stream));
     if (K > 0 && a.strict) {
@@ -977,10 +994,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     } else if (spec) {
         const uint32_t ck1 = std::getenv("LC_SPEC_CK1") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK1")) : 32u;
         const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 160u;
-        HIPCHK(lcd::launch_spec(a0, c->dargs, segs, c->spec_ws, ck1, ck2, c->stream));
+        HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, ck1, ck2, c->stream));
         HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0) {
-        HIPCHK(lcd::launch_t0(a0, c->dargs, g0, t0_wide, c->stream, ticket_base));
+        HIPCHK(lcd::launch_t0(a0, dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
     }
     if (K > 0 && a.strict) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));

@@ -1603,57 +1603,43 @@ __device__ __forceinline__ uint64_t uni(uint64_t x) {
     return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
 }
 
-// Segment boundaries balance the search's cost, not the event count: with
-// the compact lattice an :ok costs about 1.4 events' time with 7-8 ops
-// pending and about 20 with 9-10 (LC_SPEC_STAMPS fit on C2).  Weights in
-// 1/16 event.
-constexpr uint32_t SPEC_W_EV = 16, SPEC_W_DENSE = 6, SPEC_W_DEEP = 320;
-
-// Two passes over a key's events (64 per step, pending counts by wave scan):
-// the total weight, then for s = 1 .. eff-1 the first event position whose
-// preceding weight reaches s/eff of it -- lane s of pos_v -- and the ops
-// pending there (lane s of pend_v).
+// Segment boundaries: targets at s/eff of the key's events (s = 1 .. eff-1),
+// lane s of pos_v, with the ops pending there in lane s of pend_v (one pass
+// of ballots over the events before the last target, 8 chunks' loads in
+// flight).  Weighting :oks by their cost (9-10 pending ones cost ~20 events'
+// time) balanced the segments no better and cost 5x the time here.
 __device__ __forceinline__ void spec_targets(const uint32_t *evp, uint32_t nev, uint32_t eff, uint32_t &pos_v,
                                              int32_t &pend_v) {
+    constexpr uint32_t G = 8;
     const uint32_t lane = lane_id();
-    uint64_t tot = 0;
-    uint32_t next = 1;
-    uint64_t target = 0;
-    pos_v = nev;
+    pos_v = (uint32_t)((uint64_t)nev * lane / eff);
     pend_v = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        uint64_t cum = 0;  // weight before this chunk
-        int32_t cnt = 0;   // ops pending before this chunk
-        if (pass == 1) target = tot * next / eff;
-        for (uint32_t base = 0; base < nev && (pass == 0 || next < eff); base += 64) {
-            const uint32_t j = base + lane;
-            const bool in = j < nev;
-            const uint32_t w = in ? evp[j] : 0u;
-            const bool ok = (w >> 31) != 0;
-            const int32_t d = in ? (ok ? -1 : 1) : 0;
-            const int32_t after = cnt + wave_scan(d);  // pending after event j
-            const int32_t before = after - d;
-            const int32_t wt = !in ? 0 : (int32_t)SPEC_W_EV + (ok ? (before >= 9 ? (int32_t)SPEC_W_DEEP
-                                                                  : before >= 7 ? (int32_t)SPEC_W_DENSE : 0) : 0);
-            const int32_t incl = wave_scan(wt);
-            if (pass == 1) {
-                const uint64_t wb = cum + (uint64_t)(incl - wt);  // weight before event j
-                for (;;) {
-                    const uint64_t hit = __ballot(in && wb >= target);
-                    if (!hit || next >= eff) break;
-                    const uint32_t l = (uint32_t)__builtin_ctzll(hit);
-                    const uint32_t at = base + l;
-                    const int32_t pa = __builtin_amdgcn_readlane(before, l);
-                    pos_v = lane == next ? at : pos_v;
-                    pend_v = lane == next ? pa : pend_v;
-                    ++next;
-                    target = tot * next / eff;
-                }
-            }
-            cum += (uint64_t)uni((uint32_t)__builtin_amdgcn_readlane(incl, 63));
-            cnt = uni(__builtin_amdgcn_readlane(after, 63));
+    const uint32_t t_last = (uint32_t)((uint64_t)nev * (eff - 1) / eff);
+    int32_t cnt = 0;  // ops pending before the chunk
+    uint32_t next = 1, t_next = (uint32_t)((uint64_t)nev / eff);
+    for (uint32_t gb = 0; gb <= t_last; gb += 64 * G) {  // chunks covering [0, t_last]
+        uint32_t wg[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t j = gb + 64 * g + lane;
+            wg[g] = j < t_last ? evp[j] : 0u;
         }
-        tot = cum;
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t base = gb + 64 * g;
+            if (base > t_last) continue;
+            const uint64_t inv = __ballot(base + lane < t_last && !(wg[g] >> 31));
+            const uint64_t oks = __ballot(base + lane < t_last && (wg[g] >> 31));
+            while (next < eff && t_next < base + 64) {  // a target inside this chunk
+                const uint32_t k = t_next - base;
+                const uint64_t below = k >= 64 ? ~0ull : ((1ull << k) - 1ull);
+                const int32_t at = cnt + __popcll(inv & below) - __popcll(oks & below);
+                pend_v = lane == next ? at : pend_v;
+                ++next;
+                t_next = (uint32_t)((uint64_t)nev * next / eff);
+            }
+            cnt += __popcll(inv) - __popcll(oks);
+        }
     }
 }
 
@@ -1661,11 +1647,11 @@ __device__ __forceinline__ void spec_targets(const uint32_t *evp, uint32_t nev, 
 // .. t + 64 (t + i = before event t + i), the one with the fewest ops pending,
 // the earliest of those, if that is at most SPEC_MAX_PEND and it lies inside
 // the key; else SPEC_NONE.  n_at: ops pending at the cut.
-__device__ __forceinline__ uint32_t spec_cut_at(const uint32_t *evp, uint32_t nev, uint32_t t, int32_t c_t,
-                                                uint32_t &n_at) {
+// w: lane i holds event t + i (0 past the key).
+__device__ __forceinline__ uint32_t spec_cut_at(uint32_t w, uint32_t nev, uint32_t t, int32_t c_t, uint32_t &n_at) {
     const uint32_t lane = lane_id();
     const uint32_t j = t + lane;  // event j; boundary j + 1 after it
-    const int32_t d = j < nev ? 1 - 2 * (int32_t)(evp[j] >> 31) : 0;
+    const int32_t d = j < nev ? 1 - 2 * (int32_t)(w >> 31) : 0;
     const int32_t cnt = c_t + wave_scan(d);
     uint32_t key = (j + 1u < nev && cnt >= 0 && cnt <= (int32_t)SPEC_MAX_PEND) ? ((uint32_t)cnt << 7) | (lane + 1u)
                                                                                : ~0u;
@@ -2000,9 +1986,17 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
         // every cut (each wave computes them all, so all agree): a cut is
         // kept if it lies past the last kept one
         uint32_t cut = 0, end = nev, n0 = 0, last = 0;
-        for (uint32_t s2 = 1; s2 < eff; ++s2) {
+        uint32_t wc[S];  // the events after each target, loaded together
+#pragma unroll
+        for (uint32_t s2 = 1; s2 < S; ++s2) {
+            const uint32_t j = uni(__builtin_amdgcn_readlane(pos_v, s2)) + lane;
+            wc[s2] = (s2 < eff && j < nev) ? evp[j] : 0u;
+        }
+#pragma unroll
+        for (uint32_t s2 = 1; s2 < S; ++s2) {
+            if (s2 >= eff) continue;
             uint32_t n2 = 0;
-            uint32_t c2 = spec_cut_at(evp, nev, uni(__builtin_amdgcn_readlane(pos_v, s2)),
+            uint32_t c2 = spec_cut_at(wc[s2], nev, uni(__builtin_amdgcn_readlane(pos_v, s2)),
                                       uni(__builtin_amdgcn_readlane(pend_v, s2)), n2);
             if (c2 != SPEC_NONE && c2 <= last) c2 = SPEC_NONE;
             if (c2 != SPEC_NONE) last = c2;
@@ -2030,8 +2024,11 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
             if (lane < 6) s_pend[wv][lane] = words;
             if (lane == 6) s_pend[wv][6] = np;
             uint32_t fev = 0;
-            const int r = spec_walk<0, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[wv], s_ck_e[wv],
-                                       a.spec_ck1, a.spec_ck2, fev);
+            // the ops found pending must be as many as the count says (else
+            // the event stream is malformed): the key is searched unsegmented
+            const bool lost = wv != 0 && np != n0;
+            const int r = lost ? 6 : spec_walk<0, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[wv],
+                                                        s_ck_e[wv], a.spec_ck1, a.spec_ck2, fev);
             s_end[wv][lane] = st.W0;
             uint64_t map = 0;
             for (uint32_t q = 0; q < 6; ++q) {
@@ -2041,7 +2038,7 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
             SPEC_STAMP(2, __builtin_amdgcn_s_memtime())
             if (lane == 0) {
                 s_map[wv] = map;
-                s_top[wv] = r == 1 ? (int32_t)fev : r == 3 ? -2 : -1;
+                s_top[wv] = r == 1 ? (int32_t)fev : r == 3 ? -2 : r == 6 ? -3 : -1;
             }
         }
     }
@@ -2049,7 +2046,7 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     SPEC_STAMP(3, __builtin_amdgcn_s_memtime())
     // 2. every segment s >= 1 again, from the set segment s - 1 ended with,
     // until the runs meet
-    if (!plain && wv >= 1 && wv < eff && uni(s_cut[wv]) >= 0) {
+    if (!plain && wv >= 1 && wv < eff && uni(s_cut[wv]) >= 0 && uni(s_top[wv]) != -3) {
         uint32_t pw = wv - 1;
         while (uni(s_cut[pw]) < 0) --pw;  // s_cut[0] = 0
         int32_t ver = 0, vfev = -1;
@@ -2098,6 +2095,7 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
                 if (uni(s_cut[s]) < 0) continue;
                 const int32_t top = uni(s_top[s]);
                 if (top == -2) { bad = true; break; }
+                if (top == -3) { rerun = true; break; }
                 if (s == 0) { fv = top; continue; }
                 const int32_t ver = uni(s_ver[s]);
                 if (ver == 1) fv = top;

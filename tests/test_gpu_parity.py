@@ -408,6 +408,61 @@ def test_async_resident_steps():
         np.testing.assert_array_equal(ref.fail_event, orc["fail_event"])
 
 
+def test_wait_step_two_result_sets():
+    """lc_wait_step(1) waits for the asynchronous step before the latest: with
+    two result sets (the N > 1 bench's double buffer), set A is complete --
+    read while step B may still run -- and equals the oracle; a synchronous
+    step (a batch whose keys leave the register tier) between asynchronous
+    ones does not shift which step that is; a `back` beyond the steps on
+    record waits for everything."""
+    import ctypes as C
+    from lincheck import _native as N
+    from lincheck.checker import Packed
+    dev = Device(0)
+    h = H.synth(n_keys=800, ops_per_key=700, concurrency=10, anomaly_rate=0.05, seed=53)
+    pk = Packed(h)
+    db = dev.upload(pk)
+    K = pk.n_keys
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    h2 = H.synth(n_keys=16, ops_per_key=600, concurrency=16, seed=17)  # beyond T0: a synchronous step
+    db2 = dev.upload(Packed(h2))
+
+    def result_set():
+        bufs = (_HipBuf(K), _HipBuf(4 * K), _HipBuf(K))
+        for b in bufs:
+            b.fill(0x5A)
+        r = N.LcResult(C.cast(bufs[0].ptr, N.P(C.c_int8)), C.cast(bufs[1].ptr, N.P(C.c_int32)),
+                       C.cast(bufs[2].ptr, N.P(C.c_uint8)), None, None, None)
+        return bufs, r
+
+    def assert_oracle(bufs):
+        np.testing.assert_array_equal(bufs[0].get(np.int8), orc["valid"])
+        np.testing.assert_array_equal(bufs[1].get(np.int32), orc["fail_event"])
+        np.testing.assert_array_equal(bufs[2].get(np.uint8), orc["cause"])
+
+    dev.wait()
+    (a_bufs, ra), (b_bufs, rb) = result_set(), result_set()
+    db.check_into(ra, asynchronous=True)
+    db.check_into(rb, asynchronous=True)
+    dev.wait_step(1)
+    assert_oracle(a_bufs)
+    dev.wait_step(0)
+    assert_oracle(b_bufs)
+    n, _ = dev.wait()
+    assert n == 2
+
+    (a_bufs, ra), (b_bufs, rb) = result_set(), result_set()
+    db.check_into(ra, asynchronous=True)
+    db2.check(peak=False)  # synchronous: not an asynchronous step on record
+    db.check_into(rb, asynchronous=True)
+    dev.wait_step(1)
+    assert_oracle(a_bufs)
+    dev.wait_step(7)  # no such step on record: everything
+    assert_oracle(b_bufs)
+    n, _ = dev.wait()
+    assert n == 2
+
+
 def test_concurrent_calls_on_one_context():
     """independent/checker calls its inner checker from a
     bounded pmap, so one context may be entered from several threads at once.
