@@ -300,9 +300,11 @@ struct Dev {
     uint32_t *seg_cnt = nullptr, *seg_end = nullptr, *seg_out = nullptr, *seg_work = nullptr;
     uint32_t *seg_rerun = nullptr, *seg_rerun_init = nullptr;
     int32_t *seg0_fev = nullptr, *seg_ctl = nullptr;
-    // speculative segments: each wave's 9-10-pending workspace
+    // speculative segments: each wave's 9-10-pending workspace, the rerun list
     uint32_t *spec_ws = nullptr;
     size_t spec_ws_words = 0;
+    int32_t *spec_rr = nullptr;
+    int64_t spec_rr_cap = 0;
     // node records (lc_check_node): this rank's block and the gathered node
     uint64_t *send = nullptr, *node = nullptr;
     int64_t node_cap = 0, node_n = 0;
@@ -321,7 +323,7 @@ struct Dev {
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(dargs); dfree(send); dfree(node);
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
-        dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws);
+        dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr);
         if (hargs) (void)hipHostFree(hargs);
         for (hipEvent_t &e : args_ev)
             if (e) (void)hipEventDestroy(e);
@@ -904,12 +906,18 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     }
     // Speculative segments (device_lattice.hip): the same regime without
     // quiescent points -- every key a workgroup of `segs` waves, about four
-    // segment waves per SIMD in all (C2: 1,000 keys x 4).  LC_SPEC=0/1 forces
-    // the choice, LC_SPEC_SEGS the segments per key.
+    // segment waves per SIMD in all (C2: 1,000 keys x 4).  The kernel's 80
+    // VGPRs would allow six, but 6-wave workgroups land unevenly on a CU's
+    // four SIMDs (5-7 waves each): C2 0.357 ms at 4 segments per key, 0.406
+    // at 6, 0.386 at 8.  LC_SPEC=0/1 forces the choice, LC_SPEC_SEGS (2, 3, 4,
+    // 6, 8) the segments per key.
     const char *fspec = std::getenv("LC_SPEC");
     int segs = K > 0 ? (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1)) : 0;
-    if (const char *e = std::getenv("LC_SPEC_SEGS")) segs = std::atoi(e);
     segs = segs >= 8 ? 8 : segs >= 4 ? 4 : segs >= 2 ? 2 : 0;
+    if (const char *e = std::getenv("LC_SPEC_SEGS")) {
+        const int v = std::atoi(e);
+        segs = v >= 8 ? 8 : v >= 6 ? 6 : v >= 4 ? 4 : v >= 3 ? 3 : v >= 2 ? 2 : 0;
+    }
     const bool spec = !split && t0_step && fast && segs >= 2 && (fspec ? fspec[0] == '1' : true);
     if (spec) {
         const size_t need = lcd::spec_ws_words(K, segs);
@@ -920,6 +928,14 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             c->spec_ws_words = 0;
             HIPCHK(dalloc(&c->spec_ws, need));
             c->spec_ws_words = need;
+        }
+        if (K + 1 > c->spec_rr_cap) {
+            if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
+            dfree(c->spec_rr);
+            c->spec_rr = nullptr;
+            c->spec_rr_cap = 0;
+            HIPCHK(dalloc(&c->spec_rr, (size_t)K + 1));
+            c->spec_rr_cap = K + 1;
         }
     }
     uint32_t ticket_base = 0;
@@ -994,7 +1010,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     } else if (spec) {
         const uint32_t ck1 = std::getenv("LC_SPEC_CK1") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK1")) : 32u;
         const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 160u;
-        HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, ck1, ck2, c->stream));
+        HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, c->spec_rr, ck1, ck2, c->cu_count * 8, c->stream));
         HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0) {
         HIPCHK(lcd::launch_t0(a0, dargs, g0, t0_wide, c->stream, ticket_base));

@@ -233,6 +233,8 @@ struct T0Args {
     uint32_t n_trans;            // entries of trans[]
     uint32_t ticket_base;        // ticket value this launch starts from (see launch_t0)
     uint32_t spec_ck1, spec_ck2; // speculative segments: checkpoint distances past a cut
+    int32_t *spec_rr;            // speculative segments: keys left to the unsegmented search
+    int32_t *spec_nrr;           //   and their count (zeroed before the launch)
 };
 
 __device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint32_t why) {
@@ -421,7 +423,9 @@ __device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t 
             if (!__any(ch)) break;
         }
     }
-    const uint32_t up = (uint32_t)__shfl_xor((int)C, 1 << p);  // (a DPP switch on p measured slower)
+    // (a DPP switch on p measured slower, in the compact T0 and in the
+    // speculative segments' walk: 1,224 against 1,142 cycles per event)
+    const uint32_t up = (uint32_t)__shfl_xor((int)C, 1 << p);
     const uint32_t Wn = ((lane >> p) & 1u) ? 0u : up;
     if (!__any(Wn != 0u)) return 1;
     W = Wn;
@@ -1736,7 +1740,7 @@ __device__ __forceinline__ void spec_setup(SpecState &st, uint32_t words, uint32
 // ~40k cycles against ~2k in LDS).  NWS = 1, 2, 4 slots for 2, 4, 8 waves
 // keep 4 waves per SIMD within the CU's LDS.
 template <int S>
-constexpr int spec_lds_ws() { return S <= 2 ? 1 : S <= 4 ? 2 : 4; }
+constexpr int spec_lds_ws() { return S <= 3 ? 1 : S <= 6 ? 2 : 3; }
 template <int MODE, int NWS>
 __device__ __forceinline__ int spec_walk(const uint32_t *evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
                                          uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
@@ -1810,6 +1814,8 @@ __device__ __forceinline__ int spec_walk(const uint32_t *evp, const uint32_t *tr
                 int r;
                 // closed sets: exact ones (ok_lane, as the wide T0 keeps
                 // them) measured 10 % slower per event here
+                // sweeps specialised to the highest live index (one body for
+                // every live set measured 4 % slower per event here)
                 const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
                 if (top >= 6) r = ok_lane_closed<6>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
                 else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
@@ -2105,8 +2111,11 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
             }
         }
         int kr = K_DONE;
-        if (rerun) kr = lattice_key<T0_RSMALL, true>(a, key, ws);
-        else if (bad) kr = K_SPILL;
+        // the unsegmented search runs in a launch of its own (k_spec_rerun):
+        // inlined here it cost this kernel 27 VGPRs, 6 -> 4 waves per SIMD
+        if (rerun) {
+            if (lane == 0) a.spec_rr[atomicAdd(a.spec_nrr, 1)] = key;
+        } else if (bad) kr = K_SPILL;
         else if (fv >= 0) finish_key(f, key, LC_INVALID, LC_CAUSE_NONLIN, fv, 0, 0, (uint64_t)fv + 1u);
         else finish_key(f, key, LC_VALID, LC_CAUSE_NONE, -1, 0, 0, nev);
         if (kr == K_SPILL) {
@@ -2121,20 +2130,50 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     }
 }
 
+// The keys k_spec left to the unsegmented search (compact T0, FAST).
+__global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
+    __shared__ uint32_t ws[3 * T0_RMEM * 64];
+    const int32_t n = *a.spec_nrr;
+    for (int32_t w = blockIdx.x; w < n; w += gridDim.x) {
+        const int32_t key = a.spec_rr[w];
+        const int kr = lattice_key<T0_RSMALL, true>(a, key, ws);
+        if (kr == K_SPILL) {
+            const Args &f = *a.full;
+            if (a.flags & T0_STRICT) {
+                t0_malformed(a, key, LC_BATCH_E_FIT);
+                finish_key(f, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+            } else {
+                const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
+                push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key, f.list_cap);
+            }
+        }
+    }
+}
+
 size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * lat_ws_words(); }
 
-// Keys order[0 .. n_order) in workgroups of `segs` segments (2, 4 or 8);
-// ws: spec_ws_words(n_order, segs) words.
-hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, uint32_t ck1, uint32_t ck2,
-                       hipStream_t s) {
+// Keys order[0 .. n_order) in workgroups of `segs` segments (2, 3, 4, 6 or
+// 8); ws: spec_ws_words(n_order, segs) words; rr: n_order + 1 ints (the
+// rerun list and its count, zeroed here).
+hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, uint32_t ck1,
+                       uint32_t ck2, int rerun_grid, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
     t.lat_ws = ws;
     t.spec_ck1 = ck1;
     t.spec_ck2 = ck2;
+    t.spec_nrr = rr;
+    t.spec_rr = rr + 1;
+    hipError_t e = hipMemsetAsync(rr, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return e;
     const dim3 grid((unsigned)std::max(1, a.n_order));
     if (segs >= 8) hipLaunchKernelGGL(k_spec<8>, grid, dim3(512), 0, s, t);
+    else if (segs >= 6) hipLaunchKernelGGL(k_spec<6>, grid, dim3(384), 0, s, t);
     else if (segs >= 4) hipLaunchKernelGGL(k_spec<4>, grid, dim3(256), 0, s, t);
+    else if (segs >= 3) hipLaunchKernelGGL(k_spec<3>, grid, dim3(192), 0, s, t);
     else hipLaunchKernelGGL(k_spec<2>, grid, dim3(128), 0, s, t);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_spec_rerun, dim3((unsigned)std::max(1, std::min(a.n_order, rerun_grid))), dim3(64), 0, s, t);
     return hipGetLastError();
 }
 

@@ -59,7 +59,7 @@ def test_spec_matches_oracle(shape, spec_env):
     spec_env["LC_SPEC"] = "0"
     _check(dev, pk, orc, "unsegmented")
     spec_env["LC_SPEC"] = "1"
-    for segs in ("2", "4", "8"):
+    for segs in ("2", "3", "4", "6", "8"):
         spec_env["LC_SPEC_SEGS"] = segs
         for ck in (("32", "160"), ("1", "2"), ("0", "0")):
             spec_env["LC_SPEC_CK1"], spec_env["LC_SPEC_CK2"] = ck
