@@ -303,11 +303,14 @@ struct Dev {
     // speculative segments: each wave's 9-10-pending workspace, the rerun list
     uint32_t *spec_ws = nullptr;
     size_t spec_ws_words = 0;
-    int32_t *spec_rr = nullptr;
+    int32_t *spec_rr = nullptr;    // two rerun counts (used in turn), then the rerun list
     int64_t spec_rr_cap = 0;
+    int spec_parity = 0;
     // node records (lc_check_node): this rank's block and the gathered node
     uint64_t *send = nullptr, *node = nullptr;
     int64_t node_cap = 0, node_n = 0;
+    uint64_t *hnode = nullptr;  // pinned landing area of the node's records (lc_check_node)
+    int64_t hnode_cap = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
     struct Ws {
         char *base = nullptr;
@@ -325,6 +328,7 @@ struct Dev {
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
         dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr);
         if (hargs) (void)hipHostFree(hargs);
+        if (hnode) (void)hipHostFree(hnode);
         for (hipEvent_t &e : args_ev)
             if (e) (void)hipEventDestroy(e);
         delete staged;
@@ -929,13 +933,14 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             HIPCHK(dalloc(&c->spec_ws, need));
             c->spec_ws_words = need;
         }
-        if (K + 1 > c->spec_rr_cap) {
+        if (K + 2 > c->spec_rr_cap) {
             if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
             dfree(c->spec_rr);
             c->spec_rr = nullptr;
             c->spec_rr_cap = 0;
-            HIPCHK(dalloc(&c->spec_rr, (size_t)K + 1));
-            c->spec_rr_cap = K + 1;
+            HIPCHK(dalloc(&c->spec_rr, (size_t)K + 2));
+            HIPCHK(hipMemsetAsync(c->spec_rr, 0, 2 * sizeof(int32_t), c->stream));
+            c->spec_rr_cap = K + 2;
         }
     }
     uint32_t ticket_base = 0;
@@ -980,7 +985,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     lcd::Args *const dargs = c->dargs + aslot;
     HIPCHK(hipEventRecord(c->e0, c->stream));
     if (async && c->n_async == 0) HIPCHK(hipEventRecord(c->ea0, c->stream));
-    if (K > 0 && a.strict) {
+    if (K > 0 && a.strict && !spec) {
         // the event-by-event validation the host skipped: on the second
         // stream, beside T0, joined before the step's results are read
         HIPCHK(hipEventRecord(c->vin, c->stream));
@@ -1010,13 +1015,18 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     } else if (spec) {
         const uint32_t ck1 = std::getenv("LC_SPEC_CK1") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK1")) : 32u;
         const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 160u;
-        HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, c->spec_rr, ck1, ck2, c->cu_count * 8, c->stream));
+        // the validation of a host-unchecked batch runs in extra blocks of
+        // the same launch (a second stream cost ~40 us of cross-stream waits)
+        const int vblocks = a.strict ? (int)std::min<int64_t>(K, c->cu_count) : 0;
+        HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2, c->cu_count * 8,
+                                vblocks, c->stream));
+        c->spec_parity ^= 1;
         HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0) {
         HIPCHK(lcd::launch_t0(a0, dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
     }
-    if (K > 0 && a.strict) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));
+    if (K > 0 && a.strict && !spec) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));
     if (async) {
         HIPCHK(hipEventRecord(c->ea1, c->stream));
         HIPCHK(hipEventRecord(c->ring[c->async_seq % 4], c->stream));
@@ -1422,7 +1432,18 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
     const auto t_search = std::chrono::steady_clock::now();
     rc = gather_node(c, d, b->n_keys, block);
     if (rc) return drained(rc);
-    if (d->node_n && hipMemcpyAsync(node, d->node, (size_t)d->node_n * 8, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
+    // the records land in pinned memory (a copy into the caller's pageable
+    // array would be a synchronous staged copy) and are copied out after the wait
+    if (d->node_n > d->hnode_cap) {
+        if (d->hnode) (void)hipHostFree(d->hnode);
+        d->hnode = nullptr;
+        d->hnode_cap = 0;
+        if (hipHostMalloc((void **)&d->hnode, (size_t)d->node_n * 8, hipHostMallocDefault) != hipSuccess)
+            return drained(lc::fail(LC_E_NOMEM, "lc_check_node: pinned record buffer"));
+        d->hnode_cap = d->node_n;
+    }
+    if (d->node_n && hipMemcpyAsync(d->hnode, d->node, (size_t)d->node_n * 8, hipMemcpyDeviceToHost, d->stream) !=
+                         hipSuccess)
         return drained(lc::fail(LC_E_DEVICE, "lc_check_node: record download failed"));
     const auto t_gather = std::chrono::steady_clock::now();
     if (enq) {  // a T0-only step: one wait for the search, the exchange and the download
@@ -1434,6 +1455,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
     } else {
         HIPCHK(hipStreamSynchronize(d->stream));
     }
+    if (d->node_n) std::memcpy(node, d->hnode, (size_t)d->node_n * 8);
     if (std::getenv("LC_TIMING")) {
         using ms = std::chrono::duration<double, std::milli>;
         std::fprintf(stderr, "lc_check_node: prepare %.3f, upload %.3f, search enqueue %.3f, gather enqueue %.3f, "

@@ -233,8 +233,9 @@ struct T0Args {
     uint32_t n_trans;            // entries of trans[]
     uint32_t ticket_base;        // ticket value this launch starts from (see launch_t0)
     uint32_t spec_ck1, spec_ck2; // speculative segments: checkpoint distances past a cut
-    int32_t *spec_rr;            // speculative segments: keys left to the unsegmented search
-    int32_t *spec_nrr;           //   and their count (zeroed before the launch)
+    int32_t *spec_rr;            // speculative segments: keys left to the unsegmented search,
+    int32_t *spec_nrr;           //   their count (zero at the launch)
+    int32_t *spec_nrr_next;      //   and the next launch's count (zeroed by k_spec_rerun)
 };
 
 __device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint32_t why) {
@@ -1068,44 +1069,46 @@ __device__ unsigned long long lc_t0_stamps[8192 * 6];
 // event of the slot in the chunk (r from 0, wave rank among the slot's lanes)
 // must be an :ok exactly when r + b is odd.  Violations set the batch's
 // error words (the call then returns LC_E_INVALID).
-__global__ __launch_bounds__(64) void k_validate(T0Args a) {
+__device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     const uint32_t lane = lane_id();
-    for (int64_t k = blockIdx.x; k < a.n_order; k += gridDim.x) {
-        if (a.key_error && a.key_error[k]) continue;
-        const uint64_t eb = a.ev_off[k], ee = a.ev_off[k + 1];
-        const uint32_t tb = a.trans_off ? a.trans_off[k] : 0u;
-        const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
-        const uint32_t ns = a.trans_off ? (a.key_states ? a.key_states[k] : 0u) : a.shared_states;
-        uint64_t pend = 0;
-        int32_t why = 0;
-        for (uint64_t base = eb; base < ee && !why; base += 64) {
-            const uint64_t j = base + lane;
-            const bool in = j < ee;
-            const uint32_t w = in ? a.events[j] : 0u;
-            const bool ok = (w & LC_EV_OK_BIT) != 0;
-            const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
-            const uint32_t d = (in && !ok && t < ntr) ? a.trans[tb + t] : 0u;
-            if (__any(in && !ok && (t >= ntr || ((d & 3u) >= LC_T_WRITE && (d >> 17) >= ns)))) why |= LC_BATCH_E_TRANS;
-            if (__any(in && s >= 64)) why |= LC_BATCH_E_FIT;
-            if (why) break;
-            uint64_t todo = __ballot(in), npend = pend;
-            while (todo) {
-                const uint32_t sl = __builtin_amdgcn_readlane(s, (uint32_t)__builtin_ctzll(todo));
-                const uint64_t ms = __ballot(in && s == sl);
-                const uint32_t b0 = (uint32_t)(pend >> sl) & 1u;
-                const uint32_t r = rank_of(ms);
-                if (__any(in && s == sl && ok != (((r + b0) & 1u) != 0))) why |= LC_BATCH_E_SLOTS;
-                if (((uint32_t)__popcll(ms) + b0) & 1u) npend |= 1ull << sl;
-                else npend &= ~(1ull << sl);
-                todo &= ~ms;
-            }
-            pend = npend;
+    if (a.key_error && a.key_error[k]) return;
+    const uint64_t eb = a.ev_off[k], ee = a.ev_off[k + 1];
+    const uint32_t tb = a.trans_off ? a.trans_off[k] : 0u;
+    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
+    const uint32_t ns = a.trans_off ? (a.key_states ? a.key_states[k] : 0u) : a.shared_states;
+    uint64_t pend = 0;
+    int32_t why = 0;
+    for (uint64_t base = eb; base < ee && !why; base += 64) {
+        const uint64_t j = base + lane;
+        const bool in = j < ee;
+        const uint32_t w = in ? a.events[j] : 0u;
+        const bool ok = (w & LC_EV_OK_BIT) != 0;
+        const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
+        const uint32_t d = (in && !ok && t < ntr) ? a.trans[tb + t] : 0u;
+        if (__any(in && !ok && (t >= ntr || ((d & 3u) >= LC_T_WRITE && (d >> 17) >= ns)))) why |= LC_BATCH_E_TRANS;
+        if (__any(in && s >= 64)) why |= LC_BATCH_E_FIT;
+        if (why) break;
+        uint64_t todo = __ballot(in), npend = pend;
+        while (todo) {
+            const uint32_t sl = __builtin_amdgcn_readlane(s, (uint32_t)__builtin_ctzll(todo));
+            const uint64_t ms = __ballot(in && s == sl);
+            const uint32_t b0 = (uint32_t)(pend >> sl) & 1u;
+            const uint32_t r = rank_of(ms);
+            if (__any(in && s == sl && ok != (((r + b0) & 1u) != 0))) why |= LC_BATCH_E_SLOTS;
+            if (((uint32_t)__popcll(ms) + b0) & 1u) npend |= 1ull << sl;
+            else npend &= ~(1ull << sl);
+            todo &= ~ms;
         }
-        if (why && lane == 0) {
-            atomicOr(&a.err[0], why);
-            atomicMax(&a.err[1], (int32_t)k + 1);
-        }
+        pend = npend;
     }
+    if (why && lane == 0) {
+        atomicOr(&a.err[0], why);
+        atomicMax(&a.err[1], (int32_t)k + 1);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_validate(T0Args a) {
+    for (int64_t k = blockIdx.x; k < a.n_order; k += gridDim.x) validate_key(a, k);
 }
 
 template <int RM>
@@ -1961,6 +1964,13 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     __shared__ uint32_t s_ws[NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
     __shared__ int32_t s_ws_busy[NWS];
     const uint32_t lane = lane_id(), wv = uni((uint32_t)threadIdx.x >> 6);  // uniform per wave
+    if (blockIdx.x >= (uint32_t)a.n_order) {
+        // T0_STRICT steps: the event-by-event validation, in blocks after the
+        // keys' (no second stream, no cross-stream waits around the step)
+        const int64_t nb = (int64_t)gridDim.x - a.n_order;
+        for (int64_t k = ((int64_t)blockIdx.x - a.n_order) * S + wv; k < a.n_order; k += nb * S) validate_key(a, k);
+        return;  // the whole block: no barrier below is reached by half of it
+    }
     const int32_t key = a.order[blockIdx.x];
     uint32_t *ws = a.lat_ws + ((size_t)blockIdx.x * S + wv) * (3 * T0_RMEM * 64);
     const uint64_t eb = a.ev_off[key];
@@ -2134,6 +2144,7 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
 __global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
     __shared__ uint32_t ws[3 * T0_RMEM * 64];
     const int32_t n = *a.spec_nrr;
+    if (blockIdx.x == 0 && lane_id() == 0) *a.spec_nrr_next = 0;  // two counters in turn: no memset per step
     for (int32_t w = blockIdx.x; w < n; w += gridDim.x) {
         const int32_t key = a.spec_rr[w];
         const int kr = lattice_key<T0_RSMALL, true>(a, key, ws);
@@ -2153,25 +2164,26 @@ __global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
 size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * lat_ws_words(); }
 
 // Keys order[0 .. n_order) in workgroups of `segs` segments (2, 3, 4, 6 or
-// 8); ws: spec_ws_words(n_order, segs) words; rr: n_order + 1 ints (the
-// rerun list and its count, zeroed here).
-hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, uint32_t ck1,
-                       uint32_t ck2, int rerun_grid, hipStream_t s) {
+// 8); ws: spec_ws_words(n_order, segs) words; rr: n_order + 2 ints (two
+// rerun counts used in turn -- `parity` picks this launch's, which must be
+// zero, and k_spec_rerun zeroes the other -- then the rerun list).
+// validate: add the T0_STRICT validation blocks.
+hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, int parity,
+                       uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
     t.lat_ws = ws;
     t.spec_ck1 = ck1;
     t.spec_ck2 = ck2;
-    t.spec_nrr = rr;
-    t.spec_rr = rr + 1;
-    hipError_t e = hipMemsetAsync(rr, 0, sizeof(int32_t), s);
-    if (e != hipSuccess) return e;
-    const dim3 grid((unsigned)std::max(1, a.n_order));
+    t.spec_nrr = rr + (parity & 1);
+    t.spec_nrr_next = rr + ((parity & 1) ^ 1);
+    t.spec_rr = rr + 2;
+    const dim3 grid((unsigned)std::max(1, a.n_order + std::max(0, validate_blocks)));
     if (segs >= 8) hipLaunchKernelGGL(k_spec<8>, grid, dim3(512), 0, s, t);
     else if (segs >= 6) hipLaunchKernelGGL(k_spec<6>, grid, dim3(384), 0, s, t);
     else if (segs >= 4) hipLaunchKernelGGL(k_spec<4>, grid, dim3(256), 0, s, t);
     else if (segs >= 3) hipLaunchKernelGGL(k_spec<3>, grid, dim3(192), 0, s, t);
     else hipLaunchKernelGGL(k_spec<2>, grid, dim3(128), 0, s, t);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_spec_rerun, dim3((unsigned)std::max(1, std::min(a.n_order, rerun_grid))), dim3(64), 0, s, t);
     return hipGetLastError();

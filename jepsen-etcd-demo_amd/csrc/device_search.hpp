@@ -115,10 +115,12 @@ hipError_t launch_segments(const SegArgs &a, int grid, hipStream_t s);
 // a verdicts-only register-tier step, each a workgroup of `segs` waves (2, 3,
 // 4, 6, 8) searching segments from the full set and checking them against
 // each other, then a launch for the keys left to the unsegmented search;
-// results through a_dev like launch_t0.  rr: n_order + 1 ints of scratch.
+// results through a_dev like launch_t0.  rr: n_order + 2 ints of scratch
+// (both counts zero before the first launch; `parity` alternates).
+// validate_blocks > 0: the T0_STRICT validation runs in that many extra blocks.
 size_t spec_ws_words(int64_t n_keys, int segs);
-hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, uint32_t ck1,
-                       uint32_t ck2, int rerun_grid, hipStream_t s);
+hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, int parity,
+                       uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, hipStream_t s);
 uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
