@@ -362,7 +362,7 @@ def main():
         # record (valid 1 B + failing event 4 B + cause 1 B) per key.
         alg_bytes = 4 * n_events + 8 * (K + 1) + 4 * K + 4 * int(packed.view.n_trans) + 6 * K
         kt = avg_t0
-        dominant = "k_search_lattice (T0)"
+        dominant = "T0 register tier (k_spec / k_search_lattice)"
         if avg_t3 > avg_t0 and probes_t3:
             # the HBM tier dominates (C4): SURVEY D-4's one 64 B line per
             # hash probe, for that tier alone, over the span of its launches
@@ -374,9 +374,10 @@ def main():
         for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
             try:
                 d = json.load(open(fpath))
-                tag = "lattice" if "T0" in dominant else "hbm"
+                tags = ("k_spec<", "lattice") if "T0" in dominant else ("hbm",)
+                kname = d.get("kernel", "")
                 if (d.get("workload") == args.config and d.get("bytes_per_launch")
-                        and d.get("budget", args.budget) == args.budget and tag in d.get("kernel", tag)):
+                        and d.get("budget", args.budget) == args.budget and any(t in kname for t in tags)):
                     traffic = d["bytes_per_launch"]
             except (OSError, ValueError):
                 pass
