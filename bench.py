@@ -280,12 +280,13 @@ def main():
         d1_t0.append(st.tier0_ms if st.tier0_ms > 0 else st.kernel_ms)
         if st.tier3_ms > 0:
             d1_t3.append(st.tier3_ms)
+            d1_t3b.append(st.t3_bytes)
         return rec
 
-    d1_t3 = []
+    d1_t3, d1_t3b = [], []
     for _ in range(args.warmup):
         d1_step()
-    del d1_t0[:], d1_t3[:]
+    del d1_t0[:], d1_t3[:], d1_t3b[:]
     sync(); barrier(); sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -363,18 +364,24 @@ def main():
         alg_bytes = 4 * n_events + 8 * (K + 1) + 4 * K + 4 * int(packed.view.n_trans) + 6 * K
         kt = avg_t0
         dominant = "T0 register tier (k_spec / k_search_lattice)"
-        if avg_t3 > avg_t0 and probes_t3:
-            # the HBM tier dominates (C4): SURVEY D-4's one 64 B line per
-            # hash probe, for that tier alone, over the span of its launches
-            dominant = "k_search_hbm (T3)"
-            alg_bytes = 64 * probes_t3
+        d4_t3 = None
+        if avg_t3 > avg_t0:
+            # the HBM tier dominates (C4).  Its layered form (k_search_layers)
+            # touches HBM only to stream the config-set arrays: 8 B per entry
+            # read or written (lc_stats.t3_bytes, counted by the kernel).
+            # SURVEY D-4's notional 64 B line per hash probe is kept beside it
+            # (d4_model_gbs) -- the config-keyed T3 moved about that much.
+            dominant = "k_search_layers (T3L)"
+            alg_bytes = int(np.mean(d1_t3b)) if d1_t3b else 0
             kt = avg_t3
+            if probes_t3:
+                d4_t3 = 64 * probes_t3 / (kt * 1e-3) / 1e9
         achieved = alg_bytes / (kt * 1e-3) / 1e9 if kt > 0 else 0.0
         traffic = None
         for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
             try:
                 d = json.load(open(fpath))
-                tags = ("k_spec<", "lattice") if "T0" in dominant else ("hbm",)
+                tags = ("k_spec<", "lattice") if "T0" in dominant else ("k_search_layers",)
                 kname = d.get("kernel", "")
                 if (d.get("workload") == args.config and d.get("bytes_per_launch")
                         and d.get("budget", args.budget) == args.budget and any(t in kname for t in tags)):
@@ -406,7 +413,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": kt,
-                         "launches": len(d1_t0)},
+                         "launches": len(d1_t0), "d4_model_gbs": d4_t3},
             "cpu_baseline": cpu,
             "ops_total": ops_total,
             "ops_checked_per_step": ops_checked,

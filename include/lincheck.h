@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 6
+#define LC_ABI_VERSION 7
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -316,6 +316,9 @@ typedef struct lc_stats {
     double   tier0_ms;        /* device time of the register-lattice tier alone */
     double   tier3_ms;        /* device time of the HBM tier launches (0 if none) */
     uint64_t probes_t3;       /* the part of `probes` made by the HBM tier      */
+    uint64_t t3_bytes;        /* algorithmic HBM bytes of the layered HBM tier:
+                                 8 per config-set entry it streams in or out
+                                 (ABI 7)                                       */
 } lc_stats;
 
 typedef struct lc_ctx lc_ctx;

@@ -264,10 +264,10 @@ struct Dev {
     uint64_t async_seq = 0;
     // scratch, grown on demand
     int64_t cap_keys = 0;
-    int32_t *lists = nullptr;      // 4 x cap_keys: spill0, spill1, spill2, wide
+    int32_t *lists = nullptr;      // 5 x cap_keys: spill0, spill1, spill2, wide, old (T3L -> narrow T3)
     // one 96-byte control block, zeroed and read back in one operation each:
-    // acc (4 x u64: probes, events, keys_done) then counters (16 x i32:
-    // n_spill0, n_spill1, n_spill2, n_wide, err bits, 1 + bad key, -, -,
+    // acc (4 x u64: probes, events, keys_done, T3L stream bytes) then counters (16 x i32:
+    // n_spill0, n_spill1, n_spill2, n_wide, err bits, 1 + bad key, n_old, -,
     // tickets[8..15])
     unsigned long long *ctl = nullptr;
     unsigned long long *acc = nullptr;
@@ -318,13 +318,20 @@ struct Dev {
         int slots = 0;
         lcd::HbmWs w{};
     } ws[2];
+    // layered T3 workspace (device_layers.hip)
+    struct LWs {
+        char *base = nullptr;
+        size_t bytes = 0;
+        int slots = 0;
+        lcd::LayWs w{};
+    } lws;
     ~Dev() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         dfree(lists); dfree(ctl); dfree(valid); dfree(fail_event);
         if (hctl) (void)hipHostFree(hctl);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
-        dfree(ws[0].base); dfree(ws[1].base); dfree(dargs); dfree(send); dfree(node);
+        dfree(ws[0].base); dfree(ws[1].base); dfree(lws.base); dfree(dargs); dfree(send); dfree(node);
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
         dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr);
         if (hargs) (void)hipHostFree(hargs);
@@ -372,7 +379,7 @@ static int ensure_capacity(Dev *c, int64_t n_keys) {
     int64_t cap = std::max<int64_t>(n_keys, 1024);
     dfree(c->lists); dfree(c->valid); dfree(c->fail_event); dfree(c->cause);
     dfree(c->peak); dfree(c->final_cfg); dfree(c->n_final);
-    HIPCHK(dalloc(&c->lists, (size_t)cap * 4));
+    HIPCHK(dalloc(&c->lists, (size_t)cap * 5));
     HIPCHK(dalloc(&c->valid, (size_t)cap));
     HIPCHK(dalloc(&c->fail_event, (size_t)cap));
     HIPCHK(dalloc(&c->cause, (size_t)cap));
@@ -381,6 +388,41 @@ static int ensure_capacity(Dev *c, int64_t n_keys) {
     HIPCHK(dalloc(&c->n_final, (size_t)cap));
     c->cap_keys = cap;
     for (bool &v : c->args_ok) v = false;
+    return LC_OK;
+}
+
+// Lay out (and if needed allocate) the layered T3 workspace for `want`
+// blocks: four arrays of budget + slack entries (8 B) per block.
+static int ensure_lay_ws(Dev *c, int want, int *slots_out) {
+    Dev::LWs &W = c->lws;
+    const uint64_t cap = c->o->max_configs + (uint64_t)lcd::t3l_slack() + 64;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    lcd::LayWs w{};
+    size_t off = 0;
+    w.off_S0 = off; off += al(cap * 8);
+    w.off_S1 = off; off += al(cap * 8);
+    w.off_I0 = off; off += al(cap * 8);
+    w.off_I1 = off; off += al(cap * 8);
+    w.slot_bytes = off;
+    w.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFull);
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    int slots = std::min(want, c->cu_count);
+    const size_t limit = W.bytes + free_b / 2;
+    while (slots > 1 && (size_t)slots * w.slot_bytes > limit) slots /= 2;
+    if ((size_t)slots * w.slot_bytes > limit)
+        return lc::fail(LC_E_NOMEM, "T3 workspace: one slot needs %zu bytes (budget %llu)", w.slot_bytes,
+                        (unsigned long long)c->o->max_configs);
+    if (!W.base || W.w.slot_bytes != w.slot_bytes || W.slots < slots) {
+        dfree(W.base);
+        W.bytes = 0; W.slots = 0;
+        HIPCHK(hipMalloc((void **)&W.base, (size_t)slots * w.slot_bytes));
+        W.bytes = (size_t)slots * w.slot_bytes;
+        W.slots = slots;
+    }
+    w.base = W.base;
+    W.w = w;
+    *slots_out = std::min(slots, W.slots);
     return LC_OK;
 }
 
@@ -881,11 +923,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         a.final_cfg = (mode == RES_HOST && r->final_configs) ? c->final_cfg : nullptr;
         a.n_final = (mode == RES_HOST && r->n_final) ? c->n_final : nullptr;
     }
-    a.probes = c->acc + 0; a.ev_count = c->acc + 1; a.keys_done = c->acc + 2;
+    a.probes = c->acc + 0; a.ev_count = c->acc + 1; a.keys_done = c->acc + 2; a.stream_bytes = c->acc + 3;
     a.err = c->counters + 4;
     a.list_cap = (int32_t)c->cap_keys;
     int32_t *spill0 = c->lists, *spill1 = c->lists + c->cap_keys, *spill2 = c->lists + 2 * c->cap_keys;
-    int32_t *wide = c->lists + 3 * c->cap_keys;
+    int32_t *wide = c->lists + 3 * c->cap_keys, *old_narrow = c->lists + 4 * c->cap_keys;
     int32_t *n_spill0 = c->counters + 0, *n_spill1 = c->counters + 1, *n_spill2 = c->counters + 2;
     int32_t *n_wide = c->counters + 3;
 
@@ -1101,11 +1143,29 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         HIPCHK(hipEventRecord(c->et3a, c->stream));
         lcd::Args a3 = a;
         a3.wide = wide; a3.n_wide = n_wide;
-        if (n_deep > 0) {
+        // Narrow keys: the layered form first (<= 8 states; LC_T3_LAYERS=0
+        // turns it off for A/B runs), the config-keyed narrow tier for the
+        // keys it hands on (cnt[6]).
+        const bool layers = !(std::getenv("LC_T3_LAYERS") && std::atoi(std::getenv("LC_T3_LAYERS")) == 0);
+        int32_t *narrow_list = spill2, *narrow_n = n_spill2;
+        int32_t n_narrow = n_deep;
+        if (n_deep > 0 && layers) {
             int slots = 0;
-            rc = ensure_ws(c, 0, n_deep, &slots);
+            rc = ensure_lay_ws(c, n_deep, &slots);
             if (rc) return rc;
             a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 11;
+            a3.spill = old_narrow; a3.n_spill = c->counters + 6;
+            HIPCHK(lcd::launch_t3_layers(a3, c->lws.w, slots, c->stream));
+            HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            narrow_list = old_narrow; narrow_n = c->counters + 6;
+            n_narrow = cnt[6];
+        }
+        if (n_narrow > 0) {
+            int slots = 0;
+            rc = ensure_ws(c, 0, n_narrow, &slots);
+            if (rc) return rc;
+            a3.order = narrow_list; a3.n_order = 0; a3.n_in = narrow_n; a3.ticket = c->counters + 13;
             HIPCHK(lcd::launch_t3_narrow(a3, c->ws[0].w, slots, c->stream));
             HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
@@ -1130,6 +1190,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         st->tier0_ms = ms0;
         st->tier3_ms = ms3;
         st->probes_t3 = t3 ? acc[0] - probes_pre_t3 : 0;
+        st->t3_bytes = t3 ? acc[3] : 0;
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         st->probes = acc[0];
         st->events = acc[1];
@@ -1158,6 +1219,7 @@ static void merge_stats(lc_stats &t, const lc_stats &s) {
     t.tier3_ms = std::max(t.tier3_ms, s.tier3_ms);
     t.probes += s.probes;
     t.probes_t3 += s.probes_t3;
+    t.t3_bytes += s.t3_bytes;
     t.lds_keys += s.lds_keys;
     t.deep_keys += s.deep_keys;
     t.events += s.events;

@@ -44,6 +44,7 @@ struct Args {
     unsigned long long *probes;
     unsigned long long *ev_count;
     unsigned long long *keys_done;
+    unsigned long long *stream_bytes;  // layered HBM tier: set-array bytes streamed
     // output work lists
     int32_t *spill;
     int32_t *n_spill;
@@ -125,6 +126,17 @@ uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
 hipError_t launch_t2(const Args &a, int grid, hipStream_t s);
+// Layered HBM tier (device_layers.hip): per-block arrays S[2], I[2] of cap
+// entries (u64 each), one 1,024-thread block per key.  Keys with more than 8
+// states go to a.spill (the config-keyed narrow tier), wide ones to a.wide.
+struct LayWs {
+    char *base;
+    size_t slot_bytes;
+    uint32_t cap;    // entries per array (budget + t3l_slack() + margin)
+    size_t off_S0, off_S1, off_I0, off_I1;
+};
+hipError_t launch_t3_layers(const Args &a, const LayWs &w, int grid, hipStream_t s);
+int t3l_slack();
 hipError_t launch_t3_narrow(const Args &a, const HbmWs &w, int grid, hipStream_t s);
 hipError_t launch_t3_wide(const Args &a, const HbmWs &w, int grid, hipStream_t s);
 int t3_block();

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 6
+LC_ABI_VERSION = 7
 LC_MAX_DEVICES = 8
 LC_COMM_ID_BYTES = 128
 LC_OPT_COUNT_PROBES = 0x1
@@ -78,7 +78,7 @@ class LcStats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("total_ms", C.c_double), ("probes", C.c_uint64),
                 ("lds_keys", C.c_uint64), ("deep_keys", C.c_uint64), ("events", C.c_uint64),
                 ("tier0_ms", C.c_double), ("tier3_ms", C.c_double),
-                ("probes_t3", C.c_uint64)]
+                ("probes_t3", C.c_uint64), ("t3_bytes", C.c_uint64)]
 
 
 class LcSynthOpts(C.Structure):

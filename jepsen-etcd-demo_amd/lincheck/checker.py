@@ -156,7 +156,7 @@ class Device:
         return KeyResults(arrs["valid"][:K], arrs["fail_event"][:K], arrs["cause"][:K],
                           arrs["peak"][:K], arrs["final"][:K], arrs["n_final"][:K],
                           dict(kernel_ms=st.kernel_ms, tier0_ms=st.tier0_ms, tier3_ms=st.tier3_ms, total_ms=st.total_ms,
-                               probes=st.probes, probes_t3=st.probes_t3,
+                               probes=st.probes, probes_t3=st.probes_t3, t3_bytes=st.t3_bytes,
                                keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events))
 
     def check(self, packed: Packed, verdicts_only: bool = False) -> KeyResults:
