@@ -256,6 +256,10 @@ struct Dev {
     int cu_count = 256;
     hipStream_t stream = nullptr;
     hipStream_t vstream = nullptr;  // validation of host-unchecked batches, beside T0
+    hipStream_t cstream = nullptr;  // lc_check_node's chunked uploads, ahead of the searches
+    static constexpr int NODE_CHUNKS = 4;
+    DevBatch *chunk[NODE_CHUNKS] = {};
+    hipEvent_t chunk_ready[NODE_CHUNKS] = {};
     hipEvent_t vin = nullptr, vdone = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr, et3a = nullptr, et3b = nullptr;
     hipEvent_t ea0 = nullptr, ea1 = nullptr;  // span of the LC_DEV_ASYNC steps since lc_wait
@@ -339,6 +343,12 @@ struct Dev {
         for (hipEvent_t &e : args_ev)
             if (e) (void)hipEventDestroy(e);
         delete staged;
+        for (int i = 0; i < NODE_CHUNKS; ++i) {
+            delete chunk[i];
+            if (chunk_ready[i]) (void)hipEventDestroy(chunk_ready[i]);
+        }
+        if (cstream) (void)hipStreamSynchronize(cstream);
+        if (cstream) (void)hipStreamDestroy(cstream);
         if (vstream) (void)hipStreamSynchronize(vstream);
         for (hipEvent_t e : {e0, e1, et0, et3a, et3b, ea0, ea1, vin, vdone})
             if (e) (void)hipEventDestroy(e);
@@ -486,6 +496,7 @@ static int dev_init(Dev *c, int device) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->vstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->vin, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->vdone, hipEventDisableTiming));
     for (hipEvent_t *e : {&c->e0, &c->e1, &c->et0, &c->et3a, &c->et3b, &c->ea0, &c->ea1}) HIPCHK(hipEventCreate(e));
@@ -788,7 +799,8 @@ static void shard_keys(const lc_batch *b, int n, int64_t *key0) {
 // sync: wait for the copies (the caller may free its arrays on return);
 // otherwise the caller keeps them alive until its stream has passed them.
 static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, bool validated,
-                       const uint32_t *events_src = nullptr, bool sync = true) {
+                       const uint32_t *events_src = nullptr, bool sync = true, hipStream_t stream = nullptr) {
+    hipStream_t cs = stream ? stream : c->stream;
     const int64_t K = b->n_keys;
     d->device = c->device;
     d->n_keys = K;
@@ -846,10 +858,10 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     d->key_error = b->key_error ? (uint8_t *)(dm + o_err) : nullptr;
     if (d->n_events)
         HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
-                              hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(dm, h, bytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipEventRecord(d->hmeta_done, c->stream));
-    if (sync) HIPCHK(hipStreamSynchronize(c->stream));
+                              hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemcpyAsync(dm, h, bytes, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(d->hmeta_done, cs));
+    if (sync) HIPCHK(hipStreamSynchronize(cs));
     return LC_OK;
 }
 
@@ -896,7 +908,7 @@ enum ResMode { RES_HOST = 0, RES_DEV = 1, RES_CTX = 2 };
 // in c's own device arrays (r unused).  allow_async: a step that is T0 alone
 // is only enqueued (*enqueued = true; errors surface at the next wait).
 static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mode, bool allow_async, int64_t key0,
-                      lc_stats *st, bool *enqueued = nullptr) {
+                      lc_stats *st, bool *enqueued = nullptr, int64_t res_off = 0) {
     if (enqueued) *enqueued = false;
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(c->device));
@@ -918,7 +930,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         a.valid = r->valid; a.fail_event = r->fail_event; a.cause = r->cause;
         a.peak = r->peak_configs; a.final_cfg = r->final_configs; a.n_final = r->n_final;
     } else {
-        a.valid = c->valid; a.fail_event = c->fail_event; a.cause = c->cause;
+        a.valid = c->valid + res_off; a.fail_event = c->fail_event + res_off; a.cause = c->cause + res_off;
         a.peak = (mode == RES_HOST && r->peak_configs) ? c->peak : nullptr;
         a.final_cfg = (mode == RES_HOST && r->final_configs) ? c->final_cfg : nullptr;
         a.n_final = (mode == RES_HOST && r->n_final) ? c->n_final : nullptr;
@@ -1479,18 +1491,60 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
         if (!d->staged) return lc::fail(LC_E_NOMEM, "lc_check_node: out of memory");
     }
     const auto t_prep = std::chrono::steady_clock::now();
-    rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false);  // this call waits before it returns
-    if (rc) return rc;
-    const auto t_up = std::chrono::steady_clock::now();
+    // A large register-tier shard (throughput-bound: many keys per SIMD) is
+    // uploaded and searched in NODE_CHUNKS key chunks: the copies run on a
+    // stream of their own, and each chunk's search waits only for its own
+    // copy, so the host-to-device transfer overlaps the search
+    // (LC_NODE_CHUNKS=1 turns it off).
+    const int64_t K = b->n_keys;
+    const uint64_t n_ev = K ? b->ev_off[K] : 0;
+    const bool can_chunk = sh.t0_only && !(c->o.flags & LC_OPT_COUNT_PROBES) && K >= Dev::NODE_CHUNKS;
+    bool big = K >= 16 * (int64_t)d->cu_count && n_ev >= (8u << 20);
+    if (const char *e = std::getenv("LC_NODE_CHUNKS")) big = std::atoi(e) > 1;
+    const int chunks = can_chunk && big ? Dev::NODE_CHUNKS : 1;
     lc_result none{};
     bool enq = false;
     // on an error below, the copies out of the caller's arrays are waited for
     auto drained = [&](int e) {
+        (void)hipStreamSynchronize(d->cstream);
         (void)hipStreamSynchronize(d->stream);
         return e;
     };
-    rc = dev_search(d, d->staged, &none, RES_CTX, true, 0, st, &enq);
-    if (rc) return drained(rc);
+    std::chrono::steady_clock::time_point t_up;
+    if (chunks > 1) {
+        rc = ensure_capacity(d, K);
+        if (rc) return rc;
+        int64_t key0[Dev::NODE_CHUNKS + 1];
+        shard_keys(b, chunks, key0);
+        for (int i = 0; i < chunks; ++i) {
+            if (!d->chunk[i]) {
+                d->chunk[i] = new (std::nothrow) DevBatch();
+                if (!d->chunk[i]) return drained(lc::fail(LC_E_NOMEM, "lc_check_node: out of memory"));
+            }
+            if (!d->chunk_ready[i]) HIPCHK(hipEventCreateWithFlags(&d->chunk_ready[i], hipEventDisableTiming));
+            std::vector<uint64_t> off;
+            const lc_batch s = sub_batch(b, key0[i], key0[i + 1], off);
+            const uint32_t *es = src ? src + b->ev_off[key0[i]] : nullptr;
+            rc = upload_into(d, &s, d->chunk[i], sh, !sh.t0_only, es, false, d->cstream);
+            if (rc) return drained(rc);
+            HIPCHK(hipEventRecord(d->chunk_ready[i], d->cstream));
+        }
+        t_up = std::chrono::steady_clock::now();
+        for (int i = 0; i < chunks && rc == 0; ++i) {
+            HIPCHK(hipStreamWaitEvent(d->stream, d->chunk_ready[i], 0));
+            bool e = false;
+            rc = dev_search(d, d->chunk[i], &none, RES_CTX, true, key0[i], st, &e, key0[i]);
+            enq = i == 0 ? e : (enq && e);
+        }
+        if (rc) return drained(rc);
+        if (!enq) return drained(lc::fail(LC_E_DEVICE, "lc_check_node: a chunk left the register tier"));
+    } else {
+        rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false);
+        if (rc) return rc;
+        t_up = std::chrono::steady_clock::now();
+        rc = dev_search(d, d->staged, &none, RES_CTX, true, 0, st, &enq);
+        if (rc) return drained(rc);
+    }
     const auto t_search = std::chrono::steady_clock::now();
     rc = gather_node(c, d, b->n_keys, block);
     if (rc) return drained(rc);
@@ -1508,7 +1562,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
                          hipSuccess)
         return drained(lc::fail(LC_E_DEVICE, "lc_check_node: record download failed"));
     const auto t_gather = std::chrono::steady_clock::now();
-    if (enq) {  // a T0-only step: one wait for the search, the exchange and the download
+    if (enq) {  // a T0-only step (or chunks): one wait for the search, the exchange and the download
         int n_async = 0;
         float span = 0;
         rc = dev_wait(d, &n_async, &span);

@@ -256,3 +256,33 @@ def test_wait_step_waits_for_the_step_asked():
     assert n == 2
     _, orcB = cref.check_history(hB.as_c(), budget=dev.budget, threads=8)
     np.testing.assert_array_equal(outs[1][2][0].get(np.int8), orcB["valid"])
+
+
+@pytest.mark.parametrize("forced", [True, False])
+def test_node_chunked_upload_pipeline(forced, monkeypatch):
+    """lc_check_node on a large register-tier shard: key chunks uploaded on a
+    stream of their own, each chunk's search waiting for its own copy.  The
+    records equal the one-launch check (LC_NODE_CHUNKS=1), and the oracle's
+    verdicts.  forced: a small C5-shaped shard chunked by LC_NODE_CHUNKS=4;
+    otherwise a C3-shard-sized one (4,096+ keys, 8M+ events) chunked by
+    default."""
+    if forced:
+        h = H.synth(n_keys=500, ops_per_key=300, concurrency=10, anomaly_rate=0.1, seed=73)
+        monkeypatch.setenv("LC_NODE_CHUNKS", "4")
+    else:
+        h = H.synth(n_keys=6000, ops_per_key=800, concurrency=10, anomaly_rate=0.02, seed=74)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0)
+    rec, _ = dev.check_node(pk, K)
+    for _ in range(2):  # repeated steps reuse the chunk batches
+        rec2, _ = dev.check_node(pk, K)
+        np.testing.assert_array_equal(rec2, rec)
+    monkeypatch.setenv("LC_NODE_CHUNKS", "1")
+    one, _ = Device(0).check_node(pk, K)
+    np.testing.assert_array_equal(rec, one)
+    v, c, fe = _decode(rec, K)
+    keys, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)
+    np.testing.assert_array_equal(v, orc["valid"])
+    np.testing.assert_array_equal(fe, orc["fail_event"])
+    assert (v == 0).any()
