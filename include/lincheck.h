@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 7
+#define LC_ABI_VERSION 8
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -67,6 +67,13 @@ extern "C" {
 #define LC_F_OTHER 3   /* nemesis :start/:stop and anything else */
 #define LC_F_ACQUIRE 4 /* (model/mutex) :acquire                  */
 #define LC_F_RELEASE 5 /* (model/mutex) :release                  */
+#define LC_F_TXN     6 /* (model/multi-register) :txn            */
+
+/* A :txn value is a sequence of micro-ops [f k v] (knossos.model/multi-register):
+ * f LC_MOP_READ (v nil reads anything) or LC_MOP_WRITE, k a register id, v
+ * an integer or LC_NIL.  lc_history.mop holds them as int64 triples. */
+#define LC_MOP_READ  0
+#define LC_MOP_WRITE 1
 
 #define LC_NIL        INT64_MIN  /* a nil value                                */
 #define LC_NO_KEY     INT64_MIN  /* :value is not an independent tuple [k v]   */
@@ -91,6 +98,11 @@ typedef struct lc_history {
     const int64_t *v0;
     const int64_t *v1;
     const int64_t *index;    /* may be NULL: rows are then their own index */
+    /* :txn values (LC_F_TXN rows; ABI 8).  Row r's micro-ops are the triples
+     * mop[3*i .. 3*i+2] for i in [mop_off[r], mop_off[r + 1]); a row with an
+     * empty range has a nil :value.  Both may be NULL when no row is a :txn. */
+    const int64_t *mop_off;  /* [n + 1] or NULL */
+    const int64_t *mop;      /* [3 * mop_off[n]] (f, register, value)       */
 } lc_history;
 
 /* ---- packed per-key event streams (rows A3-A5) ---------------------------- */
@@ -128,6 +140,14 @@ typedef struct lc_history {
 #define LC_STATE_NONE 0x7FFFu
 #define LC_DESC(f, a, b) ((uint32_t)(f) | ((uint32_t)(a) << 2) | ((uint32_t)(b) << 17))
 
+/* Table models ((model/multi-register), whose state is a map of registers):
+ * lc_batch.table holds, per key, one row of key_states[key] u16 entries per
+ * distinct op -- the next state id from each state, LC_TABLE_NONE when the
+ * step is inconsistent -- and the op's descriptor trans[] entry is the offset
+ * of its row in table[] (knossos.model.memo's state x transition table).
+ * Such a batch needs trans_off and key_states. */
+#define LC_TABLE_NONE 0xFFFFu
+
 /* Limits of the packed form.  A key beyond them is reported :unknown with
  * cause LC_CAUSE_WINDOW / LC_CAUSE_STATES (identically in oracle/). */
 #define LC_NARROW_MAX_SLOTS  56   /* u64 config: 8-bit state | 56 slot bits   */
@@ -153,6 +173,10 @@ typedef struct lc_batch {
                                    LC_CAUSE_ERROR and its events are ignored --
                                    jepsen.checker/check-safe around that one key
                                    (etcdemo.clj:115).  NULL = no such key.       */
+    const uint16_t *table;      /* [n_table] transition table of a table model
+                                   (LC_TABLE_NONE above), or NULL: trans[] are
+                                   LC_DESC descriptors (ABI 8)                 */
+    int64_t         n_table;
 } lc_batch;
 
 /* The Knossos model a batch is checked against (knossos.model, SURVEY.md
@@ -165,9 +189,21 @@ typedef struct lc_batch {
 #define LC_MODEL_CAS_REGISTER 0
 #define LC_MODEL_REGISTER     1
 #define LC_MODEL_MUTEX        2
+/*   multi-register  knossos.model/multi-register: a map of registers, one
+ *                :f :txn whose :value is a sequence of [:read k v] /
+ *                [:write k v] micro-ops applied in order (a read of v legal
+ *                iff v is nil or register k holds v).  States are the maps
+ *                reachable from the initial one (memo), numbered per key; ops
+ *                become rows of lc_batch.table.  A key with more than
+ *                LC_WIDE_MAX_STATES reachable maps is :unknown (cause
+ *                states).  An :ok completion's micro-ops replace the
+ *                invocation's (a read learns what it read).             */
+#define LC_MODEL_MULTI_REGISTER 3
 
 typedef struct lc_pack_opts {
     int32_t model;     /* LC_MODEL_* (0 = cas-register) */
+    int32_t n_init;    /* multi-register: initial registers, pairs        */
+    const int64_t *init;  /* [2 * n_init] (register, value); others absent */
 } lc_pack_opts;
 
 typedef struct lc_packed lc_packed;  /* library-owned */
@@ -204,6 +240,11 @@ const char *lc_packed_key_error(const lc_packed *p, int64_t i);
 int lc_packed_state_value(const lc_packed *p, int64_t i, uint32_t s, int64_t *value, int *is_nil);
 /* Every key at once (n_keys entries), in packed order. */
 int lc_packed_keys(const lc_packed *p, int64_t *out);
+/* multi-register: the map state id s of key i stands for, as (register,
+ * value) pairs in register order (a register the map lacks is absent; a
+ * present nil is LC_NIL).  Writes at most cap pairs; returns how many the
+ * state has. */
+int64_t lc_packed_state_map(const lc_packed *p, int64_t i, uint32_t s, int64_t *regs, int64_t *vals, int64_t cap);
 
 /* ---- Knossos-shaped result of one key -------- */
 /* jepsen.checker/linearizable's result map (etcdemo.clj:117-118) for packed
@@ -213,7 +254,8 @@ int lc_packed_keys(const lc_packed *p, int64_t *out);
  * given to lc_pack); an op is (invoke row, completion row or -1), from which
  * a binding builds the op map knossos.history/complete would (the
  * invocation, taking the completion's :value when it has none).  Model
- * states are register values (LC_NIL for nil).  Writes int64 words:
+ * states are register values (LC_NIL for nil; multi-register: state ids, see
+ * lc_packed_state_map).  Writes int64 words:
  *   [0] :op row (the :ok that could not be linearized) or -1
  *   [1] :previous-ok row (= :last-op: the last :ok before it) or -1
  *   [2] n_configs (<= max_paths)   [3] n_paths (<= max_paths)

@@ -33,6 +33,7 @@ public final class LincheckNative {
     public static native int lc_packed_view(Pointer packed, Pointer batch);
     public static native int lc_packed_keys(Pointer packed, long[] out);
     public static native String lc_packed_key_error(Pointer packed, long i);
+    public static native long lc_packed_state_map(Pointer packed, long i, int s, long[] regs, long[] vals, long cap);
 
     public static native int lc_check_batch(Pointer ctx, Pointer batch, Pointer result, Pointer stats);
 

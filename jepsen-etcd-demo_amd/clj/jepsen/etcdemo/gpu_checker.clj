@@ -38,10 +38,20 @@
 (def ^:private nil-long Long/MIN_VALUE)  ; LC_NIL / LC_NO_KEY / LC_NO_PROCESS
 
 (def ^:private type-code {:invoke 0 :ok 1 :fail 2 :info 3})
-(def ^:private f-code    {:read 0 :write 1 :cas 2 :acquire 4 :release 5})
+(def ^:private f-code    {:read 0 :write 1 :cas 2 :acquire 4 :release 5 :txn 6})
+(def ^:private mop-code  {:read 0 :write 1})    ; LC_MOP_* of a :txn micro-op
 
 ;; LC_MODEL_*: which knossos.model the device checks against
-(def ^:private model-code {:cas-register 0 :register 1 :mutex 2})
+(def ^:private model-code {:cas-register 0 :register 1 :mutex 2 :multi-register 3})
+
+;; (model/multi-register) registers named by anything but an integer get ids
+;; from 2^62 up (lincheck.history.NAMED_REG_BASE); names holds the reverse map
+(def ^:private named-reg-base (bit-shift-left 1 62))
+(defn- reg-id [names r]
+  (if (integer? r)
+    (long r)
+    (or (get @names r)
+        (let [id (+ named-reg-base (count @names))] (vswap! names assoc r id) id))))
 
 ;; LC_ALGO_*: jepsen.checker/linearizable's :algorithm (:linear, :wgl, else
 ;; competition).  All three run the same device search; only :analyzer differs.
@@ -52,9 +62,19 @@
 (defn- long-or-nil [x] (if (nil? x) nil-long (long x)))
 
 (defn- marshal
-  "Writes the history into the struct-of-arrays lc_history (8 x 8 bytes)."
-  [history]
+  "Writes the history into the struct-of-arrays lc_history (10 x 8 bytes,
+  ABI 8).  :txn values go to mop_off / mop; `names` collects named registers."
+  [history names]
   (let [n      (count history)
+        txns   (keep-indexed (fn [i op]
+                               (when (= :txn (:f op))
+                                 (let [v (:value op)
+                                       v (if (independent/tuple? v) (val v) v)]
+                                   (when (seq v) [i v]))))
+                             history)
+        n-mop  (reduce + 0 (map (comp count second) txns))
+        mop-off (when (seq txns) (Memory. (* 8 (inc n))))
+        mop    (when (seq txns) (Memory. (max 8 (* 24 n-mop))))
         bytes  (max 8 (* 8 n))
         type   (Memory. (max 1 n))
         fn     (Memory. (max 1 n))
@@ -63,7 +83,7 @@
         v0     (Memory. bytes)
         v1     (Memory. bytes)
         index  (Memory. bytes)
-        hist   (Memory. 64)]
+        hist   (Memory. 80)]
     (loop [i 0, ops (seq history)]
       (when ops
         (let [op    (first ops)
@@ -81,10 +101,22 @@
           (.setLong v1 (* 8 i) (if (= fc 3) nil-long (long-or-nil b)))
           (.setLong index (* 8 i) (long (or (:index op) -1)))
           (recur (inc i) (next ops)))))
+    (when mop-off
+      (let [by-row (into {} txns)]
+        (loop [i 0, at 0]
+          (.setLong mop-off (* 8 i) at)
+          (when (< i n)
+            (let [ms (get by-row i)]
+              (doseq [[j [f r x]] (map-indexed vector ms)]
+                (.setLong mop (* 24 (+ at j)) (long (mop-code f)))
+                (.setLong mop (+ 8 (* 24 (+ at j))) (reg-id names r))
+                (.setLong mop (+ 16 (* 24 (+ at j))) (long-or-nil x)))
+              (recur (inc i) (+ at (count ms))))))))
     (.setLong hist 0 n)
-    (doseq [[off m] [[8 type] [16 fn] [24 proc] [32 key] [40 v0] [48 v1] [56 index]]]
+    (doseq [[off m] [[8 type] [16 fn] [24 proc] [32 key] [40 v0] [48 v1] [56 index]
+                     [64 mop-off] [72 mop]]]
       (.setPointer hist off m))
-    {:hist hist :keep [type fn proc key v0 v1 index]}))
+    {:hist hist :keep [type fn proc key v0 v1 index mop-off mop]}))
 
 ;; One lc_ctx per (device(s), budget, algorithm), created on first use and
 ;; kept: a context owns its streams, scratch and staging buffers, so repeated
@@ -132,17 +164,28 @@
     (if (independent/tuple? v) (assoc op :value (val v)) op)))
 
 (defn- model-of
-  "The knossos model record holding register value x (LC_NIL = nil)."
-  [model x]
+  "The knossos model record holding register value x (LC_NIL = nil); for
+  multi-register, x is a state id and the map comes from lc_packed_state_map."
+  [model x packed i names]
   (let [v (when-not (= x nil-long) x)]
     (case model
       :cas-register (model/cas-register v)
       :register     (model/register v)
-      :mutex        (assoc (model/mutex) :locked (= 1 v)))))
+      :mutex        (assoc (model/mutex) :locked (= 1 v))
+      :multi-register
+      (let [n     (LincheckNative/lc_packed_state_map packed i (int x) nil nil 0)
+            regs  (long-array (max 1 n))
+            vals  (long-array (max 1 n))
+            by-id (into {} (map (fn [[r id]] [id r]) names))]
+        (check-rc (LincheckNative/lc_packed_state_map packed i (int x) regs vals n) "lc_packed_state_map")
+        (model/multi-register
+          (into {} (for [j (range n)]
+                     [(get by-id (aget regs j) (aget regs j))
+                      (let [y (aget vals j)] (when-not (= y nil-long) y))])))))))
 
 (defn- report
   "Decodes lc_report's words for packed key i into the :linear map."
-  [history model algorithm packed i valid fail-ev cause ^Memory finals n-final]
+  [history model algorithm packed i valid fail-ev cause ^Memory finals n-final names]
   (let [words (long-array 256)
         fin   (.share finals (* i max-final 16))
         need  (check-rc (LincheckNative/lc_report packed i valid fail-ev fin n-final max-final words 256)
@@ -155,8 +198,12 @@
                   w))
         row   (fn [r] (when (<= 0 r) (unwrap (nth history r))))
         op    (fn [inv done]               ; knossos.history/complete's invocation
-                (let [o (row inv)]
-                  (if (and (nil? (:value o)) (<= 0 done)) (assoc o :value (:value (row done))) o)))
+                (let [o (row inv)
+                      d (when (<= 0 done) (:value (row done)))]
+                  (cond (and (= :txn (:f o)) (some? d)) (assoc o :value d)  ; a :txn learns its reads
+                        (and (nil? (:value o)) (<= 0 done)) (assoc o :value d)
+                        :else o)))
+        model-of (fn [x] (model-of model x packed i names))
         fail-op (row (aget words 0))
         prev    (row (aget words 1))
         n-cfg   (aget words 2)
@@ -165,17 +212,17 @@
         take!   (fn [] (let [x (aget words @pos)] (vswap! pos inc) x))
         ops!    (fn [] (vec (repeatedly (take!) #(op (take!) (take!)))))
         configs (vec (repeatedly n-cfg
-                                 (fn [] (let [m (model-of model (take!))
+                                 (fn [] (let [m (model-of (take!))
                                               pending (ops!)
                                               linear  (ops!)]
                                           {:model m :last-op prev :pending pending :linearized linear}))))
         paths   (vec (repeatedly n-paths
                                  (fn []
-                                   (let [m0    (model-of model (take!))
+                                   (let [m0    (model-of (take!))
                                          steps (vec (repeatedly (take!)
                                                                 (fn [] (let [o (op (take!) (take!))]
-                                                                         {:op o :model (model-of model (take!))}))))
-                                         bad   (model/step (model-of model (take!)) fail-op)]
+                                                                         {:op o :model (model-of (take!))}))))
+                                         bad   (model/step (model-of (take!)) fail-op)]
                                      (into [{:op prev :model m0}]
                                            (conj steps {:op fail-op :model {:msg (:msg bad)}}))))))
         base    {:analyzer (if (= algorithm :wgl) :wgl :linear)
@@ -189,17 +236,26 @@
 
 (defn check-history
   "Runs the device search over every key; returns {k :linear-map}."
-  [history {:keys [device devices budget model algorithm]
+  [history {:keys [device devices budget model algorithm] :as opts
             :or {device 0 budget (bit-shift-left 1 20) model :cas-register
                  algorithm :linear}}]
   (let [history    (vec history)
-        {:keys [hist keep]} (marshal history)
-        pack-opts  (doto (Memory. 4) (.setInt 0 (int (model-code model))))
+        names      (volatile! {})                  ; named register -> id
+        {:keys [hist keep]} (marshal history names)
+        init       (when (= model :multi-register) (seq (:init opts)))   ; (model/multi-register init)
+        init-mem   (when init (Memory. (* 16 (count init))))
+        _          (doseq [[j [r x]] (map-indexed vector init)]
+                     (.setLong init-mem (* 16 j) (reg-id names r))
+                     (.setLong init-mem (+ 8 (* 16 j)) (long-or-nil x)))
+        pack-opts  (doto (Memory. 16) (.clear)                 ; sizeof(lc_pack_opts), ABI 8
+                     (.setInt 0 (int (model-code model)))
+                     (.setInt 4 (int (count init)))
+                     (.setPointer 8 init-mem))
         out        (Memory. 8)
         _          (check-rc (LincheckNative/lc_pack hist pack-opts out) "lc_pack")
         packed     (.getPointer out 0)]
     (try
-      (let [batch    (Memory. 80)                ; sizeof(lc_batch)
+      (let [batch    (Memory. 96)                ; sizeof(lc_batch), ABI 8
             _        (check-rc (LincheckNative/lc_packed_view packed batch) "lc_packed_view")
             n-keys   (.getLong batch 0)
             keys     (long-array (max 1 n-keys))
@@ -237,19 +293,20 @@
                            :configs [] :final-paths []}
                           :else
                           (report history model algorithm packed i v (.getInt fail-ev (* 4 i)) c
-                                  finals (.getInt n-final (* 4 i)))))))
+                                  finals (.getInt n-final (* 4 i)) @names)))))
             (transient {})
             (range n-keys))))
       (finally
         (LincheckNative/lc_packed_free packed)
-        (identity keep)))))
+        (identity [keep init-mem])))))
 
 (defn checker
   "independent/checker over compose{:linear linearizable(cas-register),
   :timeline html}, with the :linear part batched on the GPU.  opts:
   :device (or :devices, a vector: one key shard per entry, checked at once),
-  :budget, :model (:cas-register, the default and the demo's; :register or
-  :mutex for the other Knossos models, SURVEY.md 8(f) F-4) and :algorithm
+  :budget, :model (:cas-register, the default and the demo's; :register,
+  :mutex or :multi-register -- with :init, its initial map -- for the other
+  Knossos models, SURVEY.md 8(f) F-4) and :algorithm
   (:linear, the demo's; :wgl; anything else = competition)."
   ([] (checker {}))
   ([opts]

@@ -47,6 +47,8 @@ struct lc_hist {
     std::vector<uint8_t> type, f;
     std::vector<int64_t> process, key, v0, v1, index;
     std::vector<int64_t> anomalous_keys;
+    // :txn micro-ops (lc_history.mop_off / mop); empty when no row is a :txn
+    std::vector<int64_t> mop_off, mop;
 
     void reserve(size_t n) {
         type.reserve(n); f.reserve(n); process.reserve(n); key.reserve(n);
@@ -62,6 +64,9 @@ struct lc_hist {
         h.n = size();
         h.type = type.data(); h.f = f.data(); h.process = process.data(); h.key = key.data();
         h.v0 = v0.data(); h.v1 = v1.data(); h.index = index.data();
+        const bool txn = !mop_off.empty();
+        h.mop_off = txn ? mop_off.data() : nullptr;
+        h.mop = txn ? mop.data() : nullptr;
         return h;
     }
 };

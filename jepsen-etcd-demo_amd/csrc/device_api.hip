@@ -189,6 +189,8 @@ struct DevBatch {
     uint8_t *key_width = nullptr;
     uint16_t *key_states = nullptr;
     uint8_t *key_error = nullptr;
+    uint16_t *table = nullptr; // a table model's rows (lc_batch.table), or null
+    int64_t n_table = 0;
     int32_t *order = nullptr;  // LPT: keys by event count, descending
     bool t0_only = false;      // every key declared to fit the register lattice
     bool taggable = false;     // keys may be cut into segments (shared table, states 0..5, no op installs nil)
@@ -621,6 +623,10 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
             if (b->key_error && b->key_error[k]) continue;  // not searched
             const uint64_t tb = b->trans_off ? b->trans_off[k] : 0;
             const uint32_t ns = (b->trans_off && b->key_states) ? b->key_states[k] : 0xFFFFFFFFu;
+            // a table model: each op's row must lie in table[] and name only
+            // states of the key (a key beyond LC_WIDE_MAX_STATES is never stepped)
+            const bool rows = b->table && ns <= LC_WIDE_MAX_STATES;
+            uint64_t tmax = 0;
             uint64_t pend[2] = {0, 0};
             uint32_t width = 0;
             for (uint64_t j = b->ev_off[k]; j < b->ev_off[k + 1]; ++j) {
@@ -636,7 +642,8 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
                     const uint64_t ti = tb + LC_EV_TRANS(ev);
                     if (ti >= (uint64_t)b->n_trans) { bad[t] = 2; break; }
                     const uint32_t d = b->trans[ti], f = d & 3u;
-                    if ((f == LC_T_WRITE || f == LC_T_CAS) && (d >> 17) >= ns) { bad[t] = 5; break; }
+                    if (b->table) tmax = std::max(tmax, ti + 1);
+                    else if ((f == LC_T_WRITE || f == LC_T_CAS) && (d >> 17) >= ns) { bad[t] = 5; break; }
                     if (s == 127) continue;
                     if ((pend[s >> 6] >> (s & 63)) & 1) { bad[t] = 3; break; }
                     pend[s >> 6] |= 1ull << (s & 63);
@@ -644,6 +651,12 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
                 }
             }
             if (!bad[t] && b->key_width && width > b->key_width[k]) bad[t] = 4;
+            for (uint64_t ti = tb; rows && !bad[t] && ti < tmax; ++ti) {
+                const uint64_t r0 = b->trans[ti];
+                if (r0 + ns > (uint64_t)b->n_table) { bad[t] = 5; break; }
+                for (uint64_t j = 0; j < ns; ++j)
+                    if (b->table[r0 + j] != LC_TABLE_NONE && b->table[r0 + j] >= ns) { bad[t] = 5; break; }
+            }
             if (bad[t]) badkey[t] = k;
         }
     };
@@ -675,6 +688,13 @@ static int validate_batch(const lc_batch *b) {
     }
     if (b->ev_off[b->n_keys] && !b->events) return lc::fail(LC_E_INVALID, "batch: events missing");
     if (b->init_state >= LC_STATE_NONE) return lc::fail(LC_E_INVALID, "batch: bad init_state");
+    if (b->table) {
+        // rows of a table model: trans[] are offsets into table[], checked per
+        // key against its state count with the events (validate_events)
+        if (b->n_table <= 0 || b->n_table > 0xFFFFFFFFll || !b->trans_off || !b->key_states)
+            return lc::fail(LC_E_INVALID, "batch: a table model needs n_table, trans_off and key_states");
+        return LC_OK;
+    }
     for (int64_t i = 0; i < b->n_trans; ++i) {
         uint32_t d = b->trans[i];
         uint32_t f = d & 3u, bb = d >> 17;
@@ -724,6 +744,7 @@ static bool segments_pay(const lc_batch *b) {
 
 static Shape batch_shape(const lc_batch *b) {
     Shape s;
+    if (b->table) return s;  // a table model: the set tiers only (no register lattice)
     uint32_t mx = b->init_state;
     for (int64_t i = 0; i < b->n_trans; ++i) {
         const uint32_t t = b->trans[i], f = t & 3u, a = (t >> 2) & 0x7FFFu, bb = t >> 17;
@@ -849,6 +870,13 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     char *dm = nullptr;
     HIPCHK(grow(d->mem[0], dm, bytes));
     HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
+    d->table = nullptr;
+    d->n_table = b->table ? b->n_table : 0;
+    if (b->table) {
+        // a table model's rows (small next to the events; pageable source)
+        HIPCHK(grow(d->mem[2], d->table, (size_t)b->n_table));
+        HIPCHK(hipMemcpyAsync(d->table, b->table, (size_t)b->n_table * 2, hipMemcpyHostToDevice, cs));
+    }
     d->ev_off = (uint64_t *)(dm + o_off);
     d->order = (int32_t *)(dm + o_order);
     d->trans = (uint32_t *)(dm + o_trans);
@@ -921,6 +949,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     lcd::Args a{};
     a.ev_off = d->ev_off; a.events = d->events; a.trans = d->trans; a.trans_off = d->trans_off;
     a.key_width = d->key_width; a.key_states = d->key_states; a.key_error = d->key_error;
+    a.table = d->table;
     a.init_state = d->init_state; a.shared_states = d->shared_states;
     a.n_trans = (uint32_t)d->n_trans;
     a.strict = d->validated ? 0 : 1;
@@ -1076,9 +1105,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
                                 vblocks, c->stream));
         c->spec_parity ^= 1;
         HIPCHK(hipEventRecord(c->et0, c->stream));
-    } else if (K > 0) {
+    } else if (K > 0 && !d->table) {
         HIPCHK(lcd::launch_t0(a0, dargs, g0, t0_wide, c->stream, ticket_base));
         HIPCHK(hipEventRecord(c->et0, c->stream));
+    } else if (K > 0) {
+        HIPCHK(hipEventRecord(c->et0, c->stream));  // a table model: no register lattice
     }
     if (K > 0 && a.strict && !spec) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));
     if (async) {
@@ -1096,6 +1127,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         // T1: LDS hash sets
         lcd::Args a1 = a;
         a1.order = spill0; a1.n_order = 0; a1.n_in = n_spill0; a1.ticket = c->counters + 9;
+        if (d->table) { a1.order = d->order; a1.n_order = (int32_t)K; a1.n_in = nullptr; }  // every key
         a1.spill = spill1; a1.n_spill = n_spill1; a1.wide = wide; a1.n_wide = n_wide;
         int g1 = (int)std::min<int64_t>(K, (int64_t)c->cu_count * 7);
         HIPCHK(lcd::launch_t1(a1, g1, c->stream));
@@ -1158,7 +1190,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         // Narrow keys: the layered form first (<= 8 states; LC_T3_LAYERS=0
         // turns it off for A/B runs), the config-keyed narrow tier for the
         // keys it hands on (cnt[6]).
-        const bool layers = !(std::getenv("LC_T3_LAYERS") && std::atoi(std::getenv("LC_T3_LAYERS")) == 0);
+        // (the layered form steps ops as register-state masks: not a table model)
+        const bool layers = !d->table && !(std::getenv("LC_T3_LAYERS") && std::atoi(std::getenv("LC_T3_LAYERS")) == 0);
         int32_t *narrow_list = spill2, *narrow_n = n_spill2;
         int32_t n_narrow = n_deep;
         if (n_deep > 0 && layers) {

@@ -26,7 +26,14 @@ __device__ __forceinline__ uint32_t hash64(uint64_t c) {
 // cas-register step on a descriptor (include/lincheck.h LC_T_*), branch-free:
 //   READ_ANY: legal, same state   READ: legal iff s == a, same state
 //   WRITE:    legal, state := b   CAS:  legal iff s == a, state := b
-__device__ __forceinline__ bool step(uint32_t s, uint32_t d, uint32_t &s2) {
+// A table model (tab != null, uniform per launch): d is the offset of the
+// op's row, whose entry s is the next state (LC_TABLE_NONE: inconsistent).
+__device__ __forceinline__ bool step(const uint16_t *tab, uint32_t s, uint32_t d, uint32_t &s2) {
+    if (tab) {
+        const uint32_t t = tab[d + s];
+        s2 = t;
+        return t != LC_TABLE_NONE;
+    }
     uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
     s2 = f >= LC_T_WRITE ? b : s;
     return f == LC_T_READ_ANY || f == LC_T_WRITE || s == a;

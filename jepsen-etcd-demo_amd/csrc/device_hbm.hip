@@ -378,7 +378,7 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             uint64_t m = 0;
             for (uint32_t k = 0; k < nc; ++k) {
                 uint32_t s2;
-                if (step(st, sh.cand_desc[k], s2)) m |= 1ull << sh.cand_slot[k];
+                if (step(a.table, st, sh.cand_desc[k], s2)) m |= 1ull << sh.cand_slot[k];
             }
             sh.legal[st] = m;
         }
@@ -438,7 +438,7 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
                     const uint32_t q = act ? (uint32_t)__builtin_ctzll(m) : 0u;
                     m &= m - 1;
                     uint32_t s2 = st;
-                    (void)step(st, sh.slot_desc[q], s2);
+                    (void)step(a.table, st, sh.slot_desc[q], s2);
                     probes += act;
                     if (act) stg[nst + rank_of(bm)] = C::lin(c, q, s2);
                     nst += (uint32_t)__popcll(bm);
@@ -454,7 +454,7 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             for (uint32_t k = 0; k < nc; ++k) {
                 const uint32_t q = sh.cand_slot[k];
                 uint32_t s2 = 0;
-                const bool act = in && !C::has(c, q) && step(st, sh.cand_desc[k], s2);
+                const bool act = in && !C::has(c, q) && step(a.table, st, sh.cand_desc[k], s2);
                 probes += act;
                 const uint64_t m = __ballot(act);
                 if (m == 0) continue;
@@ -487,7 +487,7 @@ __device__ int ok_pass(const Args &a, Slot<C> &sl, HbmShared<C, WG> &sh, typenam
             const uint32_t j = j0 + u * WG + tid;
             const T c = j < nI ? sl.I[j] : C::init(0);
             uint32_t s2 = 0;
-            act[u] = j < nI && step(C::state(c), dp, s2);
+            act[u] = j < nI && step(a.table, C::state(c), dp, s2);
             probes += act[u];
             k2[u] = C::restate(c, s2);
         }

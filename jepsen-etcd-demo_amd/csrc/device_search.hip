@@ -58,6 +58,10 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
     const uint32_t lane = lane_id();
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
+    if (a.key_error && a.key_error[key]) {  // a table-model batch starts here, not in T0
+        finish_key(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+        return K_DONE;
+    }
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
         finish_key(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
@@ -154,7 +158,7 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
                         const uint32_t q = t.slotlist[k];
                         const uint32_t dq = t.desclist[k];
                         uint32_t s2 = 0;
-                        act = act && !((c >> q) & 1ull) && step((uint32_t)(c >> 56), dq, s2);
+                        act = act && !((c >> q) & 1ull) && step(a.table, (uint32_t)(c >> 56), dq, s2);
                         const uint64_t c2 = ((uint64_t)s2 << 56) | (c & LMASK) | (1ull << q);
                         probes += (uint64_t)__popcll(__ballot(act));
                         uint32_t pos = 0;
@@ -186,7 +190,7 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
                 const uint32_t idx = j + lane;
                 const uint64_t c = idx < nI ? t.I[idx] : 0;
                 uint32_t s2 = 0;
-                const bool act = idx < nI && step((uint32_t)(c >> 56), dp, s2);
+                const bool act = idx < nI && step(a.table, (uint32_t)(c >> 56), dp, s2);
                 const uint64_t c2 = ((uint64_t)s2 << 56) | (c & LMASK);
                 probes += (uint64_t)__popcll(__ballot(act));
                 uint32_t pos = 0;

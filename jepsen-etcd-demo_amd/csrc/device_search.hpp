@@ -18,6 +18,7 @@ struct Args {
     const uint8_t *key_width;    // may be null
     const uint16_t *key_states;  // may be null
     const uint8_t *key_error;    // may be null: nonzero = :unknown (LC_CAUSE_ERROR), not searched
+    const uint16_t *table;       // may be null: a table model's rows (lc_batch.table); trans[] are row offsets
     uint32_t init_state;
     uint32_t shared_states;      // state ids used by the shared table (trans_off == null)
     uint64_t budget;

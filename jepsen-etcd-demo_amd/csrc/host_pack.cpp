@@ -23,6 +23,10 @@
 //   A4/A5 knossos.model/cas-register + knossos.model.memo: every surviving op
 //      becomes a transition descriptor over interned register states (state 0
 //      = nil, the initial value of (model/cas-register), etcdemo.clj:117).
+//      (model/multi-register): memo proper -- the maps
+//      reachable from the initial one under the key's distinct :txn ops are
+//      numbered breadth-first, and each op becomes a row of next-state ids
+//      (lc_batch.table).
 //
 // The pending-window slot of each op (lowest free slot at invoke, released at
 // :ok) is assigned here too: it is config-independent, so every device config
@@ -30,6 +34,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <stdexcept>
 #include <thread>
 #include <unordered_map>
 
@@ -38,8 +43,10 @@
 
 namespace {
 
-// Ops a model can step (knossos.model: cas-register, register, mutex).
+// Ops a model can step (knossos.model: cas-register, register, mutex,
+// multi-register).
 inline bool is_client_f(uint8_t f, int model) {
+    if (model == LC_MODEL_MULTI_REGISTER) return f == LC_F_TXN;
     if (model == LC_MODEL_MUTEX) return f == LC_F_ACQUIRE || f == LC_F_RELEASE;
     if (model == LC_MODEL_REGISTER) return f == LC_F_READ || f == LC_F_WRITE;
     return f == LC_F_READ || f == LC_F_WRITE || f == LC_F_CAS;
@@ -76,7 +83,14 @@ struct KOp {
     int64_t row_inv, row_ret;  // row_ret = -1: never returns
     uint8_t f, fate;           // fate: 0 pending-forever, 1 ok, 2 failed
     int64_t v0, v1;
+    int64_t mrow;              // :txn: the row whose micro-ops the op carries
 };
+
+// Micro-op range of row r of a history ([m0, m1) triples; empty if none).
+inline void mop_range(const lc_history &h, int64_t r, int64_t &m0, int64_t &m1) {
+    m0 = m1 = 0;
+    if (h.mop_off && h.mop) { m0 = h.mop_off[r]; m1 = h.mop_off[r + 1]; }
+}
 
 struct KeyOut {
     std::vector<uint32_t> ev;     // event words, trans field = local op index for now
@@ -100,14 +114,14 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
         int64_t p = h.process[r];
         if (t == LC_INVOKE) {
             if (!is_client_f(h.f[r], model)) {
-                static const char *names[] = {"cas-register", "register", "mutex"};
+                static const char *names[] = {"cas-register", "register", "mutex", "multi-register"};
                 out.err = LC_E_UNSUPPORTED;
                 out.msg = "row " + std::to_string(r) + ": " + names[model] + " cannot step this :f";
                 out.ops.clear();
                 return;
             }
             int32_t id = (int32_t)out.ops.size();
-            out.ops.push_back({r, -1, h.f[r], 0, h.v0[r], h.v1[r]});
+            out.ops.push_back({r, -1, h.f[r], 0, h.v0[r], h.v1[r], r});
             pm.set(p, id);
             row_op[(size_t)i] = id;
         } else if (t == LC_OK_T || t == LC_FAIL) {
@@ -123,7 +137,13 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
                 op.fate = 1;
                 op.row_ret = r;
                 // (or (:value invocation) (:value completion))
-                if (op.f == LC_F_CAS) {
+                if (op.f == LC_F_TXN) {
+                    // a :txn takes its completion's micro-ops when it has
+                    // some: the reads learn what they read
+                    int64_t m0, m1;
+                    mop_range(h, r, m0, m1);
+                    if (m1 > m0) op.mrow = r;
+                } else if (op.f == LC_F_CAS) {
                     if (op.v0 == LC_NIL && op.v1 == LC_NIL) { op.v0 = h.v0[r]; op.v1 = h.v1[r]; }
                 } else if (op.v0 == LC_NIL) {
                     op.v0 = h.v0[r];
@@ -172,14 +192,200 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
     out.width = std::min(maxslot + 1, 255);
 }
 
+// (model/multi-register) memo of one key: registers, reachable maps, table.
+constexpr int64_t ABSENT = LC_NIL + 1;  // a register the map lacks (reserved value)
+
+struct MrKey {
+    std::vector<int64_t> regs;      // register ids, ascending
+    std::vector<int64_t> states;    // S x R values (ABSENT / LC_NIL / integer)
+    std::vector<uint32_t> tid;      // per op of the key: its :txn id
+    std::vector<uint16_t> table;    // T x S next-state ids
+    uint32_t S = 0, T = 0;
+    bool too_many = false;          // > LC_WIDE_MAX_STATES maps
+    int err = 0;
+    std::string msg;
+};
+
+struct VecHash {
+    size_t operator()(const std::vector<int64_t> &v) const {
+        uint64_t x = 0x9E3779B97F4A7C15ull ^ v.size();
+        for (int64_t e : v) { x ^= (uint64_t)e + 0x9E3779B97F4A7C15ull + (x << 6) + (x >> 2); }
+        return (size_t)x;
+    }
+};
+
+void memo_multi_register(const lc_history &h, const KeyOut &o, const int64_t *init, int32_t n_init, MrKey &mk) {
+    // distinct :txn values (flattened triples, register ids as given)
+    std::unordered_map<std::vector<int64_t>, uint32_t, VecHash> tix;
+    std::vector<std::vector<int64_t>> txns;
+    std::vector<int64_t> regs;
+    for (int32_t i = 0; i < n_init; ++i) regs.push_back(init[2 * i]);
+    mk.tid.assign(o.ops.size(), 0);
+    for (size_t q = 0; q < o.ops.size(); ++q) {
+        const KOp &op = o.ops[q];
+        if (op.fate == 2) continue;
+        int64_t m0, m1;
+        mop_range(h, op.mrow, m0, m1);
+        std::vector<int64_t> t;
+        for (int64_t m = m0; m < m1; ++m) {
+            const int64_t f = h.mop[3 * m], k = h.mop[3 * m + 1], v = h.mop[3 * m + 2];
+            if ((f != LC_MOP_READ && f != LC_MOP_WRITE) || v == ABSENT) {
+                mk.err = LC_E_INVALID;
+                mk.msg = "row " + std::to_string(op.mrow) + ": bad :txn micro-op";
+                return;
+            }
+            t.push_back(f); t.push_back(k); t.push_back(v);
+            regs.push_back(k);
+        }
+        auto it = tix.find(t);
+        if (it == tix.end()) {
+            it = tix.emplace(t, (uint32_t)txns.size()).first;
+            txns.push_back(t);
+        }
+        mk.tid[q] = it->second;
+    }
+    std::sort(regs.begin(), regs.end());
+    regs.erase(std::unique(regs.begin(), regs.end()), regs.end());
+    mk.regs = regs;
+    const size_t R = regs.size();
+    auto ridx = [&](int64_t k) { return (size_t)(std::lower_bound(regs.begin(), regs.end(), k) - regs.begin()); };
+    // the txns with register indices
+    std::vector<std::vector<int64_t>> tx(txns.size());
+    for (size_t t = 0; t < txns.size(); ++t)
+        for (size_t j = 0; j < txns[t].size(); j += 3) {
+            tx[t].push_back(txns[t][j]);
+            tx[t].push_back((int64_t)ridx(txns[t][j + 1]));
+            tx[t].push_back(txns[t][j + 2]);
+        }
+    std::vector<int64_t> s0(R, ABSENT);
+    for (int32_t i = 0; i < n_init; ++i) s0[ridx(init[2 * i])] = init[2 * i + 1];
+    std::unordered_map<std::vector<int64_t>, uint32_t, VecHash> six;
+    std::vector<std::vector<int64_t>> st{s0};
+    six.emplace(s0, 0);
+    // breadth-first over (state, txn); next[t][s] as the states appear
+    std::vector<std::vector<uint32_t>> next(tx.size());
+    std::vector<int64_t> cur;
+    for (size_t s = 0; s < st.size(); ++s) {
+        for (size_t t = 0; t < tx.size(); ++t) {
+            cur = st[s];
+            bool ok = true;
+            for (size_t j = 0; j < tx[t].size() && ok; j += 3) {
+                const size_t r = (size_t)tx[t][j + 1];
+                const int64_t v = tx[t][j + 2];
+                if (tx[t][j] == LC_MOP_READ) ok = v == LC_NIL || (cur[r] != ABSENT && cur[r] == v);
+                else cur[r] = v;
+            }
+            uint32_t id = LC_TABLE_NONE;
+            if (ok) {
+                auto it = six.find(cur);
+                if (it == six.end()) {
+                    if (st.size() >= (size_t)LC_WIDE_MAX_STATES) { mk.too_many = true; break; }
+                    it = six.emplace(cur, (uint32_t)st.size()).first;
+                    st.push_back(cur);
+                }
+                id = it->second;
+            }
+            next[t].push_back(id);
+        }
+        if (mk.too_many) break;
+    }
+    mk.T = (uint32_t)tx.size();
+    if (mk.too_many) {
+        mk.S = LC_WIDE_MAX_STATES + 1;
+        return;
+    }
+    mk.S = (uint32_t)st.size();
+    mk.states.reserve(st.size() * R);
+    for (auto &v : st) mk.states.insert(mk.states.end(), v.begin(), v.end());
+    mk.table.reserve((size_t)mk.T * mk.S);
+    for (size_t t = 0; t < tx.size(); ++t) mk.table.insert(mk.table.end(), next[t].begin(), next[t].end());
+}
+
+// A4/A5 for (model/multi-register): memo per key (in parallel), then the
+// packed arrays.  Keys whose micro-ops are malformed become per-key errors.
+void pack_multi_register(const lc_history &h, const int64_t *init, int32_t n_init, std::vector<KeyOut> &ko,
+                         unsigned nt, lc_packed *P) {
+    const int64_t K = (int64_t)ko.size();
+    std::vector<MrKey> mr((size_t)K);
+    {
+        auto work = [&](unsigned t) {
+            for (int64_t k = t; k < K; k += nt)
+                if (!ko[(size_t)k].err) memo_multi_register(h, ko[(size_t)k], init, n_init, mr[(size_t)k]);
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
+        work(0);
+        for (auto &th : pool) th.join();
+    }
+    for (int64_t k = 0; k < K; ++k) {
+        MrKey &m = mr[(size_t)k];
+        KeyOut &o = ko[(size_t)k];
+        if (!m.err) continue;
+        if (P->key_error.empty()) {
+            P->key_error.assign((size_t)K, 0);
+            P->key_msg.assign((size_t)K, std::string());
+        }
+        P->key_error[(size_t)k] = 1;
+        P->key_msg[(size_t)k] = m.msg;
+        std::vector<uint32_t>().swap(o.ev);
+        std::vector<int64_t>().swap(o.ev_row);
+        std::vector<int32_t>().swap(o.ev_op);
+        std::vector<KOp>().swap(o.ops);
+        o.width = 0;
+        m = MrKey{};
+    }
+    P->model = LC_MODEL_MULTI_REGISTER;
+    P->key_states.assign((size_t)K, 0);
+    P->key_width.assign((size_t)K, 0);
+    P->trans_off.assign((size_t)K, 0);
+    P->ev_off.assign((size_t)K + 1, 0);
+    P->mr_reg_off.assign((size_t)K + 1, 0);
+    P->mr_state_off.assign((size_t)K + 1, 0);
+    for (int64_t k = 0; k < K; ++k) P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + ko[(size_t)k].ev.size();
+    P->events.resize((size_t)P->ev_off[(size_t)K]);
+    P->ev_row.resize((size_t)P->ev_off[(size_t)K]);
+    for (int64_t k = 0; k < K; ++k) {
+        MrKey &m = mr[(size_t)k];
+        KeyOut &o = ko[(size_t)k];
+        if (m.S == 0) m.S = 1;  // an error key: the initial map alone
+        P->key_states[(size_t)k] = (uint16_t)std::min<uint32_t>(m.S, 65535u);
+        P->key_width[(size_t)k] = (uint8_t)o.width;
+        P->trans_off[(size_t)k] = (uint32_t)P->trans.size();
+        const uint64_t tbase = P->table.size();
+        if (tbase + m.table.size() > 0xFFFFFFFFull) throw std::length_error("table");
+        for (uint32_t t = 0; t < m.T; ++t) P->trans.push_back(m.too_many ? 0u : (uint32_t)(tbase + (uint64_t)t * m.S));
+        P->table.insert(P->table.end(), m.table.begin(), m.table.end());
+        P->mr_regs.insert(P->mr_regs.end(), m.regs.begin(), m.regs.end());
+        P->mr_reg_off[(size_t)k + 1] = P->mr_regs.size();
+        P->mr_states.insert(P->mr_states.end(), m.states.begin(), m.states.end());
+        P->mr_state_off[(size_t)k + 1] = P->mr_states.size();
+        const uint64_t base = P->ev_off[(size_t)k];
+        for (size_t j = 0; j < o.ev.size(); ++j) {
+            uint32_t w = o.ev[j];
+            if (!(w & LC_EV_OK_BIT)) w = (w & 0xFF000000u) | m.tid[(size_t)o.ev_op[j]];
+            P->events[base + j] = w;
+            P->ev_row[base + j] = o.ev_row[j];
+        }
+        std::vector<uint32_t>().swap(o.ev);
+        std::vector<int64_t>().swap(o.ev_row);
+        std::vector<int32_t>().swap(o.ev_op);
+        std::vector<KOp>().swap(o.ops);
+        m = MrKey{};
+    }
+    if (P->trans.empty()) P->trans.push_back(0);
+    if (P->table.empty()) P->table.push_back(LC_TABLE_NONE);
+}
+
 }  // namespace
 
 
 extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed **out) {
     if (!h || !out) return lc::fail(LC_E_INVALID, "lc_pack: null argument");
     const int model = opts ? opts->model : LC_MODEL_CAS_REGISTER;
-    if (model < LC_MODEL_CAS_REGISTER || model > LC_MODEL_MUTEX)
+    if (model < LC_MODEL_CAS_REGISTER || model > LC_MODEL_MULTI_REGISTER)
         return lc::fail(LC_E_INVALID, "lc_pack: unknown model %d", model);
+    const int32_t n_init = (opts && model == LC_MODEL_MULTI_REGISTER) ? opts->n_init : 0;
+    if (n_init < 0 || (n_init > 0 && !opts->init)) return lc::fail(LC_E_INVALID, "lc_pack: bad initial registers");
     if (h->n < 0 || (h->n > 0 && (!h->type || !h->f || !h->process || !h->key || !h->v0 || !h->v1)))
         return lc::fail(LC_E_INVALID, "lc_pack: history arrays missing");
     const int64_t n = h->n;
@@ -192,9 +398,13 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         int64_t last_key = LC_NO_KEY;
         int32_t last_idx = -1;
         for (int64_t r = 0; r < n; ++r) {
-            if (h->type[r] > LC_INFO || h->f[r] > LC_F_RELEASE) {
+            if (h->type[r] > LC_INFO || h->f[r] > LC_F_TXN) {
                 delete P;
                 return lc::fail(LC_E_INVALID, "lc_pack: row %lld has a bad :type/:f code", (long long)r);
+            }
+            if (h->mop_off && h->mop && (h->mop_off[r] < 0 || h->mop_off[r + 1] < h->mop_off[r])) {
+                delete P;
+                return lc::fail(LC_E_INVALID, "lc_pack: mop_off not monotone at row %lld", (long long)r);
             }
             int64_t k = h->key[r];
             if (k == LC_NO_KEY) {
@@ -268,6 +478,11 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             std::vector<int32_t>().swap(o.ev_op);
             std::vector<KOp>().swap(o.ops);
             o.width = 0;
+        }
+        if (model == LC_MODEL_MULTI_REGISTER) {
+            pack_multi_register(*h, n_init ? opts->init : nullptr, n_init, ko, nt, P);
+            *out = P;
+            return LC_OK;
         }
 
         // ---- A4/A5: register states + transition descriptors ----
@@ -383,6 +598,9 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
     } catch (const std::bad_alloc &) {
         delete P;
         return lc::fail(LC_E_NOMEM, "lc_pack: out of memory");
+    } catch (const std::length_error &) {
+        delete P;
+        return lc::fail(LC_E_UNSUPPORTED, "lc_pack: transition table beyond 2^32 entries");
     }
     *out = P;
     return LC_OK;
@@ -402,7 +620,28 @@ extern "C" int lc_packed_view(const lc_packed *p, lc_batch *b) {
     b->key_states = p->key_states.data();
     b->init_state = 0;
     b->key_error = p->key_error.empty() ? nullptr : p->key_error.data();
+    b->table = p->table.empty() ? nullptr : p->table.data();
+    b->n_table = (int64_t)p->table.size();
     return LC_OK;
+}
+
+extern "C" int64_t lc_packed_state_map(const lc_packed *p, int64_t i, uint32_t s, int64_t *regs, int64_t *vals,
+                                       int64_t cap) {
+    if (!p || i < 0 || i >= (int64_t)p->keys.size() || cap < 0 || (cap && (!regs || !vals)))
+        return lc::fail(LC_E_INVALID, "lc_packed_state_map: bad argument");
+    if (p->model != LC_MODEL_MULTI_REGISTER) return lc::fail(LC_E_INVALID, "lc_packed_state_map: not a multi-register batch");
+    const uint64_t r0 = p->mr_reg_off[(size_t)i], R = p->mr_reg_off[(size_t)i + 1] - r0;
+    const uint64_t s0 = p->mr_state_off[(size_t)i], n = p->mr_state_off[(size_t)i + 1] - s0;
+    if ((uint64_t)s * R >= n && !(R == 0 && s == 0))
+        return lc::fail(LC_E_INVALID, "lc_packed_state_map: state %u out of range", s);
+    int64_t m = 0;
+    for (uint64_t r = 0; r < R; ++r) {
+        const int64_t v = p->mr_states[s0 + (uint64_t)s * R + r];
+        if (v == ABSENT) continue;
+        if (m < cap) { regs[m] = p->mr_regs[r0 + r]; vals[m] = v; }
+        ++m;
+    }
+    return m;
 }
 
 extern "C" const char *lc_packed_key_error(const lc_packed *p, int64_t i) {

@@ -68,7 +68,15 @@ struct KeyView {
         const uint64_t tb = p->trans_off.empty() ? 0 : p->trans_off[(size_t)key];
         return p->trans[tb + LC_EV_TRANS(p->events[eb + j])];
     }
+    // the op of invoke event j from state st: next state or LC_STATE_NONE
+    uint32_t step(uint64_t j, uint32_t st) const {
+        const uint32_t d = desc(j);
+        if (p->table.empty()) return desc_step(d, st);
+        const uint16_t s2 = p->table[(size_t)d + st];  // a table-model row (lc_batch.table)
+        return s2 == LC_TABLE_NONE ? LC_STATE_NONE : s2;
+    }
     int64_t value(uint32_t st) const {
+        if (p->model == LC_MODEL_MULTI_REGISTER) return st;  // a map: lc_packed_state_map
         if (st == 0) return LC_NIL;
         const uint64_t base = p->state_off.empty() ? 0 : p->state_off[(size_t)key];
         const uint64_t lim = p->state_off.empty() ? p->state_vals.size() : p->state_off[(size_t)key + 1];
@@ -125,7 +133,7 @@ extern "C" int64_t lc_report(const lc_packed *p, int64_t key, int32_t valid, int
             const uint32_t p_slot = LC_EV_SLOT(p->events[kv.eb + (uint64_t)fail_event]);
             auto ph = kv.held.find(p_slot);
             if (ph != kv.held.end()) {
-                const uint32_t p_desc = kv.desc(ph->second);
+                const uint64_t p_inv = ph->second;
                 std::vector<std::pair<uint32_t, uint64_t>> others;  // (slot, invoke event)
                 for (auto &h : kv.held)
                     if (h.first != p_slot) others.push_back(h);
@@ -152,10 +160,10 @@ extern "C" int64_t lc_report(const lc_packed *p, int64_t key, int32_t valid, int
                 auto dfs = [&](auto &&self, uint32_t st) -> void {
                     ++visits;
                     if (n_paths >= max_paths || visits > max_visits) return;
-                    if (desc_step(p_desc, st) == LC_STATE_NONE) emit(st);
+                    if (kv.step(p_inv, st) == LC_STATE_NONE) emit(st);
                     for (size_t q = 0; q < others.size(); ++q) {
                         if (used[q]) continue;
-                        const uint32_t s2 = desc_step(kv.desc(others[q].second), st);
+                        const uint32_t s2 = kv.step(others[q].second, st);
                         if (s2 == LC_STATE_NONE) continue;
                         used[q] = 1;
                         steps.push_back({others[q].second, s2});

@@ -28,4 +28,10 @@ struct lc_packed {
     // keys that could not be prepared (A9): empty = none
     std::vector<uint8_t> key_error;
     std::vector<std::string> key_msg;
+    int32_t model = LC_MODEL_CAS_REGISTER;
+    // (model/multi-register): the transition table (lc_batch.table) and, per
+    // key, its registers and the map each state id stands for
+    std::vector<uint16_t> table;
+    std::vector<uint64_t> mr_reg_off, mr_state_off;  // [K + 1]
+    std::vector<int64_t> mr_regs, mr_states;
 };

@@ -17,14 +17,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 7
+LC_ABI_VERSION = 8
 LC_MAX_DEVICES = 8
 LC_COMM_ID_BYTES = 128
 LC_OPT_COUNT_PROBES = 0x1
 LC_DEV_RESULT, LC_DEV_ASYNC = 1, 2
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
-LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE = 0, 1, 2, 3, 4, 5
-LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX = 0, 1, 2
+LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE, LC_F_TXN = 0, 1, 2, 3, 4, 5, 6
+LC_MOP_READ, LC_MOP_WRITE = 0, 1
+LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX, LC_MODEL_MULTI_REGISTER = 0, 1, 2, 3
+LC_TABLE_NONE = 0xFFFF
 LC_ALGO_LINEAR, LC_ALGO_WGL, LC_ALGO_COMPETITION = 0, 1, 2
 LC_NIL = -(1 << 63)
 LC_NO_KEY = LC_NIL
@@ -45,18 +47,20 @@ P = C.POINTER
 class LcHistory(C.Structure):
     _fields_ = [("n", C.c_int64), ("type", P(C.c_uint8)), ("f", P(C.c_uint8)),
                 ("process", P(C.c_int64)), ("key", P(C.c_int64)),
-                ("v0", P(C.c_int64)), ("v1", P(C.c_int64)), ("index", P(C.c_int64))]
+                ("v0", P(C.c_int64)), ("v1", P(C.c_int64)), ("index", P(C.c_int64)),
+                ("mop_off", P(C.c_int64)), ("mop", P(C.c_int64))]
 
 
 class LcBatch(C.Structure):
     _fields_ = [("n_keys", C.c_int64), ("ev_off", P(C.c_uint64)), ("events", P(C.c_uint32)),
                 ("trans", P(C.c_uint32)), ("n_trans", C.c_int64), ("trans_off", P(C.c_uint32)),
                 ("key_width", P(C.c_uint8)), ("key_states", P(C.c_uint16)),
-                ("init_state", C.c_uint32), ("key_error", P(C.c_uint8))]
+                ("init_state", C.c_uint32), ("key_error", P(C.c_uint8)),
+                ("table", P(C.c_uint16)), ("n_table", C.c_int64)]
 
 
 class LcPackOpts(C.Structure):
-    _fields_ = [("model", C.c_int32)]
+    _fields_ = [("model", C.c_int32), ("n_init", C.c_int32), ("init", P(C.c_int64))]
 
 
 class LcOpts(C.Structure):
@@ -116,6 +120,7 @@ SIGNATURES = {
     "lc_packed_key_error": (C.c_char_p, [C.c_void_p, C.c_int64]),
     "lc_packed_state_value": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint32, P(C.c_int64), P(C.c_int)]),
     "lc_packed_keys": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "lc_packed_state_map": (C.c_int64, [C.c_void_p, C.c_int64, C.c_uint32, P(C.c_int64), P(C.c_int64), C.c_int64]),
     "lc_report": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, P(C.c_uint64), C.c_uint32, C.c_int32,
                               P(C.c_int64), C.c_int64]),
     "lc_synth_generate": (C.c_int, [P(LcSynthOpts), P(C.c_void_p)]),

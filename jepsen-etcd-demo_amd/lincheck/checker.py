@@ -26,8 +26,8 @@ from typing import Any, Dict, List, Optional, Sequence
 import numpy as np
 
 from . import _native as N
-from .history import History
-from .model import MODELS, CASRegister, fmt
+from .history import NAMED_REG_BASE, History
+from .model import MODELS, CASRegister, MultiRegister, fmt
 
 DEFAULT_BUDGET = 1 << 20
 TRUNCATE = 10  # jepsen.checker/linearizable truncates :final-paths and :configs
@@ -43,6 +43,20 @@ class Packed:
         self._c = hist.as_c()
         handle = C.c_void_p()
         opts = N.LcPackOpts(self.model.code)
+        self.reg_names = dict(hist.reg_names)  # register id -> name (multi-register)
+        if isinstance(self.model, MultiRegister):
+            ids = {name: rid for rid, name in self.reg_names.items()}
+
+            def reg_id(r):
+                if isinstance(r, (int, np.integer)) and not isinstance(r, bool):
+                    return int(r)
+                if r not in ids:
+                    ids[r] = NAMED_REG_BASE + len(ids)
+                return ids[r]
+            pairs = self.model.init_pairs(reg_id)
+            self.reg_names = {rid: name for name, rid in ids.items()}
+            self._init = np.array([x for k, v in pairs for x in (k, N.LC_NIL if v is None else v)] or [0], np.int64)
+            opts.n_init, opts.init = len(pairs), N.ptr(self._init, C.c_int64)
         N.check(N.lib().lc_pack(C.byref(self._c), C.byref(opts), C.byref(handle)))
         self.handle = handle
         v = N.LcBatch()
@@ -89,6 +103,14 @@ class Packed:
         v = C.c_int64(); nil = C.c_int()
         N.check(N.lib().lc_packed_state_value(self.handle, i, s, C.byref(v), C.byref(nil)))
         return None if nil.value else int(v.value)
+
+    def state_map(self, i: int, s: int) -> list:
+        """multi-register: the (register, value) pairs state id s of key i
+        stands for (lc_packed_state_map), registers by name where named."""
+        n = N.check(N.lib().lc_packed_state_map(self.handle, i, s, None, None, 0))
+        regs, vals = np.zeros(max(n, 1), np.int64), np.zeros(max(n, 1), np.int64)
+        N.check(N.lib().lc_packed_state_map(self.handle, i, s, N.ptr(regs, C.c_int64), N.ptr(vals, C.c_int64), n))
+        return [(self.reg_names.get(int(r), int(r)), None if v == N.LC_NIL else int(v)) for r, v in zip(regs[:n], vals[:n])]
 
 
 # ---------------------------------------------------------------- device
@@ -312,12 +334,17 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
         completion's :value when it has none."""
         if (inv, done) not in ops:
             o = _sub_op(packed, inv)
-            if o.get("value") is None and done >= 0:
-                o["value"] = _sub_op(packed, done).get("value")
+            if done >= 0 and (o.get("value") is None or o.get("f") == "txn"):
+                # a :txn takes its completion's micro-ops when it has some
+                dv = _sub_op(packed, done).get("value")
+                if dv is not None or o.get("f") != "txn":
+                    o["value"] = dv
             ops[(inv, done)] = o
         return ops[(inv, done)]
 
     def state(x: int):
+        if isinstance(packed.model, MultiRegister):
+            return packed.model.of_map(packed.state_map(i, int(x)))
         return packed.model.of_state(None if x == N.LC_NIL else int(x))
 
     op_row, prev_row, n_cfg, n_paths = (int(x) for x in w[:4])
@@ -370,7 +397,8 @@ class Linearizable:
         if model is None:
             raise ValueError("The linearizable checker requires a model.")
         if not isinstance(model, MODELS):
-            raise NotImplementedError("supported models: (model/cas-register), (model/register), (model/mutex)")
+            raise NotImplementedError("supported models: (model/cas-register), (model/register), (model/mutex), "
+                                      "(model/multi-register)")
         # jepsen.checker/linearizable: :linear, :wgl, anything else -> competition
         algo = str(opts.get("algorithm", "competition")).lstrip(":")
         self.algorithm = {"linear": N.LC_ALGO_LINEAR, "wgl": N.LC_ALGO_WGL}.get(algo, N.LC_ALGO_COMPETITION)

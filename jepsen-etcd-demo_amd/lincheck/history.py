@@ -3,7 +3,9 @@
 An op is a dict with Jepsen's keys as strings: "type" (invoke/ok/fail/info),
 "f" (read/write/cas/...), "value", "process", optional "index", "time",
 "error".  Independent ops carry `independent.tuple(k, v)` values
-(etcdemo.clj:90, :120); cas values are [old new] lists (etcdemo.clj:69).
+(etcdemo.clj:90, :120); cas values are [old new] lists (etcdemo.clj:69);
+(model/multi-register) :txn values are lists of ["read"|"write", register, v]
+micro-ops (registers: integers or names, interned to integer ids here).
 
 `History` keeps the integer columns the C ABI consumes; this is the
 marshalling the Clojure side does before its JNA call.
@@ -22,7 +24,10 @@ from .independent import Tuple, is_tuple
 TYPES = {"invoke": N.LC_INVOKE, "ok": N.LC_OK_T, "fail": N.LC_FAIL, "info": N.LC_INFO}
 TYPE_NAMES = {v: k for k, v in TYPES.items()}
 FS = {"read": N.LC_F_READ, "write": N.LC_F_WRITE, "cas": N.LC_F_CAS,
-      "acquire": N.LC_F_ACQUIRE, "release": N.LC_F_RELEASE}
+      "acquire": N.LC_F_ACQUIRE, "release": N.LC_F_RELEASE, "txn": N.LC_F_TXN}
+MOPS = {"read": N.LC_MOP_READ, "write": N.LC_MOP_WRITE}
+MOP_NAMES = {v: k for k, v in MOPS.items()}
+NAMED_REG_BASE = 1 << 62  # register names (non-integer registers) get ids from here
 F_NAMES = {v: k for k, v in FS.items()}
 NIL = N.LC_NIL
 
@@ -41,7 +46,8 @@ def _int_or_nil(v, what: str) -> int:
 class History:
     """Columns of one history (numpy arrays, history order)."""
 
-    def __init__(self, type_, f, process, key, v0, v1, index, other_f=None):
+    def __init__(self, type_, f, process, key, v0, v1, index, other_f=None, mop_off=None, mop=None,
+                 reg_names=None):
         self.type = np.ascontiguousarray(type_, dtype=np.uint8)
         self.f = np.ascontiguousarray(f, dtype=np.uint8)
         self.process = np.ascontiguousarray(process, dtype=np.int64)
@@ -51,6 +57,10 @@ class History:
         self.index = np.ascontiguousarray(index, dtype=np.int64)
         self.other_f = other_f or {}   # row -> original :f name for LC_F_OTHER rows
         self.anomalous_keys: List[int] = []
+        # :txn micro-ops (lc_history.mop_off / mop), None when no row is a :txn
+        self.mop_off = None if mop_off is None else np.ascontiguousarray(mop_off, dtype=np.int64)
+        self.mop = None if mop is None else np.ascontiguousarray(mop, dtype=np.int64)
+        self.reg_names = dict(reg_names or {})  # register id -> name, for named registers
 
     def __len__(self):
         return int(self.type.shape[0])
@@ -65,6 +75,8 @@ class History:
         p = np.empty(n, np.int64); k = np.empty(n, np.int64)
         a = np.empty(n, np.int64); b = np.empty(n, np.int64); ix = np.empty(n, np.int64)
         other = {}
+        txn_rows = {}                  # row -> [(f, register id, value)]
+        reg_ids = {}                   # register name -> id
         for i, op in enumerate(ops):
             try:
                 t[i] = TYPES[op["type"]]
@@ -95,11 +107,39 @@ class History:
                     a[i] = _int_or_nil(v[0], f"op {i}"); b[i] = _int_or_nil(v[1], f"op {i}")
             elif f[i] == N.LC_F_OTHER:
                 a[i] = b[i] = NIL
+            elif f[i] == N.LC_F_TXN:
+                a[i] = b[i] = NIL
+                if v is not None:
+                    txn_rows[i] = [cls._mop(i, m, reg_ids) for m in v]
             else:
                 a[i] = _int_or_nil(v, f"op {i}"); b[i] = NIL
             idx = op.get("index")
             ix[i] = idx if isinstance(idx, (int, np.integer)) else -1
-        return cls(t, f, p, k, a, b, ix, other)
+        mop_off = mop = None
+        if txn_rows:
+            mop_off = np.zeros(n + 1, np.int64)
+            for i, ms in txn_rows.items():
+                mop_off[i + 1] = len(ms)
+            mop_off = np.cumsum(mop_off)
+            mop = np.array([x for i in sorted(txn_rows) for m in txn_rows[i] for x in m], np.int64)
+        return cls(t, f, p, k, a, b, ix, other, mop_off, mop, {v: k2 for k2, v in reg_ids.items()})
+
+    @staticmethod
+    def _mop(i: int, m, reg_ids: dict) -> tuple:
+        """One [f k v] micro-op of row i's :txn as (LC_MOP_*, register id, value)."""
+        if len(m) != 3 or str(m[0]).lstrip(":") not in MOPS:
+            raise ValueError(f"op {i}: a :txn micro-op is [read|write k v], got {m!r}")
+        reg = m[1]
+        if isinstance(reg, (int, np.integer)) and not isinstance(reg, bool):
+            rid = int(reg)
+            if rid >= NAMED_REG_BASE or rid == NIL:
+                raise ValueError(f"op {i}: register id {rid} is reserved")
+        else:
+            rid = reg_ids.setdefault(reg, NAMED_REG_BASE + len(reg_ids))
+        val = _int_or_nil(m[2], f"op {i}")
+        if val == NIL + 1:
+            raise ValueError(f"op {i}: {val} is reserved")
+        return (MOPS[str(m[0]).lstrip(":")], rid, val)
 
     @classmethod
     def _from_owned(cls, handle) -> "History":
@@ -127,6 +167,9 @@ class History:
         h.process = N.ptr(self.process, C.c_int64); h.key = N.ptr(self.key, C.c_int64)
         h.v0 = N.ptr(self.v0, C.c_int64); h.v1 = N.ptr(self.v1, C.c_int64)
         h.index = N.ptr(self.index, C.c_int64)
+        if self.mop_off is not None:
+            h.mop_off = N.ptr(self.mop_off, C.c_int64)
+            h.mop = N.ptr(self.mop if self.mop.size else np.zeros(1, np.int64), C.c_int64)
         h._keep = self  # arrays stay alive with the struct
         return h
 
@@ -140,6 +183,8 @@ class History:
             val = [nil(self.v0[i]), nil(self.v1[i])]
         elif f in (N.LC_F_OTHER, N.LC_F_ACQUIRE, N.LC_F_RELEASE):
             val = None
+        elif f == N.LC_F_TXN:
+            val = self.txn(i)
         else:
             val = nil(self.v0[i])
         if self.key[i] != N.LC_NO_KEY:
@@ -149,6 +194,16 @@ class History:
               "process": "nemesis" if proc == N.LC_NO_PROCESS else proc}
         op["index"] = int(self.index[i]) if self.index[i] >= 0 else i
         return op
+
+    def txn(self, i: int):
+        """Row i's :txn micro-ops as [f, register, value] lists (None: nil)."""
+        if self.mop_off is None or self.mop_off[i + 1] == self.mop_off[i]:
+            return None
+        out = []
+        for m in range(int(self.mop_off[i]), int(self.mop_off[i + 1])):
+            f, r, v = (int(x) for x in self.mop[3 * m: 3 * m + 3])
+            out.append([MOP_NAMES[f], self.reg_names.get(r, r), None if v == NIL else v])
+        return out
 
     def to_ops(self) -> List[dict]:
         return [self.op(i) for i in range(len(self))]

@@ -3,7 +3,8 @@
 The demo checks (model/cas-register) (etcdemo.clj:117).
 (model/register) and (model/mutex) are the other Knossos models whose state
 space maps onto the device's transition descriptors (include/lincheck.h
-LC_T_*, LC_MODEL_*).  The step functions here only
+LC_T_*, LC_MODEL_*); (model/multi-register) runs on the
+set tiers through a per-key transition table (lc_batch.table).  The step functions here only
 produce the result maps' :model values and "can't ..." messages on the host;
 the search itself runs on the device.  Messages follow the public knossos
 0.3.7 source as recalled (not verifiable here: knossos is absent).
@@ -99,6 +100,45 @@ class Mutex:
         return {"locked?": self.locked}
 
 
+@dataclass(frozen=True)
+class MultiRegister:
+    """knossos.model/multi-register: a map of registers; one :f, :txn, whose
+    value is a sequence of [:read k v] / [:write k v] micro-ops applied in
+    order.  A read of v is legal iff v is nil or register k holds v."""
+    registers: tuple = ()   # ((register, value), ...) in register order
+    code = N.LC_MODEL_MULTI_REGISTER
+    name = "multi-register"
+
+    @staticmethod
+    def _order(kv):
+        return (str(type(kv[0])), kv[0])
+
+    def step(self, f: str, v):
+        if f != "txn":
+            raise ValueError(f"multi-register cannot step {f!r}")
+        regs = dict(self.registers)
+        for mf, k, x in (v or ()):
+            mf = str(mf).lstrip(":")
+            if mf == "read":
+                if x is not None and (k not in regs or regs[k] != x):
+                    return Inconsistent(f"{fmt(regs.get(k))}≠{fmt(x)}")
+            elif mf == "write":
+                regs[k] = x
+            else:
+                raise ValueError(f"multi-register cannot step micro-op {mf!r}")
+        return MultiRegister(tuple(sorted(regs.items(), key=self._order)))
+
+    def init_pairs(self, reg_id) -> list:
+        """(register id, value) pairs of the initial map for lc_pack_opts."""
+        return [(reg_id(k), v) for k, v in self.registers]
+
+    def of_map(self, pairs):
+        return MultiRegister(tuple(sorted(pairs, key=self._order)))
+
+    def render(self) -> dict:
+        return dict(self.registers)
+
+
 def cas_register(value: Optional[int] = None) -> CASRegister:
     if value is not None:
         raise NotImplementedError("only the nil initial value of (model/cas-register) is supported")
@@ -115,4 +155,9 @@ def mutex() -> Mutex:
     return Mutex(False)
 
 
-MODELS = (CASRegister, Register, Mutex)
+def multi_register(values: Optional[dict] = None) -> MultiRegister:
+    """(model/multi-register values): values maps registers to initial values."""
+    return MultiRegister(tuple(sorted((values or {}).items(), key=MultiRegister._order)))
+
+
+MODELS = (CASRegister, Register, Mutex, MultiRegister)

@@ -30,6 +30,13 @@ What is restated, from the published knossos 0.3.7 / jepsen 0.2.x sources
       register: the cas-register without cas.  mutex: unlocked initially;
       :acquire legal iff unlocked (-> locked), :release legal iff locked
       (-> unlocked).
+  knossos.model/multi-register  
+      a map of registers (initially the given one); :txn applies its
+      [:read k v] / [:write k v] micro-ops in order, a read legal iff v is nil
+      or k holds v (a register the map lacks holds nothing, not even nil).
+      An :ok :txn takes its completion's micro-ops when it has some (the reads
+      learn what they read).  A key with more than 32767 maps reachable from
+      the initial one under its distinct :txn ops is :unknown "states".
   knossos.linear/analysis with :algorithm :linear  (etcdemo.clj:118)
       the just-in-time config-set search.  A config is (model state, set of
       pending ops already linearized).  :invoke adds the op to the pending
@@ -114,7 +121,7 @@ class HistoryError(Exception):
 
 
 MODEL_FS = {"cas-register": ("read", "write", "cas"), "register": ("read", "write"),
-            "mutex": ("acquire", "release")}
+            "mutex": ("acquire", "release"), "multi-register": ("txn",)}
 
 
 def complete(history: Sequence[dict], model: str = "cas-register") -> Tuple[List[Op], List[Tuple[str, int, int]]]:
@@ -139,7 +146,10 @@ def complete(history: Sequence[dict], model: str = "cas-register") -> Tuple[List
                 raise HistoryError(f"process {p!r} completed an operation without a prior invocation")
             o = ops[outstanding.pop(p)]
             if t == "ok":
-                if o.value is None:          # (or (:value invocation) (:value op))
+                if o.f == "txn":             # a :txn learns its completion's micro-ops
+                    if op.get("value") is not None:
+                        o.value = op.get("value")
+                elif o.value is None:        # (or (:value invocation) (:value op))
                     o.value = op.get("value")
                 o.complete_pos = pos
                 ok_at[pos] = o.id
@@ -193,10 +203,66 @@ def mutex_step(locked: bool, f: str, value=None):
     raise HistoryError(f"mutex cannot step {f!r}")
 
 
+def _reg_order(kv):
+    return (str(type(kv[0])), kv[0])
+
+
+def multi_register_step(state, f: str, value):
+    """knossos.model/multi-register's MultiRegister step; state = the map as a
+    sorted tuple of (register, value)."""
+    if f != "txn":
+        raise HistoryError(f"multi-register cannot step {f!r}")
+    regs = dict(state)
+    for m in (value or ()):
+        mf, k, v = m
+        mf = str(mf).lstrip(":")
+        if mf == "read":
+            if v is not None and (k not in regs or regs[k] != v):
+                return INCONSISTENT
+        elif mf == "write":
+            regs[k] = v
+        else:
+            raise HistoryError(f"multi-register cannot step micro-op {mf!r}")
+    return tuple(sorted(regs.items(), key=_reg_order))
+
+
+def multi_register_init(values=None):
+    return tuple(sorted((values or {}).items(), key=_reg_order))
+
+
+def reachable_maps(ops: Iterable[Op], initial, cap: int) -> int:
+    """knossos.model.memo for multi-register: how many maps are reachable
+    from `initial` under the distinct :txn values of the surviving ops
+    (counting stops past cap)."""
+    txns = []
+    seen_t = set()
+    for o in ops:
+        if o.failed:
+            continue
+        key = repr(o.value)
+        if key not in seen_t:
+            seen_t.add(key)
+            txns.append(o.value)
+    seen = {initial}
+    frontier = [initial]
+    while frontier and len(seen) <= cap:
+        nxt = []
+        for st in frontier:
+            for t in txns:
+                s2 = multi_register_step(st, "txn", t)
+                if s2 is not INCONSISTENT and s2 not in seen:
+                    seen.add(s2)
+                    nxt.append(s2)
+        frontier = nxt
+    return len(seen)
+
+
 def model_step(model: str):
     """(step fn, initial state) of a model."""
     if model == "mutex":
         return mutex_step, False
+    if model == "multi-register":
+        return multi_register_step, multi_register_init()
     return cas_register_step, None
 
 
@@ -241,7 +307,11 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
     if initial is None:
         initial = init
     res = Analysis(valid=True, ops=ops, events=events)
-    if len(register_values(ops)) + 1 > WIDE_MAX_STATES:
+    if model == "multi-register":
+        if reachable_maps(ops, initial, WIDE_MAX_STATES) > WIDE_MAX_STATES:
+            res.valid, res.cause = "unknown", "states"
+            return res
+    elif len(register_values(ops)) + 1 > WIDE_MAX_STATES:
         res.valid, res.cause = "unknown", "states"
         return res
     S = {(initial, frozenset())}
@@ -354,14 +424,17 @@ def final_paths(res: Analysis, sub: Sequence[dict], model: str = "cas-register",
 
 def config_sort_key(c: Config):
     st, L = c
+    if isinstance(st, tuple):  # a multi-register map
+        return (repr(st), sorted(L))
     return (-1 if st is None else int(st), sorted(L))
 
 
-def analysis_safe(history: Sequence[dict], budget: int = DEFAULT_BUDGET, model: str = "cas-register") -> Analysis:
+def analysis_safe(history: Sequence[dict], budget: int = DEFAULT_BUDGET, model: str = "cas-register",
+                  initial=None) -> Analysis:
     """check-safe around analysis: a HistoryError makes the key :unknown
     (cause "error") instead of aborting the whole check."""
     try:
-        return analysis(history, budget, model=model)
+        return analysis(history, budget, initial=initial, model=model)
     except HistoryError as e:
         a = Analysis(valid="unknown", cause="error", peak_configs=0)
         a.error = str(e)
@@ -369,6 +442,7 @@ def analysis_safe(history: Sequence[dict], budget: int = DEFAULT_BUDGET, model: 
 
 
 def check_independent(history: Sequence[dict], budget: int = DEFAULT_BUDGET,
-                      model: str = "cas-register") -> Dict[Any, Analysis]:
+                      model: str = "cas-register", initial=None) -> Dict[Any, Analysis]:
     """independent/checker over linearizable(model): per-key analyses."""
-    return {k: analysis_safe(subhistory(history, k), budget, model=model) for k in history_keys(history)}
+    return {k: analysis_safe(subhistory(history, k), budget, model=model, initial=initial)
+            for k in history_keys(history)}

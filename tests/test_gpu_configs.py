@@ -65,6 +65,35 @@ def test_known_answers_on_device(case):
             assert r["final-paths"], (case["name"], k)
 
 
+@pytest.mark.parametrize("algo", ["wgl", "competition"])
+def test_other_algorithms_on_device(algo):
+    """:algorithm :wgl and the default (knossos.competition) on the device
+    (SURVEY.md 8(f) F-3): :valid?, the failing-key set and :op :index do not
+    depend on the algorithm (the first :ok that cannot be linearized belongs
+    to the history), so every KAT and a C5-shaped history give the :linear
+    answer; :analyzer names the algorithm that answered."""
+    cases = _kats()
+    h = H.synth(n_keys=200, ops_per_key=300, concurrency=10, anomaly_rate=0.1, seed=55)
+    histories = [(c["name"], MODELS[c.get("model", "cas-register")](), c["history"]) for c in cases]
+    histories.append(("c5-shape", model.cas_register(), h.to_ops()))
+    for name, mdl, hist in histories:
+        outs = {}
+        for a in ("linear", algo):
+            opts = {"model": mdl} if a == "competition" else {"model": mdl, "algorithm": a}
+            outs[a] = independent.checker(ck.linearizable(opts)).check({}, hist, {})
+        ref, got = outs["linear"], outs[algo]
+        assert got["valid?"] == ref["valid?"], name
+        assert sorted(got["failures"]) == sorted(ref["failures"]), name
+        for k, r in ref["results"].items():
+            g = got["results"][k]
+            assert g["valid?"] == r["valid?"], (name, k)
+            if "error" not in r:  # check-safe's map for a key that could not be prepared has no analyzer
+                assert g["analyzer"] == ("wgl" if algo == "wgl" else "linear"), (name, k)
+            if r["valid?"] is False:
+                assert g["op"]["index"] == r["op"]["index"], (name, k)
+                assert g["previous-ok"]["index"] == r["previous-ok"]["index"], (name, k)
+
+
 @pytest.mark.parametrize("anomaly_rate", [0.0, 0.5])
 def test_c1_history_edn_on_device(tmp_path, anomaly_rate):
     """C1: the demo's shape (6 keys x 100 ops, 10 clients, nemesis :info ops
