@@ -177,7 +177,19 @@ typedef struct lc_batch {
                                    (LC_TABLE_NONE above), or NULL: trans[] are
                                    LC_DESC descriptors (ABI 8)                 */
     int64_t         n_table;
+    const uint16_t *events16;   /* [ev_off[n_keys]] or NULL: the same event
+                                   words in 16 bits (LC_EV16_* below), given
+                                   when every word fits; a register-tier batch
+                                   then crosses the host link at 2 bytes per
+                                   event and is widened on the device (ABI 8) */
 } lc_batch;
+
+/* 16-bit event word: bit 15 :ok, bits 14..11 slot (< 16), bits 10..0
+ * transition id (< 2048).  Widened: LC_EV16_WIDE(e). */
+#define LC_EV16_MAX_SLOT  15u
+#define LC_EV16_MAX_TRANS 2047u
+#define LC_EV16_WIDE(e) ((((uint32_t)(e) & 0x8000u) << 16) | ((((uint32_t)(e) >> 11) & 0xFu) << 24) | \
+                         ((uint32_t)(e) & 0x7FFu))
 
 /* The Knossos model a batch is checked against (knossos.model, SURVEY.md
  * 8(f) F-4).  The demo uses (model/cas-register) at etcdemo.clj:117; the

@@ -255,7 +255,7 @@
         _          (check-rc (LincheckNative/lc_pack hist pack-opts out) "lc_pack")
         packed     (.getPointer out 0)]
     (try
-      (let [batch    (Memory. 96)                ; sizeof(lc_batch), ABI 8
+      (let [batch    (Memory. 104)               ; sizeof(lc_batch), ABI 8
             _        (check-rc (LincheckNative/lc_packed_view packed batch) "lc_packed_view")
             n-keys   (.getLong batch 0)
             keys     (long-array (max 1 n-keys))

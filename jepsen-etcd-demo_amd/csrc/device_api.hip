@@ -99,6 +99,22 @@ const Rccl *rccl() {
     return r.h ? &r : nullptr;
 }
 
+// 16-bit event words (lc_batch.events16) widened to the 32-bit form every
+// kernel reads (LC_EV16_WIDE): 4 words per thread, 8-byte loads, 16-byte stores.
+__global__ void k_widen16(const uint16_t *in, uint32_t *out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n4 = n / 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const uint2 v = reinterpret_cast<const uint2 *>(in)[i];
+        uint4 w;
+        w.x = LC_EV16_WIDE(v.x & 0xFFFFu); w.y = LC_EV16_WIDE(v.x >> 16);
+        w.z = LC_EV16_WIDE(v.y & 0xFFFFu); w.w = LC_EV16_WIDE(v.y >> 16);
+        reinterpret_cast<uint4 *>(out)[i] = w;
+    }
+    for (uint64_t i = n4 * 4 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = LC_EV16_WIDE(in[i]);
+}
+
 // Verdict record of one key (include/lincheck.h LC_REC_*), 0 for padding.
 __global__ void k_pack_records(const int8_t *valid, const uint8_t *cause, const int32_t *fail_event, int64_t n,
                                int64_t block, uint64_t *out) {
@@ -209,6 +225,11 @@ struct DevBatch {
     char *hmeta = nullptr;
     size_t hmeta_cap = 0;
     hipEvent_t hmeta_done = nullptr;
+    uint16_t *events16 = nullptr;    // device staging of 16-bit event words (mem[3])
+    // the LPT order of the last upload and the offsets it was computed from
+    // (a batch re-uploaded with the same offsets reuses it)
+    std::vector<uint64_t> order_off;
+    std::vector<int32_t> order_of;
     ~DevBatch() {
         if (hmeta_done) (void)hipEventSynchronize(hmeta_done);
         for (Mem &m : mem)
@@ -796,6 +817,7 @@ static lc_batch sub_batch(const lc_batch *b, int64_t k0, int64_t k1, std::vector
     if (b->key_width) s.key_width = b->key_width + k0;
     if (b->key_states) s.key_states = b->key_states + k0;
     if (b->key_error) s.key_error = b->key_error + k0;
+    if (b->events16) s.events16 = b->events16 + base;
     return s;
 }
 
@@ -820,7 +842,8 @@ static void shard_keys(const lc_batch *b, int n, int64_t *key0) {
 // sync: wait for the copies (the caller may free its arrays on return);
 // otherwise the caller keeps them alive until its stream has passed them.
 static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, bool validated,
-                       const uint32_t *events_src = nullptr, bool sync = true, hipStream_t stream = nullptr) {
+                       const uint32_t *events_src = nullptr, bool sync = true, hipStream_t stream = nullptr,
+                       const uint32_t *events_mapped = nullptr) {
     hipStream_t cs = stream ? stream : c->stream;
     const int64_t K = b->n_keys;
     d->device = c->device;
@@ -835,6 +858,25 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     d->seg_pays = sh.seg_pays;
     d->validated = validated;
     HIPCHK(hipSetDevice(c->device));
+    // The event words first: their copy (the bulk of the bytes) runs while
+    // the host stages the per-key arrays below.  A register-tier batch with
+    // page-locked 16-bit words crosses the host link at 2 bytes per event and
+    // is widened on the device (the register tier validates what it reads).
+    HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
+    if (events_mapped) d->events = const_cast<uint32_t *>(events_mapped);
+    const bool use16 = !events_mapped && d->n_events && b->events16 && sh.t0_only &&
+                       (!events_src || events_src == b->events) && pinned(b->events16);
+    if (use16) {
+        HIPCHK(grow(d->mem[3], d->events16, (size_t)d->n_events + 4));
+        HIPCHK(hipMemcpyAsync(d->events16, b->events16, (size_t)d->n_events * 2, hipMemcpyHostToDevice, cs));
+        const uint64_t n4 = (d->n_events + 3) / 4;
+        const int blocks = (int)std::min<uint64_t>((n4 + 255) / 256, (uint64_t)c->cu_count * 8);
+        hipLaunchKernelGGL(k_widen16, dim3(std::max(blocks, 1)), dim3(256), 0, cs, d->events16, d->events, d->n_events);
+        HIPCHK(hipGetLastError());
+    } else if (d->n_events && !events_mapped) {
+        HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
+                              hipMemcpyHostToDevice, cs));
+    }
     // layout of the staging block (16-byte aligned pieces)
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const size_t Kz = (size_t)K;
@@ -855,12 +897,20 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     }
     char *h = d->hmeta;
     std::memcpy(h + o_off, b->ev_off, (Kz + 1) * 8);
-    // LPT order: longest keys first
+    // LPT order: longest keys first (kept from the last upload when the
+    // offsets are the same)
     int32_t *order = (int32_t *)(h + o_order);
-    std::iota(order, order + K, 0);
-    std::stable_sort(order, order + K, [&](int32_t x, int32_t y) {
-        return b->ev_off[x + 1] - b->ev_off[x] > b->ev_off[y + 1] - b->ev_off[y];
-    });
+    if (d->order_off.size() == Kz + 1 && std::memcmp(d->order_off.data(), b->ev_off, (Kz + 1) * 8) == 0) {
+        std::memcpy(order, d->order_of.data(), Kz * 4);
+    } else {
+        std::vector<uint64_t> lk(Kz);  // (length << 32 | key), descending = LPT, ties by key
+        for (size_t k = 0; k < Kz; ++k)
+            lk[k] = (std::min<uint64_t>(b->ev_off[k + 1] - b->ev_off[k], 0xFFFFFFFFull) << 32) | (0xFFFFFFFFu - (uint32_t)k);
+        std::sort(lk.begin(), lk.end(), std::greater<uint64_t>());
+        for (size_t k = 0; k < Kz; ++k) order[k] = (int32_t)(0xFFFFFFFFu - (uint32_t)lk[k]);
+        d->order_off.assign(b->ev_off, b->ev_off + Kz + 1);
+        d->order_of.assign(order, order + Kz);
+    }
     if (b->n_trans > 0) std::memcpy(h + o_trans, b->trans, (size_t)b->n_trans * 4);
     else std::memset(h + o_trans, 0, 4);
     if (b->trans_off) std::memcpy(h + o_toff, b->trans_off, Kz * 4);
@@ -869,7 +919,6 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     if (b->key_error) std::memcpy(h + o_err, b->key_error, Kz);
     char *dm = nullptr;
     HIPCHK(grow(d->mem[0], dm, bytes));
-    HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
     d->table = nullptr;
     d->n_table = b->table ? b->n_table : 0;
     if (b->table) {
@@ -884,9 +933,6 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     d->key_width = b->key_width ? (uint8_t *)(dm + o_width) : nullptr;
     d->key_states = b->key_states ? (uint16_t *)(dm + o_states) : nullptr;
     d->key_error = b->key_error ? (uint8_t *)(dm + o_err) : nullptr;
-    if (d->n_events)
-        HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
-                              hipMemcpyHostToDevice, cs));
     HIPCHK(hipMemcpyAsync(dm, h, bytes, hipMemcpyHostToDevice, cs));
     HIPCHK(hipEventRecord(d->hmeta_done, cs));
     if (sync) HIPCHK(hipStreamSynchronize(cs));
@@ -1534,7 +1580,16 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
     const bool can_chunk = sh.t0_only && !(c->o.flags & LC_OPT_COUNT_PROBES) && K >= Dev::NODE_CHUNKS;
     bool big = K >= 16 * (int64_t)d->cu_count && n_ev >= (8u << 20);
     if (const char *e = std::getenv("LC_NODE_CHUNKS")) big = std::atoi(e) > 1;
-    const int chunks = can_chunk && big ? Dev::NODE_CHUNKS : 1;
+    // LC_ZEROCOPY=1 (experiment): a register-tier batch whose event words
+    // are page-locked is searched from host memory in place (no copy, no chunks)
+    const uint32_t *mapped = nullptr;
+    if (std::getenv("LC_ZEROCOPY") && std::atoi(std::getenv("LC_ZEROCOPY")) && sh.t0_only && src == b->events &&
+        pinned(b->events)) {
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, const_cast<uint32_t *>(b->events), 0) == hipSuccess) mapped = (const uint32_t *)dp;
+        else (void)hipGetLastError();
+    }
+    const int chunks = can_chunk && big && !mapped ? Dev::NODE_CHUNKS : 1;
     lc_result none{};
     bool enq = false;
     // on an error below, the copies out of the caller's arrays are waited for
@@ -1572,7 +1627,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
         if (rc) return drained(rc);
         if (!enq) return drained(lc::fail(LC_E_DEVICE, "lc_check_node: a chunk left the register tier"));
     } else {
-        rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false);
+        rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false, nullptr, mapped);
         if (rc) return rc;
         t_up = std::chrono::steady_clock::now();
         rc = dev_search(d, d->staged, &none, RES_CTX, true, 0, st, &enq);

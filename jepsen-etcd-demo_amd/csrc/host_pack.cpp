@@ -595,6 +595,20 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         }
         if (!shared) P->state_off[(size_t)K] = P->state_vals.size();
         if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
+        // 16-bit event words (lc_batch.events16) when every word fits: half
+        // the bytes over the host link for the register tier
+        bool fit16 = !P->events.empty();
+        for (size_t j = 0; j < P->events.size() && fit16; ++j) {
+            const uint32_t w = P->events[j];
+            fit16 = LC_EV_SLOT(w) <= LC_EV16_MAX_SLOT && LC_EV_TRANS(w) <= LC_EV16_MAX_TRANS;
+        }
+        if (fit16) {
+            P->events16.resize(P->events.size());
+            for (size_t j = 0; j < P->events.size(); ++j) {
+                const uint32_t w = P->events[j];
+                P->events16[j] = (uint16_t)(((w >> 16) & 0x8000u) | (LC_EV_SLOT(w) << 11) | LC_EV_TRANS(w));
+            }
+        }
     } catch (const std::bad_alloc &) {
         delete P;
         return lc::fail(LC_E_NOMEM, "lc_pack: out of memory");
@@ -622,6 +636,7 @@ extern "C" int lc_packed_view(const lc_packed *p, lc_batch *b) {
     b->key_error = p->key_error.empty() ? nullptr : p->key_error.data();
     b->table = p->table.empty() ? nullptr : p->table.data();
     b->n_table = (int64_t)p->table.size();
+    b->events16 = p->events16.empty() ? nullptr : p->events16.data();
     return LC_OK;
 }
 

@@ -13,6 +13,7 @@ struct lc_packed {
     std::vector<int64_t> keys;
     lc::pinned_vector<uint64_t> ev_off;  // page-locked on a GPU host: lc_check_* DMA it directly
     lc::pinned_vector<uint32_t> events;
+    lc::pinned_vector<uint16_t> events16;  // the same words in 16 bits when all fit (empty otherwise)
     std::vector<int64_t> ev_row;
     std::vector<uint32_t> trans;
     std::vector<uint32_t> trans_off;  // empty = shared table

@@ -56,7 +56,7 @@ class LcBatch(C.Structure):
                 ("trans", P(C.c_uint32)), ("n_trans", C.c_int64), ("trans_off", P(C.c_uint32)),
                 ("key_width", P(C.c_uint8)), ("key_states", P(C.c_uint16)),
                 ("init_state", C.c_uint32), ("key_error", P(C.c_uint8)),
-                ("table", P(C.c_uint16)), ("n_table", C.c_int64)]
+                ("table", P(C.c_uint16)), ("n_table", C.c_int64), ("events16", P(C.c_uint16))]
 
 
 class LcPackOpts(C.Structure):

@@ -359,6 +359,11 @@ def test_malformed_batch_rejected_then_context_reusable():
     assert not ev[j] & N.LC_EV_OK_BIT
     saved = int(ev[j])
     ev[j] = saved | N.LC_EV_OK_BIT
+    # the 16-bit copy the register tier is uploaded from (lc_batch.events16)
+    ev16 = np.ctypeslib.as_array(pk.view.events16, shape=(n_ev,)) if pk.view.events16 else None
+    if ev16 is not None:
+        saved16 = int(ev16[j])
+        ev16[j] = saved16 | 0x8000
     with pytest.raises(N.LincheckError) as ei:
         dev.check(pk)
     assert ei.value.code == -1 and "key 317" in str(ei.value)
@@ -367,6 +372,8 @@ def test_malformed_batch_rejected_then_context_reusable():
         db.check(peak=False)
     assert ei.value.code == -1 and "key 317" in str(ei.value)
     ev[j] = saved
+    if ev16 is not None:
+        ev16[j] = saved16
     device_vs_oracle(h, dev)
 
 

@@ -173,3 +173,19 @@ def test_models_pack():
     cas = [{"type": "invoke", "f": "cas", "value": Tuple(0, [1, 2]), "process": 0}]
     assert "cannot step" in Packed(H.History.from_ops(cas), model.register()).key_error(0)
     assert "cannot step" in Packed(H.History.from_ops(ops), model.cas_register()).key_error(0)
+
+
+def test_events16_widen_to_events():
+    """lc_pack's 16-bit event words (lc_batch.events16) widen to exactly the
+    32-bit words (LC_EV16_WIDE), and are omitted when a word does not fit."""
+    import numpy as np
+    from lincheck.checker import Packed
+    pk = Packed(H.synth(n_keys=50, ops_per_key=200, concurrency=10, anomaly_rate=0.2, seed=9))
+    n = int(pk.ev_off[-1])
+    e32 = np.ctypeslib.as_array(pk.view.events, shape=(n,)).astype(np.uint32)
+    e16 = np.ctypeslib.as_array(pk.view.events16, shape=(n,)).astype(np.uint32)
+    wide = ((e16 & 0x8000) << 16) | (((e16 >> 11) & 0xF) << 24) | (e16 & 0x7FF)
+    np.testing.assert_array_equal(wide, e32)
+    # > 16 ops pending at once: slots past 15, no 16-bit form
+    pk = Packed(H.synth(n_keys=4, ops_per_key=300, concurrency=40, mean_think=0.1, seed=9))
+    assert not pk.view.events16
