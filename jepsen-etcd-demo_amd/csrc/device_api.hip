@@ -842,8 +842,7 @@ static void shard_keys(const lc_batch *b, int n, int64_t *key0) {
 // sync: wait for the copies (the caller may free its arrays on return);
 // otherwise the caller keeps them alive until its stream has passed them.
 static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, bool validated,
-                       const uint32_t *events_src = nullptr, bool sync = true, hipStream_t stream = nullptr,
-                       const uint32_t *events_mapped = nullptr) {
+                       const uint32_t *events_src = nullptr, bool sync = true, hipStream_t stream = nullptr) {
     hipStream_t cs = stream ? stream : c->stream;
     const int64_t K = b->n_keys;
     d->device = c->device;
@@ -863,8 +862,7 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     // page-locked 16-bit words crosses the host link at 2 bytes per event and
     // is widened on the device (the register tier validates what it reads).
     HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
-    if (events_mapped) d->events = const_cast<uint32_t *>(events_mapped);
-    const bool use16 = !events_mapped && d->n_events && b->events16 && sh.t0_only &&
+    const bool use16 = d->n_events && b->events16 && sh.t0_only &&
                        (!events_src || events_src == b->events) && pinned(b->events16);
     if (use16) {
         HIPCHK(grow(d->mem[3], d->events16, (size_t)d->n_events + 4));
@@ -873,7 +871,7 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
         const int blocks = (int)std::min<uint64_t>((n4 + 255) / 256, (uint64_t)c->cu_count * 8);
         hipLaunchKernelGGL(k_widen16, dim3(std::max(blocks, 1)), dim3(256), 0, cs, d->events16, d->events, d->n_events);
         HIPCHK(hipGetLastError());
-    } else if (d->n_events && !events_mapped) {
+    } else if (d->n_events) {
         HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
                               hipMemcpyHostToDevice, cs));
     }
@@ -1580,16 +1578,10 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
     const bool can_chunk = sh.t0_only && !(c->o.flags & LC_OPT_COUNT_PROBES) && K >= Dev::NODE_CHUNKS;
     bool big = K >= 16 * (int64_t)d->cu_count && n_ev >= (8u << 20);
     if (const char *e = std::getenv("LC_NODE_CHUNKS")) big = std::atoi(e) > 1;
-    // LC_ZEROCOPY=1 (experiment): a register-tier batch whose event words
-    // are page-locked is searched from host memory in place (no copy, no chunks)
-    const uint32_t *mapped = nullptr;
-    if (std::getenv("LC_ZEROCOPY") && std::atoi(std::getenv("LC_ZEROCOPY")) && sh.t0_only && src == b->events &&
-        pinned(b->events)) {
-        void *dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, const_cast<uint32_t *>(b->events), 0) == hipSuccess) mapped = (const uint32_t *)dp;
-        else (void)hipGetLastError();
-    }
-    const int chunks = can_chunk && big && !mapped ? Dev::NODE_CHUNKS : 1;
+    // (Searching page-locked event words in place, over the host link, was
+    // measured slower: 0.468 against 0.332 ms for C2's search, the link
+    // sustaining ~31 GB/s of kernel reads; the 16-bit upload won instead.)
+    const int chunks = can_chunk && big ? Dev::NODE_CHUNKS : 1;
     lc_result none{};
     bool enq = false;
     // on an error below, the copies out of the caller's arrays are waited for
@@ -1627,7 +1619,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
         if (rc) return drained(rc);
         if (!enq) return drained(lc::fail(LC_E_DEVICE, "lc_check_node: a chunk left the register tier"));
     } else {
-        rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false, nullptr, mapped);
+        rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false);
         if (rc) return rc;
         t_up = std::chrono::steady_clock::now();
         rc = dev_search(d, d->staged, &none, RES_CTX, true, 0, st, &enq);
