@@ -336,6 +336,7 @@ struct Dev {
     // node records (lc_check_node): this rank's block and the gathered node
     uint64_t *send = nullptr, *node = nullptr;
     int64_t node_cap = 0, node_n = 0;
+    uint64_t *rec_out = nullptr;  // set around a node step's search: finish_key writes the records there
     uint64_t *hnode = nullptr;  // pinned landing area of the node's records (lc_check_node)
     int64_t hnode_cap = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
@@ -1008,6 +1009,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         a.final_cfg = (mode == RES_HOST && r->final_configs) ? c->final_cfg : nullptr;
         a.n_final = (mode == RES_HOST && r->n_final) ? c->n_final : nullptr;
     }
+    a.rec = c->rec_out ? c->rec_out + res_off : nullptr;
     a.probes = c->acc + 0; a.ev_count = c->acc + 1; a.keys_done = c->acc + 2; a.stream_bytes = c->acc + 3;
     a.err = c->counters + 4;
     a.list_cap = (int32_t)c->cap_keys;
@@ -1110,7 +1112,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         c->args_ok[aslot] = true;
     }
     lcd::Args *const dargs = c->dargs + aslot;
-    HIPCHK(hipEventRecord(c->e0, c->stream));
+    // timing events only where their times are read (each recorded event
+    // costs the stream a few microseconds between kernels): an enqueued step
+    // is timed by the span ea0 .. ea1 alone
+    if (!async) HIPCHK(hipEventRecord(c->e0, c->stream));
     if (async && c->n_async == 0) HIPCHK(hipEventRecord(c->ea0, c->stream));
     if (K > 0 && a.strict && !spec) {
         // the event-by-event validation the host skipped: on the second
@@ -1135,10 +1140,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         sa.seg_cnt = c->seg_cnt; sa.seg_end = c->seg_end; sa.seg_out = c->seg_out; sa.seg0_fev = c->seg0_fev;
         sa.work = c->seg_work; sa.rerun = c->seg_rerun; sa.rerun_init = c->seg_rerun_init; sa.ctl = c->seg_ctl;
         sa.err = c->counters + 4; sa.valid = a.valid; sa.fail_event = a.fail_event; sa.cause = a.cause;
+        sa.rec = a.rec;
         sa.strict = a.strict;
         HIPCHK(hipMemsetAsync(c->seg_ctl, 0, 4 * sizeof(int32_t), c->stream));
         HIPCHK(lcd::launch_segments(sa, grid, c->stream));
-        HIPCHK(hipEventRecord(c->et0, c->stream));
+        if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (spec) {
         const uint32_t ck1 = std::getenv("LC_SPEC_CK1") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK1")) : 32u;
         const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 160u;
@@ -1148,10 +1154,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2, c->cu_count * 8,
                                 vblocks, c->stream));
         c->spec_parity ^= 1;
-        HIPCHK(hipEventRecord(c->et0, c->stream));
+        if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0 && !d->table) {
         HIPCHK(lcd::launch_t0(a0, dargs, g0, t0_wide, c->stream, ticket_base));
-        HIPCHK(hipEventRecord(c->et0, c->stream));
+        if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0) {
         HIPCHK(hipEventRecord(c->et0, c->stream));  // a table model: no register lattice
     }
@@ -1521,16 +1527,28 @@ extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_sta
 // Pack this rank's verdicts (c's device arrays) into its block and all-gather
 // the blocks of every rank over RCCL (one rank: the block is the node), on
 // c's stream.
-static int gather_node(lc_ctx *x, Dev *c, int64_t n, int64_t block) {
-    const int64_t total = block * x->size;
+// The rank's record block (and the node's), grown on demand; the search that
+// follows writes its records straight into the block (Dev::rec_out), and the
+// padding past the shard's n keys is zeroed.
+static int node_buffers(lc_ctx *x, Dev *c, int64_t n, int64_t block) {
     if (block > c->node_cap || !c->send) {
+        if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));  // an enqueued step may still write them
         dfree(c->send);
         dfree(c->node);
         HIPCHK(dalloc(&c->send, (size_t)std::max<int64_t>(block, 1)));
         HIPCHK(dalloc(&c->node, (size_t)std::max<int64_t>(block, 1) * x->size));
         c->node_cap = block;
     }
-    if (block > 0) {
+    uint64_t *blk = x->comm ? c->send : c->node;
+    if (block > n) HIPCHK(hipMemsetAsync(blk + n, 0, (size_t)(block - n) * 8, c->stream));
+    c->rec_out = blk;
+    return LC_OK;
+}
+
+static int gather_node(lc_ctx *x, Dev *c, int64_t n, int64_t block, bool packed = false) {
+    const int64_t total = block * x->size;
+    c->rec_out = nullptr;
+    if (block > 0 && !packed) {
         const int threads = 256;
         const int blocks = (int)std::min<int64_t>((block + threads - 1) / threads, 4096);
         hipLaunchKernelGGL(k_pack_records, dim3(blocks), dim3(threads), 0, c->stream, c->valid, c->cause, c->fail_event,
@@ -1567,6 +1585,12 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
         d->staged = new (std::nothrow) DevBatch();
         if (!d->staged) return lc::fail(LC_E_NOMEM, "lc_check_node: out of memory");
     }
+    rc = node_buffers(c, d, b->n_keys, block);
+    if (rc) return rc;
+    struct RecOff {  // every return below stops later searches writing records
+        Dev *d;
+        ~RecOff() { d->rec_out = nullptr; }
+    } rec_off{d};
     const auto t_prep = std::chrono::steady_clock::now();
     // A large register-tier shard (throughput-bound: many keys per SIMD) is
     // uploaded and searched in NODE_CHUNKS key chunks: the copies run on a
@@ -1626,7 +1650,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
         if (rc) return drained(rc);
     }
     const auto t_search = std::chrono::steady_clock::now();
-    rc = gather_node(c, d, b->n_keys, block);
+    rc = gather_node(c, d, b->n_keys, block, true);  // the search wrote the records
     if (rc) return drained(rc);
     // the records land in pinned memory (a copy into the caller's pageable
     // array would be a synchronous staged copy) and are copied out after the wait
@@ -1674,9 +1698,11 @@ extern "C" int lc_check_node_device(lc_ctx *c, const lc_dev_batch *db, int64_t b
     Dev *d = c->dev[0];
     lc_result none{};
     bool enq = false;
-    rc = dev_search(d, db->part[0], &none, RES_CTX, (flags & LC_DEV_ASYNC) != 0, 0, st, &enq);
+    rc = node_buffers(c, d, db->n_keys, block);
     if (rc) return rc;
-    rc = gather_node(c, d, db->n_keys, block);
+    rc = dev_search(d, db->part[0], &none, RES_CTX, (flags & LC_DEV_ASYNC) != 0, 0, st, &enq);
+    if (rc) { d->rec_out = nullptr; return rc; }
+    rc = gather_node(c, d, db->n_keys, block, true);
     if (rc) return rc;
     if (!enq) HIPCHK(hipStreamSynchronize(d->stream));
     return LC_OK;

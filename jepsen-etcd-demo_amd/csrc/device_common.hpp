@@ -91,6 +91,11 @@ __device__ __forceinline__ void finish_key(const Args &a, int32_t key, int verdi
         a.cause[key] = (uint8_t)cause;
         a.fail_event[key] = fev;
         if (a.peak) a.peak[key] = peak;
+        // the node exchange's record (include/lincheck.h LC_REC_*), written as
+        // the key finishes: no packing pass over the keys afterwards
+        if (a.rec)
+            a.rec[key] = (uint64_t)(uint8_t)(verdict + 1) | (uint64_t)(uint8_t)cause << 8 |
+                         (uint64_t)(uint32_t)(fev + 1) << 16;
         if (a.count_probes) atomicAdd(a.probes, (unsigned long long)probes);
         atomicAdd(a.ev_count, (unsigned long long)nev);
         atomicAdd(a.keys_done, 1ull);

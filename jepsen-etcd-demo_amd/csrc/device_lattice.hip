@@ -1495,17 +1495,24 @@ __global__ __launch_bounds__(64) void k_search_segments(SegArgs a) {
     }
 }
 
+// A segmented key's verdict (and its LC_REC_* record when asked for).
+__device__ __forceinline__ void seg_verdict(const SegArgs &a, int32_t key, int v, int cause, int32_t fev) {
+    a.valid[key] = (int8_t)v; a.cause[key] = (uint8_t)cause; a.fail_event[key] = fev;
+    if (a.rec)
+        a.rec[key] = (uint64_t)(uint8_t)(v + 1) | (uint64_t)(uint8_t)cause << 8 | (uint64_t)(uint32_t)(fev + 1) << 16;
+}
+
 // Per key (one thread each): compose the segments' final words.
 __global__ __launch_bounds__(256) void k_seg_compose(SegArgs a) {
     for (int32_t key = blockIdx.x * blockDim.x + threadIdx.x; key < a.n_keys; key += gridDim.x * blockDim.x) {
         if (a.key_error && a.key_error[key]) {
-            a.valid[key] = LC_UNKNOWN; a.cause[key] = LC_CAUSE_ERROR; a.fail_event[key] = -1;
+            seg_verdict(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1);
             continue;
         }
         const uint32_t n = a.seg_cnt[key];
         const uint32_t *out = a.seg_out + (size_t)key * a.max_seg;
         if (out[0] == 0u) {  // segment 0 is searched from the initial state itself
-            a.valid[key] = LC_INVALID; a.cause[key] = LC_CAUSE_NONLIN; a.fail_event[key] = a.seg0_fev[key];
+            seg_verdict(a, key, LC_INVALID, LC_CAUSE_NONLIN, a.seg0_fev[key]);
             continue;
         }
         uint32_t S = (out[0] >> 1) & 0x1Fu;  // state ids 1..5 -> start groups 0..4
@@ -1525,7 +1532,7 @@ __global__ __launch_bounds__(256) void k_seg_compose(SegArgs a) {
             S = S2;
         }
         if (!dead) {
-            a.valid[key] = LC_VALID; a.cause[key] = LC_CAUSE_NONE; a.fail_event[key] = -1;
+            seg_verdict(a, key, LC_VALID, LC_CAUSE_NONE, -1);
         }
     }
 }
@@ -1549,9 +1556,9 @@ __global__ __launch_bounds__(64) void k_seg_rerun(SegArgs a) {
         segment_search<false>(a, key, ends[s - 1], ends[s], a.rerun_init[w], ws, status, fev, fin);
         if (lane_id() == 0) {
             if (status == 1) {
-                a.valid[key] = LC_INVALID; a.cause[key] = LC_CAUSE_NONLIN; a.fail_event[key] = (int32_t)fev;
+                seg_verdict(a, key, LC_INVALID, LC_CAUSE_NONLIN, (int32_t)fev);
             } else {  // cannot happen for a consistent batch: report it as malformed
-                a.valid[key] = LC_UNKNOWN; a.cause[key] = LC_CAUSE_ERROR; a.fail_event[key] = -1;
+                seg_verdict(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1);
                 atomicOr(&a.err[0], LC_BATCH_E_FIT);
                 atomicMax(&a.err[1], key + 1);
             }

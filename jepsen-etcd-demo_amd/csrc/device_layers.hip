@@ -331,7 +331,10 @@ struct Part {
     bool multi;
     __device__ bool mine(uint32_t h) const { return !multi || (h >> shift) == part; }
 };
-constexpr int UP = 2;  // successor pairs per thread in flight
+#ifndef LC_T3L_UP
+#define LC_T3L_UP 2
+#endif
+constexpr int UP = LC_T3L_UP;  // successor pairs per thread in flight (A/B: make variant VFLAGS=-DLC_T3L_UP=n)
 // The first two entries per thread of an S layer [sb, se), loaded ahead.
 struct SPre {
     uint64_t s0, s1;

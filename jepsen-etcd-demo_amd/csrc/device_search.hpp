@@ -40,6 +40,7 @@ struct Args {
     uint32_t *peak;          // may be null
     uint64_t *final_cfg;     // may be null: [key][max_final][2]
     uint32_t *n_final;       // may be null
+    uint64_t *rec;           // may be null: the key's verdict record (LC_REC_*) is written here too
     uint32_t *lat_ws;            // T0 workspace: lat_ws_words() per resident block
     // counters
     unsigned long long *probes;
@@ -109,6 +110,7 @@ struct SegArgs {
     int8_t *valid;
     int32_t *fail_event;
     uint8_t *cause;
+    uint64_t *rec;               // may be null: LC_REC_* records (Args::rec)
     int32_t strict;
 };
 constexpr uint32_t SEG_MAX = 256;  // work items are key << 8 | segment
