@@ -37,8 +37,8 @@ static int failures = 0;
     } while (0)
 
 // pack, render every key's report, run the oracle; returns keys
-static int64_t exercise(const lc_history &h, int model) {
-    lc_pack_opts po{model};
+static int64_t exercise(const lc_history &h, int model, const int64_t *init = nullptr, int32_t n_init = 0) {
+    lc_pack_opts po{model, n_init, init};
     lc_packed *p = nullptr;
     if (lc_pack(&h, &po, &p) != LC_OK) return -1;
     lc_batch b;
@@ -67,6 +67,12 @@ static int64_t exercise(const lc_history &h, int model) {
             int64_t need = lc_report(p, i, valid, valid == LC_VALID ? -1 : fe, fin, nf, 10, w.data(), (int64_t)w.size());
             if (lc_packed_key_error(p, i)) { CHECK(need < 0); continue; }
             CHECK(need >= 4);
+            if (model == LC_MODEL_MULTI_REGISTER && b.key_states[i] <= LC_WIDE_MAX_STATES) {
+                // every map a state id stands for
+                int64_t regs[64], vals[64];
+                for (uint32_t st = 0; st < b.key_states[i]; ++st)
+                    CHECK(lc_packed_state_map(p, i, st, regs, vals, 64) >= 0);
+            }
             if (need > (int64_t)w.size()) {
                 w.resize((size_t)need);
                 CHECK(lc_report(p, i, valid, valid == LC_VALID ? -1 : fe, fin, nf, 10, w.data(), need) == need);
@@ -75,6 +81,7 @@ static int64_t exercise(const lc_history &h, int model) {
     }
     const int64_t nk = b.n_keys;
     lc_packed_free(p);
+    if (model == LC_MODEL_MULTI_REGISTER) return nk;  // the C oracle has no table models
     int64_t ok = oracle_check_history_model(&h, model, 1 << 14, 4, nullptr, nullptr, 0);
     if (ok > 0) {
         std::vector<int64_t> ok_keys((size_t)ok);
@@ -144,19 +151,32 @@ int main(int argc, char **argv) {
         lc_hist_free(h);
     }
     // random op sequences over three processes and two keys: completions
-    // without invocations, double invokes, unknown :f codes
+    // without invocations, double invokes, unknown :f codes, :txn rows with
+    // random (and malformed) micro-ops for (model/multi-register)
     std::mt19937_64 rng(3);
     for (int t = 0; t < 2000; ++t) {
         const int n = 1 + (int)(rng() % 24);
         std::vector<uint8_t> ty(n), f(n);
-        std::vector<int64_t> pr(n), key(n), v0(n), v1(n), idx(n);
+        std::vector<int64_t> pr(n), key(n), v0(n), v1(n), idx(n), mop_off(n + 1, 0), mop;
         for (int i = 0; i < n; ++i) {
-            ty[i] = (uint8_t)(rng() % 4); f[i] = (uint8_t)(rng() % 6);
+            ty[i] = (uint8_t)(rng() % 4); f[i] = (uint8_t)(rng() % 7);
             pr[i] = (int64_t)(rng() % 3); key[i] = (rng() % 5) ? (int64_t)(rng() % 2) : LC_NO_KEY;
             v0[i] = (rng() % 4) ? (int64_t)(rng() % 3) : LC_NIL; v1[i] = (int64_t)(rng() % 3); idx[i] = i;
+            const int nm = f[i] == LC_F_TXN ? (int)(rng() % 4) : 0;
+            for (int m = 0; m < nm; ++m) {
+                mop.push_back((rng() % 50) ? (int64_t)(rng() % 2) : 7);  // an unknown micro-op now and then
+                mop.push_back((int64_t)(rng() % 3));
+                mop.push_back((rng() % 4) ? (int64_t)(rng() % 3) : LC_NIL);
+            }
+            mop_off[i + 1] = (int64_t)mop.size() / 3;
         }
-        lc_history h{n, ty.data(), f.data(), pr.data(), key.data(), v0.data(), v1.data(), idx.data()};
-        for (int model : {LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX}) exercise(h, model);
+        mop.push_back(0);
+        lc_history h{n, ty.data(), f.data(), pr.data(), key.data(), v0.data(), v1.data(), idx.data(),
+                     mop_off.data(), mop.data()};
+        for (int model : {LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX, LC_MODEL_MULTI_REGISTER})
+            exercise(h, model);
+        const int64_t init[4] = {0, 1, 2, LC_NIL};
+        exercise(h, LC_MODEL_MULTI_REGISTER, init, 2);
     }
     std::remove(tmp);
     std::printf("host sanitizer driver: %d failed checks\n", failures);
