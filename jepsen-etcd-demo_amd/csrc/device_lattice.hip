@@ -647,20 +647,8 @@ __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_
 // probes): each row a one-directional lane sweep (sweep_lanes, 3 VALU per
 // position), then the register bits from the rows below it, already updated
 // in this sweep.  The bidirectional per-row form above needs about twice the
-// instructions per sweep and more sweeps.  The closure set I lives in VGPRs
-// for the sweeps (RL of them: 8 or 16, within the speculative kernel's
-// budget at 4 waves per SIMD); only the :ok's gathers along the run-time bit
-// p go through the LDS workspace (once per :ok, not per sweep).  With I in
-// the workspace every sweep paid two LDS round trips per row: a 9-10-pending
-// :ok cost ~21k cycles (tools/spec_stamps.py fit).
-// A/B switches: false keeps the 9- / 10-pending closure in the LDS workspace
-#ifndef LC_SPEC_REG8
-#define LC_SPEC_REG8 true
-#endif
-#ifndef LC_SPEC_REG16
-#define LC_SPEC_REG16 true
-#endif
-template <int RL, bool REG = true>
+// instructions per sweep and more sweeps.
+template <int RL>
 __device__ __forceinline__ int ok_event_mem_gs(const LatMem &m, uint32_t p, uint32_t n, uint32_t k_v, uint32_t cap_v,
                                                uint32_t b_v, uint32_t lane) {
     constexpr int NB = lat_bits<RL>();
@@ -673,69 +661,37 @@ __device__ __forceinline__ int ok_event_mem_gs(const LatMem &m, uint32_t p, uint
     const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
                    pb = __builtin_amdgcn_readlane(b_v, p);
     const uint32_t plm = p < 6 ? 1u << p : 0u, prm = p >= 6 ? 1u << (p - 6) : 0u;
+#pragma unroll 1
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t w = m.W[k * 64 + lane];
+        const uint32_t src = (uint32_t)__shfl_xor((int)m.W[(k ^ prm) * 64 + lane], (int)plm);
+        const bool hp = (lane & plm) || ((uint32_t)k & prm);
+        m.R[k * 64 + lane] = hp ? 0u : src;
+        m.I[k * 64 + lane] = hp ? 0u : w;
+    }
+#pragma unroll 1
+    for (int s = 0; s < NB; ++s) {
+        bool ch = false;
+#pragma unroll 1
+        for (int k = 0; k < RL; ++k) {
+            const uint32_t x = m.I[k * 64 + lane];
+            uint32_t nv = sweep_lanes<0, 6>(x, lmk);
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+                if ((k >> r) & 1) nv = xacc(nv, m.I[(k ^ (1 << r)) * 64 + lane], rk[r], lmk.sc[6 + r], lmk.sb[6 + r]);
+            if (nv != x) {
+                m.I[k * 64 + lane] = nv;
+                ch = true;
+            }
+        }
+        if (!__any(ch)) break;
+    }
     uint32_t cS = 0;
-    if constexpr (REG) {
-        uint32_t I[RL];
-#pragma unroll
-        for (int k = 0; k < RL; ++k) {
-            const uint32_t w = m.W[k * 64 + lane];
-            const uint32_t src = (uint32_t)__shfl_xor((int)m.W[(k ^ prm) * 64 + lane], (int)plm);
-            const bool hp = (lane & plm) || ((uint32_t)k & prm);
-            m.R[k * 64 + lane] = hp ? 0u : src;
-            I[k] = hp ? 0u : w;
-        }
 #pragma unroll 1
-        for (int s = 0; s < NB; ++s) {
-            bool ch = false;
-#pragma unroll
-            for (int k = 0; k < RL; ++k) {
-                uint32_t nv = sweep_lanes<0, 6>(I[k], lmk);
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    if ((k >> r) & 1) nv = xacc(nv, I[k ^ (1 << r)], rk[r], lmk.sc[6 + r], lmk.sb[6 + r]);
-                ch = ch || nv != I[k];
-                I[k] = nv;
-            }
-            if (!__any(ch)) break;
-        }
-#pragma unroll
-        for (int k = 0; k < RL; ++k) {
-            const uint32_t r = m.R[k * 64 + lane] | xapply(I[k], pk, pc, pb);
-            m.R[k * 64 + lane] = r;
-            cS |= r;
-        }
-    } else {
-#pragma unroll 1
-        for (int k = 0; k < RL; ++k) {
-            const uint32_t w = m.W[k * 64 + lane];
-            const uint32_t src = (uint32_t)__shfl_xor((int)m.W[(k ^ prm) * 64 + lane], (int)plm);
-            const bool hp = (lane & plm) || ((uint32_t)k & prm);
-            m.R[k * 64 + lane] = hp ? 0u : src;
-            m.I[k * 64 + lane] = hp ? 0u : w;
-        }
-#pragma unroll 1
-        for (int s = 0; s < NB; ++s) {
-            bool ch = false;
-#pragma unroll 1
-            for (int k = 0; k < RL; ++k) {
-                const uint32_t x = m.I[k * 64 + lane];
-                uint32_t nv = sweep_lanes<0, 6>(x, lmk);
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    if ((k >> r) & 1) nv = xacc(nv, m.I[(k ^ (1 << r)) * 64 + lane], rk[r], lmk.sc[6 + r], lmk.sb[6 + r]);
-                if (nv != x) {
-                    m.I[k * 64 + lane] = nv;
-                    ch = true;
-                }
-            }
-            if (!__any(ch)) break;
-        }
-#pragma unroll 1
-        for (int k = 0; k < RL; ++k) {
-            const uint32_t r = m.R[k * 64 + lane] | xapply(m.I[k * 64 + lane], pk, pc, pb);
-            m.R[k * 64 + lane] = r;
-            cS |= r;
-        }
+    for (int k = 0; k < RL; ++k) {
+        const uint32_t r = m.R[k * 64 + lane] | xapply(m.I[k * 64 + lane], pk, pc, pb);
+        m.R[k * 64 + lane] = r;
+        cS |= r;
     }
     if (!__any(cS != 0u)) return 1;
     const uint32_t last = n - 1;
@@ -1945,8 +1901,8 @@ __device__ __forceinline__ int spec_walk(const uint32_t *evp, const uint32_t *tr
                 else if (n == 9) r = ok_event_mem<8>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
                 else r = ok_event_mem<16>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
 #else
-                else if (n == 9) r = ok_event_mem_gs<8, LC_SPEC_REG8>(m, p, n, k_v, cap_v, b_v, lane);
-                else r = ok_event_mem_gs<16, LC_SPEC_REG16>(m, p, n, k_v, cap_v, b_v, lane);
+                else if (n == 9) r = ok_event_mem_gs<8>(m, p, n, k_v, cap_v, b_v, lane);
+                else r = ok_event_mem_gs<16>(m, p, n, k_v, cap_v, b_v, lane);
 #endif
                 const uint32_t last = n - 1;
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
@@ -2002,7 +1958,7 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 // through a.full like T0's; a.lat_ws holds each wave's 9-10-pending
 // workspace (global memory: with LDS for it, fewer segments fit a CU).
 template <int S>
-__global__ __launch_bounds__(64 * S, 4) void k_spec(T0Args a) {  // 4 waves per SIMD: <= 128 VGPRs
+__global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
     __shared__ uint32_t s_ck[S][2][64];   // TOP run's checkpoint sets
     __shared__ uint32_t s_pend[S][8];     // ops pending at the cut ([0..5] words, [6] count)
