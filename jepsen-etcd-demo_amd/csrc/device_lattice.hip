@@ -349,11 +349,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
     if (count) probes += (uint32_t)__popc(W);
     uint32_t Ret = hp ? 0u : wup;
     uint32_t I = hp ? 0u : W;
-#ifdef LC_ABL_NOSWEEP
-    const uint32_t nc = 0;  // ablation build: closure skipped
-#else
     const uint32_t nc = (uint32_t)__popc(cand);  // a closure path has at most nc steps
-#endif
 #ifdef LC_T0_COUNT_SWEEPS
     uint32_t done_s = nc;
 #endif
@@ -899,9 +895,6 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
             } else {
                 const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
                 uint32_t nSn = 0;
-#if defined(LC_ABL_NOOK) || defined(LC_ABL_NOOKALL)
-                const int r = 0;  // ablation build: bookkeeping only
-#else
                 int r;
                 if constexpr (FAST && RM == T0_RSMALL) {
                     // closed sets (compact build only: on C2's lone waves the
@@ -926,7 +919,6 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
 #ifndef LC_T0_WIDE_SPEC  // 1: specialise the wide build too (measured slower on C2)
 #define LC_T0_WIDE_SPEC 0
-#endif
                 if ((RM == T0_RBIG && !LC_T0_WIDE_SPEC) || top >= 6)
                     r = ok_lane<6>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, budget, count, probes, nSn,
                                    want_peak);
@@ -982,9 +974,6 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
                 uint32_t nSn = 0;
                 int r;
-#ifdef LC_ABL_NOOKALL
-                r = 0;  // ablation build: bookkeeping only, every width
-#else
                 if (n == 7) r = ok_reg<2>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                 else if (n == 8) r = ok_reg<4>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                 else if constexpr (RM < 16) {
@@ -996,7 +985,6 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                     if (n == 9) r = ok_reg<8>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                     else r = ok_reg<16>(W, p, k_v, cap_v, b_v, lane, budget, count, probes, nSn, want_peak);
                 }
-#endif
                 // the op at index `last` takes index p (a no-op when p == last)
                 const uint32_t last = n - 1;
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
@@ -1897,13 +1885,8 @@ __device__ __forceinline__ int spec_walk(const uint32_t *evp, const uint32_t *tr
                 int r;
                 if (n == 7) r = ok_reg<2, RM>(W, p, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
                 else if (n == 8) r = ok_reg<4, RM>(W, p, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
-#ifdef LC_SPEC_MEM_OLD  // A/B build: the bidirectional per-row closure
-                else if (n == 9) r = ok_event_mem<8>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
-                else r = ok_event_mem<16>(m, p, n, k_v, cap_v, b_v, lane, ~0ull, false, probes, nSn, false);
-#else
                 else if (n == 9) r = ok_event_mem_gs<8>(m, p, n, k_v, cap_v, b_v, lane);
                 else r = ok_event_mem_gs<16>(m, p, n, k_v, cap_v, b_v, lane);
-#endif
                 const uint32_t last = n - 1;
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
                 const uint32_t x0 = __builtin_amdgcn_readlane(k_v, last), x1 = __builtin_amdgcn_readlane(cap_v, last),
