@@ -388,11 +388,12 @@ void lc_destroy(lc_ctx *ctx);
 /* One call per batch: H2D, search, D2H into caller-owned result arrays.
  * Validation: every array index is checked before a kernel follows it.  The
  * per-event checks (an :ok names a pending slot, transition ids in range,
- * key_width / key_states honest) run on the host, except for a batch whose
- * keys are all declared to fit the register tier (key_width <= 10, <= 32
- * states): its register-tier launch carries validation waves that walk every
- * key's events beside the search (the search itself stays in bounds on any
- * input), and a malformed key ends the call with LC_E_INVALID naming it.
+ * key_width / key_states honest) run on the device, one wave per key beside
+ * the register tier (which stays in bounds on any input, and for a batch
+ * declared to fit it refuses a key that does not); the set tiers that follow
+ * trust the events, so over a refused batch they do nothing, and a malformed
+ * key ends the call with LC_E_INVALID naming it.  A table model's batch
+ * (lc_batch.table) is checked on the host, rows included.
  * The result arrays of a refused call are unspecified.  Event words in
  * page-locked memory (lc_pack's output on a GPU host) are uploaded directly;
  * others through a pinned staging copy. */

@@ -211,7 +211,7 @@ struct DevBatch {
     bool t0_only = false;      // every key declared to fit the register lattice
     bool taggable = false;     // keys may be cut into segments (shared table, states 0..5, no op installs nil)
     bool seg_pays = false;     // sampled keys have quiescent points close enough for segments to pay
-    bool validated = false;    // the host checked every event (else T0 does: T0_STRICT)
+    bool validated = false;    // the host checked every event (else the device does: T0_STRICT or k_validate<true>)
     // Device storage behind the arrays above, grown on demand: a batch that is
     // re-uploaded (a context's staging batch for lc_check_batch) keeps it, so
     // a host-to-host check allocates nothing once its sizes have been seen.
@@ -735,6 +735,7 @@ struct Shape {
     bool t0_only = false;
     bool taggable = false;  // segments (lcd::SegArgs): shared table, states 0..5 from nil, nothing installs nil
     bool seg_pays = false;  // sampled keys: the longest stretch without a quiescent point is short
+    bool host_checked = false;  // prepare_batch walked every event (table models: their rows too)
 };
 
 // Would key segments pay?  A segment ends only at a quiescent point, so the
@@ -997,7 +998,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     a.table = d->table;
     a.init_state = d->init_state; a.shared_states = d->shared_states;
     a.n_trans = (uint32_t)d->n_trans;
-    a.strict = d->validated ? 0 : 1;
+    // T0_STRICT: a register-tier batch the host did not walk (T0 refuses a key
+    // that does not fit instead of spilling it); other unwalked batches get
+    // the general validation kernel ahead of the set tiers
+    a.strict = (!d->validated && d->t0_only) ? 1 : 0;
+    const bool gen_validate = !d->validated && !d->t0_only;
     a.budget = o.max_configs; a.max_final = o.max_final; a.debug_mode = o.debug_mode;
     a.count_probes = (o.flags & LC_OPT_COUNT_PROBES) ? 1 : 0;
     if (mode == RES_DEV) {
@@ -1117,14 +1122,15 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // is timed by the span ea0 .. ea1 alone
     if (!async) HIPCHK(hipEventRecord(c->e0, c->stream));
     if (async && c->n_async == 0) HIPCHK(hipEventRecord(c->ea0, c->stream));
-    if (K > 0 && a.strict && !spec) {
+    const bool side_validate = K > 0 && ((a.strict && !spec) || gen_validate);
+    if (side_validate) {
         // the event-by-event validation the host skipped: on the second
-        // stream, beside T0, joined before the step's results are read
+        // stream, beside T0, joined before the set tiers and the readback
         HIPCHK(hipEventRecord(c->vin, c->stream));
         HIPCHK(hipStreamWaitEvent(c->vstream, c->vin, 0));
         lcd::Args av = a;
         av.n_order = (int32_t)K;
-        HIPCHK(lcd::launch_validate(av, c->vstream));
+        HIPCHK(lcd::launch_validate(av, c->vstream, gen_validate));
         HIPCHK(hipEventRecord(c->vdone, c->vstream));
     }
     if (split) {
@@ -1161,7 +1167,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     } else if (K > 0) {
         HIPCHK(hipEventRecord(c->et0, c->stream));  // a table model: no register lattice
     }
-    if (K > 0 && a.strict && !spec) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));
+    if (side_validate) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));
     if (async) {
         HIPCHK(hipEventRecord(c->ea1, c->stream));
         HIPCHK(hipEventRecord(c->ring[c->async_seq % 4], c->stream));
@@ -1356,11 +1362,16 @@ static int prepare_batch(lc_ctx *c, const lc_batch *b, Shape *sh, const uint32_t
         HIPCHK(hipHostMalloc((void **)&c->hstage, n_ev * 4, hipHostMallocDefault));
         c->hstage_cap = n_ev;
     }
-    if (!stage && sh->t0_only) return LC_OK;  // nothing to copy, T0 validates
+    // The device validates every event of a batch (k_validate beside the
+    // first tier; the later tiers do nothing over a refused batch), so the
+    // host walks the events only to stage pageable ones -- and to check a
+    // table model, whose rows are checked against the key's states here.
+    sh->host_checked = b->table != nullptr;
+    if (!stage && !sh->host_checked) return LC_OK;  // nothing to copy, the device validates
     if (K >= 256 && !c->pool)
         c->pool = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
     int64_t bk = -1;
-    if (int why = validate_events(b, &bk, stage ? c->hstage : nullptr, K >= 256 ? c->pool : nullptr, !sh->t0_only))
+    if (int why = validate_events(b, &bk, stage ? c->hstage : nullptr, K >= 256 ? c->pool : nullptr, sh->host_checked))
         return events_error(why, bk);
     if (stage) *src = c->hstage;
     return LC_OK;
@@ -1389,7 +1400,7 @@ extern "C" int lc_upload(lc_ctx *c, const lc_batch *b, lc_dev_batch **out) {
         std::vector<uint64_t> off;
         const lc_batch s = c->n_dev > 1 ? sub_batch(b, d->key0[p], d->key0[p + 1], off) : *b;
         const uint32_t *es = src ? src + (b->n_keys ? b->ev_off[d->key0[p]] : 0) : nullptr;
-        return upload_into(c->dev[p], &s, d->part[p], sh, !sh.t0_only, es);
+        return upload_into(c->dev[p], &s, d->part[p], sh, sh.host_checked, es);
     });
     if (rc) { delete d; return rc; }
     *out = d;
@@ -1496,7 +1507,7 @@ extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_sta
         std::vector<uint64_t> off;
         const lc_batch s = c->n_dev > 1 ? sub_batch(b, key0[p], key0[p + 1], off) : *b;
         const uint32_t *es = src ? src + (b->n_keys ? b->ev_off[key0[p]] : 0) : nullptr;
-        int e = upload_into(d, &s, d->staged, sh, !sh.t0_only, es);
+        int e = upload_into(d, &s, d->staged, sh, sh.host_checked, es);
         if (e) return e;
         const int64_t k0 = key0[p];
         lc_result rp = *r;
@@ -1629,7 +1640,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
             std::vector<uint64_t> off;
             const lc_batch s = sub_batch(b, key0[i], key0[i + 1], off);
             const uint32_t *es = src ? src + b->ev_off[key0[i]] : nullptr;
-            rc = upload_into(d, &s, d->chunk[i], sh, !sh.t0_only, es, false, d->cstream);
+            rc = upload_into(d, &s, d->chunk[i], sh, sh.host_checked, es, false, d->cstream);
             if (rc) return drained(rc);
             HIPCHK(hipEventRecord(d->chunk_ready[i], d->cstream));
         }
@@ -1643,7 +1654,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
         if (rc) return drained(rc);
         if (!enq) return drained(lc::fail(LC_E_DEVICE, "lc_check_node: a chunk left the register tier"));
     } else {
-        rc = upload_into(d, b, d->staged, sh, !sh.t0_only, src, false);
+        rc = upload_into(d, b, d->staged, sh, sh.host_checked, src, false);
         if (rc) return rc;
         t_up = std::chrono::steady_clock::now();
         rc = dev_search(d, d->staged, &none, RES_CTX, true, 0, st, &enq);

@@ -102,6 +102,13 @@ __device__ __forceinline__ void finish_key(const Args &a, int32_t key, int verdi
     }
 }
 
+// The batch was found malformed by the validation that ran before this
+// launch (err words, stream order): the set tiers trust validated events, so
+// over a refused batch they do nothing (the call returns LC_E_INVALID).
+__device__ __forceinline__ bool batch_refused(const Args &a) {
+    return a.err && __builtin_amdgcn_readfirstlane(*(volatile const int32_t *)a.err) != 0;
+}
+
 // Next entry of this launch's work list (dynamic: one atomic ticket per key,
 // so long keys -- listed first by the host's LPT order -- do not serialise).
 __device__ __forceinline__ int32_t next_work(const Args &a) {

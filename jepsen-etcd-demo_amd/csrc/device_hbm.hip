@@ -657,7 +657,7 @@ __global__ __launch_bounds__(WG) void k_search_hbm(Args a, HbmWs w) {
     __shared__ HbmShared<C, WG> sh;
     Slot<C> sl = slot_ptrs<C>(w, blockIdx.x);
     const int32_t n = a.n_in ? min(*a.n_in, a.list_cap) : a.n_order;
-    if (n == 0) return;  // empty work list
+    if (n == 0 || batch_refused(a)) return;  // empty work list / malformed batch
     for (;;) {
         if (threadIdx.x == 0) sh.work = atomicAdd(a.ticket, 1);
         __syncthreads();

@@ -1057,6 +1057,11 @@ __device__ unsigned long long lc_t0_stamps[8192 * 6];
 // event of the slot in the chunk (r from 0, wave rank among the slot's lanes)
 // must be an :ok exactly when r + b is odd.  Violations set the batch's
 // error words (the call then returns LC_E_INVALID).
+// GEN (a batch of any width whose events the host did not walk either):
+// window slots up to 126 (two pending words), the slot-127 marker of ops
+// beyond the encodable window exempt from the slot protocol (the search stops
+// before it follows one), and every :invoke's slot below the key's key_width.
+template <bool GEN>
 __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     const uint32_t lane = lane_id();
     if (a.key_error && a.key_error[k]) return;
@@ -1064,7 +1069,8 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     const uint32_t tb = a.trans_off ? a.trans_off[k] : 0u;
     const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
     const uint32_t ns = a.trans_off ? (a.key_states ? a.key_states[k] : 0u) : a.shared_states;
-    uint64_t pend = 0;
+    const uint32_t width = GEN ? (a.key_width ? a.key_width[k] : 127u) : 64u;
+    uint64_t pend[2] = {0, 0};
     int32_t why = 0;
     for (uint64_t base = eb; base < ee && !why; base += 64) {
         const uint64_t j = base + lane;
@@ -1074,20 +1080,23 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
         const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
         const uint32_t d = (in && !ok && t < ntr) ? a.trans[tb + t] : 0u;
         if (__any(in && !ok && (t >= ntr || ((d & 3u) >= LC_T_WRITE && (d >> 17) >= ns)))) why |= LC_BATCH_E_TRANS;
-        if (__any(in && s >= 64)) why |= LC_BATCH_E_FIT;
+        const bool beyond = GEN && s == 127u;  // past the encodable window: no slot to track
+        if (__any(in && !beyond && (GEN ? (!ok && s >= width) : s >= 64u))) why |= LC_BATCH_E_FIT;
         if (why) break;
-        uint64_t todo = __ballot(in), npend = pend;
+        uint64_t todo = __ballot(in && !beyond), npend[2] = {pend[0], pend[1]};
         while (todo) {
             const uint32_t sl = __builtin_amdgcn_readlane(s, (uint32_t)__builtin_ctzll(todo));
             const uint64_t ms = __ballot(in && s == sl);
-            const uint32_t b0 = (uint32_t)(pend >> sl) & 1u;
+            const uint32_t hi = GEN ? sl >> 6 : 0u, bit = sl & 63u;
+            const uint32_t b0 = (uint32_t)(pend[hi] >> bit) & 1u;
             const uint32_t r = rank_of(ms);
             if (__any(in && s == sl && ok != (((r + b0) & 1u) != 0))) why |= LC_BATCH_E_SLOTS;
-            if (((uint32_t)__popcll(ms) + b0) & 1u) npend |= 1ull << sl;
-            else npend &= ~(1ull << sl);
+            if (((uint32_t)__popcll(ms) + b0) & 1u) npend[hi] |= 1ull << bit;
+            else npend[hi] &= ~(1ull << bit);
             todo &= ~ms;
         }
-        pend = npend;
+        pend[0] = npend[0];
+        pend[1] = npend[1];
     }
     if (why && lane == 0) {
         atomicOr(&a.err[0], why);
@@ -1095,8 +1104,9 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     }
 }
 
+template <bool GEN>
 __global__ __launch_bounds__(64) void k_validate(T0Args a) {
-    for (int64_t k = blockIdx.x; k < a.n_order; k += gridDim.x) validate_key(a, k);
+    for (int64_t k = blockIdx.x; k < a.n_order; k += gridDim.x) validate_key<GEN>(a, k);
 }
 
 template <int RM>
@@ -1181,13 +1191,14 @@ hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_validate(const Args &a, hipStream_t s) {
+hipError_t launch_validate(const Args &a, hipStream_t s, bool general) {
     T0Args t{};
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
-    t.key_states = a.key_states; t.key_error = a.key_error; t.err = a.err;
+    t.key_states = a.key_states; t.key_error = a.key_error; t.err = a.err; t.key_width = a.key_width;
     t.n_order = a.n_order; t.shared_states = a.shared_states; t.n_trans = a.n_trans;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_order, 2048));
-    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64), 0, s, t);
+    if (general) hipLaunchKernelGGL(k_validate<true>, dim3(grid), dim3(64), 0, s, t);
+    else hipLaunchKernelGGL(k_validate<false>, dim3(grid), dim3(64), 0, s, t);
     return hipGetLastError();
 }
 
@@ -1958,7 +1969,7 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
         // T0_STRICT steps: the event-by-event validation, in blocks after the
         // keys' (no second stream, no cross-stream waits around the step)
         const int64_t nb = (int64_t)gridDim.x - a.n_order;
-        for (int64_t k = ((int64_t)blockIdx.x - a.n_order) * S + wv; k < a.n_order; k += nb * S) validate_key(a, k);
+        for (int64_t k = ((int64_t)blockIdx.x - a.n_order) * S + wv; k < a.n_order; k += nb * S) validate_key<false>(a, k);
         return;  // the whole block: no barrier below is reached by half of it
     }
     const int32_t key = a.order[blockIdx.x];

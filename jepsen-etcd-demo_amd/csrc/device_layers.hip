@@ -744,7 +744,7 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
 __global__ __launch_bounds__(LWG) void k_search_layers(Args a, LayWs w) {
     __shared__ LayShared sh;
     const int32_t n = a.n_in ? min(*a.n_in, a.list_cap) : a.n_order;
-    if (n == 0) return;  // empty work list
+    if (n == 0 || batch_refused(a)) return;  // empty work list / malformed batch
     clear_slots(sh.tab, TS);
     for (;;) {
         if (threadIdx.x == 0) sh.work = atomicAdd(a.ticket, 1);

@@ -236,7 +236,7 @@ template <int CAP_S, int CAP_I>
 __global__ __launch_bounds__(64) void k_search_lds(Args a) {
     __shared__ LdsTier<CAP_S, CAP_I> t;
     const int32_t n = a.n_in ? min(*a.n_in, a.list_cap) : a.n_order;
-    if (n == 0) return;  // empty work list: no ticket traffic
+    if (n == 0 || batch_refused(a)) return;  // empty work list / malformed batch: no ticket traffic
     for (int32_t w = next_work(a); w < n; w = next_work(a)) {
         const int32_t key = a.order[w];
         const int r = search_key_lds<CAP_S, CAP_I>(a, key, t);

@@ -81,9 +81,11 @@ size_t lds_bytes_t1();
 size_t lds_bytes_t2();
 hipError_t launch_t0(const Args &a, const Args *a_dev, int grid, bool wide, hipStream_t s, uint32_t ticket_base);
 size_t lat_ws_words();
-// T0_STRICT steps: the batch's event-by-event validation (err words), a
-// kernel of its own for a second stream
-hipError_t launch_validate(const Args &a, hipStream_t s);
+// The batch's event-by-event validation (err words), a kernel of its own for
+// a second stream: T0_STRICT steps (general = false: a register-tier batch),
+// or any batch the host did not walk (general = true: every width; the later
+// tiers read the err words first and do nothing over a malformed batch)
+hipError_t launch_validate(const Args &a, hipStream_t s, bool general);
 
 // Key segments (device_lattice.hip, "Key segments"): a register-tier step
 // whose keys are cut at quiescent points and searched as independent

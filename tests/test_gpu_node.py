@@ -286,3 +286,44 @@ def test_node_chunked_upload_pipeline(forced, monkeypatch):
     np.testing.assert_array_equal(v, orc["valid"])
     np.testing.assert_array_equal(fe, orc["fail_event"])
     assert (v == 0).any()
+
+
+def test_device_validates_batches_beyond_the_register_tier():
+    """A batch whose keys leave the register tier (crashed ops: 12-20 ops
+    pending, the LDS and HBM set tiers run) is validated on the device too
+    (k_validate<true> beside T0; the set tiers do nothing over a refused
+    batch): each malformation is refused naming its key, on the host-to-host
+    and the resident path, and the context then checks the good batch
+    bit-exactly."""
+    h = H.synth(n_keys=48, ops_per_key=400, concurrency=14, info_rate=0.01, anomaly_rate=0.2, seed=78)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0)
+    arrs, b = _batch_copy(pk)
+    assert (arrs["width"] > 10).any()  # not a register-tier batch
+    ev = arrs["events"]
+    good = _check_batch(dev, b, K)
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    np.testing.assert_array_equal(good["valid"][:K], orc["valid"])
+    np.testing.assert_array_equal(good["fail_event"][:K], orc["fail_event"])
+
+    def at(key, pred):
+        lo, hi = int(pk.ev_off[key]), int(pk.ev_off[key + 1])
+        return lo + int(np.flatnonzero(pred(ev[lo:hi]))[0])
+
+    wide_key = int(np.flatnonzero(arrs["width"] > 10)[0])
+    cases = [
+        (11, at(11, lambda e: np.ones(len(e), bool)), lambda w: w | N.LC_EV_OK_BIT),        # :ok of no pending op
+        (23, at(23, lambda e: (e & N.LC_EV_OK_BIT) != 0), lambda w: (w & 0x7F000000)),       # :invoke into a held slot
+        (37, at(37, lambda e: (e & N.LC_EV_OK_BIT) == 0), lambda w: (w & 0xFF000000) | 0xFFFFF),  # transition id
+        (wide_key, at(wide_key, lambda e: (e & N.LC_EV_OK_BIT) == 0),                          # slot past key_width
+         lambda w: (w & 0x80FFFFFF) | (100 << 24)),
+    ]
+    for key, j, mutate in cases:
+        saved = int(ev[j])
+        ev[j] = mutate(saved)
+        _expect_invalid(dev, b, K, key)
+        ev[j] = saved
+        again = _check_batch(dev, b, K)
+        np.testing.assert_array_equal(again["valid"][:K], good["valid"][:K])
+        np.testing.assert_array_equal(again["fail_event"][:K], good["fail_event"][:K])
