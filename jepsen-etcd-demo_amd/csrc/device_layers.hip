@@ -331,6 +331,15 @@ struct Part {
     bool multi;
     __device__ bool mine(uint32_t h) const { return !multi || (h >> shift) == part; }
 };
+// The fused step's sizing (A/B: make variant VFLAGS="-DLC_T3L_EST=n -DLC_T3L_FILL=m"):
+// I_{k+1} is estimated as |S_{k+1}| + EST x |I_k| + 64 entries, and a layer
+// takes the fused step while both estimates fit FILL/8 of a half table.
+#ifndef LC_T3L_EST
+#define LC_T3L_EST 2u  // C4 at 2^16: 15.62 ms against 15.78 (3) and 16.23 (1)
+#endif
+#ifndef LC_T3L_FILL
+#define LC_T3L_FILL 6u
+#endif
 #ifndef LC_T3L_UP
 #define LC_T3L_UP 2
 #endif
@@ -637,8 +646,8 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
                 if (tid == 0 && want_s) sn[k] = sh.n_sn;
                 // fused step: both tables in their LDS halves when the sizes allow
                 const uint32_t bound_s = nk + (se - sb);
-                const uint32_t est_i = (se - sb) + 3u * nk + 64u;
-                const bool fast = bound_s <= (TSH * 3u) / 4u && est_i <= (TSH * 3u) / 4u;
+                const uint32_t est_i = (se - sb) + LC_T3L_EST * nk + 64u;
+                const bool fast = bound_s <= (TSH * LC_T3L_FILL) / 8u && est_i <= (TSH * LC_T3L_FILL) / 8u;
                 bool done = false;
                 uint32_t n_next = 0;
                 uint64_t *inext = nullptr;
