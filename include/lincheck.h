@@ -486,6 +486,18 @@ int  lc_edn_read(const char *path, lc_hist **out);
 int  lc_edn_parse(const char *text, int64_t len, lc_hist **out);
 int  lc_edn_write(const char *path, const lc_history *h);
 
+/* ---- test.fressian (Jepsen store format, binary) ---------------------------- */
+/* Read the history out of a Fressian-encoded Jepsen test map (its :history
+ * entry) or a Fressian list of op maps, with the op rules of lc_edn_read.
+ * The decoder covers the whole Fressian encoding (caches, struct types,
+ * chunked strings, open lists); tagged values of unknown handlers are kept
+ * as their fields.  lc_fressian_write emits {:name "lincheck" :history [...]}.
+ * Replaces the :history of jepsen.store's test.fressian load (SURVEY.md 8(f)
+ * F-1); parity unpinned, no stored run or Fressian library to check against. */
+int  lc_fressian_read(const char *path, lc_hist **out);
+int  lc_fressian_parse(const uint8_t *buf, int64_t len, lc_hist **out);
+int  lc_fressian_write(const char *path, const lc_history *h);
+
 #ifdef __cplusplus
 }
 #endif

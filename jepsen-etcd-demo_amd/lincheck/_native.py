@@ -130,6 +130,9 @@ SIGNATURES = {
     "lc_edn_read": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
     "lc_edn_parse": (C.c_int, [C.c_char_p, C.c_int64, P(C.c_void_p)]),
     "lc_edn_write": (C.c_int, [C.c_char_p, P(LcHistory)]),
+    "lc_fressian_read": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
+    "lc_fressian_parse": (C.c_int, [C.c_char_p, C.c_int64, P(C.c_void_p)]),
+    "lc_fressian_write": (C.c_int, [C.c_char_p, P(LcHistory)]),
 }
 
 _lib: Optional[C.CDLL] = None

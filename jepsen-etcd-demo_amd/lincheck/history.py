@@ -248,3 +248,20 @@ def parse_edn(text: str) -> History:
 
 def write_edn(path: str, h: History) -> None:
     N.check(N.lib().lc_edn_write(path.encode(), C.byref(h.as_c())))
+
+
+def read_fressian(path: str) -> History:
+    """The :history of a Jepsen test.fressian (or a Fressian list of op maps)."""
+    handle = C.c_void_p()
+    N.check(N.lib().lc_fressian_read(path.encode(), C.byref(handle)))
+    return History._from_owned(handle)
+
+
+def parse_fressian(data: bytes) -> History:
+    handle = C.c_void_p()
+    N.check(N.lib().lc_fressian_parse(data, len(data), C.byref(handle)))
+    return History._from_owned(handle)
+
+
+def write_fressian(path: str, h: History) -> None:
+    N.check(N.lib().lc_fressian_write(path.encode(), C.byref(h.as_c())))

@@ -94,17 +94,21 @@ def test_other_algorithms_on_device(algo):
                 assert g["previous-ok"]["index"] == r["previous-ok"]["index"], (name, k)
 
 
+@pytest.mark.parametrize("fmt", ["edn", "fressian"])
 @pytest.mark.parametrize("anomaly_rate", [0.0, 0.5])
-def test_c1_history_edn_on_device(tmp_path, anomaly_rate):
+def test_c1_history_edn_on_device(tmp_path, anomaly_rate, fmt):
     """C1: the demo's shape (6 keys x 100 ops, 10 clients, nemesis :info ops
     every 5 time units, one time-ordered history of tuples) written as
     history.edn, read back by lc_edn_read and checked on the device.  The
-    stored run is absent, so the file is synthetic."""
+    stored run is absent, so the file is synthetic.
+    fmt "fressian": the same run as a test.fressian (lc_fressian_write /
+    lc_fressian_read) instead."""
     src = H.synth(n_keys=6, ops_per_key=100, concurrency=10, interleave=True, nemesis_period=5.0,
                   anomaly_rate=anomaly_rate, seed=1)
-    path = str(tmp_path / "history.edn")
-    H.write_edn(path, src)
-    h = H.read_edn(path)
+    path = str(tmp_path / ("history.edn" if fmt == "edn" else "test.fressian"))
+    write, read = (H.write_edn, H.read_edn) if fmt == "edn" else (H.write_fressian, H.read_fressian)
+    write(path, src)
+    h = read(path)
     for col in ("type", "f", "process", "key", "v0", "v1", "index"):
         np.testing.assert_array_equal(getattr(h, col), getattr(src, col), err_msg=col)
     assert (h.key == -(1 << 63)).sum() > 0  # the nemesis ops are in the file
@@ -118,7 +122,7 @@ def test_c1_history_edn_on_device(tmp_path, anomaly_rate):
     # the same file through the demo's checker expression
     lin = ck.linearizable({"model": model.cas_register(), "algorithm": "linear"})
     out = independent.checker(ck.compose({"linear": lin, "timeline": ck.unbridled_optimism()})).check(
-        {}, H.read_edn(path), {})
+        {}, read(path), {})
     fails = sorted(int(k) for k, r in zip(keys, orc) if r["valid"] == 0)
     assert sorted(out["failures"]) == fails
     assert out["valid?"] == (not fails)

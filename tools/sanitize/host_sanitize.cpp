@@ -1,10 +1,11 @@
 // Host-code sanitizer driver ("Race detection /
-// sanitizers"): the host half of liblincheck (history.edn reader/writer,
-// lc_pack, lc_report, the synthetic generator) and the C oracle, built with
-// -fsanitize=address,undefined (make asan) or -fsanitize=thread (make tsan)
-// and driven over generated histories, round trips through history.edn, the
-// parallel EDN split (files above 1 MB), malformed EDN text and malformed
-// op sequences.  Exit status 0 = every check passed and no sanitizer fired.
+// sanitizers"): the host half of liblincheck (history.edn and test.fressian
+// readers/writers, lc_pack, lc_report, the synthetic generator) and the C
+// oracle, built with -fsanitize=address,undefined (make asan) or
+// -fsanitize=thread (make tsan) and driven over generated histories, round
+// trips through history.edn and test.fressian, the parallel EDN split (files
+// above 1 MB), mangled EDN text and Fressian bytes, and malformed op
+// sequences.  Exit status 0 = every check passed and no sanitizer fired.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -145,6 +146,32 @@ int main(int argc, char **argv) {
                 lc_history xv;
                 lc_hist_view(x, &xv);
                 exercise(xv, LC_MODEL_CAS_REGISTER);  // may hold malformed op sequences: errors, not faults
+                lc_hist_free(x);
+            }
+        }
+        // the same history through test.fressian, then its bytes mangled
+        const std::string ftmp = std::string(tmp) + ".fressian";
+        CHECK(lc_fressian_write(ftmp.c_str(), &v) == LC_OK);
+        r = nullptr;
+        CHECK(lc_fressian_read(ftmp.c_str(), &r) == LC_OK);
+        if (r) {
+            lc_history rv;
+            CHECK(lc_hist_view(r, &rv) == LC_OK);
+            CHECK(rv.n == v.n);
+            for (int64_t i = 0; i < v.n && i < rv.n; ++i)
+                CHECK(rv.type[i] == v.type[i] && rv.key[i] == v.key[i] && rv.v0[i] == v.v0[i] &&
+                      rv.v1[i] == v.v1[i] && rv.process[i] == v.process[i] && rv.index[i] == v.index[i]);
+            lc_hist_free(r);
+        }
+        const std::string bin = slurp(ftmp.c_str());
+        for (int t = 0; t < 40 && !bin.empty(); ++t) {
+            std::string m = bin.substr(0, (size_t)(rng() % bin.size()));
+            for (int k = 0; k < 8 && !m.empty(); ++k) m[(size_t)(rng() % m.size())] = (char)(rng() & 0xFF);
+            lc_hist *x = nullptr;
+            if (lc_fressian_parse((const uint8_t *)m.data(), (int64_t)m.size(), &x) == LC_OK && x) {
+                lc_history xv;
+                lc_hist_view(x, &xv);
+                exercise(xv, LC_MODEL_CAS_REGISTER);
                 lc_hist_free(x);
             }
         }
