@@ -5,7 +5,12 @@ lc_check_node call per rank -- this rank's shard of packed struct-of-arrays
 in host memory (lc_pack's output, page-locked on a GPU host) -> validation
 -> H2D -> device search -> verdict records -> all-gather of every rank's
 records over RCCL (one rank: none) -> the node's records in host memory.
-`resident_ops_per_s` is the same search on a shard already in HBM, steps only
+The timed steps are lc_check_node_async calls: two steps in flight, each
+step's upload overlapping the search of the one before, every step still
+moving its shard's events host -> device and its records device -> host.
+`d1_sync` is the synchronous lc_check_node rate (one step at a time), run
+after them; the roofline's launch times come from those synchronous steps.
+`resident` is the same search on a shard already in HBM, steps only
 enqueued (the exchange still runs per step, on the library's stream).
 
 Workloads (BASELINE.json configs; synthetic, liblincheck's seeded generator):
@@ -67,6 +72,8 @@ def parse():
     ap.add_argument("--budget", type=int, default=1 << 20)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-resident", action="store_true", help="skip the resident-shard steps")
+    ap.add_argument("--d1-sync", action="store_true",
+                    help="time the synchronous lc_check_node step instead of the pipelined one")
     ap.add_argument("--no-probes", action="store_true", help="skip the probe-counting pass")
     ap.add_argument("--keys", type=int, default=0, help="override keys (exploration only)")
     ap.add_argument("--ops", type=int, default=0, help="override ops per key (exploration only)")
@@ -226,7 +233,7 @@ def main():
 
     from lincheck import history as H
     from lincheck import parallel as P
-    from lincheck.checker import Device, Packed, comm_id
+    from lincheck.checker import Device, Packed, PinnedRecords, comm_id
 
     cfg = dict(CONFIGS[args.config])
     if args.keys or args.ops:
@@ -272,31 +279,62 @@ def main():
         dist.all_gather_object(parts, rec.copy())
         return np.concatenate(parts)
 
-    # ---- D-1: host SoA -> node verdict records, one synchronous call per step
-    d1_t0 = []
+    # ---- D-1: host SoA -> node verdict records.  The timed steps are the
+    # pipelined call (lc_check_node_async: each step's upload overlaps the
+    # search of the step before, records land in page-locked memory); the
+    # synchronous call (lc_check_node, one step at a time) runs after them
+    # for its own rate and for the per-launch kernel times of the roofline.
+    d1_t0, d1_t3, d1_t3b = [], [], []
+    pipelined = not args.d1_sync
+    node_pin = PinnedRecords(n_node) if pipelined else None
 
-    def d1_step():
-        rec, st = dev.check_node(packed, block, out=node_buf)
+    def record(st):
         d1_t0.append(st.tier0_ms if st.tier0_ms > 0 else st.kernel_ms)
         if st.tier3_ms > 0:
             d1_t3.append(st.tier3_ms)
             d1_t3b.append(st.t3_bytes)
+
+    def d1_step():
+        rec, st = dev.check_node(packed, block, out=node_buf)
+        record(st)
         return rec
 
-    d1_t3, d1_t3b = [], []
-    for _ in range(args.warmup):
-        d1_step()
-    del d1_t0[:], d1_t3[:], d1_t3b[:]
-    sync(); barrier(); sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rec = d1_step()
-    sync(); barrier(); sync()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    n_enq = [0]
+
+    def d1_pipe_step():
+        enq, st = dev.check_node_async(packed, block, node_pin)
+        if enq:
+            n_enq[0] += 1
+        else:
+            record(st)
+        return node_pin[:n_node]
+
+    def timed(step):
+        for _ in range(args.warmup):
+            step()
+        sync(); barrier(); sync()
+        del d1_t0[:], d1_t3[:], d1_t3b[:]
+        n_enq[0] = 0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rec = step()
+        sync(); barrier(); sync()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, np.array(rec, copy=True)
+
+    d1_sync = None
+    if pipelined:
+        elapsed, rec = timed(d1_pipe_step)
+        n_pipe = n_enq[0]
+        el_s, rec_s = timed(d1_step)
+        d1_sync = {"ms_per_step": el_s / args.steps * 1e3, "elapsed_s": el_s,
+                   "pipelined_steps": n_pipe, "same_records": bool(np.array_equal(rec, rec_s))}
+    else:
+        elapsed, rec = timed(d1_step)
     node = node_records(rec.copy())
 
     # ---- resident shard: steps only enqueued, exchange on the library stream
@@ -353,6 +391,8 @@ def main():
         ops_total = (cfg["keys"] if strong else K * world) * ops
         ops_checked = decided * ops
         value = ops_checked * args.steps / elapsed
+        if d1_sync is not None:
+            d1_sync["ops_per_s"] = ops_checked * args.steps / d1_sync["elapsed_s"]
         avg_t0 = float(np.mean(d1_t0)) if d1_t0 else 0.0
         avg_t3 = float(np.mean(d1_t3)) if d1_t3 else 0.0
         n_events = int(packed.ev_off[-1])
@@ -409,7 +449,9 @@ def main():
                        "concurrency": cfg["concurrency"], "budget": args.budget,
                        "parallelism": f"keys sharded over {world} GPU(s), records all-gathered "
                                       f"({'host/gloo rehearsal' if host_gather else 'RCCL' if world > 1 else 'one rank'})"},
-            "step": "lc_check_node: packed host SoA -> H2D -> search -> verdict records -> all-gather -> host",
+            "step": ("lc_check_node_async (two steps in flight)" if pipelined else "lc_check_node") +
+                    ": packed host SoA -> H2D -> search -> verdict records -> all-gather -> host",
+            "d1_sync": d1_sync,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": kt,

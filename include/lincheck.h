@@ -442,6 +442,17 @@ int  lc_comm_id(uint8_t *out);
  * node's block * comm_size records to `node` (host).  One rank: node = the
  * shard's block. */
 int  lc_check_node(lc_ctx *ctx, const lc_batch *shard, int64_t block, uint64_t *node, lc_stats *s);
+/* Pipelined lc_check_node.  A step that is the register tier alone
+ * (every key fits it, no probe counting, node page-locked: lc_host_alloc,
+ * shard below lc_check_node's chunked size) is only enqueued and returns 1:
+ * its upload overlaps the search of the step before it (two steps in flight)
+ * and its records are in `node` once lc_wait (or lc_wait_step over it)
+ * returns; errors surface there.  The shard's arrays and `node` must stay
+ * untouched until then.  Any other step runs as lc_check_node (returns 0). */
+int  lc_check_node_async(lc_ctx *ctx, const lc_batch *shard, int64_t block, uint64_t *node, lc_stats *s);
+/* Page-locked host memory (for lc_check_node_async's records). */
+void *lc_host_alloc(size_t bytes);
+void  lc_host_free(void *p);
 /* The same from a resident shard (lc_upload), records left in HBM until
  * lc_node_records; flags LC_DEV_ASYNC: a step that is the register tier
  * alone is only enqueued (lc_wait ends the run). */

@@ -339,6 +339,13 @@ struct Dev {
     uint64_t *rec_out = nullptr;  // set around a node step's search: finish_key writes the records there
     uint64_t *hnode = nullptr;  // pinned landing area of the node's records (lc_check_node)
     int64_t hnode_cap = 0;
+    // lc_check_node_async: two staging batches used in turn, so a step's
+    // upload (on cstream) runs while the step before it searches; pipe_ready
+    // = a slot's upload is done, pipe_free = the step that read it is done
+    static constexpr int PIPE = 2;
+    DevBatch *pipe[PIPE] = {};
+    hipEvent_t pipe_ready[PIPE] = {}, pipe_free[PIPE] = {};
+    uint64_t pipe_next = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
     struct Ws {
         char *base = nullptr;
@@ -367,6 +374,11 @@ struct Dev {
         for (hipEvent_t &e : args_ev)
             if (e) (void)hipEventDestroy(e);
         delete staged;
+        for (int i = 0; i < PIPE; ++i) {
+            delete pipe[i];
+            for (hipEvent_t e : {pipe_ready[i], pipe_free[i]})
+                if (e) (void)hipEventDestroy(e);
+        }
         for (int i = 0; i < NODE_CHUNKS; ++i) {
             delete chunk[i];
             if (chunk_ready[i]) (void)hipEventDestroy(chunk_ready[i]);
@@ -1696,6 +1708,96 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
     }
     if (st) st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return LC_OK;
+}
+
+// The pipelined form of lc_check_node.  A register-tier step (every key fits
+// the register lattice, no probe counting, one upload, records to page-locked
+// memory) is only enqueued: its upload goes into the staging slot the step
+// two back used (once that step is done) on the copy stream, its search waits
+// for that upload on the search stream, and the records are downloaded into
+// `node` behind the search.  So step i + 1's host-to-device copy overlaps step
+// i's search, and the host enqueues ahead instead of waiting between steps.
+// Anything else runs as lc_check_node.
+extern "C" int lc_check_node_async(lc_ctx *c, const lc_batch *b, int64_t block, uint64_t *node, lc_stats *st) {
+    if (!c || !b || !node) return lc::fail(LC_E_INVALID, "lc_check_node_async: null argument");
+    Dev *d = nullptr;
+    Shape sh;
+    const uint32_t *src = nullptr;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        int rc = node_check_args(c, b->n_keys, block);
+        if (rc) return rc;
+        d = c->dev[0];
+        HIPCHK(hipSetDevice(d->device));
+        const int64_t K = b->n_keys;
+        const uint64_t n_ev = K ? b->ev_off[K] : 0;
+        const bool big = K >= 16 * (int64_t)d->cu_count && n_ev >= (8u << 20);  // lc_check_node's chunked regime
+        if (K > 0 && !b->table && !big && !(c->o.flags & LC_OPT_COUNT_PROBES) && pinned(node) &&
+            !std::getenv("LC_NODE_SYNC")) {
+            rc = prepare_batch(c, b, &sh, &src);
+            if (rc) return rc;
+            if (sh.t0_only) {
+                const int s = (int)(d->pipe_next % Dev::PIPE);
+                if (!d->pipe[s]) {
+                    d->pipe[s] = new (std::nothrow) DevBatch();
+                    if (!d->pipe[s]) return lc::fail(LC_E_NOMEM, "lc_check_node_async: out of memory");
+                    HIPCHK(hipEventCreateWithFlags(&d->pipe_ready[s], hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&d->pipe_free[s], hipEventDisableTiming));
+                    HIPCHK(hipEventRecord(d->pipe_free[s], d->stream));
+                }
+                // the step that last read this slot has finished (at most one
+                // other step stays in flight), so its buffers may be rewritten
+                // or regrown
+                HIPCHK(hipEventSynchronize(d->pipe_free[s]));
+                rc = node_buffers(c, d, K, block);
+                if (rc) return rc;
+                struct RecOff {
+                    Dev *d;
+                    ~RecOff() { d->rec_out = nullptr; }
+                } rec_off{d};
+                auto drained = [&](int e) {
+                    (void)hipStreamSynchronize(d->cstream);
+                    (void)hipStreamSynchronize(d->stream);
+                    return e;
+                };
+                rc = upload_into(d, b, d->pipe[s], sh, sh.host_checked, src, false, d->cstream);
+                if (rc) return drained(rc);
+                HIPCHK(hipEventRecord(d->pipe_ready[s], d->cstream));
+                // pageable events went through the context's one staging copy,
+                // which the next call rewrites: their upload finishes here
+                if (src && src != b->events) HIPCHK(hipEventSynchronize(d->pipe_ready[s]));
+                HIPCHK(hipStreamWaitEvent(d->stream, d->pipe_ready[s], 0));
+                lc_result none{};
+                bool enq = false;
+                rc = dev_search(d, d->pipe[s], &none, RES_CTX, true, 0, st, &enq);
+                if (rc) return drained(rc);
+                rc = gather_node(c, d, K, block, true);
+                if (rc) return drained(rc);
+                if (d->node_n && hipMemcpyAsync(node, d->node, (size_t)d->node_n * 8, hipMemcpyDeviceToHost,
+                                                d->stream) != hipSuccess)
+                    return drained(lc::fail(LC_E_DEVICE, "lc_check_node_async: record download failed"));
+                HIPCHK(hipEventRecord(d->pipe_free[s], d->stream));
+                ++d->pipe_next;
+                if (enq) return 1;
+                HIPCHK(hipStreamSynchronize(d->stream));  // not reached for a register-tier batch
+                return LC_OK;
+            }
+        }
+    }
+    return lc_check_node(c, b, block, node, st);
+}
+
+extern "C" void *lc_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+        lc::set_error("lc_host_alloc: page-locked allocation failed");
+        return nullptr;
+    }
+    return p;
+}
+
+extern "C" void lc_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
 }
 
 extern "C" int lc_check_node_device(lc_ctx *c, const lc_dev_batch *db, int64_t block, int flags, lc_stats *st) {

@@ -110,6 +110,9 @@ SIGNATURES = {
     "lc_comm_id": (C.c_int, [P(C.c_uint8)]),
     "lc_check_node": (C.c_int, [C.c_void_p, P(LcBatch), C.c_int64, P(C.c_uint64), P(LcStats)]),
     "lc_check_node_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, P(LcStats)]),
+    "lc_check_node_async": (C.c_int, [C.c_void_p, P(LcBatch), C.c_int64, P(C.c_uint64), P(LcStats)]),
+    "lc_host_alloc": (C.c_void_p, [C.c_size_t]),
+    "lc_host_free": (None, [C.c_void_p]),
     "lc_node_records": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int64]),
     "lc_pack": (C.c_int, [P(LcHistory), P(LcPackOpts), P(C.c_void_p)]),
     "lc_packed_free": (None, [C.c_void_p]),

@@ -132,6 +132,35 @@ def comm_id() -> bytes:
     return bytes(buf)
 
 
+class PinnedRecords(np.ndarray):
+    """A uint64 array in page-locked memory (lc_host_alloc), freed with it."""
+
+    def __new__(cls, n: int):
+        n = max(int(n), 1)
+        p = N.lib().lc_host_alloc(n * 8)
+        if not p:
+            raise N.LincheckError(-2, N.lib().lc_last_error().decode(errors="replace"))
+        buf = (C.c_uint64 * n).from_address(p)
+        obj = np.frombuffer(buf, np.uint64).view(cls)
+        obj[:] = 0
+        obj._owner = _HostBlock(p)
+        return obj
+
+    def __array_finalize__(self, obj):
+        if obj is not None:
+            self._owner = getattr(obj, "_owner", None)
+
+
+class _HostBlock:
+    def __init__(self, p):
+        self.p = p
+
+    def __del__(self):
+        if self.p:
+            N.lib().lc_host_free(self.p)
+            self.p = None
+
+
 class Device:
     """An lc_ctx (lc_create) on one GPU, on several (devices=[...]: one
     contiguous key shard per entry, checked at once), or as one rank of a
@@ -202,6 +231,20 @@ class Device:
         st = N.LcStats()
         N.check(N.lib().lc_check_node(self.handle, C.byref(packed.view), block, N.ptr(out, C.c_uint64), C.byref(st)))
         return out[:n], st
+
+    def check_node_async(self, packed: Packed, block: int, out: np.ndarray):
+        """lc_check_node_async: the pipelined step.  `out` must be page-locked
+        (pinned_records) and, like `packed`, left untouched until wait();
+        returns (enqueued, stats): enqueued True when the step was only
+        enqueued (records valid after wait; stats zero), False when it ran as
+        check_node."""
+        n = block * self.world
+        if out.size < n or out.dtype != np.uint64:
+            raise ValueError(f"records buffer of {out.size} < {n}")
+        st = N.LcStats()
+        rc = N.check(N.lib().lc_check_node_async(self.handle, C.byref(packed.view), block,
+                                                 N.ptr(out, C.c_uint64), C.byref(st)))
+        return rc == 1, st
 
     def node_records(self, n: int) -> np.ndarray:
         """lc_node_records: the first n records of the last gather."""

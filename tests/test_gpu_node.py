@@ -327,3 +327,50 @@ def test_device_validates_batches_beyond_the_register_tier():
         again = _check_batch(dev, b, K)
         np.testing.assert_array_equal(again["valid"][:K], good["valid"][:K])
         np.testing.assert_array_equal(again["fail_event"][:K], good["fail_event"][:K])
+
+
+def test_pipelined_node_steps_bit_exact():
+    """lc_check_node_async: batches of different sizes in flight two at a
+    time (each step's upload overlapping the previous search, the staging
+    slots used in turn), every step's records in its own page-locked buffer;
+    after the wait each equals lc_check_node's.  A batch beyond the register
+    tier runs synchronously, and a pageable caller batch goes through the
+    staging copy."""
+    from lincheck.checker import PinnedRecords
+    shapes = [dict(n_keys=300, ops_per_key=400, concurrency=10, anomaly_rate=0.1, seed=81),
+              dict(n_keys=120, ops_per_key=900, concurrency=8, anomaly_rate=0.2, seed=82),
+              dict(n_keys=1000, ops_per_key=200, concurrency=10, seed=83)]
+    pks = [Packed(H.synth(**s)) for s in shapes]
+    dev = Device(0)
+    refs = [dev.check_node(pk, pk.n_keys + 3)[0].copy() for pk in pks]
+    seq = [0, 1, 2, 0, 2, 1, 1, 0, 2, 2, 0, 1]
+    bufs = [PinnedRecords(pks[i].n_keys + 3) for i in seq]
+    enq = [dev.check_node_async(pks[i], pks[i].n_keys + 3, buf)[0] for i, buf in zip(seq, bufs)]
+    assert all(enq)
+    n, _ = dev.wait()
+    assert n == len(seq)
+    for i, buf in zip(seq, bufs):
+        np.testing.assert_array_equal(np.asarray(buf), refs[i])
+    # beyond the register tier: runs as lc_check_node
+    pk = Packed(H.synth(**SHAPES["crashed"]))
+    buf = PinnedRecords(pk.n_keys)
+    e, _ = dev.check_node_async(pk, pk.n_keys, buf)
+    assert not e
+    np.testing.assert_array_equal(np.asarray(buf), dev.check_node(pk, pk.n_keys)[0])
+    # a pageable caller batch (staged), then an error surfacing at the wait
+    h = H.synth(n_keys=300, ops_per_key=200, concurrency=6, seed=84)
+    pk = Packed(h)
+    arrs, b = _batch_copy(pk)
+    ref = dev.check_node(pk, pk.n_keys)[0].copy()
+    outs = [PinnedRecords(pk.n_keys) for _ in range(3)]
+    for o in outs:
+        N.check(N.lib().lc_check_node_async(dev.handle, C.byref(b), pk.n_keys, N.ptr(o, C.c_uint64), None))
+    dev.wait()
+    for o in outs:
+        np.testing.assert_array_equal(np.asarray(o), ref)
+    arrs["events"][int(pk.ev_off[42])] |= N.LC_EV_OK_BIT
+    N.check(N.lib().lc_check_node_async(dev.handle, C.byref(b), pk.n_keys, N.ptr(outs[0], C.c_uint64), None))
+    with pytest.raises(N.LincheckError) as ei:
+        dev.wait()
+    assert "key 42" in str(ei.value)
+    device_vs_oracle(h, dev)
