@@ -443,8 +443,8 @@ int  lc_comm_id(uint8_t *out);
  * shard's block. */
 int  lc_check_node(lc_ctx *ctx, const lc_batch *shard, int64_t block, uint64_t *node, lc_stats *s);
 /* Pipelined lc_check_node.  A step that is the register tier alone
- * (every key fits it, no probe counting, node page-locked: lc_host_alloc,
- * shard below lc_check_node's chunked size) is only enqueued and returns 1:
+ * (every key fits it, no probe counting, node page-locked: lc_host_alloc)
+ * is only enqueued and returns 1:
  * its upload overlaps the search of the step before it (two steps in flight)
  * and its records are in `node` once lc_wait (or lc_wait_step over it)
  * returns; errors surface there.  The shard's arrays and `node` must stay

@@ -1731,8 +1731,9 @@ extern "C" int lc_check_node_async(lc_ctx *c, const lc_batch *b, int64_t block, 
         HIPCHK(hipSetDevice(d->device));
         const int64_t K = b->n_keys;
         const uint64_t n_ev = K ? b->ev_off[K] : 0;
-        const bool big = K >= 16 * (int64_t)d->cu_count && n_ev >= (8u << 20);  // lc_check_node's chunked regime
-        if (K > 0 && !b->table && !big && !(c->o.flags & LC_OPT_COUNT_PROBES) && pinned(node) &&
+        // (a large shard is not cut into chunks here: its whole upload
+        // overlaps the previous step's search instead)
+        if (K > 0 && n_ev > 0 && !b->table && !(c->o.flags & LC_OPT_COUNT_PROBES) && pinned(node) &&
             !std::getenv("LC_NODE_SYNC")) {
             rc = prepare_batch(c, b, &sh, &src);
             if (rc) return rc;
