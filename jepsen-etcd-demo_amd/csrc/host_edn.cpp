@@ -81,6 +81,8 @@ struct Parser {
     }
     // Metadata (^m) and discards (#_ x) in front of a value.
     bool prefixes() {
+        ws();
+        if (p < end && *p != '^' && *p != '#') return true;  // the common case
         for (;;) {
             ws();
             if (p >= end) return fail("unexpected end of input");
@@ -208,7 +210,17 @@ struct RawOp {
     Top value;
 };
 
-bool kw_is(std::string_view a, const char *b) { return a == b; }
+// The op-map keys read, by length and spelling (one compare per key).
+enum Field { FLD_OTHER, FLD_TYPE, FLD_F, FLD_PROCESS, FLD_INDEX, FLD_VALUE };
+inline Field field_of(std::string_view k) {
+    switch (k.size()) {
+        case 1: return k[0] == 'f' ? FLD_F : FLD_OTHER;
+        case 4: return k == std::string_view("type", 4) ? FLD_TYPE : FLD_OTHER;
+        case 5: return k == std::string_view("value", 5) ? FLD_VALUE : k == std::string_view("index", 5) ? FLD_INDEX : FLD_OTHER;
+        case 7: return k == std::string_view("process", 7) ? FLD_PROCESS : FLD_OTHER;
+        default: return FLD_OTHER;
+    }
+}
 
 bool read_op(Parser &ps, RawOp &op) {
     ++ps.p;  // at '{'
@@ -223,11 +235,12 @@ bool read_op(Parser &ps, RawOp &op) {
             if (!ps.skip()) return false;
             continue;
         }
-        if (kw_is(k, "type") || kw_is(k, "f")) {
+        const Field fld = field_of(k);
+        if (fld == FLD_TYPE || fld == FLD_F) {
             std::string_view v;
             bool vk = false;
             if (!ps.keyword(v, vk)) return false;
-            if (kw_is(k, "type")) {
+            if (fld == FLD_TYPE) {
                 if (!vk) return ps.fail(":type is not a keyword");
                 if (v == "invoke") op.type = LC_INVOKE;
                 else if (v == "ok") op.type = LC_OK_T;
@@ -247,12 +260,12 @@ bool read_op(Parser &ps, RawOp &op) {
                     else if (v == "stop") op.nem = 0;
                 }
             }
-        } else if (kw_is(k, "process") || kw_is(k, "index")) {
+        } else if (fld == FLD_PROCESS || fld == FLD_INDEX) {
             Leaf v;
             if (!ps.shaped(v)) return false;
-            if (kw_is(k, "process")) op.process = v.kind == K_INT ? v.i : LC_NO_PROCESS;
+            if (fld == FLD_PROCESS) op.process = v.kind == K_INT ? v.i : LC_NO_PROCESS;
             else op.index = v.kind == K_INT ? v.i : -1;
-        } else if (kw_is(k, "value")) {
+        } else if (fld == FLD_VALUE) {
             if (!ps.shaped(op.value)) return false;
         } else {
             if (!ps.skip()) return false;
