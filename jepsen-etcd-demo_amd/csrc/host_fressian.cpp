@@ -68,6 +68,7 @@ struct Reader {
     std::vector<Val> nodes;
     std::vector<uint32_t> kids;
     std::string pool;
+    std::vector<uint32_t> stk;    // elements of the collections being read (one stack for all)
     std::vector<uint32_t> cache;  // priority cache: node ids
     struct SType { int64_t tag; int64_t n; };
     std::vector<SType> stypes;  // struct cache
@@ -117,37 +118,36 @@ struct Reader {
         if (n < 0 || n > end - p) return fail("bad length");  // every element takes a byte at least
         return true;
     }
-    bool bytes_into(std::string &s, int64_t n) {
+    bool bytes_into(bool keep, int64_t n) {
         if (n < 0 || end - p < n) return fail("unexpected end of input");
-        s.append((const char *)p, (size_t)n);
+        if (keep) pool.append((const char *)p, (size_t)n);
         p += n;
         return true;
     }
     // Chunked strings / bytes: CHUNK len bytes ... then a final packed or full form.
-    bool chunks(uint8_t c, bool str, std::string &s) {
+    // String bytes go to the pool; bytes values are skipped.
+    bool chunks(uint8_t c, bool str) {
         const uint8_t packed0 = str ? STRING_PACKED_LENGTH_START : BYTES_PACKED_LENGTH_START;
         const uint8_t chunk = str ? STRING_CHUNK : BYTES_CHUNK, full = str ? STRING : BYTES;
         for (;;) {
             int64_t n;
-            if (c >= packed0 && c < packed0 + 8) return bytes_into(s, c - packed0);
+            if (c >= packed0 && c < packed0 + 8) return bytes_into(str, c - packed0);
             if (c != chunk && c != full) return fail(str ? "bad string chunk" : "bad bytes chunk");
-            if (!read_int(n) || !bytes_into(s, n)) return false;
+            if (!read_int(n) || !bytes_into(str, n)) return false;
             if (c == full) return true;
             if (!byte(c)) return false;
         }
     }
     bool string_node(uint8_t c, uint8_t kind, uint32_t &out) {
-        std::string s;
-        if (!chunks(c, true, s)) return false;
         Val v;
         v.kind = kind;
         v.a = pool.size();
-        v.n = (uint32_t)s.size();
-        pool += s;
+        if (!chunks(c, true)) return false;
+        v.n = (uint32_t)(pool.size() - v.a);
         out = node(v);
         return true;
     }
-    bool list_items(int64_t n, bool until_end, bool open, std::vector<uint32_t> &items) {
+    bool list_items(int64_t n, bool until_end, bool open) {
         for (int64_t k = 0; until_end || k < n; ++k) {
             if (until_end) {
                 if (p >= end) {
@@ -158,34 +158,36 @@ struct Reader {
             }
             uint32_t x;
             if (!value(x)) return false;
-            items.push_back(x);
+            stk.push_back(x);
         }
         return true;
     }
-    uint32_t coll(uint8_t kind, const std::vector<uint32_t> &items, int64_t tag = -1) {
+    // A collection of the elements stacked since `mark`.
+    uint32_t coll(uint8_t kind, size_t mark, int64_t tag = -1) {
         Val v;
         v.kind = kind;
         v.a = kids.size();
-        v.n = (uint32_t)items.size();
+        v.n = (uint32_t)(stk.size() - mark);
         v.ns = tag;
-        kids.insert(kids.end(), items.begin(), items.end());
+        kids.insert(kids.end(), stk.begin() + (std::ptrdiff_t)mark, stk.end());
+        stk.resize(mark);
         return node(v);
     }
     // A list object (what MAP / SET / OBJECT_ARRAY wrap).
-    bool list(std::vector<uint32_t> &items) {
+    bool list() {
         uint8_t c;
         if (!byte(c)) return false;
         int64_t n;
-        if (c >= LIST_PACKED_LENGTH_START && c < LIST_PACKED_LENGTH_START + 8) return list_items(c - LIST_PACKED_LENGTH_START, false, false, items);
-        if (c == LIST) return count(n) && list_items(n, false, false, items);
-        if (c == BEGIN_CLOSED_LIST) return list_items(0, true, false, items);
-        if (c == BEGIN_OPEN_LIST) return list_items(0, true, true, items);
+        if (c >= LIST_PACKED_LENGTH_START && c < LIST_PACKED_LENGTH_START + 8) return list_items(c - LIST_PACKED_LENGTH_START, false, false);
+        if (c == LIST) return count(n) && list_items(n, false, false);
+        if (c == BEGIN_CLOSED_LIST) return list_items(0, true, false);
+        if (c == BEGIN_OPEN_LIST) return list_items(0, true, true);
         --p;
         uint32_t x;  // any other value in that place (a cached list): use its elements
         if (!value(x)) return false;
         const Val &v = nodes[x];
         if (v.kind != V_LIST) return fail("expected a list");
-        items.insert(items.end(), kids.begin() + v.a, kids.begin() + v.a + v.n);
+        stk.insert(stk.end(), kids.begin() + (std::ptrdiff_t)v.a, kids.begin() + (std::ptrdiff_t)(v.a + v.n));
         return true;
     }
     bool value(uint32_t &out) {
@@ -200,7 +202,7 @@ struct Reader {
         Val v;
         uint64_t r;
         int64_t n;
-        std::vector<uint32_t> items;
+        const size_t mark = stk.size();
         if (c <= 0x7F || c == 0xFF || c == INT) {
             v.kind = V_INT;
             if (!int_of(c, v.i)) return false;
@@ -212,30 +214,29 @@ struct Reader {
         if ((c >= STRING_PACKED_LENGTH_START && c < STRING_PACKED_LENGTH_START + 8) || c == STRING_CHUNK || c == STRING)
             return string_node(c, V_STR, out);
         if ((c >= BYTES_PACKED_LENGTH_START && c < BYTES_PACKED_LENGTH_START + 8) || c == BYTES_CHUNK || c == BYTES) {
-            std::string s;
-            if (!chunks(c, false, s)) return false;
+            if (!chunks(c, false)) return false;
             v.kind = V_BLOB;
             out = node(v);
             return true;
         }
         if (c >= LIST_PACKED_LENGTH_START && c < LIST_PACKED_LENGTH_START + 8) {
-            if (!list_items(c - LIST_PACKED_LENGTH_START, false, false, items)) return false;
-            out = coll(V_LIST, items);
+            if (!list_items(c - LIST_PACKED_LENGTH_START, false, false)) return false;
+            out = coll(V_LIST, mark);
             return true;
         }
         switch (c) {
-            case LIST: if (!count(n) || !list_items(n, false, false, items)) return false; out = coll(V_LIST, items); return true;
-            case BEGIN_CLOSED_LIST: if (!list_items(0, true, false, items)) return false; out = coll(V_LIST, items); return true;
-            case BEGIN_OPEN_LIST: if (!list_items(0, true, true, items)) return false; out = coll(V_LIST, items); return true;
+            case LIST: if (!count(n) || !list_items(n, false, false)) return false; out = coll(V_LIST, mark); return true;
+            case BEGIN_CLOSED_LIST: if (!list_items(0, true, false)) return false; out = coll(V_LIST, mark); return true;
+            case BEGIN_OPEN_LIST: if (!list_items(0, true, true)) return false; out = coll(V_LIST, mark); return true;
             case MAP:
-                if (!list(items)) return false;
-                if (items.size() & 1) return fail("map with an odd number of forms");
-                out = coll(V_MAP, items);
+                if (!list()) return false;
+                if ((stk.size() - mark) & 1) return fail("map with an odd number of forms");
+                out = coll(V_MAP, mark);
                 return true;
             case SET: case OBJECT_ARRAY:
-                if (c == OBJECT_ARRAY) { if (!count(n) || !list_items(n, false, false, items)) return false; }
-                else if (!list(items)) return false;
-                out = coll(c == SET ? V_SET : V_LIST, items);
+                if (c == OBJECT_ARRAY) { if (!count(n) || !list_items(n, false, false)) return false; }
+                else if (!list()) return false;
+                out = coll(c == SET ? V_SET : V_LIST, mark);
                 return true;
             case KEY: case SYM: {
                 uint32_t ns, nm;
@@ -248,7 +249,7 @@ struct Reader {
                 return true;
             }
             case TRUE: case FALSE: v.kind = V_BOOL; v.i = c == TRUE; out = node(v); return true;
-            case NULL_: out = node(v); return true;
+            case NULL_: out = 0; return true;  // the shared nil node
             case FLOAT: if (!raw(r, 4)) return false; v.kind = V_DBL; out = node(v); return true;
             case DOUBLE: if (!raw(r, 8)) return false; v.kind = V_DBL; out = node(v); return true;
             case DOUBLE_0: case DOUBLE_1: v.kind = V_DBL; out = node(v); return true;
@@ -268,13 +269,8 @@ struct Reader {
                 return true;
             }
             case LONG_ARRAY: case INT_ARRAY: case BOOLEAN_ARRAY: {
-                if (!count(n)) return false;
-                for (int64_t k = 0; k < n; ++k) {
-                    uint32_t x;
-                    if (!value(x)) return false;
-                    items.push_back(x);
-                }
-                out = coll(V_LIST, items);
+                if (!count(n) || !list_items(n, false, false)) return false;
+                out = coll(V_LIST, mark);
                 return true;
             }
             case DOUBLE_ARRAY: case FLOAT_ARRAY: {
@@ -331,17 +327,20 @@ struct Reader {
     bool fields(int64_t t, uint32_t &out) {
         if (t < 0 || (uint64_t)t >= stypes.size()) return fail("struct cache index out of range");
         const SType st = stypes[(size_t)t];
-        std::vector<uint32_t> items;
-        if (!list_items(st.n, false, false, items)) return false;
+        const size_t mark = stk.size();
+        if (!list_items(st.n, false, false)) return false;
         const std::string_view tag = str(st.tag);
-        if ((tag == "map" || tag == "set" || tag == "vec" || tag == "list") && items.size() == 1 && nodes[items[0]].kind == V_LIST) {
-            const Val &l = nodes[items[0]];  // a collection handler writing its elements as one list field
-            std::vector<uint32_t> el(kids.begin() + l.a, kids.begin() + l.a + l.n);
-            if (tag == "map" && (el.size() & 1)) return fail("map with an odd number of forms");
-            out = coll(tag == "map" ? V_MAP : tag == "set" ? V_SET : V_LIST, el);
+        if ((tag == "map" || tag == "set" || tag == "vec" || tag == "list") && stk.size() - mark == 1 &&
+            nodes[stk[mark]].kind == V_LIST) {
+            const Val l = nodes[stk[mark]];  // a collection handler writing its elements as one list field
+            if (tag == "map" && (l.n & 1)) return fail("map with an odd number of forms");
+            stk.resize(mark);
+            Val v = l;
+            v.kind = tag == "map" ? V_MAP : tag == "set" ? V_SET : V_LIST;
+            out = node(v);  // the same elements, read as that collection
             return true;
         }
-        out = coll(V_TAGGED, items, st.tag);
+        out = coll(V_TAGGED, mark, st.tag);
         return true;
     }
     std::string_view str(int64_t id) const {
@@ -430,6 +429,7 @@ int decode(const uint8_t *buf, int64_t len, lc_hist **out) {
     Reader r{buf, buf + len, buf};
     r.nodes.reserve((size_t)len / 4 + 16);
     r.kids.reserve((size_t)len / 4 + 16);
+    r.nodes.push_back(Val{});  // node 0: nil
     uint32_t top;
     if (len == 0) return lc::fail(LC_E_PARSE, "lc_fressian: empty input");
     if (!r.value(top)) return lc::fail(LC_E_PARSE, "lc_fressian: byte %zu: %s", r.err_off, r.err.c_str());
@@ -470,13 +470,11 @@ int decode(const uint8_t *buf, int64_t len, lc_hist **out) {
         if (o.f == LC_F_OTHER) {
             if (o.nem >= 0) v0 = o.nem;
         } else {
-            const Val nil{};
-            uint32_t val = o.value >= 0 ? (uint32_t)o.value : 0;
-            if (o.value < 0) { r.nodes.push_back(nil); val = (uint32_t)(r.nodes.size() - 1); }
+            uint32_t val = o.value >= 0 ? (uint32_t)o.value : 0;  // a missing :value reads as nil
             if (indep) {
-                const uint32_t *e;
-                uint32_t m;
-                r.seq(val, e, m);
+                const uint32_t *e = nullptr;
+                uint32_t m = 0;
+                if (!r.seq(val, e, m) || m != 2) { delete h; return lc::fail(LC_E_UNSUPPORTED, "lc_fressian: op %u: not a [k v] tuple", i); }
                 const uint32_t e0 = e[0], e1 = e[1];
                 if (!scal(r, e0, key) || key == LC_NIL) { delete h; return lc::fail(LC_E_UNSUPPORTED, "lc_fressian: op %u: tuple key is not an integer", i); }
                 val = e1;
