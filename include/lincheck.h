@@ -74,6 +74,10 @@ extern "C" {
  * an integer or LC_NIL.  lc_history.mop holds them as int64 triples. */
 #define LC_MOP_READ  0
 #define LC_MOP_WRITE 1
+/* Register ids from LC_NAMED_REG_BASE up name non-integer registers (:x ...):
+ * lc_edn_read gives the i-th distinct name LC_NAMED_REG_BASE + i
+ * (lc_hist_reg_name). */
+#define LC_NAMED_REG_BASE ((int64_t)1 << 62)
 
 #define LC_NIL        INT64_MIN  /* a nil value                                */
 #define LC_NO_KEY     INT64_MIN  /* :value is not an independent tuple [k v]   */
@@ -487,12 +491,20 @@ int  lc_hist_view(const lc_hist *h, lc_history *out);  /* borrowed view */
  * query the count. */
 int64_t lc_hist_anomalous_keys(const lc_hist *h, int64_t *out_keys);
 void lc_hist_free(lc_hist *h);
+/* Named registers of a history read by lc_edn_read: their count, and the
+ * i-th name as written in the file (e.g. ":x"), or NULL past the end. */
+int64_t     lc_hist_n_reg_names(const lc_hist *h);
+const char *lc_hist_reg_name(const lc_hist *h, int64_t i);
 
 /* ---- history.edn (Jepsen store format) ------------------------------------- */
 /* Parse a Jepsen history.edn (one op map per line, or one vector of maps)
  * into an owned history.  Supports the op maps this workload produces:
  * :type :f :process :value (nil, ints, [k v] tuples, [old new]) :index :time
- * :error; other keys are skipped. */
+ * :error; other keys are skipped.  (model/multi-register) :f :txn values
+ * [[:read k v] [:write k v] ...] (also :r / :w), optionally as [key txn]
+ * tuples, fill lc_history.mop_off / mop: integer registers keep their ids,
+ * other register names get LC_NAMED_REG_BASE + i.  lc_edn_write writes
+ * :txn rows back, named registers as :r<i> keywords. */
 int  lc_edn_read(const char *path, lc_hist **out);
 int  lc_edn_parse(const char *text, int64_t len, lc_hist **out);
 int  lc_edn_write(const char *path, const lc_history *h);

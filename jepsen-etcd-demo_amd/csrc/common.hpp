@@ -49,6 +49,8 @@ struct lc_hist {
     std::vector<int64_t> anomalous_keys;
     // :txn micro-ops (lc_history.mop_off / mop); empty when no row is a :txn
     std::vector<int64_t> mop_off, mop;
+    // names of named registers (lc_edn_read): id LC_NAMED_REG_BASE + i is reg_names[i]
+    std::vector<std::string> reg_names;
 
     void reserve(size_t n) {
         type.reserve(n); f.reserve(n); process.reserve(n); key.reserve(n);
@@ -57,6 +59,20 @@ struct lc_hist {
     void push(uint8_t t, uint8_t fn, int64_t p, int64_t k, int64_t a, int64_t b, int64_t idx) {
         type.push_back(t); f.push_back(fn); process.push_back(p); key.push_back(k);
         v0.push_back(a); v1.push_back(b); index.push_back(idx);
+    }
+    // Row `size() - 1`'s micro-ops (call right after its push); the offsets
+    // of earlier rows are filled in on the first :txn row.
+    void set_mops(const int64_t *triples, size_t n) {
+        const size_t rows = type.size();
+        if (mop_off.empty()) mop_off.assign(rows, 0);
+        while (mop_off.size() < rows) mop_off.push_back((int64_t)(mop.size() / 3));
+        mop.insert(mop.end(), triples, triples + 3 * n);
+        mop_off.push_back((int64_t)(mop.size() / 3));
+    }
+    // Close the offsets (n + 1 entries) once every row is pushed.
+    void finish_mops() {
+        if (mop_off.empty()) return;
+        while (mop_off.size() < type.size() + 1) mop_off.push_back((int64_t)(mop.size() / 3));
     }
     int64_t size() const { return (int64_t)type.size(); }
     lc_history view() const {

@@ -23,6 +23,7 @@
 #include <string_view>
 #include <system_error>
 #include <thread>
+#include <unordered_map>
 
 #include "common.hpp"
 
@@ -208,7 +209,26 @@ struct RawOp {
     int8_t nem = -1;  // nemesis :f :start (1) / :stop (0)
     int64_t process = LC_NO_PROCESS, index = -1;
     Top value;
+    const char *vb = nullptr;  // where the :value's text starts (a :txn value is read again from there)
 };
+
+// Register names of :txn micro-ops, interned in order of first appearance.
+struct Names {
+    std::unordered_map<std::string, int64_t> id;
+    std::vector<std::string> names;
+    int64_t of(std::string_view t) {
+        auto it = id.find(std::string(t));
+        if (it != id.end()) return it->second;
+        const int64_t v = LC_NAMED_REG_BASE + (int64_t)names.size();
+        names.emplace_back(t);
+        id.emplace(names.back(), v);
+        return v;
+    }
+};
+
+// A :txn op's value is [k txn] (an independent tuple) when its first element
+// is an integer; a txn of two micro-ops starts with a vector instead.
+bool txn_tuple(const Top &v) { return v.kind == K_VEC && v.n == 2 && v.e[0].kind == K_INT; }
 
 // The op-map keys read, by length and spelling (one compare per key).
 enum Field { FLD_OTHER, FLD_TYPE, FLD_F, FLD_PROCESS, FLD_INDEX, FLD_VALUE };
@@ -256,6 +276,7 @@ bool read_op(Parser &ps, RawOp &op) {
                     else if (v == "cas") op.f = LC_F_CAS;
                     else if (v == "acquire") op.f = LC_F_ACQUIRE;  // (model/mutex)
                     else if (v == "release") op.f = LC_F_RELEASE;
+                    else if (v == "txn") op.f = LC_F_TXN;           // (model/multi-register)
                     else if (v == "start") op.nem = 1;              // nemesis
                     else if (v == "stop") op.nem = 0;
                 }
@@ -266,6 +287,8 @@ bool read_op(Parser &ps, RawOp &op) {
             if (fld == FLD_PROCESS) op.process = v.kind == K_INT ? v.i : LC_NO_PROCESS;
             else op.index = v.kind == K_INT ? v.i : -1;
         } else if (fld == FLD_VALUE) {
+            if (!ps.prefixes()) return false;
+            op.vb = ps.p;
             if (!ps.shaped(op.value)) return false;
         } else {
             if (!ps.skip()) return false;
@@ -275,7 +298,62 @@ bool read_op(Parser &ps, RawOp &op) {
     return true;
 }
 
-enum { CONV_OK = 0, CONV_KEY = 1, CONV_VALUE = 2 };
+enum { CONV_OK = 0, CONV_KEY = 1, CONV_VALUE = 2, CONV_TXN = 3 };
+
+// One micro-op [f k v]: f :read/:write (or :r/:w), k an integer or a name,
+// v an integer or nil.
+bool micro_op(Parser &ps, Names &names, std::vector<int64_t> &out) {
+    if (!ps.prefixes() || *ps.p != '[') return false;
+    ++ps.p;
+    std::string_view f;
+    bool fk = false;
+    if (!ps.keyword(f, fk) || !fk) return false;
+    int64_t code;
+    if (f == "read" || f == "r") code = LC_MOP_READ;
+    else if (f == "write" || f == "w") code = LC_MOP_WRITE;
+    else return false;
+    if (!ps.prefixes()) return false;
+    int64_t reg;
+    const char c = *ps.p;
+    if (c == ':' || c == '"' || (c != '-' && c != '+' && (c < '0' || c > '9'))) {
+        const char *b = ps.p;
+        if (!ps.skip()) return false;
+        const std::string_view t(b, (size_t)(ps.p - b));
+        if (t == "nil" || t.empty()) return false;
+        reg = names.of(t);
+    } else {
+        uint8_t kind;
+        if (!ps.scalar(kind, reg) || kind != K_INT || reg >= LC_NAMED_REG_BASE) return false;
+    }
+    Leaf v;
+    if (!ps.shaped(v) || (v.kind != K_INT && v.kind != K_NIL)) return false;
+    const int64_t val = v.kind == K_NIL ? LC_NIL : v.i;
+    if (val == LC_NIL + 1) return false;  // the multi-register model's "absent"
+    ps.ws();
+    if (ps.p >= ps.end || *ps.p != ']') return false;
+    ++ps.p;
+    out.push_back(code);
+    out.push_back(reg);
+    out.push_back(val);
+    return true;
+}
+
+// A :txn value (nil, or a vector of micro-ops), read from its text.
+bool txn_value(Parser &ps, Names &names, std::vector<int64_t> &out) {
+    if (!ps.prefixes()) return false;
+    if (*ps.p != '[') {
+        uint8_t kind;
+        int64_t v;
+        return ps.scalar(kind, v) && kind == K_NIL;
+    }
+    ++ps.p;
+    for (;;) {
+        ps.ws();
+        if (ps.p >= ps.end) return false;
+        if (*ps.p == ']') { ++ps.p; return true; }
+        if (!micro_op(ps, names, out)) return false;
+    }
+}
 
 template <class V>
 int64_t scal(const V &v, bool &ok) {
@@ -298,9 +376,27 @@ bool register_value(uint8_t f, const V &val, int64_t &v0, int64_t &v1) {
     return ok;
 }
 
-// One row from a parsed op.  indep: values are [k v] tuples.
-int convert(const RawOp &o, bool indep, lc_hist &h) {
+// One row from a parsed op.  indep: values are [k v] tuples.  A :txn row's
+// micro-ops are read from the value's text (names: the register interner).
+int convert(const RawOp &o, bool indep, lc_hist &h, Names *names, const char *end, const char *base) {
     int64_t key = LC_NO_KEY, v0 = LC_NIL, v1 = LC_NIL;
+    if (o.f == LC_F_TXN) {
+        std::vector<int64_t> mops;
+        if (o.vb) {
+            Parser tp{o.vb, end, base};
+            if (indep) {
+                tp.ws();
+                ++tp.p;  // '[' of the [k txn] tuple (txn_tuple checked it)
+                uint8_t kind;
+                tp.ws();
+                if (!tp.scalar(kind, key) || kind != K_INT) return CONV_KEY;
+            }
+            if (!txn_value(tp, *names, mops)) return CONV_TXN;
+        }
+        h.push(o.type, o.f, o.process, key, v0, v1, o.index);
+        h.set_mops(mops.data(), mops.size() / 3);
+        return CONV_OK;
+    }
     if (o.f == LC_F_OTHER) {
         if (o.nem >= 0) v0 = o.nem;
     } else if (indep) {
@@ -325,6 +421,8 @@ struct alignas(256) Chunk {
     int conv_err = CONV_OK;
     int64_t conv_row = -1;  // chunk-local op number of a conversion error
     bool not_indep = false, any_client = false;
+    bool need_serial = false;  // a :txn op in a parallel chunk (one interner for the whole file)
+    Names names;
 };
 
 void parse_range(const char *base, const char *b, const char *e, bool indep, bool whole, Chunk &out) {
@@ -333,11 +431,13 @@ void parse_range(const char *base, const char *b, const char *e, bool indep, boo
     auto one = [&](void) -> bool {
         RawOp op;
         if (!read_op(ps, op)) return false;
+        if (op.f == LC_F_TXN && !whole) { out.need_serial = true; return false; }
         if (op.f != LC_F_OTHER) {
             out.any_client = true;
-            if (indep && !(op.value.kind == K_VEC && op.value.n == 2)) { out.not_indep = true; return false; }
+            const bool tup = op.f == LC_F_TXN ? txn_tuple(op.value) : (op.value.kind == K_VEC && op.value.n == 2);
+            if (indep && !tup) { out.not_indep = true; return false; }
         }
-        const int rc = convert(op, indep, out.rows);
+        const int rc = convert(op, indep, out.rows, &out.names, e, base);
         if (rc != CONV_OK) { out.conv_err = rc; out.conv_row = out.rows.size(); return false; }
         return true;
     };
@@ -389,6 +489,10 @@ int finish_serial(const char *text, int64_t len, lc_hist **out) {
             const int rc = c->conv_err == CONV_KEY
                                ? lc::fail(LC_E_UNSUPPORTED, "lc_edn: op %lld: tuple key is not an integer",
                                           (long long)c->conv_row)
+                           : c->conv_err == CONV_TXN
+                               ? lc::fail(LC_E_UNSUPPORTED,
+                                          "lc_edn: op %lld: :txn value is not nil or [[:read|:write k v] ...]",
+                                          (long long)c->conv_row)
                                : lc::fail(LC_E_UNSUPPORTED,
                                           "lc_edn: op %lld: value is not an integer, nil or [old new]",
                                           (long long)c->conv_row);
@@ -396,6 +500,10 @@ int finish_serial(const char *text, int64_t len, lc_hist **out) {
             return rc;
         }
         lc_hist *h = new (std::nothrow) lc_hist(std::move(c->rows));
+        if (h) {
+            h->reg_names = std::move(c->names.names);
+            h->finish_mops();
+        }
         delete c;
         if (!h) return lc::fail(LC_E_NOMEM, "lc_edn: out of memory");
         *out = h;
@@ -438,7 +546,7 @@ extern "C" int lc_edn_parse(const char *text, int64_t len, lc_hist **out) {
         if (!spawned) return finish_serial(text, len, out);
         bool any_client = false;
         for (auto &c : ch) {
-            if (!c.err.empty() || c.not_indep || c.conv_err != CONV_OK) return finish_serial(text, len, out);
+            if (!c.err.empty() || c.not_indep || c.need_serial || c.conv_err != CONV_OK) return finish_serial(text, len, out);
             any_client |= c.any_client;
         }
         if (!any_client) return finish_serial(text, len, out);
@@ -495,13 +603,34 @@ extern "C" int lc_edn_write(const char *path, const lc_history *h) {
     FILE *f = std::fopen(path, "wb");
     if (!f) return lc::fail(LC_E_IO, "lc_edn_write: cannot open %s", path);
     static const char *types[] = {"invoke", "ok", "fail", "info"};
-    static const char *fs[] = {"read", "write", "cas", "", "acquire", "release"};
+    static const char *fs[] = {"read", "write", "cas", "", "acquire", "release", "txn"};
     std::string line;
     for (int64_t r = 0; r < h->n; ++r) {
         line.clear();
-        if (h->type[r] > LC_INFO || h->f[r] > LC_F_RELEASE) { std::fclose(f); return lc::fail(LC_E_INVALID, "lc_edn_write: bad row %lld", (long long)r); }
+        if (h->type[r] > LC_INFO || h->f[r] > LC_F_TXN) { std::fclose(f); return lc::fail(LC_E_INVALID, "lc_edn_write: bad row %lld", (long long)r); }
         line += "{:type :"; line += types[h->type[r]];
-        if (h->f[r] == LC_F_OTHER) {
+        if (h->f[r] == LC_F_TXN) {
+            // [[:read k v] ...]; named registers (ids from LC_NAMED_REG_BASE) as :r<i>
+            std::string v = "nil";
+            const int64_t mb = h->mop_off ? h->mop_off[r] : 0, me = h->mop_off ? h->mop_off[r + 1] : 0;
+            if (me > mb) {
+                v = "[";
+                for (int64_t m = mb; m < me; ++m) {
+                    const int64_t *t = h->mop + 3 * m;
+                    v += m > mb ? " [:" : "[:";
+                    v += t[0] == LC_MOP_WRITE ? "write " : "read ";
+                    if (t[1] >= LC_NAMED_REG_BASE) { v += ":r"; v += std::to_string(t[1] - LC_NAMED_REG_BASE); }
+                    else v += std::to_string(t[1]);
+                    v += " ";
+                    put_scalar(v, t[2]);
+                    v += "]";
+                }
+                v += "]";
+            }
+            line += ", :f :txn, :value ";
+            if (h->key[r] != LC_NO_KEY) { line += "["; line += std::to_string(h->key[r]); line += " "; line += v; line += "]"; }
+            else line += v;
+        } else if (h->f[r] == LC_F_OTHER) {
             line += ", :f :"; line += h->v0[r] == 1 ? "start" : h->v0[r] == 0 ? "stop" : "nemesis";
             line += ", :value nil";
         } else {

@@ -254,3 +254,13 @@ extern "C" int64_t lc_hist_anomalous_keys(const lc_hist *h, int64_t *out_keys) {
 }
 
 extern "C" void lc_hist_free(lc_hist *h) { delete h; }
+
+extern "C" int64_t lc_hist_n_reg_names(const lc_hist *h) {
+    if (!h) return lc::fail(LC_E_INVALID, "lc_hist_n_reg_names: null argument");
+    return (int64_t)h->reg_names.size();
+}
+
+extern "C" const char *lc_hist_reg_name(const lc_hist *h, int64_t i) {
+    if (!h || i < 0 || (uint64_t)i >= h->reg_names.size()) return nullptr;
+    return h->reg_names[(size_t)i].c_str();
+}

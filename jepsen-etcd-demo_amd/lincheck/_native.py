@@ -133,6 +133,8 @@ SIGNATURES = {
     "lc_edn_read": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
     "lc_edn_parse": (C.c_int, [C.c_char_p, C.c_int64, P(C.c_void_p)]),
     "lc_edn_write": (C.c_int, [C.c_char_p, P(LcHistory)]),
+    "lc_hist_n_reg_names": (C.c_int64, [C.c_void_p]),
+    "lc_hist_reg_name": (C.c_char_p, [C.c_void_p, C.c_int64]),
     "lc_fressian_read": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
     "lc_fressian_parse": (C.c_int, [C.c_char_p, C.c_int64, P(C.c_void_p)]),
     "lc_fressian_write": (C.c_int, [C.c_char_p, P(LcHistory)]),

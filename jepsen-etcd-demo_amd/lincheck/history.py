@@ -151,6 +151,11 @@ class History:
                 N.carray(v.process, n, np.int64), N.carray(v.key, n, np.int64),
                 N.carray(v.v0, n, np.int64), N.carray(v.v1, n, np.int64),
                 N.carray(v.index, n, np.int64))
+        if v.mop_off:
+            h.mop_off = N.carray(v.mop_off, n + 1, np.int64)
+            h.mop = N.carray(v.mop, 3 * int(h.mop_off[-1]), np.int64) if h.mop_off[-1] else np.zeros(0, np.int64)
+        for i in range(L.lc_hist_n_reg_names(handle)):
+            h.reg_names[NAMED_REG_BASE + i] = L.lc_hist_reg_name(handle, i).decode()
         na = L.lc_hist_anomalous_keys(handle, None)
         if na > 0:
             buf = np.zeros(na, np.int64)

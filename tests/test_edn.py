@@ -118,3 +118,69 @@ def test_non_independent_values():
     h = H.parse_edn(text)
     assert list(h.key) == [N.LC_NO_KEY] * 3
     assert (h.v0[2], h.v1[2]) == (3, 4) and h.v0[0] == 3
+
+
+def _edn(x):
+    """EDN text of a Python value from histgen's op maps (strings as keywords)."""
+    if x is None:
+        return "nil"
+    if isinstance(x, str):
+        return ":" + x
+    if isinstance(x, (list, tuple)):
+        return "[" + " ".join(_edn(y) for y in x) + "]"
+    return str(int(x))
+
+
+def _txn_lines(ops):
+    out = []
+    for o in ops:
+        proc = ":nemesis" if o.get("process") is None or isinstance(o.get("process"), str) else str(o["process"])
+        out.append("{:type :%s, :f :%s, :value %s, :process %s, :time 1, :index %d}" % (
+            o["type"], o["f"], _edn(o.get("value")), proc, o["index"]))
+    return "\n".join(out) + "\n"
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_txn_histories(seed):
+    """(model/multi-register) :txn ops in history.edn: [k txn] tuples of
+    [:read|:write register value] micro-ops, registers as keywords, read back
+    with the same rows, micro-ops and register ids as History.from_ops gives
+    the op maps (names in order of first appearance)."""
+    from histgen import multi_register_history
+    ops = multi_register_history(seed, n_keys=6, n_ops=40, corrupt=0.3, p_info=0.05)
+    for i, o in enumerate(ops):
+        o["index"] = i
+    ref = H.History.from_ops(ops)
+    g = H.parse_edn(_txn_lines(ops))
+    for col in ("type", "f", "process", "key", "v0", "v1", "index", "mop_off", "mop"):
+        np.testing.assert_array_equal(getattr(g, col), getattr(ref, col), err_msg=col)
+    assert {k: v.lstrip(":") for k, v in g.reg_names.items()} == ref.reg_names
+    from lincheck import model
+    assert Packed(g, model.multi_register()).keys == Packed(ref, model.multi_register()).keys
+
+
+def test_txn_forms_and_round_trip(tmp_path):
+    text = ("{:type :invoke, :f :txn, :value [[:r :x nil] [:w 7 2]], :process 0, :index 0}\n"
+            "{:type :ok, :f :txn, :value [[:read :x 1] [:write 7 2]], :process 0, :index 1}\n"
+            "{:type :invoke, :f :txn, :value nil, :process 1, :index 2}\n"
+            "{:type :fail, :f :txn, :value [[:write \"y\" 3]], :process 1, :index 3}\n")
+    h = H.parse_edn(text)
+    base = H.NAMED_REG_BASE
+    assert list(h.f) == [N.LC_F_TXN] * 4 and (h.key == N.LC_NO_KEY).all()
+    assert list(h.mop_off) == [0, 2, 4, 4, 5]
+    assert h.mop.reshape(-1, 3).tolist() == [[0, base, N.LC_NIL], [1, 7, 2], [0, base, 1], [1, 7, 2],
+                                             [1, base + 1, 3]]
+    assert h.reg_names == {base: ":x", base + 1: '"y"'}
+    path = str(tmp_path / "history.edn")
+    H.write_edn(path, h)
+    g = H.read_edn(path)
+    for col in ("type", "f", "process", "key", "v0", "v1", "index", "mop_off", "mop"):
+        np.testing.assert_array_equal(getattr(g, col), getattr(h, col), err_msg=col)
+    assert g.reg_names == {base: ":r0", base + 1: ":r1"}
+
+
+@pytest.mark.parametrize("value", ["[[:cas :x 1]]", "[[:read :x]]", "[[:read :x 1 2]]", "[:read :x 1]",
+                                   "[[:read nil 1]]", "[[:read :x :y]]", "7"])
+def test_txn_errors(value):
+    with pytest.raises(N.LincheckError, match="txn"):
+        H.parse_edn("{:type :invoke, :f :txn, :value %s, :process 0, :index 0}\n" % value)

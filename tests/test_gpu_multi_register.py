@@ -74,3 +74,25 @@ def test_multi_register_on_device(shape, budget):
             assert paths <= allp
             if len(allp) <= ck.TRUNCATE:
                 assert paths == allp
+
+
+def test_multi_register_history_edn_on_device(tmp_path):
+    """The same kind of history as a history.edn file (keyword registers,
+    [k txn] tuples), read by lc_edn_read and checked on the device: verdicts
+    and failing events equal the restatement's on the op maps."""
+    from test_edn import _txn_lines
+    ops = multi_register_history(21, n_keys=30, n_ops=40, procs=5, regs=("x", "y", "z"), values=(0, 1, 2, 3),
+                                 corrupt=0.3, p_info=0.05)
+    for i, o in enumerate(ops):
+        o["index"] = i
+    path = tmp_path / "history.edn"
+    path.write_text(_txn_lines(ops))
+    h = H.read_edn(str(path))
+    pk = Packed(h, model.multi_register())
+    res = Device(0).check(pk)
+    orc = LR.check_independent(ops, model="multi-register")
+    want_v = {True: 1, False: 0, "unknown": -1}
+    for i, k in enumerate(pk.keys):
+        assert int(res.valid[i]) == want_v[orc[k].valid], k
+        assert int(res.fail_event[i]) == (orc[k].fail_event if orc[k].fail_event is not None else -1), k
+    assert (res.valid == 0).any() and (res.valid == 1).any()
