@@ -177,6 +177,45 @@ int main(int argc, char **argv) {
         }
         lc_hist_free(h);
     }
+    // :txn histories in EDN (multi-register): parsed, packed, and mangled
+    {
+        std::string txt;
+        std::mt19937_64 rng(9);
+        const char *regs[] = {":x", ":y", "3", "\"z\""};
+        for (int i = 0; i < 400; ++i) {
+            const int k = (int)(rng() % 4), p = (int)(rng() % 5);
+            std::string v = "[";
+            for (int m = 0, nm = 1 + (int)(rng() % 3); m < nm; ++m) {
+                v += (rng() & 1) ? "[:read " : "[:w ";
+                v += regs[rng() % 4];
+                v += (rng() % 3) ? " " + std::to_string(rng() % 4) + "]" : " nil]";
+            }
+            v += "]";
+            for (const char *t : {"invoke", "ok"})
+                txt += std::string("{:type :") + t + ", :f :txn, :value [" + std::to_string(k) + " " + v +
+                       "], :process " + std::to_string(p) + ", :index " + std::to_string(i) + "}\n";
+        }
+        lc_hist *x = nullptr;
+        CHECK(lc_edn_parse(txt.data(), (int64_t)txt.size(), &x) == LC_OK);
+        if (x) {
+            lc_history xv;
+            lc_hist_view(x, &xv);
+            CHECK(xv.mop_off != nullptr && lc_hist_n_reg_names(x) == 3);
+            exercise(xv, LC_MODEL_MULTI_REGISTER);
+            lc_hist_free(x);
+        }
+        for (int t = 0; t < 60; ++t) {
+            std::string m = txt.substr(0, (size_t)(rng() % txt.size()));
+            for (int k = 0; k < 8 && !m.empty(); ++k) m[(size_t)(rng() % m.size())] = (char)(rng() & 0xFF);
+            x = nullptr;
+            if (lc_edn_parse(m.data(), (int64_t)m.size(), &x) == LC_OK && x) {
+                lc_history mv;
+                lc_hist_view(x, &mv);
+                exercise(mv, LC_MODEL_MULTI_REGISTER);
+                lc_hist_free(x);
+            }
+        }
+    }
     // random op sequences over three processes and two keys: completions
     // without invocations, double invokes, unknown :f codes, :txn rows with
     // random (and malformed) micro-ops for (model/multi-register)
