@@ -452,7 +452,9 @@ int  lc_check_node(lc_ctx *ctx, const lc_batch *shard, int64_t block, uint64_t *
  * its upload overlaps the search of the step before it (two steps in flight)
  * and its records are in `node` once lc_wait (or lc_wait_step over it)
  * returns; errors surface there.  The shard's arrays and `node` must stay
- * untouched until then.  Any other step runs as lc_check_node (returns 0). */
+ * untouched until then.  One rank (no communicator): the search writes the
+ * records straight into `node` (device-mapped), and lc_node_records has none
+ * of them.  Any other step runs as lc_check_node (returns 0). */
 int  lc_check_node_async(lc_ctx *ctx, const lc_batch *shard, int64_t block, uint64_t *node, lc_stats *s);
 /* Page-locked host memory (for lc_check_node_async's records). */
 void *lc_host_alloc(size_t bytes);
