@@ -329,19 +329,22 @@ def test_device_validates_batches_beyond_the_register_tier():
         np.testing.assert_array_equal(again["fail_event"][:K], good["fail_event"][:K])
 
 
-def test_pipelined_node_steps_bit_exact():
+@pytest.mark.parametrize("rccl", [False, True])
+def test_pipelined_node_steps_bit_exact(rccl):
     """lc_check_node_async: batches of different sizes in flight two at a
     time (each step's upload overlapping the previous search, the staging
     slots used in turn), every step's records in its own page-locked buffer;
-    after the wait each equals lc_check_node's.  A batch beyond the register
-    tier runs synchronously, and a pageable caller batch goes through the
-    staging copy."""
+    after the wait each equals lc_check_node's.  Without a communicator the
+    search writes the records into that buffer itself; with a (one-rank) RCCL
+    communicator they go through the all-gather and a download.  A batch
+    beyond the register tier runs synchronously, and a pageable caller batch
+    goes through the staging copy."""
     from lincheck.checker import PinnedRecords
     shapes = [dict(n_keys=300, ops_per_key=400, concurrency=10, anomaly_rate=0.1, seed=81),
               dict(n_keys=120, ops_per_key=900, concurrency=8, anomaly_rate=0.2, seed=82),
               dict(n_keys=1000, ops_per_key=200, concurrency=10, seed=83)]
     pks = [Packed(H.synth(**s)) for s in shapes]
-    dev = Device(0)
+    dev = Device(0, comm=(0, 1, comm_id()) if rccl else None)
     refs = [dev.check_node(pk, pk.n_keys + 3)[0].copy() for pk in pks]
     seq = [0, 1, 2, 0, 2, 1, 1, 0, 2, 2, 0, 1]
     bufs = [PinnedRecords(pks[i].n_keys + 3) for i in seq]
