@@ -1165,7 +1165,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (spec) {
         const uint32_t ck1 = std::getenv("LC_SPEC_CK1") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK1")) : 32u;
-        const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 160u;
+        const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 120u;
         // the validation of a host-unchecked batch runs in extra blocks of
         // the same launch (a second stream cost ~40 us of cross-stream waits)
         const int vblocks = a.strict ? (int)std::min<int64_t>(K, c->cu_count) : 0;
