@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r2i
+O=gpurun_out/r2j
 mkdir -p $O/prof
 step() { echo "== $1"; }
 step tests
