@@ -75,14 +75,14 @@
         n-mop  (reduce + 0 (map (comp count second) txns))
         mop-off (when (seq txns) (Memory. (* 8 (inc n))))
         mop    (when (seq txns) (Memory. (max 8 (* 24 n-mop))))
-        bytes  (max 8 (* 8 n))
-        type   (Memory. (max 1 n))
-        fn     (Memory. (max 1 n))
-        proc   (Memory. bytes)
-        key    (Memory. bytes)
-        v0     (Memory. bytes)
-        v1     (Memory. bytes)
-        index  (Memory. bytes)
+        nbytes (max 8 (* 8 n))
+        types  (Memory. (max 1 n))
+        fs     (Memory. (max 1 n))
+        procs  (Memory. nbytes)
+        ks     (Memory. nbytes)
+        v0     (Memory. nbytes)
+        v1     (Memory. nbytes)
+        idx    (Memory. nbytes)
         hist   (Memory. 80)]
     (loop [i 0, ops (seq history)]
       (when ops
@@ -93,13 +93,13 @@
               [a b] (cond (= fc 2) (if (nil? v) [nil nil] v)
                           (<= 4 fc) [nil nil]      ; mutex ops carry no value
                           :else     [v nil])]
-          (.setByte type i (byte (type-code (:type op))))
-          (.setByte fn i (byte fc))
-          (.setLong proc (* 8 i) (if (integer? (:process op)) (long (:process op)) nil-long))
-          (.setLong key (* 8 i) (long-or-nil k))
+          (.setByte types i (byte (type-code (:type op))))
+          (.setByte fs i (byte fc))
+          (.setLong procs (* 8 i) (if (integer? (:process op)) (long (:process op)) nil-long))
+          (.setLong ks (* 8 i) (long-or-nil k))
           (.setLong v0 (* 8 i) (if (= fc 3) nil-long (long-or-nil a)))
           (.setLong v1 (* 8 i) (if (= fc 3) nil-long (long-or-nil b)))
-          (.setLong index (* 8 i) (long (or (:index op) -1)))
+          (.setLong idx (* 8 i) (long (or (:index op) -1)))
           (recur (inc i) (next ops)))))
     (when mop-off
       (let [by-row (into {} txns)]
@@ -113,10 +113,10 @@
                 (.setLong mop (+ 16 (* 24 (+ at j))) (long-or-nil x)))
               (recur (inc i) (+ at (count ms))))))))
     (.setLong hist 0 n)
-    (doseq [[off m] [[8 type] [16 fn] [24 proc] [32 key] [40 v0] [48 v1] [56 index]
+    (doseq [[off m] [[8 types] [16 fs] [24 procs] [32 ks] [40 v0] [48 v1] [56 idx]
                      [64 mop-off] [72 mop]]]
       (.setPointer hist off m))
-    {:hist hist :keep [type fn proc key v0 v1 index mop-off mop]}))
+    {:hist hist :held [types fs procs ks v0 v1 idx mop-off mop]}))
 
 ;; One lc_ctx per (device(s), budget, algorithm), created on first use and
 ;; kept: a context owns its streams, scratch and staging buffers, so repeated
@@ -173,15 +173,15 @@
       :register     (model/register v)
       :mutex        (assoc (model/mutex) :locked (= 1 v))
       :multi-register
-      (let [n     (LincheckNative/lc_packed_state_map packed i (int x) nil nil 0)
-            regs  (long-array (max 1 n))
-            vals  (long-array (max 1 n))
-            by-id (into {} (map (fn [[r id]] [id r]) names))]
-        (check-rc (LincheckNative/lc_packed_state_map packed i (int x) regs vals n) "lc_packed_state_map")
+      (let [n-regs (LincheckNative/lc_packed_state_map packed i (int x) nil nil 0)
+            regs   (long-array (max 1 n-regs))
+            xs     (long-array (max 1 n-regs))
+            by-id  (into {} (map (fn [[r id]] [id r]) names))]
+        (check-rc (LincheckNative/lc_packed_state_map packed i (int x) regs xs n-regs) "lc_packed_state_map")
         (model/multi-register
-          (into {} (for [j (range n)]
+          (into {} (for [j (range n-regs)]
                      [(get by-id (aget regs j) (aget regs j))
-                      (let [y (aget vals j)] (when-not (= y nil-long) y))])))))))
+                      (let [y (aget xs j)] (when-not (= y nil-long) y))])))))))
 
 (defn- report
   "Decodes lc_report's words for packed key i into the :linear map."
@@ -203,7 +203,7 @@
                   (cond (and (= :txn (:f o)) (some? d)) (assoc o :value d)  ; a :txn learns its reads
                         (and (nil? (:value o)) (<= 0 done)) (assoc o :value d)
                         :else o)))
-        model-of (fn [x] (model-of model x packed i names))
+        state-model (fn [x] (model-of model x packed i names))
         fail-op (row (aget words 0))
         prev    (row (aget words 1))
         n-cfg   (aget words 2)
@@ -212,17 +212,17 @@
         take!   (fn [] (let [x (aget words @pos)] (vswap! pos inc) x))
         ops!    (fn [] (vec (repeatedly (take!) #(op (take!) (take!)))))
         configs (vec (repeatedly n-cfg
-                                 (fn [] (let [m (model-of (take!))
+                                 (fn [] (let [m (state-model (take!))
                                               pending (ops!)
                                               linear  (ops!)]
                                           {:model m :last-op prev :pending pending :linearized linear}))))
         paths   (vec (repeatedly n-paths
                                  (fn []
-                                   (let [m0    (model-of (take!))
+                                   (let [m0    (state-model (take!))
                                          steps (vec (repeatedly (take!)
                                                                 (fn [] (let [o (op (take!) (take!))]
-                                                                         {:op o :model (model-of (take!))}))))
-                                         bad   (model/step (model-of (take!)) fail-op)]
+                                                                         {:op o :model (state-model (take!))}))))
+                                         bad   (model/step (state-model (take!)) fail-op)]
                                      (into [{:op prev :model m0}]
                                            (conj steps {:op fail-op :model {:msg (:msg bad)}}))))))
         base    {:analyzer (if (= algorithm :wgl) :wgl :linear)
@@ -241,7 +241,7 @@
                  algorithm :linear}}]
   (let [history    (vec history)
         names      (volatile! {})                  ; named register -> id
-        {:keys [hist keep]} (marshal history names)
+        {:keys [hist held]} (marshal history names)
         init       (when (= model :multi-register) (seq (:init opts)))   ; (model/multi-register init)
         init-mem   (when init (Memory. (* 16 (count init))))
         _          (doseq [[j [r x]] (map-indexed vector init)]
@@ -258,8 +258,8 @@
       (let [batch    (Memory. 104)               ; sizeof(lc_batch), ABI 8
             _        (check-rc (LincheckNative/lc_packed_view packed batch) "lc_packed_view")
             n-keys   (.getLong batch 0)
-            keys     (long-array (max 1 n-keys))
-            _        (check-rc (LincheckNative/lc_packed_keys packed keys) "lc_packed_keys")
+            key-ids  (long-array (max 1 n-keys))
+            _        (check-rc (LincheckNative/lc_packed_keys packed key-ids) "lc_packed_keys")
             ctx      (context (or devices [device]) budget algorithm)
             n1       (max 1 n-keys)
             valid    (Memory. n1)
@@ -278,7 +278,7 @@
         (persistent!
           (reduce
             (fn [m i]
-              (let [k  (aget keys i)
+              (let [k  (aget key-ids i)
                     v  (.getByte valid i)
                     c  (.getByte cause i)]
                 (assoc! m k
@@ -298,7 +298,7 @@
             (range n-keys))))
       (finally
         (LincheckNative/lc_packed_free packed)
-        (identity [keep init-mem])))))
+        (identity [held init-mem])))))
 
 (defn checker
   "independent/checker over compose{:linear linearizable(cas-register),
