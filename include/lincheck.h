@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 8
+#define LC_ABI_VERSION 9
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -328,8 +328,29 @@ typedef struct lc_opts {
     int32_t  comm_rank;
     int32_t  comm_size;
     uint8_t  comm_id[LC_COMM_ID_BYTES];
-    int32_t  reserved[4];   /* must be 0                                         */
+    /* Search-path choices (ABI 9, in the bytes ABI 8 reserved; all 0 =
+     * automatic, the library's own choice per batch).  They pin one choice for
+     * A/B measurements and tests, never change a result, and are read at
+     * lc_create only: the caller's environment does not steer the kernels. */
+    int32_t  path_flags;    /* LC_PATH_*                                         */
+    int32_t  spec_segs;     /* speculative segments per key: 2, 3, 4, 6 or 8      */
+    int32_t  spec_ck;       /* speculative checkpoints, events past a cut:
+                               (ck1 + 1) | (ck2 + 1) << 16 (0: 32 and 120)      */
+    int32_t  seg_len;       /* quiescent-point segments: events per segment      */
 } lc_opts;
+
+/* lc_opts.path_flags */
+#define LC_PATH_SPLIT_ON     0x01  /* quiescent-point key segments where they apply  */
+#define LC_PATH_SPLIT_OFF    0x02  /* never (else: when sampled keys say they pay)    */
+#define LC_PATH_SPEC_OFF     0x04  /* no speculative key segments                     */
+#define LC_PATH_LAYERS_OFF   0x08  /* HBM tier: config-keyed sets only (no T3L)       */
+#define LC_PATH_NODE_SYNC    0x10  /* lc_check_node_async runs as lc_check_node        */
+#define LC_PATH_NODE_STAGED  0x20  /* one rank: records through HBM, not device-mapped */
+#define LC_PATH_CHUNKS_ON    0x40  /* lc_check_node: chunked upload whatever the size  */
+#define LC_PATH_CHUNKS_OFF   0x80  /* lc_check_node: one upload whatever the size      */
+#define LC_PATH_SPEC_EVEN    0x100 /* speculative cuts at equal event counts (round 2)
+                                      instead of equal estimated cost               */
+#define LC_PATH_ALL          0x1FF
 
 /* lc_opts.flags */
 #define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,
@@ -425,7 +446,10 @@ int  lc_check_device(lc_ctx *ctx, const lc_dev_batch *db, lc_result *r,
 int  lc_wait(lc_ctx *ctx, lc_stats *s);
 /* Wait until the LC_DEV_ASYNC step `back` steps before the latest (0 = the
  * latest, at most 3) has finished, leaving later ones running; with no such
- * step on record, wait for everything on the context's stream. */
+ * step on record, wait for everything on the context's stream.  Returns
+ * LC_E_INVALID, naming the key, when a finished step's batch was malformed
+ * (an error a later, still running step has raised already may be reported
+ * here too); the error is cleared then. */
 int  lc_wait_step(lc_ctx *ctx, int back);
 
 /* ---- one process per GPU: node-wide verdict records ------- */
@@ -506,10 +530,15 @@ const char *lc_hist_reg_name(const lc_hist *h, int64_t i);
  * [[:read k v] [:write k v] ...] (also :r / :w), optionally as [key txn]
  * tuples, fill lc_history.mop_off / mop: integer registers keep their ids,
  * other register names get LC_NAMED_REG_BASE + i.  lc_edn_write writes
- * :txn rows back, named registers as :r<i> keywords. */
+ * :txn rows back, named registers as :r<i> keywords (lc_edn_write_named: by
+ * their names). */
 int  lc_edn_read(const char *path, lc_hist **out);
 int  lc_edn_parse(const char *text, int64_t len, lc_hist **out);
 int  lc_edn_write(const char *path, const lc_history *h);
+/* lc_edn_write with named registers written back under their names:
+ * reg_names[i] names register LC_NAMED_REG_BASE + i as lc_hist_reg_name gives
+ * it (":x"); a name that is not one EDN token is written as :r<i>.  (ABI 9) */
+int  lc_edn_write_named(const char *path, const lc_history *h, const char *const *reg_names, int64_t n_reg_names);
 
 /* ---- test.fressian (Jepsen store format, binary) ---------------------------- */
 /* Read the history out of a Fressian-encoded Jepsen test map (its :history

@@ -570,8 +570,17 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
     if (o.max_final <= 0) o.max_final = 10;
     if (o.max_final > 16) return lc::fail(LC_E_INVALID, "lc_create: max_final above 16");
     if (o.flags & ~LC_OPT_COUNT_PROBES) return lc::fail(LC_E_INVALID, "lc_create: unknown flags 0x%x", o.flags);
-    for (int32_t r : o.reserved)
-        if (r) return lc::fail(LC_E_INVALID, "lc_create: reserved fields must be 0");
+    if (o.path_flags & ~LC_PATH_ALL) return lc::fail(LC_E_INVALID, "lc_create: unknown path_flags 0x%x", o.path_flags);
+    if ((o.path_flags & LC_PATH_SPLIT_ON) && (o.path_flags & LC_PATH_SPLIT_OFF))
+        return lc::fail(LC_E_INVALID, "lc_create: LC_PATH_SPLIT_ON and _OFF together");
+    if ((o.path_flags & LC_PATH_CHUNKS_ON) && (o.path_flags & LC_PATH_CHUNKS_OFF))
+        return lc::fail(LC_E_INVALID, "lc_create: LC_PATH_CHUNKS_ON and _OFF together");
+    if (o.spec_segs != 0 && o.spec_segs != 2 && o.spec_segs != 3 && o.spec_segs != 4 && o.spec_segs != 6 &&
+        o.spec_segs != 8)
+        return lc::fail(LC_E_INVALID, "lc_create: spec_segs must be 0, 2, 3, 4, 6 or 8");
+    if (o.seg_len < 0) return lc::fail(LC_E_INVALID, "lc_create: seg_len < 0");
+    if (o.spec_ck && (((uint32_t)o.spec_ck & 0xFFFFu) == 0 || ((uint32_t)o.spec_ck >> 16) == 0))
+        return lc::fail(LC_E_INVALID, "lc_create: spec_ck must be 0 or (ck1 + 1) | (ck2 + 1) << 16");
     if (o.n_devices < 0 || o.n_devices > MAX_DEV)
         return lc::fail(LC_E_INVALID, "lc_create: n_devices must be 0..%d", MAX_DEV);
     if (o.comm_size < 0 || o.comm_size > 4096 || (o.comm_size > 1 && (o.comm_rank < 0 || o.comm_rank >= o.comm_size)))
@@ -953,12 +962,13 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
 
 // ---- one device's search ----------------------------------------------------
 
-// After a readback of the control block: a malformed batch T0 found.
-static int take_error(Dev *c, int64_t key0) {
+// After a readback of the control block: a malformed batch T0 found.  The
+// kernels name the key by its index in the caller's batch (Args::err_base).
+static int take_error(Dev *c) {
     int32_t *cnt = (int32_t *)(c->hctl + 4);
     if (!cnt[4]) return LC_OK;
     const int why = cnt[4];
-    const int64_t key = key0 + (int64_t)cnt[5] - 1;
+    const int64_t key = (int64_t)cnt[5] - 1;
     cnt[4] = cnt[5] = 0;
     HIPCHK(hipMemsetAsync(c->counters + 4, 0, 2 * sizeof(int32_t), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1029,6 +1039,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     a.rec = c->rec_out ? c->rec_out + res_off : nullptr;
     a.probes = c->acc + 0; a.ev_count = c->acc + 1; a.keys_done = c->acc + 2; a.stream_bytes = c->acc + 3;
     a.err = c->counters + 4;
+    a.err_base = (int32_t)key0;  // malformed keys are reported by their index in the caller's batch
     a.list_cap = (int32_t)c->cap_keys;
     int32_t *spill0 = c->lists, *spill1 = c->lists + c->cap_keys, *spill2 = c->lists + 2 * c->cap_keys;
     int32_t *wide = c->lists + 3 * c->cap_keys, *old_narrow = c->lists + 4 * c->cap_keys;
@@ -1045,10 +1056,9 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // quiescent points close enough for the cuts to pay (segments_pay: on
     // C2, whose clients think about as long as an op takes, the longest
     // stretch without one is most of a key, so its keys stay whole).
-    // LC_SPLIT=0/1 forces the choice (A/B and tests).
-    const char *force = std::getenv("LC_SPLIT");
+    // lc_opts.path_flags LC_PATH_SPLIT_ON / _OFF pin the choice (A/B and tests).
     const bool fast = !a.peak && !a.final_cfg && o.max_configs >= 16ull * 64 * 32;
-    const bool want = force ? force[0] == '1' : d->seg_pays;
+    const bool want = (o.path_flags & LC_PATH_SPLIT_ON) ? true : (o.path_flags & LC_PATH_SPLIT_OFF) ? false : d->seg_pays;
     const bool split = t0_step && fast && d->taggable && want && K <= (int64_t)c->cu_count * 8;
     if (split) {
         rc = ensure_segments(c, K);
@@ -1059,16 +1069,12 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // segment waves per SIMD in all (C2: 1,000 keys x 4).  The kernel's 80
     // VGPRs would allow six, but 6-wave workgroups land unevenly on a CU's
     // four SIMDs (5-7 waves each): C2 0.357 ms at 4 segments per key, 0.406
-    // at 6, 0.386 at 8.  LC_SPEC=0/1 forces the choice, LC_SPEC_SEGS (2, 3, 4,
-    // 6, 8) the segments per key.
-    const char *fspec = std::getenv("LC_SPEC");
+    // at 6, 0.386 at 8.  lc_opts: LC_PATH_SPEC_OFF turns them off, spec_segs
+    // pins the segments per key.
     int segs = K > 0 ? (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1)) : 0;
     segs = segs >= 8 ? 8 : segs >= 4 ? 4 : segs >= 2 ? 2 : 0;
-    if (const char *e = std::getenv("LC_SPEC_SEGS")) {
-        const int v = std::atoi(e);
-        segs = v >= 8 ? 8 : v >= 6 ? 6 : v >= 4 ? 4 : v >= 3 ? 3 : v >= 2 ? 2 : 0;
-    }
-    const bool spec = !split && t0_step && fast && segs >= 2 && (fspec ? fspec[0] == '1' : true);
+    if (o.spec_segs) segs = o.spec_segs;
+    const bool spec = !split && t0_step && fast && segs >= 2 && !(o.path_flags & LC_PATH_SPEC_OFF);
     if (spec) {
         const size_t need = lcd::spec_ws_words(K, segs);
         if (need > c->spec_ws_words) {
@@ -1150,22 +1156,23 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         sa.ev_off = d->ev_off; sa.events = d->events; sa.trans = d->trans; sa.key_error = d->key_error;
         sa.n_trans = (uint32_t)d->n_trans; sa.n_keys = (int32_t)K; sa.max_seg = lcd::SEG_MAX;
         // segments of about fill x (resident waves / keys) per key
-        const double fill = std::getenv("LC_SEG_FILL") ? std::atof(std::getenv("LC_SEG_FILL")) : 2.0;
         const int grid = c->cu_count * 12;
-        const double per_key = std::max(1.0, fill * grid / (double)K);
+        const double per_key = std::max(1.0, 2.0 * grid / (double)K);
         sa.seg_len = (uint32_t)std::max<double>(64.0, (double)d->n_events / (double)K / per_key);
-        if (const char *e = std::getenv("LC_SEG_LEN")) sa.seg_len = (uint32_t)std::max(1, std::atoi(e));
+        if (o.seg_len > 0) sa.seg_len = (uint32_t)o.seg_len;
         sa.seg_cnt = c->seg_cnt; sa.seg_end = c->seg_end; sa.seg_out = c->seg_out; sa.seg0_fev = c->seg0_fev;
         sa.work = c->seg_work; sa.rerun = c->seg_rerun; sa.rerun_init = c->seg_rerun_init; sa.ctl = c->seg_ctl;
         sa.err = c->counters + 4; sa.valid = a.valid; sa.fail_event = a.fail_event; sa.cause = a.cause;
         sa.rec = a.rec;
         sa.strict = a.strict;
+        sa.err_base = a.err_base;
         HIPCHK(hipMemsetAsync(c->seg_ctl, 0, 4 * sizeof(int32_t), c->stream));
         HIPCHK(lcd::launch_segments(sa, grid, c->stream));
         if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (spec) {
-        const uint32_t ck1 = std::getenv("LC_SPEC_CK1") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK1")) : 32u;
-        const uint32_t ck2 = std::getenv("LC_SPEC_CK2") ? (uint32_t)std::atoi(std::getenv("LC_SPEC_CK2")) : 120u;
+        // (spec_ck == 0: the defaults; else (ck1 + 1) | (ck2 + 1) << 16)
+        const uint32_t ck1 = o.spec_ck ? ((uint32_t)o.spec_ck & 0xFFFFu) - 1u : 32u;
+        const uint32_t ck2 = o.spec_ck ? ((uint32_t)o.spec_ck >> 16) - 1u : 120u;
         // the validation of a host-unchecked batch runs in extra blocks of
         // the same launch (a second stream cost ~40 us of cross-stream waits)
         const int vblocks = a.strict ? (int)std::min<int64_t>(K, c->cu_count) : 0;
@@ -1226,7 +1233,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
                 HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
-        return take_error(c, key0);
+        return take_error(c);
     };
     if (t0_step) {
         if (mode != RES_HOST) {
@@ -1234,7 +1241,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             HIPCHK(hipEventRecord(c->e1, c->stream));
             HIPCHK(hipMemcpyAsync(c->hctl + 6, c->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
-            rc = take_error(c, key0);
+            rc = take_error(c);
         } else {
             rc = readback();
         }
@@ -1255,11 +1262,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         HIPCHK(hipEventRecord(c->et3a, c->stream));
         lcd::Args a3 = a;
         a3.wide = wide; a3.n_wide = n_wide;
-        // Narrow keys: the layered form first (<= 8 states; LC_T3_LAYERS=0
+        // Narrow keys: the layered form first (<= 8 states; LC_PATH_LAYERS_OFF
         // turns it off for A/B runs), the config-keyed narrow tier for the
         // keys it hands on (cnt[6]).
         // (the layered form steps ops as register-state masks: not a table model)
-        const bool layers = !d->table && !(std::getenv("LC_T3_LAYERS") && std::atoi(std::getenv("LC_T3_LAYERS")) == 0);
+        const bool layers = !d->table && !(o.path_flags & LC_PATH_LAYERS_OFF);
         int32_t *narrow_list = spill2, *narrow_n = n_spill2;
         int32_t n_narrow = n_deep;
         if (n_deep > 0 && layers) {
@@ -1323,7 +1330,7 @@ static int dev_wait(Dev *c, int *n_async, float *span_ms) {
     *span_ms = 0;
     if (c->n_async) HIPCHK(hipEventElapsedTime(span_ms, c->ea0, c->ea1));
     c->n_async = 0;
-    return take_error(c, 0);
+    return take_error(c);
 }
 
 static void merge_stats(lc_stats &t, const lc_stats &s) {
@@ -1484,6 +1491,7 @@ extern "C" int lc_wait(lc_ctx *c, lc_stats *st) {
 extern "C" int lc_wait_step(lc_ctx *c, int back) {
     if (!c) return lc::fail(LC_E_INVALID, "lc_wait_step: null context");
     std::lock_guard<std::mutex> g(c->mu);
+    int rc = LC_OK;
     for (int p = 0; p < c->n_dev; ++p) {
         Dev *d = c->dev[p];
         HIPCHK(hipSetDevice(d->device));
@@ -1492,8 +1500,16 @@ extern "C" int lc_wait_step(lc_ctx *c, int back) {
         } else {
             HIPCHK(hipEventSynchronize(d->ring[(d->async_seq - 1 - (uint64_t)back) % 4]));
         }
+        // Errors of the finished steps surface here (include/lincheck.h): the
+        // error words are read on the copy stream, which does not wait for
+        // the later steps still running (an error one of them has already
+        // raised is reported now too, and cleared).
+        HIPCHK(hipMemcpyAsync(d->hctl + 6, d->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, d->cstream));
+        HIPCHK(hipStreamSynchronize(d->cstream));
+        const int r = take_error(d);
+        if (r && !rc) rc = r;
     }
-    return LC_OK;
+    return rc;
 }
 
 extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_stats *st) {
@@ -1619,12 +1635,13 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
     // uploaded and searched in NODE_CHUNKS key chunks: the copies run on a
     // stream of their own, and each chunk's search waits only for its own
     // copy, so the host-to-device transfer overlaps the search
-    // (LC_NODE_CHUNKS=1 turns it off).
+    // (lc_opts.path_flags LC_PATH_CHUNKS_ON / _OFF pin the choice).
     const int64_t K = b->n_keys;
     const uint64_t n_ev = K ? b->ev_off[K] : 0;
     const bool can_chunk = sh.t0_only && !(c->o.flags & LC_OPT_COUNT_PROBES) && K >= Dev::NODE_CHUNKS;
     bool big = K >= 16 * (int64_t)d->cu_count && n_ev >= (8u << 20);
-    if (const char *e = std::getenv("LC_NODE_CHUNKS")) big = std::atoi(e) > 1;
+    if (c->o.path_flags & LC_PATH_CHUNKS_ON) big = true;
+    if (c->o.path_flags & LC_PATH_CHUNKS_OFF) big = false;
     // (Searching page-locked event words in place, over the host link, was
     // measured slower: 0.468 against 0.332 ms for C2's search, the link
     // sustaining ~31 GB/s of kernel reads; the 16-bit upload won instead.)
@@ -1734,7 +1751,7 @@ extern "C" int lc_check_node_async(lc_ctx *c, const lc_batch *b, int64_t block, 
         // (a large shard is not cut into chunks here: its whole upload
         // overlaps the previous step's search instead)
         if (K > 0 && n_ev > 0 && !b->table && !(c->o.flags & LC_OPT_COUNT_PROBES) && pinned(node) &&
-            !std::getenv("LC_NODE_SYNC")) {
+            !(c->o.path_flags & LC_PATH_NODE_SYNC)) {
             rc = prepare_batch(c, b, &sh, &src);
             if (rc) return rc;
             if (sh.t0_only) {
@@ -1755,7 +1772,7 @@ extern "C" int lc_check_node_async(lc_ctx *c, const lc_batch *b, int64_t block, 
                 // follows it; with a communicator they go through HBM for the
                 // all-gather.
                 uint64_t *dnode = nullptr;
-                const bool direct = !c->comm && !std::getenv("LC_NODE_STAGED") &&
+                const bool direct = !c->comm && !(c->o.path_flags & LC_PATH_NODE_STAGED) &&
                                     hipHostGetDevicePointer((void **)&dnode, node, 0) == hipSuccess && dnode;
                 if (direct) {
                     if (block > K) std::memset(node + K, 0, (size_t)(block - K) * 8);

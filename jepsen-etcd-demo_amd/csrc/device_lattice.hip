@@ -225,6 +225,7 @@ struct T0Args {
     const int32_t *order;
     int32_t *ticket;
     int32_t *err;                // [0] LC_BATCH_E_* bits, [1] 1 + largest malformed key
+    int32_t err_base;            // that key's index in the caller's batch = err_base + key
     uint32_t *lat_ws;            // unused (the 9-10-pending workspace is in LDS)
     const Args *full;            // device copy: results, counters, spill list
     uint64_t budget;
@@ -241,7 +242,7 @@ struct T0Args {
 __device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint32_t why) {
     if (lane_id() == 0) {
         atomicOr(&a.err[0], (int32_t)why);
-        atomicMax(&a.err[1], key + 1);
+        atomicMax(&a.err[1], a.err_base + key + 1);
     }
 }
 
@@ -1100,7 +1101,7 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     }
     if (why && lane == 0) {
         atomicOr(&a.err[0], why);
-        atomicMax(&a.err[1], (int32_t)k + 1);
+        atomicMax(&a.err[1], a.err_base + (int32_t)k + 1);
     }
 }
 
@@ -1174,6 +1175,7 @@ static T0Args make_t0(const Args &a, const Args *a_dev) {
     t.key_width = a.key_width; t.key_states = a.key_states; t.key_error = a.key_error; t.order = a.order;
     t.ticket = a.ticket;
     t.err = a.err;
+    t.err_base = a.err_base;
     t.n_trans = a.n_trans;
     t.lat_ws = a.lat_ws; t.full = a_dev; t.budget = a.budget; t.n_order = a.n_order;
     t.init_state = a.init_state; t.shared_states = a.shared_states;
@@ -1195,6 +1197,7 @@ hipError_t launch_validate(const Args &a, hipStream_t s, bool general) {
     T0Args t{};
     t.ev_off = a.ev_off; t.events = a.events; t.trans = a.trans; t.trans_off = a.trans_off;
     t.key_states = a.key_states; t.key_error = a.key_error; t.err = a.err; t.key_width = a.key_width;
+    t.err_base = a.err_base;
     t.n_order = a.n_order; t.shared_states = a.shared_states; t.n_trans = a.n_trans;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_order, 2048));
     if (general) hipLaunchKernelGGL(k_validate<true>, dim3(grid), dim3(64), 0, s, t);
@@ -1488,7 +1491,7 @@ __global__ __launch_bounds__(64) void k_search_segments(SegArgs a) {
             if (s == 0) a.seg0_fev[key] = status == 1 ? (int32_t)fev : -1;
             if (status == 3) {  // declared to fit the register tier, and it does not
                 atomicOr(&a.err[0], LC_BATCH_E_FIT);
-                atomicMax(&a.err[1], key + 1);
+                atomicMax(&a.err[1], a.err_base + key + 1);
             }
         }
     }
@@ -1559,7 +1562,7 @@ __global__ __launch_bounds__(64) void k_seg_rerun(SegArgs a) {
             } else {  // cannot happen for a consistent batch: report it as malformed
                 seg_verdict(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1);
                 atomicOr(&a.err[0], LC_BATCH_E_FIT);
-                atomicMax(&a.err[1], key + 1);
+                atomicMax(&a.err[1], a.err_base + key + 1);
             }
         }
     }

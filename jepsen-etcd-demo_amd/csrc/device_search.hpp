@@ -33,6 +33,8 @@ struct Args {
     int32_t *err;            // T0: [0] LC_BATCH_E_* bits, [1] 1 + largest malformed key
     uint32_t n_trans;        // entries of trans[]
     int32_t strict;          // T0: the host did not validate the events (T0_STRICT)
+    int32_t err_base;        // added to a malformed key's index in err[1]: the launch's
+                             // first key in the caller's batch (a chunk or shard of it)
     // per-key results (device pointers)
     int8_t *valid;
     int32_t *fail_event;
@@ -114,6 +116,7 @@ struct SegArgs {
     uint8_t *cause;
     uint64_t *rec;               // may be null: LC_REC_* records (Args::rec)
     int32_t strict;
+    int32_t err_base;            // as Args::err_base
 };
 constexpr uint32_t SEG_MAX = 256;  // work items are key << 8 | segment
 hipError_t launch_segments(const SegArgs &a, int grid, hipStream_t s);

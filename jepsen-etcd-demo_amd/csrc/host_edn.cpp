@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -598,8 +599,29 @@ static void put_scalar(std::string &o, int64_t v) {
     if (v == LC_NIL) o += "nil"; else o += std::to_string(v);
 }
 
-extern "C" int lc_edn_write(const char *path, const lc_history *h) {
+// A register name as lc_edn_read keeps it (":x", "\"z\"", ...) is written back
+// verbatim when it reads as one EDN token; anything else becomes :r<i>.
+static bool edn_token(const char *s) {
+    if (!s || !*s) return false;
+    if (*s == '"') {
+        const size_t n = std::strlen(s);
+        if (n < 2 || s[n - 1] != '"') return false;
+        for (size_t i = 1; i + 1 < n; ++i)
+            if (s[i] == '"' || s[i] == '\\' || s[i] == '\n') return false;
+        return true;
+    }
+    for (const char *c = s; *c; ++c)
+        if (std::isspace((unsigned char)*c) || std::strchr("[](){}\",;\\", *c)) return false;
+    return true;
+}
+
+extern "C" int lc_edn_write(const char *path, const lc_history *h) { return lc_edn_write_named(path, h, nullptr, 0); }
+
+extern "C" int lc_edn_write_named(const char *path, const lc_history *h, const char *const *reg_names,
+                                  int64_t n_reg_names) {
     if (!path || !h || h->n < 0) return lc::fail(LC_E_INVALID, "lc_edn_write: null argument");
+    if (n_reg_names < 0 || (n_reg_names > 0 && !reg_names))
+        return lc::fail(LC_E_INVALID, "lc_edn_write_named: bad register names");
     FILE *f = std::fopen(path, "wb");
     if (!f) return lc::fail(LC_E_IO, "lc_edn_write: cannot open %s", path);
     static const char *types[] = {"invoke", "ok", "fail", "info"};
@@ -610,7 +632,8 @@ extern "C" int lc_edn_write(const char *path, const lc_history *h) {
         if (h->type[r] > LC_INFO || h->f[r] > LC_F_TXN) { std::fclose(f); return lc::fail(LC_E_INVALID, "lc_edn_write: bad row %lld", (long long)r); }
         line += "{:type :"; line += types[h->type[r]];
         if (h->f[r] == LC_F_TXN) {
-            // [[:read k v] ...]; named registers (ids from LC_NAMED_REG_BASE) as :r<i>
+            // [[:read k v] ...]; named registers (ids from LC_NAMED_REG_BASE) by
+            // their names when given, else as :r<i>
             std::string v = "nil";
             const int64_t mb = h->mop_off ? h->mop_off[r] : 0, me = h->mop_off ? h->mop_off[r + 1] : 0;
             if (me > mb) {
@@ -619,7 +642,9 @@ extern "C" int lc_edn_write(const char *path, const lc_history *h) {
                     const int64_t *t = h->mop + 3 * m;
                     v += m > mb ? " [:" : "[:";
                     v += t[0] == LC_MOP_WRITE ? "write " : "read ";
-                    if (t[1] >= LC_NAMED_REG_BASE) { v += ":r"; v += std::to_string(t[1] - LC_NAMED_REG_BASE); }
+                    const int64_t ni = t[1] - LC_NAMED_REG_BASE;
+                    if (t[1] >= LC_NAMED_REG_BASE && ni < n_reg_names && edn_token(reg_names[ni])) v += reg_names[ni];
+                    else if (t[1] >= LC_NAMED_REG_BASE) { v += ":r"; v += std::to_string(ni); }
                     else v += std::to_string(t[1]);
                     v += " ";
                     put_scalar(v, t[2]);

@@ -47,7 +47,7 @@ enum : uint8_t {
     DOUBLE_0 = 0xFB, DOUBLE_1 = 0xFC, END_COLLECTION = 0xFD, RESET_CACHES = 0xFE,
 };
 
-enum : uint8_t { V_NIL, V_BOOL, V_INT, V_DBL, V_STR, V_KW, V_SYM, V_LIST, V_MAP, V_SET, V_TAGGED, V_BLOB, V_END };
+enum : uint8_t { V_NIL, V_BOOL, V_INT, V_DBL, V_STR, V_KW, V_SYM, V_LIST, V_MAP, V_SET, V_TAGGED, V_BLOB };
 
 // One decoded value.  Strings live in the string pool (a, n); collections
 // hold their children's node ids in the kids array (a, n; a map's are k, v
@@ -155,6 +155,9 @@ struct Reader {
                     return fail("unterminated list");
                 }
                 if (*p == END_COLLECTION) { ++p; return true; }
+                // an open list may run into the file's footer (it ends there;
+                // the footer is left for the top level, which stops reading)
+                if (open && *p == FOOTER) return true;
             }
             uint32_t x;
             if (!value(x)) return false;
@@ -282,15 +285,22 @@ struct Reader {
                 out = node(v);
                 return true;
             }
+            // The slot is taken BEFORE the value is read, as org.fressian's
+            // readAndCacheObject does (and its writer numbers the outer value
+            // first): a cached value holding cached strings gets the lower index.
             case PUT_PRIORITY_CACHE: {
+                const size_t slot = cache.size();
+                cache.push_back(0);
                 if (!value(out)) return false;
-                cache.push_back(out);
+                cache[slot] = out;
                 return true;
             }
             case PRECACHE: {
+                const size_t slot = cache.size();
+                cache.push_back(0);
                 uint32_t x;
                 if (!value(x)) return false;
-                cache.push_back(x);
+                cache[slot] = x;
                 return value(out);
             }
             case GET_PRIORITY_CACHE: if (!read_int(n)) return false; return cached(n, out);
@@ -307,7 +317,11 @@ struct Reader {
                 return value(m) && value(out);  // metadata, then the value it annotates
             }
             case RESET_CACHES: cache.clear(); stypes.clear(); return value(out);
-            case FOOTER: --p; v.kind = V_END; out = node(v); return true;
+            // the footer follows the top-level value (which decode() stops
+            // after) or ends an open list (list_items); anywhere else -- in a
+            // closed or counted list, a struct's fields, as the first byte --
+            // the file is malformed
+            case FOOTER: return fail("unexpected footer");
             case END_COLLECTION: return fail("unexpected end of collection");
             default: return fail("unknown code 0x" + hex(c));
         }

@@ -17,10 +17,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 8
+LC_ABI_VERSION = 9
 LC_MAX_DEVICES = 8
 LC_COMM_ID_BYTES = 128
 LC_OPT_COUNT_PROBES = 0x1
+# lc_opts.path_flags (ABI 9): pinned search-path choices for A/B runs and tests
+LC_PATH_SPLIT_ON, LC_PATH_SPLIT_OFF, LC_PATH_SPEC_OFF, LC_PATH_LAYERS_OFF = 0x01, 0x02, 0x04, 0x08
+LC_PATH_NODE_SYNC, LC_PATH_NODE_STAGED, LC_PATH_CHUNKS_ON, LC_PATH_CHUNKS_OFF = 0x10, 0x20, 0x40, 0x80
+LC_PATH_SPEC_EVEN = 0x100
 LC_DEV_RESULT, LC_DEV_ASYNC = 1, 2
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
 LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE, LC_F_TXN = 0, 1, 2, 3, 4, 5, 6
@@ -69,7 +73,8 @@ class LcOpts(C.Structure):
                 ("flags", C.c_int32), ("debug_mode", C.c_int32),
                 ("n_devices", C.c_int32), ("devices", C.c_int32 * LC_MAX_DEVICES),
                 ("comm_rank", C.c_int32), ("comm_size", C.c_int32), ("comm_id", C.c_uint8 * LC_COMM_ID_BYTES),
-                ("reserved", C.c_int32 * 4)]
+                ("path_flags", C.c_int32), ("spec_segs", C.c_int32), ("spec_ck", C.c_int32),
+                ("seg_len", C.c_int32)]
 
 
 class LcResult(C.Structure):
@@ -133,6 +138,7 @@ SIGNATURES = {
     "lc_edn_read": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
     "lc_edn_parse": (C.c_int, [C.c_char_p, C.c_int64, P(C.c_void_p)]),
     "lc_edn_write": (C.c_int, [C.c_char_p, P(LcHistory)]),
+    "lc_edn_write_named": (C.c_int, [C.c_char_p, P(LcHistory), P(C.c_char_p), C.c_int64]),
     "lc_hist_n_reg_names": (C.c_int64, [C.c_void_p]),
     "lc_hist_reg_name": (C.c_char_p, [C.c_void_p, C.c_int64]),
     "lc_fressian_read": (C.c_int, [C.c_char_p, P(C.c_void_p)]),

@@ -169,11 +169,17 @@ class Device:
 
     def __init__(self, device: int = 0, budget: int = DEFAULT_BUDGET, max_final: int = TRUNCATE,
                  debug_mode: int = 0, count_probes: bool = False, algorithm: int = N.LC_ALGO_LINEAR,
-                 devices: Optional[Sequence[int]] = None, comm: Optional[tuple] = None):
+                 devices: Optional[Sequence[int]] = None, comm: Optional[tuple] = None,
+                 path_flags: int = 0, spec_segs: int = 0, spec_ck: Optional[tuple] = None, seg_len: int = 0):
+        """path_flags / spec_segs / spec_ck (ck1, ck2) / seg_len pin search-path
+        choices (lc_opts, ABI 9; A/B runs and tests): results never depend on them."""
         o = N.LcOpts()
         o.device, o.algorithm, o.max_configs, o.max_final = device, algorithm, budget, max_final
         o.flags = N.LC_OPT_COUNT_PROBES if count_probes else 0
         o.debug_mode = debug_mode  # ablation builds only; 0 = the real search
+        o.path_flags, o.spec_segs, o.seg_len = path_flags, spec_segs, seg_len
+        if spec_ck is not None:
+            o.spec_ck = (int(spec_ck[0]) + 1) | ((int(spec_ck[1]) + 1) << 16)
         if devices is not None and len(devices) > 1:
             o.n_devices = len(devices)
             for g, d in enumerate(devices):

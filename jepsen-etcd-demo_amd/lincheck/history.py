@@ -252,7 +252,13 @@ def parse_edn(text: str) -> History:
 
 
 def write_edn(path: str, h: History) -> None:
-    N.check(N.lib().lc_edn_write(path.encode(), C.byref(h.as_c())))
+    """lc_edn_write_named: named :txn registers keep their names (":x")."""
+    names = [h.reg_names.get(NAMED_REG_BASE + i) for i in range(len(h.reg_names))]
+    if names and all(isinstance(n, str) for n in names):
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        N.check(N.lib().lc_edn_write_named(path.encode(), C.byref(h.as_c()), arr, len(names)))
+    else:
+        N.check(N.lib().lc_edn_write(path.encode(), C.byref(h.as_c())))
 
 
 def read_fressian(path: str) -> History:

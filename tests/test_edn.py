@@ -1,5 +1,7 @@
 """history.edn ingestion: round trips and Jepsen's
 line format with fields and values this workload never reads."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -176,7 +178,15 @@ def test_txn_forms_and_round_trip(tmp_path):
     g = H.read_edn(path)
     for col in ("type", "f", "process", "key", "v0", "v1", "index", "mop_off", "mop"):
         np.testing.assert_array_equal(getattr(g, col), getattr(h, col), err_msg=col)
-    assert g.reg_names == {base: ":r0", base + 1: ":r1"}
+    assert g.reg_names == {base: ":x", base + 1: '"y"'}  # names written back verbatim
+    assert ":x" in open(path).read() and '"y"' in open(path).read()
+    # without names (lc_edn_write on a bare view) they become :r<i>
+    N.check(N.lib().lc_edn_write(path.encode(), C.byref(h.as_c())))
+    assert H.read_edn(path).reg_names == {base: ":r0", base + 1: ":r1"}
+    # a name that is not one EDN token falls back to :r<i> too
+    arr = (C.c_char_p * 2)(b":x", b"bad name")
+    N.check(N.lib().lc_edn_write_named(path.encode(), C.byref(h.as_c()), arr, 2))
+    assert H.read_edn(path).reg_names == {base: ":x", base + 1: ":r1"}
 
 
 @pytest.mark.parametrize("value", ["[[:cas :x 1]]", "[[:read :x]]", "[[:read :x 1 2]]", "[:read :x 1]",

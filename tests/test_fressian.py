@@ -380,3 +380,61 @@ def test_deep_nesting_is_refused():
     data = b"\xe5" * 10000 + b"\x01"
     with pytest.raises(N.LincheckError, match="too deep"):
         H.parse_fressian(data)
+
+
+@pytest.mark.parametrize("data", [b"\xed\xcf", b"\xe6\x01\xcf\xcf\xcf\xcf", b"\xcf\xcf\xcf\xcf",
+                                  b"\xc0\xed\xca\xf7\xcd\xdetype\xcf"])
+def test_footer_inside_a_collection_is_refused(data):
+    """A FOOTER code inside a closed or counted list (or as the first byte) is
+    a malformed file: refused at once, never read again and again."""
+    with pytest.raises(N.LincheckError, match="footer"):
+        H.parse_fressian(data)
+
+
+def test_open_list_ends_at_the_footer(c1):
+    """An open list of op maps followed by the file's footer: the list ends
+    there (org.fressian's writer closes a top-level open list with it)."""
+    w = FressianOut()
+    w.obj(Open(op_maps(c1, extra=False)))
+    w.footer()
+    same(H.parse_fressian(bytes(w.b)), c1)
+
+
+def test_nested_priority_cache_indices():
+    """PUT_PRIORITY_CACHE around a value that itself puts strings in the cache
+    (a whole keyword cached, its name cached inside it): org.fressian's reader
+    takes the outer slot before reading the value (readAndCacheObject) and its
+    writer numbers the outer value first, so the keyword gets index i and its
+    name i + 1.  Later packed references (0x80 + i) must find the keyword."""
+    h = H.parse_edn("{:type :invoke, :f :write, :value [0 3], :process 0, :index 0}\n"
+                    "{:type :ok, :f :write, :value [0 3], :process 0, :index 1}\n"
+                    "{:type :invoke, :f :read, :value [0 nil], :process 1, :index 2}\n"
+                    "{:type :ok, :f :read, :value [0 3], :process 1, :index 3}\n")
+    w = FressianOut()
+    slot = {}
+
+    def kw(name):
+        if name in slot:
+            w.b.append(0x80 + slot[name])
+            return
+        w.b.append(0xCD)                     # PUT_PRIORITY_CACHE: the keyword itself ...
+        slot[name] = len(w.cache)
+        w.cache[("kw", name)] = slot[name]   # (the outer slot, taken first)
+        w.b += b"\xca\xf7"                   # ... KEY, nil namespace,
+        w.cached(name)                       # ... and its name, cached at the next slot
+        assert w.cache[name] == slot[name] + 1
+
+    ops = op_maps(h, extra=False)
+    w.b.append(0xE4 + len(ops))
+    for m in ops:
+        w.b.append(0xC0)
+        w.b.append(0xEC)
+        w.int_(2 * len(m))
+        for k, v in m.items():
+            kw(str(k))
+            if isinstance(v, Kw):
+                kw(str(v))
+            else:
+                w.obj(v)
+    assert sum(1 for x in w.b if 0x80 <= x < 0xA0) > 10  # keywords referenced by slot
+    same(H.parse_fressian(bytes(w.b)), h)

@@ -2,14 +2,13 @@
 merged one |L| layer at a time in an LDS table, bit-exact with the oracle
 (verdict, cause, failing event; peaks and probe counts where keys finish).
 Keys with more than 8 register states are handed to the config-keyed narrow
-tier, keys needing window slots >= 56 to the wide one; LC_T3_LAYERS=0 (the
+tier, keys needing window slots >= 56 to the wide one; LC_PATH_LAYERS_OFF (the
 config-keyed narrow tier alone) must give the same records."""
-import os
-
 import numpy as np
 import pytest
 
 from helpers import device_vs_oracle
+from lincheck import _native as N
 from lincheck import history as H
 from lincheck.checker import Device, Packed
 
@@ -18,14 +17,9 @@ pytestmark = pytest.mark.gpu
 
 def _same_records(h, budget, count_probes=False):
     """The layered and the config-keyed narrow tiers on one history."""
-    dev = Device(0, budget=budget, count_probes=count_probes)
     p = Packed(h)
-    a = dev.check(p)
-    os.environ["LC_T3_LAYERS"] = "0"
-    try:
-        b = dev.check(p)
-    finally:
-        del os.environ["LC_T3_LAYERS"]
+    a = Device(0, budget=budget, count_probes=count_probes).check(p)
+    b = Device(0, budget=budget, count_probes=count_probes, path_flags=N.LC_PATH_LAYERS_OFF).check(p)
     for f in ("valid", "cause", "fail_event"):
         np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
     return a, b
@@ -81,14 +75,9 @@ def test_layers_final_configs(device):
     enumeration in test_counterexamples for the other tiers; here: same
     records as the config-keyed tier's set, as sets)."""
     h = H.synth(n_keys=40, ops_per_key=400, concurrency=16, info_rate=0.01, anomaly_rate=0.5, seed=45)
-    dev = Device(0, budget=1 << 20)
     p = Packed(h)
-    a = dev.check(p)
-    os.environ["LC_T3_LAYERS"] = "0"
-    try:
-        b = dev.check(p)
-    finally:
-        del os.environ["LC_T3_LAYERS"]
+    a = Device(0, budget=1 << 20).check(p)
+    b = Device(0, budget=1 << 20, path_flags=N.LC_PATH_LAYERS_OFF).check(p)
     bad = np.nonzero(a.valid == 0)[0]
     assert len(bad) > 0
     np.testing.assert_array_equal(a.fail_event, b.fail_event)

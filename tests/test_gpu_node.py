@@ -227,6 +227,53 @@ def test_async_errors_surface_at_wait():
     device_vs_oracle(h, dev)
 
 
+def test_pipelined_step_error_surfaces_at_wait_step():
+    """A malformed batch in a pipelined node step (lc_check_node_async): the
+    refusal comes from the lc_wait_step that waits for that step, naming the
+    key; the error is then cleared, and the next steps are bit-exact."""
+    from lincheck.checker import PinnedRecords
+    h = H.synth(n_keys=300, ops_per_key=200, concurrency=6, anomaly_rate=0.1, seed=79)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0)
+    arrs, b = _batch_copy(pk)
+    arrs["events"][int(pk.ev_off[137])] |= N.LC_EV_OK_BIT
+    bad = PinnedRecords(K)
+    st = N.LcStats()
+    rc = N.check(N.lib().lc_check_node_async(dev.handle, C.byref(b), K, N.ptr(bad, C.c_uint64), C.byref(st)))
+    assert rc == 1  # enqueued
+    with pytest.raises(N.LincheckError) as ei:
+        dev.wait_step(0)
+    assert ei.value.code == -1 and "key 137" in str(ei.value), str(ei.value)
+    assert dev.wait()[0] >= 0  # nothing left to report
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    for _ in range(2):
+        good = PinnedRecords(K)
+        assert dev.check_node_async(pk, K, good)[0]
+        dev.wait_step(0)
+        v, _, fe = _decode(np.asarray(good), K)
+        np.testing.assert_array_equal(v, orc["valid"])
+        np.testing.assert_array_equal(fe, orc["fail_event"])
+
+
+def test_chunked_node_step_names_the_batch_key():
+    """A malformed key in the third of four upload chunks of lc_check_node:
+    the error names its index in the caller's batch, not in its chunk."""
+    h = H.synth(n_keys=400, ops_per_key=200, concurrency=6, seed=80)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0, path_flags=N.LC_PATH_CHUNKS_ON)
+    arrs, b = _batch_copy(pk)
+    arrs["events"][int(pk.ev_off[263])] |= N.LC_EV_OK_BIT
+    out = np.zeros(K, np.uint64)
+    with pytest.raises(N.LincheckError) as ei:
+        N.check(N.lib().lc_check_node(dev.handle, C.byref(b), K, N.ptr(out, C.c_uint64), None))
+    assert "key 263" in str(ei.value), str(ei.value)
+    rec, _ = dev.check_node(pk, K)
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    np.testing.assert_array_equal(_decode(rec, K)[0], orc["valid"])
+
+
 def test_wait_step_waits_for_the_step_asked():
     """lc_wait_step(1) returns once the step before the latest is done: step
     A's records (one node buffer per step would be overwritten, so A and B
@@ -259,27 +306,25 @@ def test_wait_step_waits_for_the_step_asked():
 
 
 @pytest.mark.parametrize("forced", [True, False])
-def test_node_chunked_upload_pipeline(forced, monkeypatch):
+def test_node_chunked_upload_pipeline(forced):
     """lc_check_node on a large register-tier shard: key chunks uploaded on a
     stream of their own, each chunk's search waiting for its own copy.  The
-    records equal the one-launch check (LC_NODE_CHUNKS=1), and the oracle's
-    verdicts.  forced: a small C5-shaped shard chunked by LC_NODE_CHUNKS=4;
+    records equal the one-launch check (LC_PATH_CHUNKS_OFF), and the oracle's
+    verdicts.  forced: a small C5-shaped shard chunked by LC_PATH_CHUNKS_ON;
     otherwise a C3-shard-sized one (4,096+ keys, 8M+ events) chunked by
     default."""
     if forced:
         h = H.synth(n_keys=500, ops_per_key=300, concurrency=10, anomaly_rate=0.1, seed=73)
-        monkeypatch.setenv("LC_NODE_CHUNKS", "4")
     else:
         h = H.synth(n_keys=6000, ops_per_key=800, concurrency=10, anomaly_rate=0.02, seed=74)
     pk = Packed(h)
     K = pk.n_keys
-    dev = Device(0)
+    dev = Device(0, path_flags=N.LC_PATH_CHUNKS_ON if forced else 0)
     rec, _ = dev.check_node(pk, K)
     for _ in range(2):  # repeated steps reuse the chunk batches
         rec2, _ = dev.check_node(pk, K)
         np.testing.assert_array_equal(rec2, rec)
-    monkeypatch.setenv("LC_NODE_CHUNKS", "1")
-    one, _ = Device(0).check_node(pk, K)
+    one, _ = Device(0, path_flags=N.LC_PATH_CHUNKS_OFF).check_node(pk, K)
     np.testing.assert_array_equal(rec, one)
     v, c, fe = _decode(rec, K)
     keys, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)

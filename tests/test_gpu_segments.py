@@ -4,12 +4,11 @@ points, search every segment from all start states at once (tagged lattice
 words) and compose per key; a key that dies is searched again, untagged, in
 the segment it died in.  Verdicts, causes and failing events must equal the
 oracle's and the unsplit search's, whatever the segment length."""
-import os
-
 import numpy as np
 import pytest
 
 import cref
+from lincheck import _native as N
 from lincheck import history as H
 from lincheck.checker import Device, Packed
 
@@ -25,32 +24,14 @@ SHAPES = {
 }
 
 
-@pytest.fixture
-def seg_env():
-    saved = {k: os.environ.get(k) for k in ("LC_SEG_LEN", "LC_SPLIT")}
-    yield os.environ
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
-
-
 @pytest.mark.parametrize("shape", sorted(SHAPES))
-@pytest.mark.parametrize("seg_len", [None, "64", "1"])
-def test_segments_match_oracle(shape, seg_len, seg_env):
+@pytest.mark.parametrize("seg_len", [0, 64, 1])
+def test_segments_match_oracle(shape, seg_len):
     h = H.synth(**SHAPES[shape])
     pk = Packed(h)
-    dev = Device(0)
-    if seg_len:
-        seg_env["LC_SEG_LEN"] = seg_len
-    else:
-        seg_env.pop("LC_SEG_LEN", None)
-    seg_env["LC_SPLIT"] = "1"
-    got = dev.check(pk, verdicts_only=True)
-    seg_env["LC_SPLIT"] = "0"
-    ref = dev.check(pk, verdicts_only=True)
-    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+    got = Device(0, path_flags=N.LC_PATH_SPLIT_ON, seg_len=seg_len).check(pk, verdicts_only=True)
+    ref = Device(0, path_flags=N.LC_PATH_SPLIT_OFF).check(pk, verdicts_only=True)
+    _, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)
     for name, r in (("split", got), ("unsplit", ref)):
         np.testing.assert_array_equal(r.valid, orc["valid"], err_msg=f"{name} valid")
         np.testing.assert_array_equal(r.cause, orc["cause"], err_msg=f"{name} cause")
@@ -59,13 +40,11 @@ def test_segments_match_oracle(shape, seg_len, seg_env):
         assert (orc["valid"] == 0).any()
 
 
-def test_segments_resident_async(seg_env):
+def test_segments_resident_async():
     """The bench's resident steps (node records, asynchronous) on the split path."""
-    seg_env["LC_SPLIT"] = "1"
-    seg_env.pop("LC_SEG_LEN", None)
     h = H.synth(n_keys=1000, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=87)
     pk = Packed(h)
-    dev = Device(0)
+    dev = Device(0, path_flags=N.LC_PATH_SPLIT_ON)
     db = dev.upload(pk)
     for _ in range(5):
         db.check_node(pk.n_keys, asynchronous=True)
@@ -76,12 +55,10 @@ def test_segments_resident_async(seg_env):
     np.testing.assert_array_equal((rec >> 16) - 1, orc["fail_event"])
 
 
-def test_low_overlap_split_by_default(seg_env):
+def test_low_overlap_split_by_default():
     """Clients that think longer than an op takes (the demo's 10 Hz per
     thread against millisecond latencies): quiescent points are frequent,
     the default choice cuts the keys, and the verdicts equal the oracle's."""
-    seg_env.pop("LC_SPLIT", None)
-    seg_env.pop("LC_SEG_LEN", None)
     h = H.synth(n_keys=64, ops_per_key=4000, concurrency=10, mean_think=20.0, anomaly_rate=0.25, seed=88)
     pk = Packed(h)
     dev = Device(0)

@@ -6,12 +6,11 @@ meet -- and walk the segments in order.  Verdicts, causes and failing events
 must equal the oracle's and the unsegmented search's, whatever the segment
 count and checkpoint distances (tiny distances make runs miss each other and
 exercise the fallback to the unsegmented search)."""
-import os
-
 import numpy as np
 import pytest
 
 import cref
+from lincheck import _native as N
 from lincheck import history as H
 from lincheck.checker import Device, Packed
 
@@ -28,18 +27,6 @@ SHAPES = {
     "short_keys": dict(n_keys=500, ops_per_key=150, concurrency=10, anomaly_rate=0.2, seed=98),
     "think20": dict(n_keys=64, ops_per_key=3000, concurrency=10, mean_think=20.0, anomaly_rate=0.25, seed=99),
 }
-ENV = ("LC_SPEC", "LC_SPEC_SEGS", "LC_SPEC_CK1", "LC_SPEC_CK2", "LC_SPLIT")
-
-
-@pytest.fixture
-def spec_env():
-    saved = {k: os.environ.get(k) for k in ENV}
-    yield os.environ
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
 
 
 def _check(dev, pk, orc, what):
@@ -50,29 +37,25 @@ def _check(dev, pk, orc, what):
 
 
 @pytest.mark.parametrize("shape", sorted(SHAPES))
-def test_spec_matches_oracle(shape, spec_env):
+def test_spec_matches_oracle(shape):
     h = H.synth(**SHAPES[shape])
     pk = Packed(h)
-    dev = Device(0)
-    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
-    spec_env["LC_SPLIT"] = "0"
-    spec_env["LC_SPEC"] = "0"
-    _check(dev, pk, orc, "unsegmented")
-    spec_env["LC_SPEC"] = "1"
-    for segs in ("2", "3", "4", "6", "8"):
-        spec_env["LC_SPEC_SEGS"] = segs
-        for ck in (("32", "160"), ("1", "2"), ("0", "0")):
-            spec_env["LC_SPEC_CK1"], spec_env["LC_SPEC_CK2"] = ck
+    _, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)
+    _check(Device(0, path_flags=N.LC_PATH_SPLIT_OFF | N.LC_PATH_SPEC_OFF), pk, orc, "unsegmented")
+    for segs in (2, 3, 4, 6, 8):
+        for ck in ((32, 160), (1, 2), (0, 0)):
+            dev = Device(0, path_flags=N.LC_PATH_SPLIT_OFF, spec_segs=segs, spec_ck=ck)
             _check(dev, pk, orc, f"segs {segs} ck {ck}")
+    # the round-2 cut placement (equal event counts instead of equal cost)
+    even = Device(0, path_flags=N.LC_PATH_SPLIT_OFF | N.LC_PATH_SPEC_EVEN, spec_segs=4)
+    _check(even, pk, orc, "segs 4, even cuts")
     if SHAPES[shape].get("anomaly_rate"):
         assert (orc["valid"] == 0).any()
 
 
-def test_spec_default_on_c2_shape(spec_env):
+def test_spec_default_on_c2_shape():
     """The default choice for a C2-sized verdicts-only batch is the
     speculative path (checked through its result only: same as the oracle)."""
-    for k in ENV:
-        spec_env.pop(k, None)
     h = H.synth(n_keys=1000, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=100)
     pk = Packed(h)
     dev = Device(0)
@@ -80,11 +63,8 @@ def test_spec_default_on_c2_shape(spec_env):
     _check(dev, pk, orc, "default")
 
 
-def test_spec_resident_async(spec_env):
+def test_spec_resident_async():
     """The bench's resident steps (node records, asynchronous) on the speculative path."""
-    for k in ENV:
-        spec_env.pop(k, None)
-    spec_env["LC_SPEC"] = "1"
     h = H.synth(n_keys=1000, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=101)
     pk = Packed(h)
     dev = Device(0)

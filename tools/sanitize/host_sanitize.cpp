@@ -175,6 +175,18 @@ int main(int argc, char **argv) {
                 lc_hist_free(x);
             }
         }
+        // footers where they do not belong: inside a closed list (refused, no
+        // loop), after an open list of op maps (the list ends there)
+        {
+            const uint8_t closed_footer[] = {0xED, 0xCF};
+            lc_hist *x = nullptr;
+            CHECK(lc_fressian_parse(closed_footer, 2, &x) != LC_OK && !x);
+            const uint8_t counted_footer[] = {0xE6, 0x01, 0xCF, 0xCF, 0xCF, 0xCF};
+            CHECK(lc_fressian_parse(counted_footer, 6, &x) != LC_OK && !x);
+            const uint8_t open_footer[] = {0xEE, 0xCF, 0xCF, 0xCF, 0xCF, 0, 0, 0, 1, 0, 0, 0, 0};
+            CHECK(lc_fressian_parse(open_footer, (int64_t)sizeof open_footer, &x) == LC_OK && x);
+            if (x) lc_hist_free(x);
+        }
         lc_hist_free(h);
     }
     // :txn histories in EDN (multi-register): parsed, packed, and mangled

@@ -14,13 +14,13 @@ from lincheck import history as H  # noqa: E402
 from lincheck.checker import Device, Packed  # noqa: E402
 
 keys = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
-os.environ["LC_SPEC"] = "1"
+S = int(sys.argv[2]) if len(sys.argv) > 2 else 4         # segments per key (lc_opts.spec_segs)
+flags = int(sys.argv[3], 0) if len(sys.argv) > 3 else 0  # lc_opts.path_flags (e.g. 0x100: even cuts)
 h = H.synth(n_keys=keys, ops_per_key=1000, concurrency=10, seed=2)
 pk = Packed(h)
-dev = Device(0)
+dev = Device(0, spec_segs=S, path_flags=flags)
 for _ in range(10):
     st = dev.check(pk, verdicts_only=True).stats
-S = int(os.environ.get("LC_SPEC_SEGS", "4"))
 nb = min(keys, 4096)
 buf = np.zeros(nb * 8 * 12, np.uint64)
 N.lib().lc_debug_spec_stamps(buf.ctypes.data_as(C.c_void_p), nb)
