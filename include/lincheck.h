@@ -350,7 +350,9 @@ typedef struct lc_opts {
 #define LC_PATH_CHUNKS_OFF   0x80  /* lc_check_node: one upload whatever the size      */
 #define LC_PATH_SPEC_EVEN    0x100 /* speculative cuts at equal event counts (round 2)
                                       instead of equal estimated cost               */
-#define LC_PATH_ALL          0x1FF
+#define LC_PATH_EV32         0x200 /* upload 32-bit event words even when 16-bit ones
+                                      are given (lc_batch.events16)                 */
+#define LC_PATH_ALL          0x3FF
 
 /* lc_opts.flags */
 #define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -32,6 +33,12 @@ struct PinnedAlloc {
         return (T *)p;
     }
     void deallocate(T *p, size_t) { pinned_free(p); }
+    // resize() default-initialises (no zero fill: the arrays are written
+    // whole, in parallel, right after)
+    template <class U>
+    void construct(U *p) noexcept { ::new ((void *)p) U; }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) { ::new ((void *)p) U(static_cast<A &&>(a)...); }
     template <class U>
     bool operator==(const PinnedAlloc<U> &) const { return true; }
     template <class U>
@@ -40,12 +47,29 @@ struct PinnedAlloc {
 template <class T>
 using pinned_vector = std::vector<T, PinnedAlloc<T>>;
 
+// std::allocator whose resize() default-initialises (no zero fill)
+template <class T>
+struct UninitAlloc : std::allocator<T> {
+    using value_type = T;
+    UninitAlloc() = default;
+    template <class U>
+    UninitAlloc(const UninitAlloc<U> &) {}
+    template <class U>
+    struct rebind { using other = UninitAlloc<U>; };
+    template <class U>
+    void construct(U *p) noexcept { ::new ((void *)p) U; }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) { ::new ((void *)p) U(static_cast<A &&>(a)...); }
+};
+template <class T>
+using uninit_vector = std::vector<T, UninitAlloc<T>>;
+
 }  // namespace lc
 
 // Owned history: the storage behind lc_synth_generate / lc_edn_read.
 struct lc_hist {
-    std::vector<uint8_t> type, f;
-    std::vector<int64_t> process, key, v0, v1, index;
+    lc::uninit_vector<uint8_t> type, f;
+    lc::uninit_vector<int64_t> process, key, v0, v1, index;
     std::vector<int64_t> anomalous_keys;
     // :txn micro-ops (lc_history.mop_off / mop); empty when no row is a :txn
     std::vector<int64_t> mop_off, mop;

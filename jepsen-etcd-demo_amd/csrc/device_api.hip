@@ -225,7 +225,10 @@ struct DevBatch {
     char *hmeta = nullptr;
     size_t hmeta_cap = 0;
     hipEvent_t hmeta_done = nullptr;
-    uint16_t *events16 = nullptr;    // device staging of 16-bit event words (mem[3])
+    uint16_t *events16 = nullptr;    // 16-bit event words (mem[3]), or null: a register-tier batch
+                                     // uploaded at 2 bytes per event (lc_batch.events16)
+    mutable bool ev32_ready = true;  // `events` holds the 32-bit words (else widened, once, by the
+                                     // first step whose kernels read them: all but k_spec)
     // the LPT order of the last upload and the offsets it was computed from
     // (a batch re-uploaded with the same offsets reuses it)
     std::vector<uint64_t> order_off;
@@ -885,16 +888,16 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     // page-locked 16-bit words crosses the host link at 2 bytes per event and
     // is widened on the device (the register tier validates what it reads).
     HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
-    const bool use16 = d->n_events && b->events16 && sh.t0_only &&
+    const bool use16 = d->n_events && b->events16 && sh.t0_only && !(c->o->path_flags & LC_PATH_EV32) &&
                        (!events_src || events_src == b->events) && pinned(b->events16);
+    d->ev32_ready = !use16;
     if (use16) {
+        // widened on the device only if a step's kernels need the 32-bit
+        // words (dev_search); the speculative segments read these in place
         HIPCHK(grow(d->mem[3], d->events16, (size_t)d->n_events + 4));
         HIPCHK(hipMemcpyAsync(d->events16, b->events16, (size_t)d->n_events * 2, hipMemcpyHostToDevice, cs));
-        const uint64_t n4 = (d->n_events + 3) / 4;
-        const int blocks = (int)std::min<uint64_t>((n4 + 255) / 256, (uint64_t)c->cu_count * 8);
-        hipLaunchKernelGGL(k_widen16, dim3(std::max(blocks, 1)), dim3(256), 0, cs, d->events16, d->events, d->n_events);
-        HIPCHK(hipGetLastError());
     } else if (d->n_events) {
+        d->events16 = nullptr;
         HIPCHK(hipMemcpyAsync(d->events, events_src ? events_src : b->events, (size_t)d->n_events * 4,
                               hipMemcpyHostToDevice, cs));
     }
@@ -1095,6 +1098,17 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             c->spec_rr_cap = K + 2;
         }
     }
+    // The speculative segments read 16-bit event words in place; every other
+    // kernel reads the 32-bit form, widened here once per upload.
+    const uint16_t *ev16 = (spec && d->events16) ? d->events16 : nullptr;
+    if (!ev16 && !d->ev32_ready && d->n_events) {
+        const uint64_t n4 = (d->n_events + 3) / 4;
+        const int blocks = (int)std::min<uint64_t>((n4 + 255) / 256, (uint64_t)c->cu_count * 8);
+        hipLaunchKernelGGL(k_widen16, dim3(std::max(blocks, 1)), dim3(256), 0, c->stream, d->events16, d->events,
+                           d->n_events);
+        HIPCHK(hipGetLastError());
+        d->ev32_ready = true;
+    }
     uint32_t ticket_base = 0;
     if (t0_step && c->ticket_live) {
         ticket_base = c->ticket_next;
@@ -1177,7 +1191,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         // the same launch (a second stream cost ~40 us of cross-stream waits)
         const int vblocks = a.strict ? (int)std::min<int64_t>(K, c->cu_count) : 0;
         HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2, c->cu_count * 8,
-                                vblocks, c->stream));
+                                vblocks, ev16, (o.path_flags & LC_PATH_SPEC_EVEN) != 0, c->stream));
         c->spec_parity ^= 1;
         if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0 && !d->table) {

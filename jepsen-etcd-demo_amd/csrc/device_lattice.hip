@@ -66,6 +66,22 @@ uint32_t t0_max_states() { return T0_MAX_STATES; }
 
 struct Xfer { uint32_t k, cap, b, m; };
 
+// A key's event words as the register tier reads them: the 32-bit form, or
+// the 16-bit form lc_pack emits when every word fits (lc_batch.events16,
+// LC_EV16_WIDE), read in place -- half the bytes per event and no widening
+// pass over the batch before the search.
+template <bool E16> struct EvSrc;
+template <> struct EvSrc<false> {
+    const uint32_t *p;
+    __device__ __forceinline__ uint32_t operator[](uint64_t j) const { return p[j]; }
+    __device__ __forceinline__ EvSrc operator+(uint64_t o) const { return {p + o}; }
+};
+template <> struct EvSrc<true> {
+    const uint16_t *p;
+    __device__ __forceinline__ uint32_t operator[](uint64_t j) const { return LC_EV16_WIDE(p[j]); }
+    __device__ __forceinline__ EvSrc operator+(uint64_t o) const { return {p + o}; }
+};
+
 __device__ __forceinline__ Xfer xfer_of(uint32_t d) {
     const uint32_t f = d & 3u, a = (d >> 2) & 0x7FFFu, b = d >> 17;
     const uint32_t abit = a < 32u ? 1u << (a & 31u) : 0u;
@@ -214,9 +230,12 @@ constexpr uint32_t T0_COUNT = 1, T0_WANT_PEAK = 2, T0_DBG_NOEVENTS = 4, T0_DBG_N
 // as it walks it, and a key that would leave T0 is an error, not a spill (no
 // later tier is launched to take it).
 constexpr uint32_t T0_STRICT = 32;
+// k_spec: cuts at equal event counts (round 2) instead of equal estimated cost
+constexpr uint32_t T0_SPEC_EVEN = 64;
 struct T0Args {
     const uint64_t *ev_off;
     const uint32_t *events;
+    const uint16_t *events16;    // the same words in 16 bits, or null (E16 kernels read these)
     const uint32_t *trans;
     const uint32_t *trans_off;   // may be null
     const uint8_t *key_width;    // may be null
@@ -238,6 +257,12 @@ struct T0Args {
     int32_t *spec_nrr;           //   their count (zero at the launch)
     int32_t *spec_nrr_next;      //   and the next launch's count (zeroed by k_spec_rerun)
 };
+
+template <bool E16>
+__device__ __forceinline__ EvSrc<E16> ev_src(const T0Args &a) {
+    if constexpr (E16) return {a.events16};
+    else return {a.events};
+}
 
 __device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint32_t why) {
     if (lane_id() == 0) {
@@ -772,7 +797,7 @@ extern "C" int lc_debug_t0_prof(unsigned long long *host) {
 // FAST: no probe counting, no peak sizes and a budget no lattice can exceed
 // (>= 16 x 64 x 32 configs), so every size reduction and budget test folds
 // away -- the common case, and the bench's.
-template <int RM, bool FAST>
+template <int RM, bool FAST, bool E16 = false>
 __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_t *ws) {
     const uint32_t lane = lane_id();
     const LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
@@ -792,7 +817,7 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
     const uint64_t budget = FAST ? ~0ull : a.budget;
     const bool want_peak = !FAST && (a.flags & T0_WANT_PEAK) != 0;
     const bool count = !FAST && (a.flags & T0_COUNT) != 0;
-    const uint32_t *const evp = a.events + eb;
+    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
     // The key may name transitions trans[tb + t], t < ntr.  A batch the host
     // did not validate may hold larger ids: they load nothing (the event is
     // then a read of nil), and the batch's validation waves report them.
@@ -1062,7 +1087,7 @@ __device__ unsigned long long lc_t0_stamps[8192 * 6];
 // window slots up to 126 (two pending words), the slot-127 marker of ops
 // beyond the encodable window exempt from the slot protocol (the search stops
 // before it follows one), and every :invoke's slot below the key's key_width.
-template <bool GEN>
+template <bool GEN, bool E16 = false>
 __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     const uint32_t lane = lane_id();
     if (a.key_error && a.key_error[k]) return;
@@ -1076,7 +1101,7 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     for (uint64_t base = eb; base < ee && !why; base += 64) {
         const uint64_t j = base + lane;
         const bool in = j < ee;
-        const uint32_t w = in ? a.events[j] : 0u;
+        const uint32_t w = in ? (E16 ? LC_EV16_WIDE(a.events16[j]) : a.events[j]) : 0u;
         const bool ok = (w & LC_EV_OK_BIT) != 0;
         const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
         const uint32_t d = (in && !ok && t < ntr) ? a.trans[tb + t] : 0u;
@@ -1619,12 +1644,12 @@ __device__ __forceinline__ uint64_t uni(uint64_t x) {
     return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
 }
 
-// Segment boundaries: targets at s/eff of the key's events (s = 1 .. eff-1),
-// lane s of pos_v, with the ops pending there in lane s of pend_v (one pass
-// of ballots over the events before the last target, 8 chunks' loads in
-// flight).  Weighting :oks by their cost (9-10 pending ones cost ~20 events'
-// time) balanced the segments no better and cost 5x the time here.
-__device__ __forceinline__ void spec_targets(const uint32_t *evp, uint32_t nev, uint32_t eff, uint32_t &pos_v,
+// Segment boundaries (T0_SPEC_EVEN, the round-2 placement): targets at s/eff
+// of the key's events (s = 1 .. eff-1), lane s of pos_v, with the ops pending
+// there in lane s of pend_v (one pass of ballots over the events before the
+// last target, 8 chunks' loads in flight).
+template <class EvT>
+__device__ __forceinline__ void spec_targets(EvT evp, uint32_t nev, uint32_t eff, uint32_t &pos_v,
                                              int32_t &pend_v) {
     constexpr uint32_t G = 8;
     const uint32_t lane = lane_id();
@@ -1659,6 +1684,106 @@ __device__ __forceinline__ void spec_targets(const uint32_t *evp, uint32_t nev, 
     }
 }
 
+// Estimated cost of an event, in 1/8 of a lane-phase event: the per-event fit
+// of DESIGN.md section 3 (707 cycles per event, +171 per :ok with 7-8 ops
+// pending, ~21k per :ok with 9-10 pending -- the last in the LDS workspace).
+constexpr uint32_t SPEC_W_EV = 8, SPEC_W_MID = 2, SPEC_W_HEAVY = 240;
+
+// One 64-event chunk's classes (w: lane i holds event base + i; cnt: ops
+// pending before the chunk): the lanes that are events, :oks with 7-8 and
+// with 9-10 ops pending, each lane's pending count before its event, and the
+// chunk's cost.  Pending counts come from two ballots and mbcnt (no scan).
+struct ChunkCost {
+    uint64_t in, inv, oks, mid, heavy;
+    int32_t pend;   // per lane: ops pending before the lane's event
+    uint32_t cost;  // the chunk's, uniform
+};
+__device__ __forceinline__ ChunkCost chunk_cost(uint32_t w, uint32_t base, uint32_t nev, int32_t cnt) {
+    const uint32_t lane = lane_id();
+    ChunkCost c;
+    const bool in = base + lane < nev;
+    const bool ok = in && (w >> 31);
+    c.in = __ballot(in);
+    c.inv = __ballot(in && !ok);
+    c.oks = __ballot(ok);
+    c.pend = cnt + (int32_t)rank_of(c.inv) - (int32_t)rank_of(c.oks);
+    c.mid = __ballot(ok && c.pend >= 7 && c.pend <= 8);
+    c.heavy = __ballot(ok && c.pend >= 9);
+    c.cost = SPEC_W_EV * (uint32_t)__popcll(c.in) + SPEC_W_MID * (uint32_t)__popcll(c.mid) +
+             SPEC_W_HEAVY * (uint32_t)__popcll(c.heavy);
+    return c;
+}
+
+// Segment boundaries at equal estimated cost: target s (1 .. eff-1) at
+// s/eff of the key's total cost (chunk_cost), lane s of pos_v, with the ops
+// pending there in lane s of pend_v.  Two passes of ballots over the key's
+// events (the total, then the targets), 8 chunks' loads in flight.  A
+// segment's walk time is its events plus its 9-10-pending :oks (~30 events'
+// time each, 2-5 of them in the slowest walks): equal event counts left the
+// slowest of C2's 4,000 walks at 1.65x the median.
+template <class EvT>
+__device__ __forceinline__ void spec_targets_cost(EvT evp, uint32_t nev, uint32_t eff, uint32_t &pos_v,
+                                                  int32_t &pend_v) {
+    constexpr uint32_t G = 8;
+    const uint32_t lane = lane_id();
+    uint32_t total = 0;
+    int32_t cnt = 0;
+    for (uint32_t gb = 0; gb < nev; gb += 64 * G) {
+        uint32_t wg[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t j = gb + 64 * g + lane;
+            wg[g] = j < nev ? evp[j] : 0u;
+        }
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t base = gb + 64 * g;
+            if (base >= nev) continue;
+            const ChunkCost c = chunk_cost(wg[g], base, nev, cnt);
+            total += c.cost;
+            cnt += __popcll(c.inv) - __popcll(c.oks);
+        }
+    }
+    pos_v = 0;
+    pend_v = 0;
+    uint32_t next = 1, acc = 0;
+    uint32_t t_next = (uint32_t)((uint64_t)total / eff);
+    cnt = 0;
+    for (uint32_t gb = 0; gb < nev && next < eff; gb += 64 * G) {
+        uint32_t wg[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t j = gb + 64 * g + lane;
+            wg[g] = j < nev ? evp[j] : 0u;
+        }
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t base = gb + 64 * g;
+            if (base >= nev || next >= eff) continue;
+            const ChunkCost c = chunk_cost(wg[g], base, nev, cnt);
+            if (acc + c.cost >= t_next) {
+                // each lane's cost up to and including its event
+                const uint64_t me = 1ull << lane;
+                const uint32_t incl = SPEC_W_EV * (rank_of(c.in) + 1u) +
+                                      SPEC_W_MID * (rank_of(c.mid) + ((c.mid & me) ? 1u : 0u)) +
+                                      SPEC_W_HEAVY * (rank_of(c.heavy) + ((c.heavy & me) ? 1u : 0u));
+                const bool in = (c.in & me) != 0;
+                while (next < eff && acc + c.cost >= t_next) {
+                    const uint64_t hit = __ballot(in && acc + incl >= t_next);
+                    const uint32_t l = (uint32_t)__builtin_ctzll(hit);
+                    const int32_t at = __builtin_amdgcn_readlane(c.pend, l);
+                    pos_v = lane == next ? base + l : pos_v;
+                    pend_v = lane == next ? at : pend_v;
+                    ++next;
+                    t_next = (uint32_t)((uint64_t)total * next / eff);
+                }
+            }
+            acc += c.cost;
+            cnt += __popcll(c.inv) - __popcll(c.oks);
+        }
+    }
+}
+
 // The cut for target position t (c_t ops pending there): of the boundaries t
 // .. t + 64 (t + i = before event t + i), the one with the fewest ops pending,
 // the earliest of those, if that is at most SPEC_MAX_PEND and it lies inside
@@ -1681,7 +1806,8 @@ __device__ __forceinline__ uint32_t spec_cut_at(uint32_t w, uint32_t nev, uint32
 // The ops pending at boundary c (n expected, n <= 6): each slot is decided by
 // its last event before c, walking back.  Returns their :invoke words in slot
 // order, word j in lane j; found = how many.
-__device__ __forceinline__ uint32_t spec_pending(const uint32_t *evp, uint32_t c, uint32_t n, uint32_t &found) {
+template <class EvT>
+__device__ __forceinline__ uint32_t spec_pending(EvT evp, uint32_t c, uint32_t n, uint32_t &found) {
     const uint32_t lane = lane_id();
     uint64_t seen = 0, pm = 0;
     uint32_t byslot = 0;
@@ -1753,8 +1879,8 @@ __device__ __forceinline__ void spec_setup(SpecState &st, uint32_t words, uint32
 // keep 4 waves per SIMD within the CU's LDS.
 template <int S>
 constexpr int spec_lds_ws() { return S <= 3 ? 1 : S <= 6 ? 2 : 3; }
-template <int MODE, int NWS>
-__device__ __forceinline__ int spec_walk(const uint32_t *evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
+template <int MODE, int NWS, class EvT>
+__device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
                                          uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
                                          int32_t *lds_busy, uint32_t (*ck_w)[64], int32_t *ck_e, uint32_t ck1,
                                          uint32_t ck2, uint32_t &fev_out) {
@@ -1762,7 +1888,7 @@ __device__ __forceinline__ int spec_walk(const uint32_t *evp, const uint32_t *tr
     const uint32_t lane = lane_id();
     LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
     int32_t held = -1;  // LDS slot held
-    const uint32_t *const ep = evp + b;
+    const EvT ep = evp + b;
     const uint32_t nev = e_end - b;
     auto ldesc = [&](uint32_t w, bool have) -> uint32_t {
         const uint32_t t = LC_EV_TRANS(w);
@@ -1954,7 +2080,7 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 // One workgroup of S waves per key (blockIdx = LPT position).  Results go
 // through a.full like T0's; a.lat_ws holds each wave's 9-10-pending
 // workspace (global memory: with LDS for it, fewer segments fit a CU).
-template <int S>
+template <int S, bool E16>
 __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
     __shared__ uint32_t s_ck[S][2][64];   // TOP run's checkpoint sets
@@ -1972,14 +2098,15 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
         // T0_STRICT steps: the event-by-event validation, in blocks after the
         // keys' (no second stream, no cross-stream waits around the step)
         const int64_t nb = (int64_t)gridDim.x - a.n_order;
-        for (int64_t k = ((int64_t)blockIdx.x - a.n_order) * S + wv; k < a.n_order; k += nb * S) validate_key<false>(a, k);
+        for (int64_t k = ((int64_t)blockIdx.x - a.n_order) * S + wv; k < a.n_order; k += nb * S)
+            validate_key<false, E16>(a, k);
         return;  // the whole block: no barrier below is reached by half of it
     }
     const int32_t key = a.order[blockIdx.x];
     uint32_t *ws = a.lat_ws + ((size_t)blockIdx.x * S + wv) * (3 * T0_RMEM * 64);
     const uint64_t eb = a.ev_off[key];
     const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
-    const uint32_t *const evp = a.events + eb;
+    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
     const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
@@ -2002,7 +2129,8 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     if (!plain && wv < eff) {
         uint32_t pos_v;
         int32_t pend_v;
-        spec_targets(evp, nev, eff, pos_v, pend_v);
+        if (a.flags & T0_SPEC_EVEN) spec_targets(evp, nev, eff, pos_v, pend_v);
+        else spec_targets_cost(evp, nev, eff, pos_v, pend_v);
         // every cut (each wave computes them all, so all agree): a cut is
         // kept if it lies past the last kept one
         uint32_t cut = 0, end = nev, n0 = 0, last = 0;
@@ -2145,13 +2273,14 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
 }
 
 // The keys k_spec left to the unsegmented search (compact T0, FAST).
+template <bool E16>
 __global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
     __shared__ uint32_t ws[3 * T0_RMEM * 64];
     const int32_t n = *a.spec_nrr;
     if (blockIdx.x == 0 && lane_id() == 0) *a.spec_nrr_next = 0;  // two counters in turn: no memset per step
     for (int32_t w = blockIdx.x; w < n; w += gridDim.x) {
         const int32_t key = a.spec_rr[w];
-        const int kr = lattice_key<T0_RSMALL, true>(a, key, ws);
+        const int kr = lattice_key<T0_RSMALL, true, E16>(a, key, ws);
         if (kr == K_SPILL) {
             const Args &f = *a.full;
             if (a.flags & T0_STRICT) {
@@ -2173,8 +2302,11 @@ size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t
 // zero, and k_spec_rerun zeroes the other -- then the rerun list).
 // validate: add the T0_STRICT validation blocks.
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, int parity,
-                       uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, hipStream_t s) {
+                       uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
+                       bool even_cuts, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
+    t.events16 = events16;
+    if (even_cuts) t.flags |= T0_SPEC_EVEN;
     t.lat_ws = ws;
     t.spec_ck1 = ck1;
     t.spec_ck2 = ck2;
@@ -2182,14 +2314,24 @@ hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws,
     t.spec_nrr_next = rr + ((parity & 1) ^ 1);
     t.spec_rr = rr + 2;
     const dim3 grid((unsigned)std::max(1, a.n_order + std::max(0, validate_blocks)));
-    if (segs >= 8) hipLaunchKernelGGL(k_spec<8>, grid, dim3(512), 0, s, t);
-    else if (segs >= 6) hipLaunchKernelGGL(k_spec<6>, grid, dim3(384), 0, s, t);
-    else if (segs >= 4) hipLaunchKernelGGL(k_spec<4>, grid, dim3(256), 0, s, t);
-    else if (segs >= 3) hipLaunchKernelGGL(k_spec<3>, grid, dim3(192), 0, s, t);
-    else hipLaunchKernelGGL(k_spec<2>, grid, dim3(128), 0, s, t);
+    const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid)));
+    if (events16) {
+        if (segs >= 8) hipLaunchKernelGGL((k_spec<8, true>), grid, dim3(512), 0, s, t);
+        else if (segs >= 6) hipLaunchKernelGGL((k_spec<6, true>), grid, dim3(384), 0, s, t);
+        else if (segs >= 4) hipLaunchKernelGGL((k_spec<4, true>), grid, dim3(256), 0, s, t);
+        else if (segs >= 3) hipLaunchKernelGGL((k_spec<3, true>), grid, dim3(192), 0, s, t);
+        else hipLaunchKernelGGL((k_spec<2, true>), grid, dim3(128), 0, s, t);
+    } else {
+        if (segs >= 8) hipLaunchKernelGGL((k_spec<8, false>), grid, dim3(512), 0, s, t);
+        else if (segs >= 6) hipLaunchKernelGGL((k_spec<6, false>), grid, dim3(384), 0, s, t);
+        else if (segs >= 4) hipLaunchKernelGGL((k_spec<4, false>), grid, dim3(256), 0, s, t);
+        else if (segs >= 3) hipLaunchKernelGGL((k_spec<3, false>), grid, dim3(192), 0, s, t);
+        else hipLaunchKernelGGL((k_spec<2, false>), grid, dim3(128), 0, s, t);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_spec_rerun, dim3((unsigned)std::max(1, std::min(a.n_order, rerun_grid))), dim3(64), 0, s, t);
+    if (events16) hipLaunchKernelGGL(k_spec_rerun<true>, rgrid, dim3(64), 0, s, t);
+    else hipLaunchKernelGGL(k_spec_rerun<false>, rgrid, dim3(64), 0, s, t);
     return hipGetLastError();
 }
 

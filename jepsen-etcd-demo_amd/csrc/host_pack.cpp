@@ -35,6 +35,9 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <thread>
 #include <unordered_map>
 
@@ -391,53 +394,118 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
     const int64_t n = h->n;
     lc_packed *P = new (std::nothrow) lc_packed();
     if (!P) return lc::fail(LC_E_NOMEM, "lc_pack: out of memory");
+    static const bool timing = std::getenv("LC_TIMING") != nullptr;
+    auto tprev = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "lc_pack: %-28s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - tprev).count());
+        tprev = t;
+    };
     try {
         // ---- A2: key discovery + bucketing (stable) ----
-        std::unordered_map<int64_t, int32_t> kidx;
+        // Rows in contiguous ranges, one per thread: each range numbers its
+        // keys in order of first appearance; the ranges' key lists are then
+        // merged in range order (= the order of first appearance in the
+        // history), and the rows are bucketed by key through per-range counts.
+        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        const unsigned nr = n >= (1 << 20) ? hw : 1u;
+        auto range_rows = [&](const auto &fn) {
+            auto work = [&](unsigned t) { fn(t, n * (int64_t)t / nr, n * (int64_t)(t + 1) / nr); };
+            std::vector<std::thread> pool;
+            for (unsigned t = 1; t < nr; ++t) pool.emplace_back(work, t);
+            work(0);
+            for (auto &th : pool) th.join();
+        };
         std::vector<int32_t> row_key((size_t)n);
-        int64_t last_key = LC_NO_KEY;
-        int32_t last_idx = -1;
-        for (int64_t r = 0; r < n; ++r) {
-            if (h->type[r] > LC_INFO || h->f[r] > LC_F_TXN) {
-                delete P;
-                return lc::fail(LC_E_INVALID, "lc_pack: row %lld has a bad :type/:f code", (long long)r);
-            }
-            if (h->mop_off && h->mop && (h->mop_off[r] < 0 || h->mop_off[r + 1] < h->mop_off[r])) {
-                delete P;
-                return lc::fail(LC_E_INVALID, "lc_pack: mop_off not monotone at row %lld", (long long)r);
-            }
-            int64_t k = h->key[r];
-            if (k == LC_NO_KEY) {
-                row_key[(size_t)r] = -1;
-                // Non-tuple ops are shared by every sub-history (subhistory keeps
-                // them): the nemesis's :info ops are no-ops there, and any other
-                // op is paired and stepped in every key as it stands.
-                P->shared_rows.push_back(r);
-                continue;
-            }
-            if (k != last_key || last_idx < 0) {
-                auto it = kidx.find(k);
-                if (it == kidx.end()) {
-                    it = kidx.emplace(k, (int32_t)P->keys.size()).first;
-                    P->keys.push_back(k);
+        std::vector<std::vector<int64_t>> rkeys(nr), rshared(nr);
+        std::vector<int64_t> bad_row(nr, -1), bad_mop(nr, -1);
+        range_rows([&](unsigned t, int64_t r0, int64_t r1) {
+            std::unordered_map<int64_t, int32_t> kidx;
+            int64_t last_key = LC_NO_KEY;
+            int32_t last_idx = -1;
+            for (int64_t r = r0; r < r1; ++r) {
+                if (h->type[r] > LC_INFO || h->f[r] > LC_F_TXN) { bad_row[t] = r; return; }
+                if (h->mop_off && h->mop && (h->mop_off[r] < 0 || h->mop_off[r + 1] < h->mop_off[r])) {
+                    bad_mop[t] = r;
+                    return;
                 }
-                last_key = k;
-                last_idx = it->second;
+                const int64_t k = h->key[r];
+                if (k == LC_NO_KEY) {
+                    row_key[(size_t)r] = -1;
+                    // Non-tuple ops are shared by every sub-history (subhistory keeps
+                    // them): the nemesis's :info ops are no-ops there, and any other
+                    // op is paired and stepped in every key as it stands.
+                    rshared[t].push_back(r);
+                    continue;
+                }
+                if (k != last_key || last_idx < 0) {
+                    auto it = kidx.find(k);
+                    if (it == kidx.end()) {
+                        it = kidx.emplace(k, (int32_t)rkeys[t].size()).first;
+                        rkeys[t].push_back(k);
+                    }
+                    last_key = k;
+                    last_idx = it->second;
+                }
+                row_key[(size_t)r] = last_idx;  // the range's own number, for now
             }
-            row_key[(size_t)r] = last_idx;
+        });
+        for (unsigned t = 0; t < nr; ++t) {
+            if (bad_row[t] >= 0) {
+                delete P;
+                return lc::fail(LC_E_INVALID, "lc_pack: row %lld has a bad :type/:f code", (long long)bad_row[t]);
+            }
+            if (bad_mop[t] >= 0) {
+                delete P;
+                return lc::fail(LC_E_INVALID, "lc_pack: mop_off not monotone at row %lld", (long long)bad_mop[t]);
+            }
+        }
+        std::vector<std::vector<int32_t>> rglobal(nr);  // range key number -> packed key
+        {
+            std::unordered_map<int64_t, int32_t> kidx;
+            for (unsigned t = 0; t < nr; ++t) {
+                for (int64_t k : rkeys[t]) {
+                    auto it = kidx.emplace(k, (int32_t)P->keys.size());
+                    if (it.second) P->keys.push_back(k);
+                    rglobal[t].push_back(it.first->second);
+                }
+                P->shared_rows.insert(P->shared_rows.end(), rshared[t].begin(), rshared[t].end());
+            }
         }
         const int64_t K = (int64_t)P->keys.size();
+        // per-range counts of each key's rows: the range's write positions
+        std::vector<std::vector<uint64_t>> rcount(nr, std::vector<uint64_t>());
+        range_rows([&](unsigned t, int64_t r0, int64_t r1) {
+            std::vector<uint64_t> &c = rcount[t];
+            c.assign((size_t)K, 0);
+            const std::vector<int32_t> &g = rglobal[t];
+            for (int64_t r = r0; r < r1; ++r) {
+                int32_t &rk = row_key[(size_t)r];
+                if (rk < 0) continue;
+                rk = g[(size_t)rk];
+                ++c[(size_t)rk];
+            }
+        });
+        lap("A2 key discovery");
         P->krow_off.assign((size_t)K + 1, 0);
-        for (int64_t r = 0; r < n; ++r)
-            if (row_key[(size_t)r] >= 0) P->krow_off[(size_t)row_key[(size_t)r] + 1]++;
-        for (int64_t k = 0; k < K; ++k) P->krow_off[(size_t)k + 1] += P->krow_off[(size_t)k];
-        P->krows.resize((size_t)P->krow_off[(size_t)K]);
-        {
-            std::vector<uint64_t> cur(P->krow_off.begin(), P->krow_off.end() - 1);
-            for (int64_t r = 0; r < n; ++r)
-                if (row_key[(size_t)r] >= 0) P->krows[cur[(size_t)row_key[(size_t)r]]++] = r;
+        for (int64_t k = 0; k < K; ++k) {
+            uint64_t at = P->krow_off[(size_t)k];
+            for (unsigned t = 0; t < nr; ++t) {
+                const uint64_t c = rcount[t][(size_t)k];
+                rcount[t][(size_t)k] = at;  // where range t writes key k's rows
+                at += c;
+            }
+            P->krow_off[(size_t)k + 1] = at;
         }
+        P->krows.resize((size_t)P->krow_off[(size_t)K]);
+        range_rows([&](unsigned t, int64_t r0, int64_t r1) {
+            std::vector<uint64_t> &cur = rcount[t];
+            for (int64_t r = r0; r < r1; ++r)
+                if (row_key[(size_t)r] >= 0) P->krows[cur[(size_t)row_key[(size_t)r]]++] = r;
+        });
         std::vector<int32_t>().swap(row_key);
+        lap("A2 bucketing");
 
         // ---- A3: per-key pairing, fail-drop, slots (parallel over keys) ----
         std::vector<KeyOut> ko((size_t)K);
@@ -463,6 +531,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             work(0);
             for (auto &th : pool) th.join();
         }
+        lap("A3 pairing (parallel)");
         for (int64_t k = 0; k < K; ++k) {
             KeyOut &o = ko[(size_t)k];
             if (!o.err) continue;
@@ -486,28 +555,57 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         }
 
         // ---- A4/A5: register states + transition descriptors ----
-        // A state is a value some surviving write / cas could install.
-        auto state_values = [&](const KeyOut &o, std::vector<int64_t> &vals) {
+        // A state is a value some surviving write / cas could install.  Keys
+        // are independent up to the shared numbering, so: (1) per key, in
+        // parallel, its state values in order of first appearance; (2)
+        // serially, the shared state numbering (or per-key tables past 254
+        // values); (3) per key, in parallel, its distinct descriptors in order
+        // of first appearance and each invoke's index among them; (4)
+        // serially over keys (a few dozen descriptors each), their global
+        // transition ids; (5) per key, in parallel, the event words.  The ids
+        // are those of one serial pass over keys and events.
+        auto par_keys = [&](const auto &fn) {
+            auto work = [&](unsigned t) {
+                for (int64_t k = t; k < K; k += nt) fn(k);
+            };
+            std::vector<std::thread> pool;
+            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
+            work(0);
+            for (auto &th : pool) th.join();
+        };
+        // (1) distinct state values per key, in order of first appearance
+        std::vector<std::vector<int64_t>> kvals((size_t)K);
+        par_keys([&](int64_t k) {
+            std::vector<int64_t> &vals = kvals[(size_t)k];
             if (model == LC_MODEL_MUTEX) {  // state 1 = locked (state 0, "nil", = unlocked)
                 vals.push_back(1);
                 return;
             }
-            for (const KOp &op : o.ops) {
+            std::unordered_map<int64_t, char> seen;
+            auto add = [&](int64_t v) {
+                if (v == LC_NIL) return;
+                if (vals.size() < 16) {
+                    if (std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
+                    return;
+                }
+                if (seen.empty())
+                    for (int64_t x : vals) seen.emplace(x, 0);
+                if (seen.emplace(v, 0).second) vals.push_back(v);
+            };
+            for (const KOp &op : ko[(size_t)k].ops) {
                 if (op.fate == 2) continue;
-                if (op.f == LC_F_WRITE && op.v0 != LC_NIL) vals.push_back(op.v0);
-                if (op.f == LC_F_CAS && op.v1 != LC_NIL) vals.push_back(op.v1);
+                if (op.f == LC_F_WRITE) add(op.v0);
+                if (op.f == LC_F_CAS) add(op.v1);
             }
-        };
+        });
+        // (2) one numbering shared by every key while the batch has < 255 values
         std::unordered_map<int64_t, uint32_t> gstate;
         bool shared = true;
-        for (int64_t k = 0; k < K && shared; ++k) {
-            std::vector<int64_t> vals;
-            state_values(ko[(size_t)k], vals);
-            for (int64_t v : vals) {
+        for (int64_t k = 0; k < K && shared; ++k)
+            for (int64_t v : kvals[(size_t)k]) {
                 if (gstate.size() >= LC_NARROW_MAX_STATES - 1 && !gstate.count(v)) { shared = false; break; }
                 gstate.emplace(v, (uint32_t)gstate.size() + 1);
             }
-        }
         if (shared) {
             P->state_vals.assign(gstate.size() + 1, LC_NIL);
             for (auto &kv : gstate) P->state_vals[kv.second] = kv.first;
@@ -534,57 +632,80 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             if (op.f == LC_F_WRITE) return LC_DESC(LC_T_WRITE, 0, sid(m, op.v0));
             return LC_DESC(LC_T_CAS, sid(m, op.v0), sid(m, op.v1));
         };
+        // (3) per key: its state table (unshared), distinct descriptors, and
+        // each invoke event's index among them (in the word's trans field)
+        std::vector<std::vector<uint32_t>> kdesc((size_t)K);
+        par_keys([&](int64_t k) {
+            KeyOut &o = ko[(size_t)k];
+            const std::vector<int64_t> &vals = kvals[(size_t)k];
+            std::unordered_map<int64_t, uint32_t> lstate;
+            if (!shared) {
+                for (int64_t v : vals) lstate.emplace(v, lstate.size() < LC_STATE_NONE - 1 ? (uint32_t)lstate.size() + 1
+                                                                                            : LC_STATE_NONE);
+            }
+            const std::unordered_map<int64_t, uint32_t> &sm = shared ? gstate : lstate;
+            P->key_states[(size_t)k] = (uint16_t)std::min<size_t>(vals.size() + 1, 65535);
+            std::vector<uint32_t> &ud = kdesc[(size_t)k];
+            std::unordered_map<uint32_t, uint32_t> local;
+            for (size_t j = 0; j < o.ev.size(); ++j) {
+                uint32_t &w = o.ev[j];
+                if (w & LC_EV_OK_BIT) continue;
+                const uint32_t d = make_desc(sm, o.ops[(size_t)o.ev_op[j]]);
+                uint32_t li = (uint32_t)ud.size();
+                if (ud.size() < 48) {
+                    for (uint32_t q = 0; q < ud.size(); ++q)
+                        if (ud[q] == d) { li = q; break; }
+                    if (li == ud.size()) ud.push_back(d);
+                } else {
+                    if (local.empty())
+                        for (uint32_t q = 0; q < ud.size(); ++q) local.emplace(ud[q], q);
+                    auto it = local.emplace(d, (uint32_t)ud.size());
+                    li = it.first->second;
+                    if (it.second) ud.push_back(d);
+                }
+                w = (w & 0xFF000000u) | li;  // (< 2^24: the key's distinct descriptors are fewer)
+            }
+            if (!shared) {  // the key's state table, kept in lstate order as state ids
+                std::vector<int64_t> tab(lstate.size() + 1, LC_NIL);
+                for (auto &kv : lstate)
+                    if (kv.second != LC_STATE_NONE) tab[kv.second] = kv.first;
+                kvals[(size_t)k].swap(tab);
+            }
+        });
+        // (4) global transition ids, in key order
         std::unordered_map<uint32_t, uint32_t> gtrans;
         if (!shared) P->trans_off.assign((size_t)K, 0);
-        for (int64_t k = 0; k < K; ++k) {
-            KeyOut &o = ko[(size_t)k];
-            std::unordered_map<int64_t, uint32_t> lstate;
-            std::unordered_map<uint32_t, uint32_t> ltrans;
-            const std::unordered_map<int64_t, uint32_t> *sm = &gstate;
-            std::unordered_map<uint32_t, uint32_t> *tm = &gtrans;
+        bool too_many = false;
+        for (int64_t k = 0; k < K && !too_many; ++k) {
+            std::vector<uint32_t> &ud = kdesc[(size_t)k];
             if (!shared) {
-                std::vector<int64_t> vals;
-                state_values(o, vals);
-                for (int64_t v : vals)
-                    if (lstate.size() < LC_STATE_NONE - 1) lstate.emplace(v, (uint32_t)lstate.size() + 1);
-                    else if (!lstate.count(v)) { lstate.emplace(v, LC_STATE_NONE); }
-                sm = &lstate;
-                tm = &ltrans;
                 P->state_off[(size_t)k] = P->state_vals.size();
-                size_t base_sv = P->state_vals.size();
-                P->state_vals.resize(base_sv + lstate.size() + 1, LC_NIL);
-                for (auto &kv : lstate)
-                    if (kv.second != LC_STATE_NONE) P->state_vals[base_sv + kv.second] = kv.first;
+                P->state_vals.insert(P->state_vals.end(), kvals[(size_t)k].begin(), kvals[(size_t)k].end());
                 P->trans_off[(size_t)k] = (uint32_t)P->trans.size();
-                P->key_states[(size_t)k] = (uint16_t)std::min<size_t>(lstate.size() + 1, 65535);
+                P->trans.insert(P->trans.end(), ud.begin(), ud.end());
+                too_many = ud.size() > 0x1000000u;
+                for (uint32_t q = 0; q < ud.size(); ++q) ud[q] = q;  // local ids are the key's own
             } else {
-                std::vector<int64_t> vals;
-                state_values(o, vals);
-                std::sort(vals.begin(), vals.end());
-                P->key_states[(size_t)k] =
-                    (uint16_t)(std::unique(vals.begin(), vals.end()) - vals.begin() + 1);
-            }
-            uint64_t base = P->ev_off[(size_t)k];
-            for (size_t j = 0; j < o.ev.size(); ++j) {
-                uint32_t w = o.ev[j];
-                if (!(w & LC_EV_OK_BIT)) {
-                    uint32_t d = make_desc(*sm, o.ops[(size_t)o.ev_op[j]]);
-                    auto it = tm->find(d);
-                    uint32_t tid;
-                    if (it == tm->end()) {
-                        tid = (uint32_t)(P->trans.size() - (shared ? 0 : P->trans_off[(size_t)k]));
-                        tm->emplace(d, tid);
-                        P->trans.push_back(d);
-                    } else {
-                        tid = it->second;
-                    }
-                    if (tid > 0xFFFFFFu) {
-                        delete P;
-                        return lc::fail(LC_E_UNSUPPORTED, "lc_pack: more than 2^24 distinct operations");
-                    }
-                    w = (w & 0xFF000000u) | tid;
+                for (uint32_t &d : ud) {
+                    auto it = gtrans.emplace(d, (uint32_t)P->trans.size());
+                    if (it.second) P->trans.push_back(d);
+                    d = it.first->second;  // now: the global id
                 }
-                P->events[base + j] = w;
+                too_many = P->trans.size() > 0x1000000u;
+            }
+        }
+        if (too_many) {
+            delete P;
+            return lc::fail(LC_E_UNSUPPORTED, "lc_pack: more than 2^24 distinct operations");
+        }
+        // (5) event words with transition ids, rows, widths
+        par_keys([&](int64_t k) {
+            KeyOut &o = ko[(size_t)k];
+            const std::vector<uint32_t> &ud = kdesc[(size_t)k];
+            const uint64_t base = P->ev_off[(size_t)k];
+            for (size_t j = 0; j < o.ev.size(); ++j) {
+                const uint32_t w = o.ev[j];
+                P->events[base + j] = (w & LC_EV_OK_BIT) ? w : (w & 0xFF000000u) | ud[w & 0xFFFFFFu];
                 P->ev_row[base + j] = o.ev_row[j];
             }
             P->key_width[(size_t)k] = (uint8_t)o.width;
@@ -592,23 +713,41 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             std::vector<int64_t>().swap(o.ev_row);
             std::vector<int32_t>().swap(o.ev_op);
             std::vector<KOp>().swap(o.ops);
-        }
+            std::vector<uint32_t>().swap(kdesc[(size_t)k]);
+            std::vector<int64_t>().swap(kvals[(size_t)k]);
+        });
         if (!shared) P->state_off[(size_t)K] = P->state_vals.size();
         if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
+        lap("A4/A5 states, descriptors");
         // 16-bit event words (lc_batch.events16) when every word fits: half
-        // the bytes over the host link for the register tier
-        bool fit16 = !P->events.empty();
-        for (size_t j = 0; j < P->events.size() && fit16; ++j) {
-            const uint32_t w = P->events[j];
-            fit16 = LC_EV_SLOT(w) <= LC_EV16_MAX_SLOT && LC_EV_TRANS(w) <= LC_EV16_MAX_TRANS;
-        }
-        if (fit16) {
-            P->events16.resize(P->events.size());
-            for (size_t j = 0; j < P->events.size(); ++j) {
+        // the bytes over the host link for the register tier (both passes
+        // split over the threads in contiguous ranges)
+        const size_t n_ev = P->events.size();
+        std::vector<char> fits(nt, 1);
+        auto range_pass = [&](const auto &fn) {
+            auto work = [&](unsigned t) { fn(t, n_ev * t / nt, n_ev * (t + 1) / nt); };
+            std::vector<std::thread> pool;
+            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
+            work(0);
+            for (auto &th : pool) th.join();
+        };
+        range_pass([&](unsigned t, size_t j0, size_t j1) {
+            for (size_t j = j0; j < j1 && fits[t]; ++j) {
                 const uint32_t w = P->events[j];
-                P->events16[j] = (uint16_t)(((w >> 16) & 0x8000u) | (LC_EV_SLOT(w) << 11) | LC_EV_TRANS(w));
+                fits[t] = LC_EV_SLOT(w) <= LC_EV16_MAX_SLOT && LC_EV_TRANS(w) <= LC_EV16_MAX_TRANS;
             }
+        });
+        const bool fit16 = n_ev > 0 && std::all_of(fits.begin(), fits.end(), [](char c) { return c != 0; });
+        if (fit16) {
+            P->events16.resize(n_ev);
+            range_pass([&](unsigned, size_t j0, size_t j1) {
+                for (size_t j = j0; j < j1; ++j) {
+                    const uint32_t w = P->events[j];
+                    P->events16[j] = (uint16_t)(((w >> 16) & 0x8000u) | (LC_EV_SLOT(w) << 11) | LC_EV_TRANS(w));
+                }
+            });
         }
+        lap("16-bit words");
     } catch (const std::bad_alloc &) {
         delete P;
         return lc::fail(LC_E_NOMEM, "lc_pack: out of memory");

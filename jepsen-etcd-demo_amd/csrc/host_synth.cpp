@@ -171,7 +171,6 @@ extern "C" int lc_synth_generate(const lc_synth_opts *o, lc_hist **out) {
     if (!h) return lc::fail(LC_E_NOMEM, "lc_synth_generate: out of memory");
     const int64_t K = o->n_keys;
     try {
-        h->reserve((size_t)(K * o->ops_per_key * 2 + 16));
         if (!o->interleave) {
             // Key-major: keys are independent; generate in parallel, concatenate in order.
             unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -190,17 +189,34 @@ extern "C" int lc_synth_generate(const lc_synth_opts *o, lc_hist **out) {
             for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
             work(0);
             for (auto &th : pool) th.join();
-            int64_t idx = 0;
-            for (int64_t k = 0; k < K; ++k) {
-                for (const Row &r : per[(size_t)k])
-                    h->push(r.type, r.f, r.p, o->key_base + k, r.v0, r.v1, idx++);
-                std::vector<Row>().swap(per[(size_t)k]);
+            // concatenation: every key's rows at its offset, in parallel
+            std::vector<int64_t> off((size_t)K + 1, 0);
+            for (int64_t k = 0; k < K; ++k) off[(size_t)k + 1] = off[(size_t)k] + (int64_t)per[(size_t)k].size();
+            const size_t n = (size_t)off[(size_t)K];
+            h->type.resize(n); h->f.resize(n); h->process.resize(n); h->key.resize(n);
+            h->v0.resize(n); h->v1.resize(n); h->index.resize(n);
+            auto fill = [&](unsigned t) {
+                for (int64_t k = t; k < K; k += nt) {
+                    size_t i = (size_t)off[(size_t)k];
+                    for (const Row &r : per[(size_t)k]) {
+                        h->type[i] = r.type; h->f[i] = r.f; h->process[i] = r.p; h->key[i] = o->key_base + k;
+                        h->v0[i] = r.v0; h->v1[i] = r.v1; h->index[i] = (int64_t)i;
+                        ++i;
+                    }
+                    std::vector<Row>().swap(per[(size_t)k]);
+                }
+            };
+            pool.clear();
+            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(fill, t);
+            fill(0);
+            for (auto &th : pool) th.join();
+            for (int64_t k = 0; k < K; ++k)
                 if (anom[(size_t)k]) h->anomalous_keys.push_back(o->key_base + k);
-            }
         } else {
             // One Jepsen-style history: a single thread group works through the
             // keys in sequence (independent/concurrent-generator), process ids
             // carry across keys, nemesis :info ops interleave on a fixed period.
+            h->reserve((size_t)(K * o->ops_per_key * 2 + 16));
             std::vector<int64_t> proc((size_t)o->concurrency);
             for (int i = 0; i < o->concurrency; ++i) proc[(size_t)i] = i;
             struct GRow { double t; int64_t seq; uint8_t type, f; int64_t p, k, v0, v1; };

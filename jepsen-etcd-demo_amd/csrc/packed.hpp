@@ -14,14 +14,14 @@ struct lc_packed {
     lc::pinned_vector<uint64_t> ev_off;  // page-locked on a GPU host: lc_check_* DMA it directly
     lc::pinned_vector<uint32_t> events;
     lc::pinned_vector<uint16_t> events16;  // the same words in 16 bits when all fit (empty otherwise)
-    std::vector<int64_t> ev_row;
+    lc::uninit_vector<int64_t> ev_row;
     std::vector<uint32_t> trans;
     std::vector<uint32_t> trans_off;  // empty = shared table
     std::vector<uint8_t> key_width;
     std::vector<uint16_t> key_states;
     // sub-history rows: per-key rows + rows shared by every key
     std::vector<uint64_t> krow_off;
-    std::vector<int64_t> krows;
+    lc::uninit_vector<int64_t> krows;
     std::vector<int64_t> shared_rows;
     // state id -> register value: shared table, or per key (state_off[k] ..)
     std::vector<int64_t> state_vals;  // index 0 unused (nil)

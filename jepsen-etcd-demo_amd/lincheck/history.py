@@ -43,6 +43,28 @@ def _int_or_nil(v, what: str) -> int:
     return v
 
 
+class _HistOwner:
+    """An lc_hist handle, freed when the last numpy view of it goes."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def __del__(self):
+        if self.handle:
+            N.lib().lc_hist_free(self.handle)
+            self.handle = None
+
+
+def _borrow(owner: _HistOwner, p, n: int, ctype) -> np.ndarray:
+    """n elements at p as a numpy view; the buffer under it holds `owner`."""
+    n = int(n)
+    if not p or n == 0:
+        return np.zeros(0, np.dtype(ctype))
+    buf = (ctype * n).from_address(C.addressof(p.contents))
+    buf._owner = owner
+    return np.frombuffer(buf, np.dtype(ctype))
+
+
 class History:
     """Columns of one history (numpy arrays, history order)."""
 
@@ -143,17 +165,23 @@ class History:
 
     @classmethod
     def _from_owned(cls, handle) -> "History":
+        """The columns of a library-owned history (lc_synth / lc_edn_read /
+        lc_fressian_read) as numpy views of its memory, not copies (a C3
+        history is 17 GB): every view keeps the lc_hist alive, and the last
+        one to go frees it."""
         L = N.lib()
         v = N.LcHistory()
         N.check(L.lc_hist_view(handle, C.byref(v)))
         n = v.n
-        h = cls(N.carray(v.type, n, np.uint8), N.carray(v.f, n, np.uint8),
-                N.carray(v.process, n, np.int64), N.carray(v.key, n, np.int64),
-                N.carray(v.v0, n, np.int64), N.carray(v.v1, n, np.int64),
-                N.carray(v.index, n, np.int64))
+        owner = _HistOwner(handle)
+        h = cls(_borrow(owner, v.type, n, C.c_uint8), _borrow(owner, v.f, n, C.c_uint8),
+                _borrow(owner, v.process, n, C.c_int64), _borrow(owner, v.key, n, C.c_int64),
+                _borrow(owner, v.v0, n, C.c_int64), _borrow(owner, v.v1, n, C.c_int64),
+                _borrow(owner, v.index, n, C.c_int64))
         if v.mop_off:
-            h.mop_off = N.carray(v.mop_off, n + 1, np.int64)
-            h.mop = N.carray(v.mop, 3 * int(h.mop_off[-1]), np.int64) if h.mop_off[-1] else np.zeros(0, np.int64)
+            h.mop_off = _borrow(owner, v.mop_off, n + 1, C.c_int64)
+            nm = 3 * int(h.mop_off[-1])
+            h.mop = _borrow(owner, v.mop, nm, C.c_int64) if nm else np.zeros(0, np.int64)
         for i in range(L.lc_hist_n_reg_names(handle)):
             h.reg_names[NAMED_REG_BASE + i] = L.lc_hist_reg_name(handle, i).decode()
         na = L.lc_hist_anomalous_keys(handle, None)
@@ -161,7 +189,6 @@ class History:
             buf = np.zeros(na, np.int64)
             L.lc_hist_anomalous_keys(handle, N.ptr(buf, C.c_int64))
             h.anomalous_keys = buf.tolist()
-        L.lc_hist_free(handle)
         return h
 
     # -- views --------------------------------------------------------------
