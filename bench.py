@@ -15,11 +15,17 @@ enqueued (the exchange still runs per step, on the library's stream).
 
 Workloads (BASELINE.json configs; synthetic, liblincheck's seeded generator):
   N = 1 (default): C2, 1,000 keys x 1,000 client ops, concurrency 10,
-        cas-register over values 0..4 (etcdemo.clj:67-69), seed 2.
+        cas-register over values 0..4 (etcdemo.clj:67-69), seed 2 -- the
+        `value`.  The same run then checks C3's whole key space on this one
+        GPU (`c3_strong`: the N = 1 point of the 2/4/8-GPU curve, measured by
+        the same command; --no-c3 skips it).
   N > 1 (default): C3, 100,000 keys x 2,000 ops in total, concurrency 10,
         contiguous key shards, one per rank (strong scaling).
   --config C1|C4|C5 select the others (C1: history.edn -> result map, the
   demo's check phase end to end).
+Every line carries the host marshalling cost beside the step: `pack_ms` /
+`pack_ops_per_s` time lc_pack alone (history -> packed SoA)
+on the history the step consumes; `synth_s` is the generator's time.
 
 Also reported (one JSON line on rank 0):
   roofline      the dominant kernel's algorithmic HBM bytes per launch over
@@ -45,6 +51,7 @@ for p in (os.path.join(ROOT, "jepsen-etcd-demo_amd"), os.path.join(ROOT, "oracle
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SHADER_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 METRIC = "history ops linearizability-checked/sec (whole node)"
 
 CONFIGS = {
@@ -75,6 +82,8 @@ def parse():
     ap.add_argument("--d1-sync", action="store_true",
                     help="time the synchronous lc_check_node step instead of the pipelined one")
     ap.add_argument("--no-probes", action="store_true", help="skip the probe-counting pass")
+    ap.add_argument("--no-c3", action="store_true", help="N = 1: skip the C3-on-one-GPU block (c3_strong)")
+    ap.add_argument("--c3-steps", type=int, default=10, help="timed pipelined steps of the c3_strong block")
     ap.add_argument("--keys", type=int, default=0, help="override keys (exploration only)")
     ap.add_argument("--ops", type=int, default=0, help="override ops per key (exploration only)")
     return ap.parse_args()
@@ -212,6 +221,59 @@ def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quo
     return cpu, parity
 
 
+def bench_c3_strong(args, local):
+    """C3's whole key space (100,000 keys x 2,000 ops) on this one GPU: the
+    N = 1 point of the strong-scaling curve that `bench.py --gpus N` measures
+    with the same step (lc_check_node_async, pipelined), so the driver's
+    2/4/8-GPU runs have a same-workload base from the default command.  Also
+    the host side at C3 scale: generator and lc_pack times.
+    Verdicts are property-checked (C3 has no anomalies: every key valid)."""
+    import numpy as np
+    import torch
+
+    from lincheck import _native as NN
+    from lincheck import history as H
+    from lincheck import parallel as P
+    from lincheck.checker import Device, Packed, PinnedRecords
+    cfg = CONFIGS["C3"]
+    t = time.perf_counter()
+    hist = H.synth(n_keys=cfg["keys"], ops_per_key=cfg["ops"], concurrency=cfg["concurrency"], seed=cfg["seed"])
+    synth_s = time.perf_counter() - t
+    t = time.perf_counter()
+    packed = Packed(hist)
+    pack_s = time.perf_counter() - t
+    K, n_ev = packed.n_keys, int(packed.ev_off[-1])
+    print(f"[c3_strong] {K} keys synthesised in {synth_s:.1f} s, packed in {pack_s:.2f} s", file=sys.stderr, flush=True)
+    dev = Device(local, budget=args.budget)
+    buf = PinnedRecords(K)
+    dev.check_node_async(packed, K, buf)  # warmup (allocations, first upload)
+    dev.wait()
+    torch.cuda.synchronize()
+    steps = max(1, args.c3_steps)
+    t = time.perf_counter()
+    for _ in range(steps):
+        dev.check_node_async(packed, K, buf)
+    dev.wait()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t
+    v, c, fe = P.unpack_records(np.asarray(buf)[:K].astype(np.int64))
+    _, st = dev.check_node(packed, K)  # one synchronous step: the register tier's launch time
+    ops_total = cfg["keys"] * cfg["ops"]
+    ewb = int(st.ev_word_bytes) or 4
+    alg = ewb * n_ev + 8 * (K + 1) + 4 * K + 4 * int(packed.view.n_trans) + 8 * K
+    out = {"workload": cfg["desc"] + " -- all on one GPU", "keys": K, "ops_per_key": cfg["ops"],
+           "ops_per_s": ops_total * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
+           "step": "lc_check_node_async (two steps in flight), as at N > 1",
+           "t0_kernel": NN.T0_PATH_NAMES.get(int(st.t0_path)), "t0_ms_sync_step": float(st.tier0_ms),
+           "t0_achieved_gbs": alg / (st.tier0_ms * 1e-3) / 1e9 if st.tier0_ms > 0 else None,
+           "events": n_ev, "synth_s": round(synth_s, 2), "pack_ms": pack_s * 1e3,
+           "pack_ops_per_s": ops_total / pack_s if pack_s > 0 else None,
+           "verdicts": {"valid": int((v == 1).sum()), "invalid": int((v == 0).sum()), "unknown": int((v == -1).sum())},
+           "property_check": bool((v == 1).all() and (fe == -1).all())}
+    del dev, buf, packed, hist
+    return out
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -257,12 +319,16 @@ def main():
         key0, k1 = P.shard_range(cfg["keys"], world, rank)
         K = k1 - key0
     block = -(-cfg["keys"] // world) if strong else K  # equal all-gather blocks
-    t_gen = time.time()
+    t_gen = time.perf_counter()
     hist = H.synth(n_keys=K, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
                    anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"], key_base=key0)
+    synth_s = time.perf_counter() - t_gen
+    t_pack = time.perf_counter()
     packed = Packed(hist)
-    t_gen = time.time() - t_gen
-    print(f"[rank {rank}] {K} keys x {ops} ops synthesised + packed in {t_gen:.1f} s", file=sys.stderr, flush=True)
+    pack_s = time.perf_counter() - t_pack
+    t_gen = synth_s + pack_s
+    print(f"[rank {rank}] {K} keys x {ops} ops synthesised in {synth_s:.1f} s, packed in {pack_s:.2f} s",
+          file=sys.stderr, flush=True)
 
     cid = None
     if world > 1 and not host_gather:
@@ -295,10 +361,12 @@ def main():
     # synchronous call (lc_check_node, one step at a time) runs after them
     # for its own rate and for the per-launch kernel times of the roofline.
     d1_t0, d1_t3, d1_t3b = [], [], []
+    d1_path = {}  # the register tier's kernel and event word width (lc_stats, synchronous steps)
     pipelined = not args.d1_sync
     node_pin = PinnedRecords(n_node) if pipelined else None
 
     def record(st):
+        d1_path["t0_path"], d1_path["ev_word_bytes"] = int(st.t0_path), int(st.ev_word_bytes)
         d1_t0.append(st.tier0_ms if st.tier0_ms > 0 else st.kernel_ms)
         if st.tier3_ms > 0:
             d1_t3.append(st.tier3_ms)
@@ -408,12 +476,16 @@ def main():
         n_events = int(packed.ev_off[-1])
         max_events = int(np.diff(packed.ev_off.astype(np.int64)).max()) if K else 0
         # Algorithmic HBM bytes of one launch of the dominant kernel (DESIGN.md
-        # section 3): T0 reads every event word (4 B), the key offsets (8 B)
-        # and LPT order (4 B), the transition table once, and writes a verdict
-        # record (valid 1 B + failing event 4 B + cause 1 B) per key.
-        alg_bytes = 4 * n_events + 8 * (K + 1) + 4 * K + 4 * int(packed.view.n_trans) + 6 * K
+        # section 3): T0 reads every event word once (2 B when the 16-bit
+        # words are read in place, as k_spec does, else 4 B), the key offsets
+        # (8 B) and LPT order (4 B), the transition table once, and writes a
+        # verdict record (8 B) per key.
+        from lincheck import _native as NN
+        ewb = d1_path.get("ev_word_bytes") or 4
+        alg_bytes = ewb * n_events + 8 * (K + 1) + 4 * K + 4 * int(packed.view.n_trans) + 8 * K
         kt = avg_t0
-        dominant = "T0 register tier (k_spec / k_search_lattice)"
+        t0_name = NN.T0_PATH_NAMES.get(d1_path.get("t0_path", 1), "T0")
+        dominant = f"T0 register tier ({t0_name})"
         d4_t3 = None
         if avg_t3 > avg_t0:
             # the HBM tier dominates (C4).  Its layered form (k_search_layers)
@@ -427,21 +499,39 @@ def main():
             if probes_t3:
                 d4_t3 = 64 * probes_t3 / (kt * 1e-3) / 1e9
         achieved = alg_bytes / (kt * 1e-3) / 1e9 if kt > 0 else 0.0
-        traffic = None
-        for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        # measured HBM traffic and VALU issue of the same kernel on the same
+        # workload, from the committed rocprofv3 --pmc summaries (profiles/)
+        traffic = traffic_src = issue = None
+        tags = (t0_name,) if "T0" in dominant else ("k_search_layers",)
+        for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*.json"))):
             try:
                 d = json.load(open(fpath))
-                tags = ("k_spec<", "lattice") if "T0" in dominant else ("k_search_layers",)
-                kname = d.get("kernel", "")
-                if (d.get("workload") == args.config and d.get("bytes_per_launch")
-                        and d.get("budget", args.budget) == args.budget and any(t in kname for t in tags)):
-                    traffic = d["bytes_per_launch"]
             except (OSError, ValueError):
-                pass
+                continue
+            if not isinstance(d, dict):
+                continue
+            kname = d.get("kernel") or ""
+            if (d.get("workload") != args.config or d.get("budget", args.budget) != args.budget
+                    or not any(t in kname for t in tags)):
+                continue
+            if d.get("bytes_per_launch"):
+                traffic, traffic_src = d["bytes_per_launch"], os.path.basename(fpath)
+            if d.get("sq_insts_valu_per_launch") and kt > 0:
+                # VALU issue capacity over the launch: every SIMD issues one
+                # wave64 VALU instruction per 2 cycles (MI355X_MICROARCH.md)
+                import torch as _t
+                simds = 4 * _t.cuda.get_device_properties(local).multi_processor_count
+                cap = simds * SHADER_CLOCK_HZ / 2 * kt * 1e-3
+                issue = {"valu_per_launch": d["sq_insts_valu_per_launch"], "capacity": cap,
+                         "frac": d["sq_insts_valu_per_launch"] / cap, "simds": simds,
+                         "clock_ghz": SHADER_CLOCK_HZ / 1e9, "source": os.path.basename(fpath)}
         nproc, aff, quota = host_cores()
         cpu = parity = None
         if world == 1 and not args.no_cpu:
             cpu, parity = cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quota)
+        c3 = None
+        if world == 1 and args.config == "C2" and not (args.no_c3 or args.keys or args.ops):
+            c3 = bench_c3_strong(args, local)
         line = {
             "metric": METRIC,
             "value": value,
@@ -464,7 +554,9 @@ def main():
             "d1_sync": d1_sync,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
-                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": kt,
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": kt, "event_word_bytes": ewb,
+                         "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
+                         "traffic_source": traffic_src, "issue": issue,
                          "launches": len(d1_t0), "d4_model_gbs": d4_t3},
             "cpu_baseline": cpu,
             "ops_total": ops_total,
@@ -480,6 +572,10 @@ def main():
                          "unknown": int((nv == -1).sum())},
             "parity_vs_oracle": parity,
             "setup_s": round(t_gen, 2),
+            "synth_s": round(synth_s, 2),
+            "pack_ms": pack_s * 1e3,
+            "pack_ops_per_s": K * ops / pack_s if pack_s > 0 else None,
+            "c3_strong": c3,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -348,11 +348,13 @@ typedef struct lc_opts {
 #define LC_PATH_NODE_STAGED  0x20  /* one rank: records through HBM, not device-mapped */
 #define LC_PATH_CHUNKS_ON    0x40  /* lc_check_node: chunked upload whatever the size  */
 #define LC_PATH_CHUNKS_OFF   0x80  /* lc_check_node: one upload whatever the size      */
-#define LC_PATH_SPEC_EVEN    0x100 /* speculative cuts at equal event counts (round 2)
-                                      instead of equal estimated cost               */
+#define LC_PATH_SPEC_COST    0x100 /* speculative cuts at equal estimated cost
+                                      instead of equal event counts                 */
 #define LC_PATH_EV32         0x200 /* upload 32-bit event words even when 16-bit ones
                                       are given (lc_batch.events16)                 */
-#define LC_PATH_ALL          0x3FF
+#define LC_PATH_SPEC_NOPRIO  0x400 /* speculative walks: issue priority by wave age
+                                      alone, not by progress                        */
+#define LC_PATH_ALL          0x7FF
 
 /* lc_opts.flags */
 #define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,
@@ -400,7 +402,17 @@ typedef struct lc_stats {
     uint64_t t3_bytes;        /* algorithmic HBM bytes of the layered HBM tier:
                                  8 per config-set entry it streams in or out
                                  (ABI 7)                                       */
+    uint32_t t0_path;         /* the register tier's kernel this step (ABI 9):
+                                 LC_T0_PATH_*                                   */
+    uint32_t ev_word_bytes;   /* bytes per event word it read: 2 (lc_batch.events16
+                                 read in place) or 4                            */
 } lc_stats;
+
+/* lc_stats.t0_path */
+#define LC_T0_PATH_NONE      0  /* no register-tier launch (table model, no keys) */
+#define LC_T0_PATH_LATTICE   1  /* k_search_lattice: one wave per key            */
+#define LC_T0_PATH_SPEC      2  /* k_spec: speculative key segments              */
+#define LC_T0_PATH_SEGMENTS  3  /* k_search_segments: quiescent-point segments    */
 
 typedef struct lc_ctx lc_ctx;
 typedef struct lc_dev_batch lc_dev_batch;

@@ -1101,6 +1101,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // The speculative segments read 16-bit event words in place; every other
     // kernel reads the 32-bit form, widened here once per upload.
     const uint16_t *ev16 = (spec && d->events16) ? d->events16 : nullptr;
+    const uint32_t t0_path = K == 0 || d->table ? LC_T0_PATH_NONE
+                             : split            ? LC_T0_PATH_SEGMENTS
+                             : spec             ? LC_T0_PATH_SPEC
+                                                : LC_T0_PATH_LATTICE;
     if (!ev16 && !d->ev32_ready && d->n_events) {
         const uint64_t n4 = (d->n_events + 3) / 4;
         const int blocks = (int)std::min<uint64_t>((n4 + 255) / 256, (uint64_t)c->cu_count * 8);
@@ -1191,7 +1195,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         // the same launch (a second stream cost ~40 us of cross-stream waits)
         const int vblocks = a.strict ? (int)std::min<int64_t>(K, c->cu_count) : 0;
         HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2, c->cu_count * 8,
-                                vblocks, ev16, (o.path_flags & LC_PATH_SPEC_EVEN) != 0, c->stream));
+                                vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
+                                !(o.path_flags & LC_PATH_SPEC_NOPRIO), c->stream));
         c->spec_parity ^= 1;
         if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0 && !d->table) {
@@ -1208,7 +1213,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         ++c->n_async;
         c->ticket_next = (split || spec) ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
         c->ticket_live = true;
-        if (st) *st = lc_stats{};  // times come from lc_wait
+        if (st) {  // times come from lc_wait
+            *st = lc_stats{};
+            st->t0_path = t0_path;
+            st->ev_word_bytes = t0_path ? (ev16 ? 2u : 4u) : 0u;
+        }
         if (enqueued) *enqueued = true;
         return LC_OK;
     }
@@ -1330,6 +1339,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         st->events = acc[1];
         st->lds_keys = acc[2];
         st->deep_keys = (uint64_t)(n_deep + n_widek);  // keys the HBM tier (re)searched
+        st->t0_path = t0_path;
+        st->ev_word_bytes = t0_path ? (ev16 ? 2u : 4u) : 0u;
     }
     return LC_OK;
 }
@@ -1357,6 +1368,8 @@ static void merge_stats(lc_stats &t, const lc_stats &s) {
     t.lds_keys += s.lds_keys;
     t.deep_keys += s.deep_keys;
     t.events += s.events;
+    t.t0_path = std::max(t.t0_path, s.t0_path);
+    t.ev_word_bytes = std::max(t.ev_word_bytes, s.ev_word_bytes);
 }
 
 // Run fn(g) for every device g of c at once (one driver thread per device

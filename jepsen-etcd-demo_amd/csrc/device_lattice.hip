@@ -230,8 +230,11 @@ constexpr uint32_t T0_COUNT = 1, T0_WANT_PEAK = 2, T0_DBG_NOEVENTS = 4, T0_DBG_N
 // as it walks it, and a key that would leave T0 is an error, not a spill (no
 // later tier is launched to take it).
 constexpr uint32_t T0_STRICT = 32;
-// k_spec: cuts at equal event counts (round 2) instead of equal estimated cost
-constexpr uint32_t T0_SPEC_EVEN = 64;
+// k_spec: cuts at equal estimated cost (spec_targets_cost) instead of equal
+// event counts
+constexpr uint32_t T0_SPEC_COST = 64;
+// k_spec: TOP walks leave issue priority to age alone (no progress priority)
+constexpr uint32_t T0_SPEC_NOPRIO = 128;
 struct T0Args {
     const uint64_t *ev_off;
     const uint32_t *events;
@@ -1644,44 +1647,30 @@ __device__ __forceinline__ uint64_t uni(uint64_t x) {
     return (uint64_t)uni((uint32_t)x) | ((uint64_t)uni((uint32_t)(x >> 32)) << 32);
 }
 
-// Segment boundaries (T0_SPEC_EVEN, the round-2 placement): targets at s/eff
-// of the key's events (s = 1 .. eff-1), lane s of pos_v, with the ops pending
-// there in lane s of pend_v (one pass of ballots over the events before the
-// last target, 8 chunks' loads in flight).
+// Ops invoked minus ops completed over events [b, e) of a key (the change in
+// the pending count across them): one ballot pair per 64 events, 8 chunks'
+// loads in flight.
 template <class EvT>
-__device__ __forceinline__ void spec_targets(EvT evp, uint32_t nev, uint32_t eff, uint32_t &pos_v,
-                                             int32_t &pend_v) {
+__device__ __forceinline__ int32_t spec_net(EvT evp, uint32_t b, uint32_t e) {
     constexpr uint32_t G = 8;
     const uint32_t lane = lane_id();
-    pos_v = (uint32_t)((uint64_t)nev * lane / eff);
-    pend_v = 0;
-    const uint32_t t_last = (uint32_t)((uint64_t)nev * (eff - 1) / eff);
-    int32_t cnt = 0;  // ops pending before the chunk
-    uint32_t next = 1, t_next = (uint32_t)((uint64_t)nev / eff);
-    for (uint32_t gb = 0; gb <= t_last; gb += 64 * G) {  // chunks covering [0, t_last]
+    int32_t cnt = 0;
+    for (uint32_t gb = b; gb < e; gb += 64 * G) {
         uint32_t wg[G];
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
             const uint32_t j = gb + 64 * g + lane;
-            wg[g] = j < t_last ? evp[j] : 0u;
+            wg[g] = j < e ? evp[j] : 0u;
         }
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) {
             const uint32_t base = gb + 64 * g;
-            if (base > t_last) continue;
-            const uint64_t inv = __ballot(base + lane < t_last && !(wg[g] >> 31));
-            const uint64_t oks = __ballot(base + lane < t_last && (wg[g] >> 31));
-            while (next < eff && t_next < base + 64) {  // a target inside this chunk
-                const uint32_t k = t_next - base;
-                const uint64_t below = k >= 64 ? ~0ull : ((1ull << k) - 1ull);
-                const int32_t at = cnt + __popcll(inv & below) - __popcll(oks & below);
-                pend_v = lane == next ? at : pend_v;
-                ++next;
-                t_next = (uint32_t)((uint64_t)nev * next / eff);
-            }
-            cnt += __popcll(inv) - __popcll(oks);
+            if (base >= e) continue;
+            const bool in = base + lane < e;
+            cnt += __popcll(__ballot(in && !(wg[g] >> 31))) - __popcll(__ballot(in && (wg[g] >> 31)));
         }
     }
+    return cnt;
 }
 
 // Estimated cost of an event, in 1/8 of a lane-phase event: the per-event fit
@@ -1879,11 +1868,24 @@ __device__ __forceinline__ void spec_setup(SpecState &st, uint32_t words, uint32
 // keep 4 waves per SIMD within the CU's LDS.
 template <int S>
 constexpr int spec_lds_ws() { return S <= 3 ? 1 : S <= 6 ? 2 : 3; }
+// Issue priority of a TOP walk by progress (MODE 0, prio): the SIMD's
+// arbiter favours the higher s_setprio, then the older wave, so with age
+// alone the last-dispatched blocks' walks trail by up to a quarter of a walk
+// and end running alone on their SIMDs.  A walk in its first quarter runs at
+// priority 3, its last quarter at 0: the four walks a SIMD holds advance
+// together and keep it busy to the end.
+__device__ __forceinline__ void spec_prio(uint32_t quarter) {
+    if (quarter == 0) __builtin_amdgcn_s_setprio(3);
+    else if (quarter == 1) __builtin_amdgcn_s_setprio(2);
+    else if (quarter == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 template <int MODE, int NWS, class EvT>
 __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
                                          uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
                                          int32_t *lds_busy, uint32_t (*ck_w)[64], int32_t *ck_e, uint32_t ck1,
-                                         uint32_t ck2, uint32_t &fev_out) {
+                                         uint32_t ck2, uint32_t &fev_out, bool prio = false) {
     constexpr int RM = T0_RSMALL;
     const uint32_t lane = lane_id();
     LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
@@ -1912,6 +1914,9 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
     uint32_t ev_nn = 128 + lane < nev ? ep[128 + lane] : 0u;
     Xfer xc = xfer_of(dsc);
     uint32_t e = 0, i = 0, base = 0, lim = nev;
+    // progress quarters of the walk (its priority steps down at each)
+    const uint32_t q1 = nev / 4u, q2 = nev / 2u, q3 = nev - nev / 4u;
+    if (MODE == 0 && prio) spec_prio(0);
     auto advance = [&]() {
         ++e;
         if (++i == 64u) {
@@ -1920,6 +1925,7 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
             xc = xfer_of(dsc);
             dsc_n = ldesc(ev_n, base + 64 + lane < nev);
             ev_nn = base + 128 + lane < nev ? ep[base + 128 + lane] : 0u;
+            if (MODE == 0 && prio) spec_prio(base >= q3 ? 3u : base >= q2 ? 2u : base >= q1 ? 1u : 0u);
         }
     };
     // next checkpoint (relative event; ~0u: none)
@@ -2058,6 +2064,7 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
         dirty = true;
     }
     if (held >= 0 && lane == 0) atomicExch(&lds_busy[held], 0);
+    if (MODE == 0 && prio) __builtin_amdgcn_s_setprio(0);
     st.W0 = W0;
     st.k_v = k_v; st.cap_v = cap_v; st.b_v = b_v; st.slot_v = slot_v; st.dense_v = dense_v;
     st.n = n; st.live = live;
@@ -2090,6 +2097,8 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     __shared__ int32_t s_cut[S], s_segend[S];  // segment [cut, end); cut -1: no segment
     __shared__ int32_t s_top[S];          // TOP run: -1 alive, -2 does not fit, else its failing event
     __shared__ int32_t s_ver[S], s_vfev[S];
+    __shared__ int32_t s_net[S];          // cut search: pending-count change over each part
+    __shared__ int32_t s_cand[S], s_ncand[S];  // each target's cut (-1: none) and ops pending there
     constexpr int NWS = spec_lds_ws<S>();
     __shared__ uint32_t s_ws[NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
     __shared__ int32_t s_ws_busy[NWS];
@@ -2125,30 +2134,65 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     SPEC_STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                       ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32))
     SPEC_STAMP(9, (unsigned long long)key)
-    // 1. every segment from TOP (segment 0 exactly)
-    if (!plain && wv < eff) {
+    // 0. the cuts.  Targets at s/eff of the key's events (T0_SPEC_COST: of its
+    // estimated cost, each wave computing every target); each moved to the
+    // boundary with the fewest ops pending within 64 events.  Equal event
+    // counts: wave w counts the pending-count change over its own part
+    // [t_w, t_w+1), the parts' prefix gives the count at each target, and
+    // wave w places cut w -- a quarter of the scan each, two barriers.
+    uint32_t cut = 0, end = nev, n0 = 0;
+    const bool cost = (a.flags & T0_SPEC_COST) != 0;
+    if (!plain && !cost && wv + 1 < eff) {
+        const uint32_t t0 = (uint32_t)((uint64_t)nev * wv / eff), t1 = (uint32_t)((uint64_t)nev * (wv + 1) / eff);
+        const int32_t d = spec_net(evp, t0, t1);
+        if (lane == 0) s_net[wv] = d;
+    }
+    __syncthreads();
+    if (!plain && !cost && wv >= 1 && wv < eff) {
+        int32_t pend = 0;
+        for (uint32_t q = 0; q < wv; ++q) pend += uni(s_net[q]);
+        const uint32_t t = (uint32_t)((uint64_t)nev * wv / eff);
+        const uint32_t w = t + lane < nev ? evp[t + lane] : 0u;
+        uint32_t n2 = 0;
+        const uint32_t c2 = spec_cut_at(w, nev, t, pend, n2);
+        if (lane == 0) {
+            s_cand[wv] = c2 == SPEC_NONE ? -1 : (int32_t)c2;
+            s_ncand[wv] = (int32_t)n2;
+        }
+    }
+    if (!plain && cost && wv < eff) {
         uint32_t pos_v;
         int32_t pend_v;
-        if (a.flags & T0_SPEC_EVEN) spec_targets(evp, nev, eff, pos_v, pend_v);
-        else spec_targets_cost(evp, nev, eff, pos_v, pend_v);
-        // every cut (each wave computes them all, so all agree): a cut is
-        // kept if it lies past the last kept one
-        uint32_t cut = 0, end = nev, n0 = 0, last = 0;
-        uint32_t wc[S];  // the events after each target, loaded together
-#pragma unroll
-        for (uint32_t s2 = 1; s2 < S; ++s2) {
-            const uint32_t j = uni(__builtin_amdgcn_readlane(pos_v, s2)) + lane;
-            wc[s2] = (s2 < eff && j < nev) ? evp[j] : 0u;
-        }
-#pragma unroll
-        for (uint32_t s2 = 1; s2 < S; ++s2) {
-            if (s2 >= eff) continue;
+        spec_targets_cost(evp, nev, eff, pos_v, pend_v);
+        if (wv >= 1) {  // every wave has every target: each places its own cut
+            const uint32_t t = uni(__builtin_amdgcn_readlane(pos_v, wv));
+            const uint32_t w = t + lane < nev ? evp[t + lane] : 0u;
             uint32_t n2 = 0;
-            uint32_t c2 = spec_cut_at(wc[s2], nev, uni(__builtin_amdgcn_readlane(pos_v, s2)),
-                                      uni(__builtin_amdgcn_readlane(pend_v, s2)), n2);
+            const uint32_t c2 = spec_cut_at(w, nev, t, uni(__builtin_amdgcn_readlane(pend_v, wv)), n2);
+            if (lane == 0) {
+                s_cand[wv] = c2 == SPEC_NONE ? -1 : (int32_t)c2;
+                s_ncand[wv] = (int32_t)n2;
+            }
+        }
+    }
+    __syncthreads();
+    // 1. every segment from TOP (segment 0 exactly)
+    if (!plain && wv < eff) {
+        // a cut is kept if it lies past the last kept one (every wave reads
+        // the same candidates, so all agree); a segment ends at the next kept cut
+        uint32_t last = 0;
+        cut = 0;
+        end = nev;
+        n0 = 0;
+        for (uint32_t s2 = 1; s2 < eff; ++s2) {
+            const int32_t cc = uni(s_cand[s2]);
+            uint32_t c2 = cc < 0 ? SPEC_NONE : (uint32_t)cc;
             if (c2 != SPEC_NONE && c2 <= last) c2 = SPEC_NONE;
             if (c2 != SPEC_NONE) last = c2;
-            if (s2 == wv) { cut = c2; n0 = n2; }
+            if (s2 == wv) {
+                cut = c2;
+                n0 = (uint32_t)uni(s_ncand[s2]);
+            }
             if (s2 > wv && c2 != SPEC_NONE && end == nev) end = c2;
         }
         if (lane == 0) {
@@ -2176,7 +2220,8 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
             // the event stream is malformed): the key is searched unsegmented
             const bool lost = wv != 0 && np != n0;
             const int r = lost ? 6 : spec_walk<0, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[wv],
-                                                        s_ck_e[wv], a.spec_ck1, a.spec_ck2, fev);
+                                                        s_ck_e[wv], a.spec_ck1, a.spec_ck2, fev,
+                                                        !(a.flags & T0_SPEC_NOPRIO));
             s_end[wv][lane] = st.W0;
             uint64_t map = 0;
             for (uint32_t q = 0; q < 6; ++q) {
@@ -2303,10 +2348,11 @@ size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t
 // validate: add the T0_STRICT validation blocks.
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
-                       bool even_cuts, hipStream_t s) {
+                       bool cost_cuts, bool prio, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
     t.events16 = events16;
-    if (even_cuts) t.flags |= T0_SPEC_EVEN;
+    if (cost_cuts) t.flags |= T0_SPEC_COST;
+    if (!prio) t.flags |= T0_SPEC_NOPRIO;
     t.lat_ws = ws;
     t.spec_ck1 = ck1;
     t.spec_ck2 = ck2;

@@ -129,10 +129,12 @@ hipError_t launch_segments(const SegArgs &a, int grid, hipStream_t s);
 // validate_blocks > 0: the T0_STRICT validation runs in that many extra blocks.
 size_t spec_ws_words(int64_t n_keys, int segs);
 // events16: the batch's 16-bit event words (read in place), or null (the
-// 32-bit words); even_cuts: cuts at equal event counts instead of equal cost.
+// 32-bit words); cost_cuts: cuts at equal estimated cost instead of equal
+// event counts;
+// prio: TOP walks' issue priority by progress (s_setprio).
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
-                       bool even_cuts, hipStream_t s);
+                       bool cost_cuts, bool prio, hipStream_t s);
 uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);

@@ -214,7 +214,8 @@ class Device:
                           arrs["peak"][:K], arrs["final"][:K], arrs["n_final"][:K],
                           dict(kernel_ms=st.kernel_ms, tier0_ms=st.tier0_ms, tier3_ms=st.tier3_ms, total_ms=st.total_ms,
                                probes=st.probes, probes_t3=st.probes_t3, t3_bytes=st.t3_bytes,
-                               keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events))
+                               keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events,
+                               t0_path=N.T0_PATH_NAMES.get(st.t0_path, st.t0_path), ev_word_bytes=st.ev_word_bytes))
 
     def check(self, packed: Packed, verdicts_only: bool = False) -> KeyResults:
         """lc_check_batch: H2D, search, D2H.  verdicts_only: no peak sizes and

@@ -46,9 +46,10 @@ def test_spec_matches_oracle(shape):
         for ck in ((32, 160), (1, 2), (0, 0)):
             dev = Device(0, path_flags=N.LC_PATH_SPLIT_OFF, spec_segs=segs, spec_ck=ck)
             _check(dev, pk, orc, f"segs {segs} ck {ck}")
-    # the round-2 cut placement (equal event counts instead of equal cost)
-    even = Device(0, path_flags=N.LC_PATH_SPLIT_OFF | N.LC_PATH_SPEC_EVEN, spec_segs=4)
-    _check(even, pk, orc, "segs 4, even cuts")
+    # the other cut placement (equal estimated cost), the 32-bit words, age priority
+    for flags in (N.LC_PATH_SPEC_COST, N.LC_PATH_EV32, N.LC_PATH_SPEC_NOPRIO):
+        dev = Device(0, path_flags=N.LC_PATH_SPLIT_OFF | flags, spec_segs=4)
+        _check(dev, pk, orc, f"segs 4, path_flags {flags:#x}")
     if SHAPES[shape].get("anomaly_rate"):
         assert (orc["valid"] == 0).any()
 

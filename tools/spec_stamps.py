@@ -25,6 +25,8 @@ nb = min(keys, 4096)
 buf = np.zeros(nb * 8 * 12, np.uint64)
 N.lib().lc_debug_spec_stamps(buf.ctypes.data_as(C.c_void_p), nb)
 b = buf.reshape(nb, 8, 12).astype(np.int64)[:, :S, :]
+if len(sys.argv) > 4:  # raw stamps for offline fits (the keys regenerate from the seed)
+    np.savez(sys.argv[4], b=b, keys=keys, S=S, flags=flags)
 t0 = b[:, :, 0].min()
 print("T0 ms", st["tier0_ms"], "blocks", nb, "segments", S)
 start = b[:, :, 0] - t0
