@@ -287,6 +287,14 @@ int64_t lc_packed_state_map(const lc_packed *p, int64_t i, uint32_t s, int64_t *
  * with a larger buffer). */
 int64_t lc_report(const lc_packed *p, int64_t i, int32_t valid, int32_t fail_event, const uint64_t *final_configs,
                   uint32_t n_final, int32_t max_paths, int64_t *out, int64_t cap);
+/* The same key shaped as knossos.wgl's analysis (:algorithm :wgl,
+ * etcdemo.clj:118 slot; ABI 9; parity unpinned, restated in oracle/wgl_ref.py):
+ * the same words, with :configs = the Wing-Gong search's frontier at the
+ * return entry it is stuck on (the failing :ok) -- every (state, linearized
+ * pending ops) reachable from the given final configs by linearizing further
+ * pending ops other than the failing one, breadth first, at most max_paths. */
+int64_t lc_report_wgl(const lc_packed *p, int64_t i, int32_t valid, int32_t fail_event,
+                      const uint64_t *final_configs, uint32_t n_final, int32_t max_paths, int64_t *out, int64_t cap);
 
 /* ---- device checking (rows A6-A9) ------------------------------------------ */
 #define LC_ALGO_LINEAR      0  /* :algorithm :linear (etcdemo.clj:118)              */
@@ -294,7 +302,8 @@ int64_t lc_report(const lc_packed *p, int64_t i, int32_t valid, int32_t fail_eve
 #define LC_ALGO_COMPETITION 2  /* jepsen.checker/linearizable's default             */
 /* The three run the same device search: :valid? and the first :ok that cannot
  * be linearized are properties of the history, not of the algorithm.  Only
- * the host-side result shaping (:analyzer) differs. */
+ * the host-side result shaping differs (:analyzer; :configs of :wgl through
+ * lc_report_wgl). */
 
 #define LC_MAX_DEVICES   8    /* devices one context drives (one node)        */
 #define LC_COMM_ID_BYTES 128  /* an RCCL unique id (ncclUniqueId)             */

@@ -39,4 +39,6 @@ public final class LincheckNative {
 
     public static native long lc_report(Pointer packed, long i, int valid, int failEvent, Pointer finalConfigs,
                                         int nFinal, int maxPaths, long[] out, long cap);
+    public static native long lc_report_wgl(Pointer packed, long i, int valid, int failEvent, Pointer finalConfigs,
+                                            int nFinal, int maxPaths, long[] out, long cap);
 }

@@ -188,13 +188,16 @@
   [history model algorithm packed i valid fail-ev cause ^Memory finals n-final names]
   (let [words (long-array 256)
         fin   (.share finals (* i max-final 16))
-        need  (check-rc (LincheckNative/lc_report packed i valid fail-ev fin n-final max-final words 256)
-                        "lc_report")
+        ;; :wgl's :configs are the Wing-Gong frontier at the stuck :ok (lc_report_wgl)
+        render (fn [^longs w cap]
+                 (if (= algorithm :wgl)
+                   (LincheckNative/lc_report_wgl packed i valid fail-ev fin n-final max-final w cap)
+                   (LincheckNative/lc_report packed i valid fail-ev fin n-final max-final w cap)))
+        need  (check-rc (render words 256) "lc_report")
         words (if (<= need 256)
                 words
                 (let [w (long-array need)]
-                  (check-rc (LincheckNative/lc_report packed i valid fail-ev fin n-final max-final w need)
-                            "lc_report")
+                  (check-rc (render w need) "lc_report")
                   w))
         row   (fn [r] (when (<= 0 r) (unwrap (nth history r))))
         op    (fn [inv done]               ; knossos.history/complete's invocation

@@ -11,6 +11,17 @@
 // order, up to max_paths distinct ones (jepsen truncates to 10).  Both
 // bindings (Python lincheck.checker, the JVM's gpu_checker.clj) decode this
 // one rendering.
+//
+// lc_report_wgl shapes the same key for :algorithm :wgl (knossos.wgl, SURVEY
+// 8(f) F-3; parity unpinned -- restated in oracle/wgl_ref.py).  The Wing-Gong
+// search with Lowe's cache gets stuck, at its deepest, on the same :ok (the
+// first whose prefix cannot be linearized: a property of the history), and
+// its frontier there is every (model, linearized pending ops) it reached at
+// that return entry: the closure of the config set standing before the :ok
+// under the pending ops other than the failing one.  :configs are those
+// frontier configs, breadth first from the device's configs (so a subset of
+// the frontier when the device truncated them); :op, :previous-ok,
+// :last-op and :final-paths are shaped as for :linear.
 
 #include <algorithm>
 #include <map>
@@ -86,9 +97,9 @@ struct KeyView {
 
 }  // namespace
 
-extern "C" int64_t lc_report(const lc_packed *p, int64_t key, int32_t valid, int32_t fail_event,
-                             const uint64_t *final_configs, uint32_t n_final, int32_t max_paths, int64_t *out,
-                             int64_t cap) {
+static int64_t report(const lc_packed *p, int64_t key, int32_t valid, int32_t fail_event,
+                      const uint64_t *final_configs, uint32_t n_final, int32_t max_paths, bool wgl, int64_t *out,
+                      int64_t cap) {
     if (!p || key < 0 || key >= (int64_t)p->keys.size() || (n_final && !final_configs) || cap < 0 ||
         (cap && !out))
         return lc::fail(LC_E_INVALID, "lc_report: bad argument");
@@ -114,14 +125,40 @@ extern "C" int64_t lc_report(const lc_packed *p, int64_t key, int32_t valid, int
         auto in_mask = [](const std::pair<uint64_t, uint64_t> &m, uint32_t s) {
             return s < 64 ? ((m.first >> s) & 1) != 0 : ((m.second >> (s - 64)) & 1) != 0;
         };
-        const size_t n_cfg = std::min<size_t>(finals.size(), (size_t)std::max(max_paths, 0));
+        const uint32_t p_slot = fail_event >= 0 ? LC_EV_SLOT(p->events[kv.eb + (uint64_t)fail_event]) : 0xFFFFFFFFu;
+        const size_t want = (size_t)std::max(max_paths, 0);
+        std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> shown(
+            finals.begin(), finals.begin() + (ptrdiff_t)std::min(finals.size(), want));
+        if (wgl && valid == LC_INVALID && fail_event >= 0) {
+            // WGL's frontier at the stuck return entry: breadth first from the
+            // device's configs, every legal linearization of a further pending
+            // op other than the failing one, each distinct config once
+            std::set<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> seen(finals.begin(), finals.end());
+            std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> q(finals.begin(), finals.end());
+            for (size_t at = 0; at < q.size() && shown.size() < want && seen.size() < (1u << 16); ++at) {
+                const auto c = q[at];
+                for (auto &h : kv.held) {
+                    if (h.first == p_slot || in_mask(c.second, h.first)) continue;
+                    const uint32_t s2 = kv.step(h.second, c.first);
+                    if (s2 == LC_STATE_NONE) continue;
+                    auto m2 = c.second;
+                    if (h.first < 64) m2.first |= 1ull << h.first;
+                    else m2.second |= 1ull << (h.first - 64);
+                    const std::pair<uint32_t, std::pair<uint64_t, uint64_t>> c2{s2, m2};
+                    if (!seen.insert(c2).second) continue;
+                    q.push_back(c2);
+                    if (shown.size() < want) shown.push_back(c2);
+                }
+            }
+        }
+        const size_t n_cfg = shown.size();
         for (size_t c = 0; c < n_cfg; ++c) {
-            o.push_back(kv.value(finals[c].first));
+            o.push_back(kv.value(shown[c].first));
             for (int lin = 0; lin < 2; ++lin) {
                 const size_t at = o.size();
                 o.push_back(0);
                 for (auto &h : kv.held)
-                    if (in_mask(finals[c].second, h.first) == (lin == 1)) {
+                    if (in_mask(shown[c].second, h.first) == (lin == 1)) {
                         o.push_back(kv.row(h.second));
                         o.push_back(kv.done_row(h.second));
                         ++o[at];
@@ -130,7 +167,6 @@ extern "C" int64_t lc_report(const lc_packed *p, int64_t key, int32_t valid, int
         }
         o[2] = (int64_t)n_cfg;
         if (valid == LC_INVALID && fail_event >= 0 && max_paths > 0) {
-            const uint32_t p_slot = LC_EV_SLOT(p->events[kv.eb + (uint64_t)fail_event]);
             auto ph = kv.held.find(p_slot);
             if (ph != kv.held.end()) {
                 const uint64_t p_inv = ph->second;
@@ -187,6 +223,18 @@ extern "C" int64_t lc_report(const lc_packed *p, int64_t key, int32_t valid, int
     } catch (const std::bad_alloc &) {
         return lc::fail(LC_E_NOMEM, "lc_report: out of memory");
     }
+}
+
+extern "C" int64_t lc_report(const lc_packed *p, int64_t key, int32_t valid, int32_t fail_event,
+                             const uint64_t *final_configs, uint32_t n_final, int32_t max_paths, int64_t *out,
+                             int64_t cap) {
+    return report(p, key, valid, fail_event, final_configs, n_final, max_paths, false, out, cap);
+}
+
+extern "C" int64_t lc_report_wgl(const lc_packed *p, int64_t key, int32_t valid, int32_t fail_event,
+                                 const uint64_t *final_configs, uint32_t n_final, int32_t max_paths, int64_t *out,
+                                 int64_t cap) {
+    return report(p, key, valid, fail_event, final_configs, n_final, max_paths, true, out, cap);
 }
 
 extern "C" int lc_packed_keys(const lc_packed *p, int64_t *out) {

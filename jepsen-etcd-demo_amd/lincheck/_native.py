@@ -134,6 +134,8 @@ SIGNATURES = {
     "lc_packed_state_map": (C.c_int64, [C.c_void_p, C.c_int64, C.c_uint32, P(C.c_int64), P(C.c_int64), C.c_int64]),
     "lc_report": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, P(C.c_uint64), C.c_uint32, C.c_int32,
                               P(C.c_int64), C.c_int64]),
+    "lc_report_wgl": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, P(C.c_uint64), C.c_uint32, C.c_int32,
+                                  P(C.c_int64), C.c_int64]),
     "lc_synth_generate": (C.c_int, [P(LcSynthOpts), P(C.c_void_p)]),
     "lc_hist_view": (C.c_int, [C.c_void_p, P(LcHistory)]),
     "lc_hist_anomalous_keys": (C.c_int64, [C.c_void_p, P(C.c_int64)]),

@@ -350,17 +350,18 @@ def _sub_op(packed: Packed, row: int) -> Dict:
     return op
 
 
-def _report(packed: Packed, i: int, res: "KeyResults") -> np.ndarray:
-    """lc_report: the key's Knossos-shaped counterexample as int64 words
-    (include/lincheck.h), rendered natively -- the same rendering the JVM
-    binding decodes."""
+def _report(packed: Packed, i: int, res: "KeyResults", analyzer: str = "linear") -> np.ndarray:
+    """lc_report (lc_report_wgl for :wgl): the key's Knossos-shaped
+    counterexample as int64 words (include/lincheck.h), rendered natively --
+    the same rendering the JVM binding decodes."""
     fin = np.ascontiguousarray(res.final[i], dtype=np.uint64) if len(res.final) else np.zeros((1, 2), np.uint64)
     nf = int(res.n_final[i]) if len(res.n_final) else 0
+    fn = N.lib().lc_report_wgl if analyzer == "wgl" else N.lib().lc_report
     cap = 256
     while True:
         buf = np.zeros(cap, np.int64)
-        n = N.check(N.lib().lc_report(packed.handle, i, int(res.valid[i]), int(res.fail_event[i]),
-                                      N.ptr(fin, C.c_uint64), nf, TRUNCATE, N.ptr(buf, C.c_int64), cap))
+        n = N.check(fn(packed.handle, i, int(res.valid[i]), int(res.fail_event[i]),
+                       N.ptr(fin, C.c_uint64), nf, TRUNCATE, N.ptr(buf, C.c_int64), cap))
         if n <= cap:
             return buf[:n]
         cap = n
@@ -376,7 +377,7 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
         # the key's sub-history could not be prepared: what check-safe makes
         # of the exception knossos would throw (etcdemo.clj:115)
         return {"valid?": "unknown", "error": packed.key_error(i) or "error"}
-    w = _report(packed, i, res)
+    w = _report(packed, i, res, analyzer)
     ops: Dict[tuple, Dict] = {}
 
     def op(inv: int, done: int) -> Dict:

@@ -422,3 +422,46 @@ def test_pipelined_node_steps_bit_exact(rccl):
         dev.wait()
     assert "key 42" in str(ei.value)
     device_vs_oracle(h, dev)
+
+
+def test_c3_full_key_space_eight_shards():
+    """BASELINE C3's whole key space (100,000 keys x 2,000 ops, concurrency
+    10; 0.1 % of keys corrupted) through a context of eight key shards on
+    this one GPU (devices [0] * 8: the node's 8-GPU split, one stream and
+    scratch per shard), the pmap at etcdemo.clj:115 as the 8-GPU node runs
+    it.  Properties at full size: every uncorrupted key is valid (the
+    generator's histories are linearizable by construction) and every
+    invalid key is a corrupted one; the first shard's records -- the keys one
+    GPU of the node checks -- equal the oracle's, and the node step on
+    eight contiguous shards gives the same verdicts as the whole batch."""
+    h = H.synth(n_keys=100_000, ops_per_key=2000, concurrency=10, anomaly_rate=0.001, seed=3)
+    pk = Packed(h)
+    K = pk.n_keys
+    assert K == 100_000
+    res = Device(0, devices=[0] * 8).check(pk, verdicts_only=True)
+    bad = np.zeros(K, bool)
+    idx = {k: i for i, k in enumerate(pk.keys)}
+    for k in h.anomalous_keys:
+        bad[idx[k]] = True
+    assert bad.sum() > 50
+    assert (res.valid[~bad] == 1).all() and (res.fail_event[~bad] == -1).all()
+    assert (res.valid[res.valid != 1] == 0).all()  # no key :unknown
+    assert bad[res.valid == 0].all() and (res.valid == 0).sum() > 0
+    # the first of the eight shards against the oracle (12,500 keys)
+    e = int(pk.ev_off[K // 8])
+    assert e > 0
+    sub = H.synth(n_keys=K // 8, ops_per_key=2000, concurrency=10, anomaly_rate=0.001, seed=3)
+    _, orc = cref.check_history(sub.as_c(), budget=1 << 20, threads=16)
+    np.testing.assert_array_equal(res.valid[:K // 8], orc["valid"])
+    np.testing.assert_array_equal(res.fail_event[:K // 8], orc["fail_event"])
+    # the node step over the same key space as eight rank-shards (the
+    # records the 8-GPU all-gather assembles), one after another on this GPU
+    dev = Device(0)
+    for r in range(8):
+        k0, k1 = P.shard_range(K, 8, r)
+        shard = Packed(H.synth(n_keys=k1 - k0, ops_per_key=2000, concurrency=10, anomaly_rate=0.001, seed=3,
+                               key_base=k0))
+        rec, _ = dev.check_node(shard, -(-K // 8))
+        v, _, fe = _decode(rec, k1 - k0)
+        np.testing.assert_array_equal(v, res.valid[k0:k1])
+        np.testing.assert_array_equal(fe, res.fail_event[k0:k1])
