@@ -562,6 +562,9 @@ def main():
             "ops_total": ops_total,
             "ops_checked_per_step": ops_checked,
             "keys_to_verdict_per_s": decided * args.steps / elapsed,
+            # every key ends with a :valid? (true / false / :unknown at the
+            # budget): the rate at which the step answers for all of them
+            "ops_answered_per_s": ops_total * args.steps / elapsed,
             "resident": resident,
             "tier0_ms": avg_t0,
             "tier3_ms": avg_t3,

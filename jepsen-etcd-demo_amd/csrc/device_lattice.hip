@@ -1076,20 +1076,53 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
 __device__ unsigned long long lc_t0_stamps[8192 * 6];
 #endif
 
+// Inclusive XOR prefix over the wave's lanes (DPP row shifts, then the
+// row broadcasts across the wave's four rows).
+__device__ __forceinline__ uint32_t wave_xor_scan(uint32_t x) {
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// The slot protocol of one 64-event chunk, all slots at once: the events of a
+// slot alternate :invoke, :ok, :invoke ... from its state at the chunk's
+// start.  Each lane's slot as a one-hot bit over NW 32-bit words, XOR-scanned
+// over the lanes: bit s of the exclusive prefix is the parity of slot s's
+// earlier events in the chunk, so an event is an :ok exactly when its slot was
+// pending at the chunk's start XOR that parity.  pend: the slots pending at
+// the chunk's start (NW words, wave-uniform), updated to its end.  Returns
+// whether any tracked lane breaks the protocol.
+template <int NW>
+__device__ __forceinline__ bool slot_protocol(bool tracked, bool ok, uint32_t s, uint32_t (&pend)[NW]) {
+    const uint32_t q = s >> 5, bit = 1u << (s & 31u);
+    uint32_t par = 0, b = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint32_t oh = (tracked && q == (uint32_t)w) ? bit : 0u;
+        const uint32_t x = wave_xor_scan(oh);
+        par = q == (uint32_t)w ? (x ^ oh) : par;  // the exclusive prefix of the lane's word
+        b = q == (uint32_t)w ? pend[w] : b;
+        pend[w] ^= (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    }
+    const bool pending = (((par ^ b) & bit) != 0);
+    return __any(tracked && ok != pending);
+}
+
 // Validation of a batch the host did not check event by event (T0_STRICT
 // steps): a kernel of its own on a second stream, running beside the search
 // (which stays in bounds on any input).  One wave per key, 64 events per
 // pass: every transition id in range and installing only states the key
-// has, every slot below 64, and the slot protocol -- the events of one slot
-// alternate :invoke, :ok, :invoke ... -- checked per distinct slot of the
-// chunk: with b = 1 when the slot is pending at the chunk's start, the r-th
-// event of the slot in the chunk (r from 0, wave rank among the slot's lanes)
-// must be an :ok exactly when r + b is odd.  Violations set the batch's
-// error words (the call then returns LC_E_INVALID).
+// has, every slot below 64, and the slot protocol (slot_protocol: one XOR
+// scan per 32 slots and chunk, all slots at once).  Violations set the
+// batch's error words (the call then returns LC_E_INVALID).
 // GEN (a batch of any width whose events the host did not walk either):
-// window slots up to 126 (two pending words), the slot-127 marker of ops
-// beyond the encodable window exempt from the slot protocol (the search stops
-// before it follows one), and every :invoke's slot below the key's key_width.
+// window slots up to 126, the slot-127 marker of ops beyond the encodable
+// window exempt from the slot protocol (the search stops before it follows
+// one), and every :invoke's slot below the key's key_width.
 template <bool GEN, bool E16 = false>
 __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     const uint32_t lane = lane_id();
@@ -1099,12 +1132,18 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
     const uint32_t ns = a.trans_off ? (a.key_states ? a.key_states[k] : 0u) : a.shared_states;
     const uint32_t width = GEN ? (a.key_width ? a.key_width[k] : 127u) : 64u;
-    uint64_t pend[2] = {0, 0};
+    constexpr int NW = GEN ? 4 : 2;
+    uint32_t pend[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) pend[w] = 0;
     int32_t why = 0;
+    uint32_t w_next = lane < ee - eb ? (E16 ? LC_EV16_WIDE(a.events16[eb + lane]) : a.events[eb + lane]) : 0u;
     for (uint64_t base = eb; base < ee && !why; base += 64) {
         const uint64_t j = base + lane;
         const bool in = j < ee;
-        const uint32_t w = in ? (E16 ? LC_EV16_WIDE(a.events16[j]) : a.events[j]) : 0u;
+        const uint32_t w = w_next;
+        const uint64_t jn = j + 64;
+        w_next = jn < ee ? (E16 ? LC_EV16_WIDE(a.events16[jn]) : a.events[jn]) : 0u;  // the next chunk, in flight
         const bool ok = (w & LC_EV_OK_BIT) != 0;
         const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
         const uint32_t d = (in && !ok && t < ntr) ? a.trans[tb + t] : 0u;
@@ -1112,20 +1151,7 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
         const bool beyond = GEN && s == 127u;  // past the encodable window: no slot to track
         if (__any(in && !beyond && (GEN ? (!ok && s >= width) : s >= 64u))) why |= LC_BATCH_E_FIT;
         if (why) break;
-        uint64_t todo = __ballot(in && !beyond), npend[2] = {pend[0], pend[1]};
-        while (todo) {
-            const uint32_t sl = __builtin_amdgcn_readlane(s, (uint32_t)__builtin_ctzll(todo));
-            const uint64_t ms = __ballot(in && s == sl);
-            const uint32_t hi = GEN ? sl >> 6 : 0u, bit = sl & 63u;
-            const uint32_t b0 = (uint32_t)(pend[hi] >> bit) & 1u;
-            const uint32_t r = rank_of(ms);
-            if (__any(in && s == sl && ok != (((r + b0) & 1u) != 0))) why |= LC_BATCH_E_SLOTS;
-            if (((uint32_t)__popcll(ms) + b0) & 1u) npend[hi] |= 1ull << bit;
-            else npend[hi] &= ~(1ull << bit);
-            todo &= ~ms;
-        }
-        pend[0] = npend[0];
-        pend[1] = npend[1];
+        if (slot_protocol<NW>(in && !beyond, ok, s, pend)) why |= LC_BATCH_E_SLOTS;
     }
     if (why && lane == 0) {
         atomicOr(&a.err[0], why);
@@ -1914,8 +1940,15 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
     uint32_t ev_nn = 128 + lane < nev ? ep[128 + lane] : 0u;
     Xfer xc = xfer_of(dsc);
     uint32_t e = 0, i = 0, base = 0, lim = nev;
-    // progress quarters of the walk (its priority steps down at each)
+    // progress steps of the walk (its priority steps down at each)
+#ifndef LC_SPEC_PRIO_STEPS  // diagnostic builds: 1 = at 1/2, 3/4 and 7/8 of the walk
+#define LC_SPEC_PRIO_STEPS 0
+#endif
+#if LC_SPEC_PRIO_STEPS == 1
+    const uint32_t q1 = nev / 2u, q2 = nev - nev / 4u, q3 = nev - nev / 8u;
+#else
     const uint32_t q1 = nev / 4u, q2 = nev / 2u, q3 = nev - nev / 4u;
+#endif
     if (MODE == 0 && prio) spec_prio(0);
     auto advance = [&]() {
         ++e;
