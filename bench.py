@@ -472,6 +472,14 @@ def main():
         if d1_sync is not None:
             d1_sync["ops_per_s"] = ops_checked * args.steps / d1_sync["elapsed_s"]
         avg_t0 = float(np.mean(d1_t0)) if d1_t0 else 0.0
+        # the register tier's launch time: the resident steps' HIP-event span
+        # per launch when they ran (one launch per step); the synchronous
+        # steps' per-launch time otherwise (a large shard's synchronous step is
+        # four chunk launches waiting on their uploads: not a launch time)
+        t0_src = "synchronous D-1 steps (HIP events)"
+        if resident and resident.get("tier0_ms_per_launch") and not d1_t3:
+            avg_t0 = float(resident["tier0_ms_per_launch"])
+            t0_src = "resident asynchronous steps (HIP-event span / launches)"
         avg_t3 = float(np.mean(d1_t3)) if d1_t3 else 0.0
         n_events = int(packed.ev_off[-1])
         max_events = int(np.diff(packed.ev_off.astype(np.int64)).max()) if K else 0
@@ -556,7 +564,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": kt, "event_word_bytes": ewb,
                          "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
-                         "traffic_source": traffic_src, "issue": issue,
+                         "traffic_source": traffic_src, "issue": issue, "launch_time_from": t0_src,
                          "launches": len(d1_t0), "d4_model_gbs": d4_t3},
             "cpu_baseline": cpu,
             "ops_total": ops_total,
