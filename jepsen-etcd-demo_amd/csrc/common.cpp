@@ -1,6 +1,8 @@
 // Error reporting shared by every entry point of liblincheck.
 #include <hip/hip_runtime_api.h>
 
+#include <dlfcn.h>
+
 #include <cstdarg>
 #include <cstdlib>
 #include <mutex>
@@ -22,6 +24,37 @@ int fail(int code, const char *fmt, ...) {
     va_end(ap);
     g_last_error = buf;
     return code;
+}
+
+namespace {
+struct Roctx {
+    int (*push)(const char *) = nullptr;
+    int (*pop)() = nullptr;
+};
+const Roctx &roctx() {
+    static Roctx r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        for (const char *name : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4"})
+            if (!h) h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        r.push = (int (*)(const char *))dlsym(h, "roctxRangePushA");
+        r.pop = (int (*)())dlsym(h, "roctxRangePop");
+        if (!r.push || !r.pop) r.push = nullptr, r.pop = nullptr;
+    });
+    return r;
+}
+}  // namespace
+
+void range_push(const char *name) {
+    const Roctx &r = roctx();
+    if (r.push) r.push(name);
+}
+
+void range_pop() {
+    const Roctx &r = roctx();
+    if (r.pop) r.pop();
 }
 
 // Page-locked host memory for arrays the device reads whole (lc_pack's event

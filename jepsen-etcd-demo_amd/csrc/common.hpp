@@ -17,6 +17,19 @@ namespace lc {
 void set_error(const std::string &msg);
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// roctx ranges (tracing) around the host steps of a check --
+// pack, upload, search enqueue, gather, wait -- visible in rocprofv3
+// --marker-trace timelines beside the kernels.  The roctx library is opened
+// at first use (no link-time dependency); without it the ranges cost nothing.
+void range_push(const char *name);
+void range_pop();
+struct Range {
+    explicit Range(const char *name) { range_push(name); }
+    ~Range() { range_pop(); }
+    Range(const Range &) = delete;
+    Range &operator=(const Range &) = delete;
+};
+
 // Page-locked when a GPU is visible (a direct DMA source), else malloc.
 void *pinned_alloc(size_t bytes);
 void pinned_free(void *p);

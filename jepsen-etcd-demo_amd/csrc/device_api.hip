@@ -869,6 +869,7 @@ static void shard_keys(const lc_batch *b, int n, int64_t *key0) {
 // otherwise the caller keeps them alive until its stream has passed them.
 static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, bool validated,
                        const uint32_t *events_src = nullptr, bool sync = true, hipStream_t stream = nullptr) {
+    lc::Range range("lincheck: upload");
     hipStream_t cs = stream ? stream : c->stream;
     const int64_t K = b->n_keys;
     d->device = c->device;
@@ -1008,6 +1009,7 @@ enum ResMode { RES_HOST = 0, RES_DEV = 1, RES_CTX = 2 };
 // is only enqueued (*enqueued = true; errors surface at the next wait).
 static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mode, bool allow_async, int64_t key0,
                       lc_stats *st, bool *enqueued = nullptr, int64_t res_off = 0) {
+    lc::Range range("lincheck: search");
     if (enqueued) *enqueued = false;
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(c->device));
@@ -1348,6 +1350,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
 // Wait for everything enqueued on c; *n_async / *span_ms: the asynchronous
 // steps since the last wait and their HIP-event span.
 static int dev_wait(Dev *c, int *n_async, float *span_ms) {
+    lc::Range range("lincheck: wait");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->hctl + 6, c->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1391,6 +1394,7 @@ static int each_device(lc_ctx *c, const std::function<int(int)> &fn) {
 // page-locked, copy them into the context's pinned staging buffer.  *src:
 // where the uploads read the events from (b->events or the staging copy).
 static int prepare_batch(lc_ctx *c, const lc_batch *b, Shape *sh, const uint32_t **src) {
+    lc::Range range("lincheck: prepare");
     int rc = validate_batch(b);
     if (rc) return rc;
     *sh = batch_shape(b);
@@ -1494,6 +1498,7 @@ extern "C" int lc_check_device(lc_ctx *c, const lc_dev_batch *d, lc_result *r, i
 
 extern "C" int lc_wait(lc_ctx *c, lc_stats *st) {
     if (!c) return lc::fail(LC_E_INVALID, "lc_wait: null context");
+    lc::Range range("lc_wait");
     std::lock_guard<std::mutex> g(c->mu);
     int n = 0;
     float ms = 0;
@@ -1540,6 +1545,7 @@ extern "C" int lc_wait_step(lc_ctx *c, int back) {
 }
 
 extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_stats *st) {
+    lc::Range range("lc_check_batch");
     auto t0 = std::chrono::steady_clock::now();
     if (!c || !b || !r || !r->valid || !r->fail_event || !r->cause)
         return lc::fail(LC_E_INVALID, "lc_check_batch: null argument");
@@ -1612,6 +1618,7 @@ static int node_buffers(lc_ctx *x, Dev *c, int64_t n, int64_t block) {
 }
 
 static int gather_node(lc_ctx *x, Dev *c, int64_t n, int64_t block, bool packed = false) {
+    lc::Range range("lincheck: gather");
     const int64_t total = block * x->size;
     c->rec_out = nullptr;
     if (block > 0 && !packed) {
@@ -1637,6 +1644,7 @@ static int node_check_args(lc_ctx *c, int64_t n_keys, int64_t block) {
 }
 
 extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64_t *node, lc_stats *st) {
+    lc::Range range("lc_check_node");
     auto t0 = std::chrono::steady_clock::now();
     if (!c || !b || !node) return lc::fail(LC_E_INVALID, "lc_check_node: null argument");
     std::lock_guard<std::mutex> g(c->mu);
@@ -1763,6 +1771,7 @@ extern "C" int lc_check_node(lc_ctx *c, const lc_batch *b, int64_t block, uint64
 // i's search, and the host enqueues ahead instead of waiting between steps.
 // Anything else runs as lc_check_node.
 extern "C" int lc_check_node_async(lc_ctx *c, const lc_batch *b, int64_t block, uint64_t *node, lc_stats *st) {
+    lc::Range range("lc_check_node_async");
     if (!c || !b || !node) return lc::fail(LC_E_INVALID, "lc_check_node_async: null argument");
     Dev *d = nullptr;
     Shape sh;

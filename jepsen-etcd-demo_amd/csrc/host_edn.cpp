@@ -516,6 +516,7 @@ int finish_serial(const char *text, int64_t len, lc_hist **out) {
 }  // namespace
 
 extern "C" int lc_edn_parse(const char *text, int64_t len, lc_hist **out) {
+    lc::Range range("lc_edn_parse");
     if (!text || !out || len < 0) return lc::fail(LC_E_INVALID, "lc_edn_parse: null argument");
     try {
         const char *b = text, *e = text + len;

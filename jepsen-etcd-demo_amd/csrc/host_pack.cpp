@@ -392,6 +392,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
     if (h->n < 0 || (h->n > 0 && (!h->type || !h->f || !h->process || !h->key || !h->v0 || !h->v1)))
         return lc::fail(LC_E_INVALID, "lc_pack: history arrays missing");
     const int64_t n = h->n;
+    lc::Range range("lc_pack");
     lc_packed *P = new (std::nothrow) lc_packed();
     if (!P) return lc::fail(LC_E_NOMEM, "lc_pack: out of memory");
     static const bool timing = std::getenv("LC_TIMING") != nullptr;
