@@ -331,12 +331,37 @@ def main():
           file=sys.stderr, flush=True)
 
     cid = None
+    rccl_error = None
     if world > 1 and not host_gather:
-        obj = [comm_id() if rank == 0 else None]
+        try:
+            obj = [comm_id() if rank == 0 else None]
+        except Exception as e:  # RCCL missing or refusing: rank 0 tells every rank
+            obj = [("error", repr(e))]
         dist.broadcast_object_list(obj, src=0)
-        cid = obj[0]
+        if isinstance(obj[0], tuple):
+            rccl_error = obj[0][1]
+        else:
+            cid = obj[0]
     torch.cuda.set_device(local)
-    dev = Device(local, budget=args.budget, comm=(rank, world, cid) if cid is not None else None)
+    try:
+        dev = Device(local, budget=args.budget, comm=(rank, world, cid) if cid is not None else None)
+    except Exception as e:
+        if cid is None:
+            raise
+        dev, rccl_error = None, repr(e)
+    if world > 1 and not host_gather:
+        # every rank must hold a communicator, else none uses one: the records
+        # then go over gloo on the host, and the line says why
+        ok = torch.tensor([0 if dev is None or rccl_error else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            host_gather = True
+            if rccl_error is None:
+                rccl_error = "another rank's communicator failed"
+            print(f"[rank {rank}] RCCL unavailable ({rccl_error}); records gathered over gloo",
+                  file=sys.stderr, flush=True)
+            del dev
+            dev = Device(local, budget=args.budget)
     n_node = block * (1 if host_gather else world)
     node_buf = np.zeros(max(n_node, 1), np.uint64)
 
@@ -556,7 +581,7 @@ def main():
             "config": {"workload": cfg["desc"], "keys_total": n_keys_total, "keys_per_gpu": K, "ops_per_key": ops,
                        "concurrency": cfg["concurrency"], "budget": args.budget,
                        "parallelism": f"keys sharded over {world} GPU(s), records all-gathered "
-                                      f"({'host/gloo rehearsal' if host_gather else 'RCCL' if world > 1 else 'one rank'})"},
+                                      f"({('host/gloo, RCCL unavailable: ' + rccl_error) if rccl_error else 'host/gloo rehearsal' if host_gather else 'RCCL' if world > 1 else 'one rank'})"},
             "step": ("lc_check_node_async (two steps in flight)" if pipelined else "lc_check_node") +
                     ": packed host SoA -> H2D -> search -> verdict records -> all-gather -> host",
             "d1_sync": d1_sync,

@@ -119,6 +119,13 @@ __device__ __forceinline__ Xfer xfer_tag(uint32_t d) {
     return x;
 }
 
+// v with lane l (uniform, < 64) set to x: one v_writelane_b32.  Written as
+// `lane == l ? x : v` the compiler masks EXEC around a move per value.
+extern "C" __device__ int lc_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t setl(uint32_t v, uint32_t l, uint32_t x) {
+    return (uint32_t)lc_writelane((int)x, (int)l, (int)v);
+}
+
 // s & v as one v_and_b32 (kept opaque: the compiler would turn an AND with a
 // 0/~0 lane mask into a select through an SGPR pair)
 __device__ __forceinline__ uint32_t vand(uint32_t s, uint32_t v) {
@@ -235,6 +242,10 @@ constexpr uint32_t T0_STRICT = 32;
 constexpr uint32_t T0_SPEC_COST = 64;
 // k_spec: TOP walks leave issue priority to age alone (no progress priority)
 constexpr uint32_t T0_SPEC_NOPRIO = 128;
+// k_spec: the T0_STRICT validation blocks come first in the grid (batches of
+// more keys than the chip holds at once: dispatched last, they would run
+// after the last round of keys, alone)
+constexpr uint32_t T0_SPEC_VFIRST = 256;
 struct T0Args {
     const uint64_t *ev_off;
     const uint32_t *events;
@@ -259,6 +270,16 @@ struct T0Args {
     int32_t *spec_rr;            // speculative segments: keys left to the unsegmented search,
     int32_t *spec_nrr;           //   their count (zero at the launch)
     int32_t *spec_nrr_next;      //   and the next launch's count (zeroed by k_spec_rerun)
+    // queued speculative segments (k_specq_*): per item (LPT position x
+    // segs + segment) a header, the cut's pending :invoke words, the end
+    // set's op-index map, the end set and the two checkpoint sets
+    int32_t *q_hdr;              // 8 per item: cut, end, np, n0, top, ck_e[2], -
+    uint32_t *q_words;           // 8 per item (6 used)
+    uint64_t *q_map;             // 1 per item
+    uint32_t *q_end;             // 64 per item
+    uint32_t *q_ck;              // 128 per item
+    int32_t *q_ticket;           // the walks' queue (zeroed by k_specq_cuts)
+    int32_t q_segs;              // segments per key
 };
 
 template <bool E16>
@@ -911,12 +932,11 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                                  (uint32_t)__builtin_amdgcn_readlane(xc.cap, i),
                                  (uint32_t)__builtin_amdgcn_readlane(xc.b, i)};
                     const uint32_t idx = (uint32_t)__builtin_ctz(~live);  // lowest free index
-                    const bool me = lane == idx;
-                    slot_v = me ? slot : slot_v;
-                    k_v = me ? x.k : k_v;
-                    cap_v = me ? x.cap : cap_v;
-                    b_v = me ? x.b : b_v;
-                    dense_v = lane == slot ? idx : dense_v;
+                    slot_v = setl(slot_v, idx, slot);
+                    k_v = setl(k_v, idx, x.k);
+                    cap_v = setl(cap_v, idx, x.cap);
+                    b_v = setl(b_v, idx, x.b);
+                    dense_v = setl(dense_v, slot, idx);
                     live |= 1u << idx;
                     ++n;
                     dirty = true;
@@ -933,13 +953,13 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                     else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
                     else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
                     dirty = false;
-                    k_v = lane == p ? 0u : k_v;
+                    k_v = setl(k_v, p, 0u);
                 } else {
                 // p's transfer, then p's lane cleared for good: its index is
                 // free after this :ok (and an invalid key stops here)
                 const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
                                pb = __builtin_amdgcn_readlane(b_v, p);
-                k_v = lane == p ? 0u : k_v;
+                k_v = setl(k_v, p, 0u);
                 // Compact build (many keys per SIMD, throughput): sweeps cover
                 // the positions below the highest live index only.  Wide build
                 // (one key per SIMD, latency): one sweep body for every event --
@@ -990,12 +1010,11 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                                  (uint32_t)__builtin_amdgcn_readlane(xc.cap, i),
                                  (uint32_t)__builtin_amdgcn_readlane(xc.b, i)};
                     const uint32_t idx = n;  // dense: every index below n is taken
-                    const bool me = lane == idx;
-                    slot_v = me ? slot : slot_v;
-                    k_v = me ? x.k : k_v;
-                    cap_v = me ? x.cap : cap_v;
-                    b_v = me ? x.b : b_v;
-                    dense_v = lane == slot ? idx : dense_v;
+                    slot_v = setl(slot_v, idx, slot);
+                    k_v = setl(k_v, idx, x.k);
+                    cap_v = setl(cap_v, idx, x.cap);
+                    b_v = setl(b_v, idx, x.b);
+                    dense_v = setl(dense_v, slot, idx);
                     live |= 1u << idx;
                     ++n;
                 }
@@ -1019,14 +1038,15 @@ __device__ __forceinline__ int lattice_key(const T0Args &a, int32_t key, uint32_
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
                 const uint32_t x0 = __builtin_amdgcn_readlane(k_v, last),
                                x1 = __builtin_amdgcn_readlane(cap_v, last), x2 = __builtin_amdgcn_readlane(b_v, last);
-                const bool mp = lane == p && !r;
-                slot_v = mp ? s_last : slot_v;
-                k_v = mp ? x0 : k_v;
-                cap_v = mp ? x1 : cap_v;
-                b_v = mp ? x2 : b_v;
-                dense_v = (lane == s_last && !r) ? p : dense_v;
-                // index `last` is free now: zero transfer (the lane phase relies on it)
-                k_v = (lane == last && !r) ? 0u : k_v;
+                if (!r) {
+                    slot_v = setl(slot_v, p, s_last);
+                    k_v = setl(k_v, p, x0);
+                    cap_v = setl(cap_v, p, x1);
+                    b_v = setl(b_v, p, x2);
+                    dense_v = setl(dense_v, s_last & 63u, p);
+                    // index `last` is free now: zero transfer (the lane phase relies on it)
+                    k_v = setl(k_v, last, 0u);
+                }
                 live = r ? live : (1u << last) - 1u;
                 if (RM < 16 && in_mem && n == 9 && !r) {  // back to registers: no config holds index 8 or 9
 #pragma unroll
@@ -1430,7 +1450,7 @@ __device__ __forceinline__ void segment_search(const SegArgs &a, int32_t key, ui
                 else if (top == 5) r = ok_lane_closed<5, TAG>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty, m_v);
                 else r = ok_lane_closed<4, TAG>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty, m_v);
                 dirty = false;
-                k_v = lane == p ? 0u : k_v;
+                k_v = setl(k_v, p, 0u);
                 live = r ? live : live & ~(1u << p);
                 n = r ? n : n - 1;
                 status = r;
@@ -1976,12 +1996,11 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                     status = 3;
                 } else {
                     const uint32_t idx = (uint32_t)__builtin_ctz(~live);
-                    const bool me = lane == idx;
-                    slot_v = me ? slot : slot_v;
-                    k_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.k, i) : k_v;
-                    cap_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.cap, i) : cap_v;
-                    b_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.b, i) : b_v;
-                    dense_v = lane == slot ? idx : dense_v;
+                    slot_v = setl(slot_v, idx, slot);
+                    k_v = setl(k_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.k, i));
+                    cap_v = setl(cap_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.cap, i));
+                    b_v = setl(b_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.b, i));
+                    dense_v = setl(dense_v, slot, idx);
                     live |= 1u << idx;
                     ++n;
                     dirty = true;
@@ -1998,7 +2017,7 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                 else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
                 else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
                 dirty = false;
-                k_v = lane == p ? 0u : k_v;
+                k_v = setl(k_v, p, 0u);
                 live = r ? live : live & ~(1u << p);
                 n = r ? n : n - 1;
                 status = r;
@@ -2049,12 +2068,11 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                         in_mem = true;
                     }
                     const uint32_t idx = n;
-                    const bool me = lane == idx;
-                    slot_v = me ? slot : slot_v;
-                    k_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.k, i) : k_v;
-                    cap_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.cap, i) : cap_v;
-                    b_v = me ? (uint32_t)__builtin_amdgcn_readlane(xc.b, i) : b_v;
-                    dense_v = lane == slot ? idx : dense_v;
+                    slot_v = setl(slot_v, idx, slot);
+                    k_v = setl(k_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.k, i));
+                    cap_v = setl(cap_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.cap, i));
+                    b_v = setl(b_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.b, i));
+                    dense_v = setl(dense_v, slot, idx);
                     live |= 1u << idx;
                     ++n;
                 }
@@ -2070,13 +2088,14 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                 const uint32_t s_last = __builtin_amdgcn_readlane(slot_v, last);
                 const uint32_t x0 = __builtin_amdgcn_readlane(k_v, last), x1 = __builtin_amdgcn_readlane(cap_v, last),
                                x2 = __builtin_amdgcn_readlane(b_v, last);
-                const bool mp = lane == p && !r;
-                slot_v = mp ? s_last : slot_v;
-                k_v = mp ? x0 : k_v;
-                cap_v = mp ? x1 : cap_v;
-                b_v = mp ? x2 : b_v;
-                dense_v = (lane == s_last && !r) ? p : dense_v;
-                k_v = (lane == last && !r) ? 0u : k_v;
+                if (!r) {
+                    slot_v = setl(slot_v, p, s_last);
+                    k_v = setl(k_v, p, x0);
+                    cap_v = setl(cap_v, p, x1);
+                    b_v = setl(b_v, p, x2);
+                    dense_v = setl(dense_v, s_last & 63u, p);
+                    k_v = setl(k_v, last, 0u);
+                }
                 live = r ? live : (1u << last) - 1u;
                 if (in_mem && n == 9 && !r) {
 #pragma unroll
@@ -2112,7 +2131,7 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(lc_spec_stamps), (size_t)n * 8 * 12 * 8, 0, hipMemcpyDeviceToHost);
 }
 #define SPEC_STAMP(k, v) \
-    if (lane == 0 && blockIdx.x < 4096) lc_spec_stamps[((size_t)blockIdx.x * 8 + wv) * 12 + (k)] = (v);
+    if (lane == 0 && blk < 4096) lc_spec_stamps[((size_t)blk * 8 + wv) * 12 + (k)] = (v);
 #else
 #define SPEC_STAMP(k, v)
 #endif
@@ -2136,16 +2155,19 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     __shared__ uint32_t s_ws[NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
     __shared__ int32_t s_ws_busy[NWS];
     const uint32_t lane = lane_id(), wv = uni((uint32_t)threadIdx.x >> 6);  // uniform per wave
-    if (blockIdx.x >= (uint32_t)a.n_order) {
-        // T0_STRICT steps: the event-by-event validation, in blocks after the
-        // keys' (no second stream, no cross-stream waits around the step)
-        const int64_t nb = (int64_t)gridDim.x - a.n_order;
-        for (int64_t k = ((int64_t)blockIdx.x - a.n_order) * S + wv; k < a.n_order; k += nb * S)
-            validate_key<false, E16>(a, k);
+    // T0_STRICT steps: the event-by-event validation, in nb blocks after the
+    // keys' (no second stream, no cross-stream waits around the step), or
+    // before them (T0_SPEC_VFIRST)
+    const uint32_t nb = gridDim.x - (uint32_t)a.n_order;
+    const bool vfirst = (a.flags & T0_SPEC_VFIRST) != 0;
+    const uint32_t blk = vfirst ? blockIdx.x - nb : blockIdx.x;  // the key block's LPT position
+    if (vfirst ? blockIdx.x < nb : blockIdx.x >= (uint32_t)a.n_order) {
+        const uint32_t vb = vfirst ? blockIdx.x : blockIdx.x - (uint32_t)a.n_order;
+        for (int64_t k = (int64_t)vb * S + wv; k < a.n_order; k += (int64_t)nb * S) validate_key<false, E16>(a, k);
         return;  // the whole block: no barrier below is reached by half of it
     }
-    const int32_t key = a.order[blockIdx.x];
-    uint32_t *ws = a.lat_ws + ((size_t)blockIdx.x * S + wv) * (3 * T0_RMEM * 64);
+    const int32_t key = a.order[blk];
+    uint32_t *ws = a.lat_ws + ((size_t)blk * S + wv) * (3 * T0_RMEM * 64);
     const uint64_t eb = a.ev_off[key];
     const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
     const EvSrc<E16> evp = ev_src<E16>(a) + eb;
@@ -2372,6 +2394,271 @@ __global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
     }
 }
 
+// ---- Queued speculative segments (k_specq_cuts, k_specq_walks, k_specq_join)
+//
+// The same search as k_spec, scheduled differently.  k_spec gives every key a
+// workgroup of S waves and ends when the slowest of its 4,000 walks ends: on
+// C2 the median TOP walk took 423k cycles, the slowest 578k, and a SIMD's
+// waves issue at 26 % of its VALU rate while they wait on their own chains.
+// A wave's chain is latency-bound, so a SIMD does more work with more waves
+// (the fit's +18 cycles per event per co-resident wave), and shorter walks
+// end the launch sooner.  Here:
+//   k_specq_cuts  -- one wave per key: the cuts (segs per key at equal event
+//                    counts, each moved to the fewest ops pending within 64
+//                    events), the pending ops at each, into the item headers;
+//   k_specq_walks -- independent waves, each taking one item (key x
+//                    segment, LPT key order) from a queue: every TOP walk
+//                    (segment 0 exactly), then the T0_STRICT validation of
+//                    the keys as the queue's last items, which fill the
+//                    walks' tail.  Small workgroups (SPECQ_WPB waves sharing
+//                    a 9-10-pending LDS workspace) free their slots as their
+//                    walks end, so the dispatcher keeps every SIMD full.  (A
+//                    persistent grid looping over the queue needs ~20 more
+//                    VGPRs: 4 waves per SIMD instead of 6.)
+//   k_specq_join  -- one workgroup of segs waves per key: the verifying runs
+//                    from each predecessor's end set (to the checkpoints the
+//                    TOP walk recorded) and the key's verdict, as k_spec.
+// Items live in HBM (840 B each); k_spec_rerun follows for keys whose runs
+// never met.
+#ifndef LC_SPECQ_WPB
+#define LC_SPECQ_WPB 2
+#endif
+constexpr int SPECQ_WPB = LC_SPECQ_WPB;  // independent waves per k_specq_walks workgroup
+constexpr int SPECQ_NWS = SPECQ_WPB >= 4 ? SPECQ_WPB / 2 : 1;  // their shared LDS workspaces
+
+__device__ __forceinline__ bool spec_plain(const T0Args &a, int32_t key, uint32_t nev, uint32_t &nstates) {
+    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
+    (void)tb;
+    nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
+    const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;
+    return (a.key_error && a.key_error[key]) || nstates > T0_MAX_STATES || nstates == 0 || width > T0_MAX_WIDTH ||
+           a.init_state >= T0_MAX_STATES || nev < 2 * SPEC_MIN_LEN;
+}
+
+template <bool E16>
+__global__ __launch_bounds__(256) void k_specq_cuts(T0Args a) {
+    const uint32_t lane = lane_id();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.q_ticket = 0;  // the walks' queue
+    const int64_t kp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (kp >= a.n_order) return;
+    const uint32_t S = (uint32_t)a.q_segs;
+    const int32_t key = a.order[kp];
+    const uint64_t eb = a.ev_off[key];
+    const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
+    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
+    uint32_t nstates;
+    const bool plain = spec_plain(a, key, nev, nstates);
+    const uint32_t eff = plain ? 0u : min(S, nev / SPEC_MIN_LEN);
+    int32_t *const hdr = a.q_hdr + (size_t)kp * S * 8;
+    // candidate cut s (lane s) and the ops pending there
+    uint32_t cand_v = SPEC_NONE, ncand_v = 0;
+    int32_t pend = 0;
+    uint32_t prev = 0;
+    for (uint32_t s = 1; s < eff; ++s) {
+        const uint32_t t = (uint32_t)((uint64_t)nev * s / eff);
+        pend += spec_net(evp, prev, t);
+        prev = t;
+        const uint32_t w = t + lane < nev ? evp[t + lane] : 0u;
+        uint32_t n2 = 0;
+        const uint32_t c2 = spec_cut_at(w, nev, t, pend, n2);
+        cand_v = lane == s ? c2 : cand_v;
+        ncand_v = lane == s ? n2 : ncand_v;
+    }
+    // kept cuts: each past the last kept one
+    uint32_t kept_v = SPEC_NONE, last = 0;
+    for (uint32_t s = 1; s < eff; ++s) {
+        uint32_t c2 = uni((uint32_t)__builtin_amdgcn_readlane(cand_v, s));
+        if (c2 != SPEC_NONE && c2 <= last) c2 = SPEC_NONE;
+        if (c2 != SPEC_NONE) last = c2;
+        kept_v = lane == s ? c2 : kept_v;
+    }
+    if (eff > 0) kept_v = lane == 0 ? 0u : kept_v;  // segment 0 from the key's start
+    // headers: cut (-1: no segment), end (the next kept cut), pending ops
+    uint32_t end_v = nev;
+    for (uint32_t s = eff; s-- > 1;) {
+        const uint32_t c2 = uni((uint32_t)__builtin_amdgcn_readlane(kept_v, s));
+        end_v = lane < s && c2 != SPEC_NONE ? c2 : end_v;
+    }
+    if (lane < S) {
+        const bool on = lane < eff && kept_v != SPEC_NONE;
+        int32_t *h = hdr + lane * 8;
+        h[0] = on ? (int32_t)kept_v : -1;
+        h[1] = (int32_t)end_v;
+        h[3] = lane == 0 ? 0 : (int32_t)ncand_v;
+        h[4] = -1;
+        h[5] = h[6] = -1;
+    }
+    for (uint32_t s = 0; s < eff; ++s) {
+        const uint32_t c2 = uni((uint32_t)__builtin_amdgcn_readlane(kept_v, s));
+        if (c2 == SPEC_NONE) continue;
+        uint32_t words = 0, np = 0;
+        if (s > 0) words = spec_pending(evp, c2, uni((uint32_t)__builtin_amdgcn_readlane(ncand_v, s)), np);
+        const size_t it = (size_t)kp * S + s;
+        if (lane < 8) a.q_words[it * 8 + lane] = lane < 6 ? words : 0u;
+        if (lane == 0) a.q_hdr[it * 8 + 2] = (int32_t)np;
+    }
+}
+
+// One item's TOP walk (segment 0 exactly from the initial state): its status
+// into the header, its end set and op-index map, its checkpoints.
+template <bool E16>
+__device__ __forceinline__ void specq_walk_item(const T0Args &a, int64_t it, uint32_t *ws, uint32_t *lds_ws,
+                                                int32_t *lds_busy) {
+    const uint32_t lane = lane_id();
+    const uint32_t S = (uint32_t)a.q_segs;
+    int32_t *const h = a.q_hdr + it * 8;
+    const int32_t cut_i = uni(h[0]);
+    if (cut_i < 0) return;
+    const uint32_t s = (uint32_t)(it % S);
+    const int32_t key = a.order[it / S];
+    const uint64_t eb = a.ev_off[key];
+    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
+    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
+    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
+    const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
+    const uint32_t nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
+    const uint32_t topmask = nstates >= 32 ? ~0u : (1u << nstates) - 1u;
+    const uint32_t cut = (uint32_t)cut_i, end = (uint32_t)uni(h[1]);
+    const uint32_t np = (uint32_t)uni(h[2]), n0 = (uint32_t)uni(h[3]);
+    SpecState st{};
+    if (s == 0) {
+        st.W0 = lane == 0 ? 1u << a.init_state : 0u;
+    } else {
+        spec_setup(st, lane < 6 ? a.q_words[it * 8 + lane] : 0u, np, trp, ntr);
+        st.W0 = lane < (1u << np) ? topmask : 0u;
+    }
+    // the ops found pending must be as many as the count says (else the
+    // event stream is malformed): the key is searched unsegmented
+    const bool lost = s != 0 && np != n0;
+    uint32_t fev = 0;
+    const int r = lost ? 6 : spec_walk<0, SPECQ_NWS>(evp, trp, ntr, cut, end, st, ws, lds_ws, lds_busy,
+                                             (uint32_t(*)[64])(a.q_ck + it * 128), h + 5, a.spec_ck1, a.spec_ck2, fev);
+    a.q_end[it * 64 + lane] = st.W0;
+    uint64_t map = 0;
+    for (uint32_t q = 0; q < 6; ++q) {
+        const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, q);
+        if ((st.live >> q) & 1u) map |= (uint64_t)(0x80u | sl) << (8 * q);
+    }
+    if (lane == 0) {
+        a.q_map[it] = map;
+        h[4] = r == 1 ? (int32_t)fev : r == 3 ? -2 : r == 6 ? -3 : -1;
+    }
+}
+
+template <bool E16>
+__global__ __launch_bounds__(64 * SPECQ_WPB) void k_specq_walks(T0Args a) {
+    __shared__ uint32_t s_ws[SPECQ_NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
+    __shared__ int32_t s_ws_busy[SPECQ_NWS];
+    if (threadIdx.x < SPECQ_NWS) s_ws_busy[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const int64_t n_items = (int64_t)a.n_order * a.q_segs;
+    const int64_t n_val = (a.flags & T0_STRICT) ? a.n_order : 0;
+    int32_t t = 0;
+    if (lane == 0) t = atomicAdd(a.q_ticket, 1);
+    t = uni(t);
+    if ((int64_t)t >= n_items + n_val) return;
+    if ((int64_t)t >= n_items) {
+        validate_key<false, E16>(a, (int64_t)t - n_items);
+    } else {
+        uint32_t *const ws = a.lat_ws + (size_t)t * (3 * T0_RMEM * 64);  // the item's global workspace
+        specq_walk_item<E16>(a, t, ws, s_ws, s_ws_busy);
+    }
+}
+
+template <int S, bool E16>
+__global__ __launch_bounds__(64 * S) void k_specq_join(T0Args a) {
+    __shared__ int32_t s_ver[S], s_vfev[S];
+    __shared__ uint32_t s_ws[3 * T0_RMEM * 64];
+    __shared__ int32_t s_ws_busy[1];
+    const uint32_t lane = lane_id(), wv = uni((uint32_t)threadIdx.x >> 6);
+    const int64_t kp = blockIdx.x;
+    const int32_t key = a.order[kp];
+    const uint64_t eb = a.ev_off[key];
+    const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
+    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
+    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
+    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
+    const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
+    uint32_t nstates;
+    const bool plain = spec_plain(a, key, nev, nstates);
+    const uint32_t eff = plain ? 0u : min((uint32_t)S, nev / SPEC_MIN_LEN);
+    const size_t it0 = (size_t)kp * S;
+    const int32_t *const hk = a.q_hdr + it0 * 8;  // the key's item headers
+    uint32_t *const ws = a.lat_ws + (it0 + wv) * (3 * T0_RMEM * 64);
+    if (threadIdx.x == 0) s_ws_busy[0] = 0;
+    __syncthreads();
+    if (wv >= 1 && wv < eff && uni(hk[wv * 8 + 0]) >= 0 && uni(hk[wv * 8 + 4]) != -3) {
+        uint32_t pw = wv - 1;
+        while (uni(hk[pw * 8 + 0]) < 0) --pw;  // segment 0 always exists
+        int32_t ver = 0, vfev = -1;
+        if (uni(hk[pw * 8 + 4]) == -1) {
+            const size_t it = it0 + wv;
+            const uint32_t cut = (uint32_t)uni(hk[wv * 8 + 0]), end = (uint32_t)uni(hk[wv * 8 + 1]);
+            const uint32_t np = (uint32_t)uni(hk[wv * 8 + 2]);
+            SpecState st{};
+            spec_setup(st, lane < 6 ? a.q_words[it * 8 + lane] : 0u, np, trp, ntr);
+            // the predecessor's end set, relabelled from its op indices to these
+            const uint64_t map = uni(a.q_map[it0 + pw]);
+            uint32_t src = 0;
+            for (uint32_t j = 0; j < np; ++j) {
+                const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, j);
+                uint32_t at = 31;
+                for (uint32_t q = 0; q < 6; ++q)
+                    if (((map >> (8 * q)) & 0xFFu) == (0x80u | sl)) at = q;
+                src |= ((lane >> j) & 1u) << at;
+            }
+            const uint32_t E = (uint32_t)__shfl((int)a.q_end[(it0 + pw) * 64 + lane], (int)(src & 63u));
+            st.W0 = lane < (1u << np) ? E : 0u;
+            uint32_t fev = 0;
+            const int r = spec_walk<1, 1>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
+                                          (uint32_t(*)[64])(a.q_ck + it * 128), a.q_hdr + it * 8 + 5, 0, 0, fev);
+            bool last = true;
+            for (uint32_t q = wv + 1; q < eff; ++q) last = last && uni(hk[q * 8 + 0]) < 0;
+            if (r == 4) ver = 1;                                // met the TOP run
+            else if (r == 1) { ver = 2; vfev = (int32_t)fev; }  // died before meeting it
+            else if (r == 3) ver = 6;                           // does not fit
+            else if (r == 5) ver = 3;                           // never met
+            else if (last) ver = 5;                             // the last segment, searched exactly to its end
+            else ver = (st.n <= 6 && !__any(st.W0 != a.q_end[it * 64 + lane])) ? 1 : 3;
+        }
+        if (lane == 0) { s_ver[wv] = ver; s_vfev[wv] = vfev; }
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    // the key's verdict: the first segment whose real run dies
+    const Args &f = *a.full;
+    bool rerun = plain, bad = false;
+    int32_t fv = -1;
+    for (uint32_t s = 0; s < eff && fv < 0 && !rerun && !bad; ++s) {
+        if (uni(hk[s * 8 + 0]) < 0) continue;
+        const int32_t top = uni(hk[s * 8 + 4]);
+        if (top == -2) { bad = true; break; }
+        if (top == -3) { rerun = true; break; }
+        if (s == 0) { fv = top; continue; }
+        const int32_t ver = uni(s_ver[s]);
+        if (ver == 1) fv = top;
+        else if (ver == 2) fv = uni(s_vfev[s]);
+        else if (ver == 6) bad = true;
+        else if (ver != 5) rerun = true;  // never met (or nothing to start from): unsegmented
+    }
+    if (rerun) {
+        if (lane == 0) a.spec_rr[atomicAdd(a.spec_nrr, 1)] = key;
+    } else if (bad) {
+        if (a.flags & T0_STRICT) {
+            t0_malformed(a, key, LC_BATCH_E_FIT);
+            finish_key(f, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+        } else {
+            const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
+            push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key, f.list_cap);
+        }
+    } else if (fv >= 0) {
+        finish_key(f, key, LC_INVALID, LC_CAUSE_NONLIN, fv, 0, 0, (uint64_t)fv + 1u);
+    } else {
+        finish_key(f, key, LC_VALID, LC_CAUSE_NONE, -1, 0, 0, nev);
+    }
+}
+
 size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * lat_ws_words(); }
 
 // Keys order[0 .. n_order) in workgroups of `segs` segments (2, 3, 4, 6 or
@@ -2381,10 +2668,11 @@ size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t
 // validate: add the T0_STRICT validation blocks.
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
-                       bool cost_cuts, bool prio, hipStream_t s) {
+                       bool cost_cuts, bool prio, bool vfirst, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
     t.events16 = events16;
     if (cost_cuts) t.flags |= T0_SPEC_COST;
+    if (vfirst && validate_blocks > 0) t.flags |= T0_SPEC_VFIRST;
     if (!prio) t.flags |= T0_SPEC_NOPRIO;
     t.lat_ws = ws;
     t.spec_ck1 = ck1;
@@ -2411,6 +2699,48 @@ hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws,
     if (e != hipSuccess) return e;
     if (events16) hipLaunchKernelGGL(k_spec_rerun<true>, rgrid, dim3(64), 0, s, t);
     else hipLaunchKernelGGL(k_spec_rerun<false>, rgrid, dim3(64), 0, s, t);
+    return hipGetLastError();
+}
+
+size_t specq_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * 210 + 2; }
+
+// Queued speculative segments: k_specq_cuts, k_specq_walks (one wave per
+// queue ticket: items, then validation), k_specq_join, k_spec_rerun.
+// q: specq_words(n_order, segs) words; ws: spec_ws_words(n_order, segs)
+// (12 KB per item); rr as for launch_spec.
+hipError_t launch_specq(const Args &a, const Args *a_dev, int segs, uint32_t *q, uint32_t *ws, int32_t *rr,
+                        int parity, uint32_t ck1, uint32_t ck2, int rerun_grid, const uint16_t *events16,
+                        hipStream_t s) {
+    T0Args t = make_t0(a, a_dev);
+    t.events16 = events16;
+    t.lat_ws = ws;
+    t.spec_ck1 = ck1;
+    t.spec_ck2 = ck2;
+    t.spec_nrr = rr + (parity & 1);
+    t.spec_nrr_next = rr + ((parity & 1) ^ 1);
+    t.spec_rr = rr + 2;
+    const size_t ni = (size_t)std::max<int64_t>(a.n_order, 1) * segs;
+    t.q_segs = segs;
+    t.q_hdr = (int32_t *)q;
+    t.q_words = q + ni * 8;
+    t.q_map = (uint64_t *)(q + ni * 16);
+    t.q_end = q + ni * 18;
+    t.q_ck = q + ni * 82;
+    t.q_ticket = (int32_t *)(q + ni * 210);
+    const int K = std::max(1, a.n_order);
+    const dim3 cgrid((unsigned)((K + 3) / 4)), jgrid((unsigned)K);
+    const int64_t tickets = (int64_t)K * segs + (a.strict ? K : 0);
+    const dim3 wgrid((unsigned)((tickets + SPECQ_WPB - 1) / SPECQ_WPB));
+    const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid)));
+#define LC_SPECQ(E)                                                                                   \
+    hipLaunchKernelGGL(k_specq_cuts<E>, cgrid, dim3(256), 0, s, t);                                   \
+    hipLaunchKernelGGL(k_specq_walks<E>, wgrid, dim3(64 * SPECQ_WPB), 0, s, t);                       \
+    if (segs >= 8) hipLaunchKernelGGL((k_specq_join<8, E>), jgrid, dim3(512), 0, s, t);               \
+    else if (segs >= 4) hipLaunchKernelGGL((k_specq_join<4, E>), jgrid, dim3(256), 0, s, t);          \
+    else hipLaunchKernelGGL((k_specq_join<2, E>), jgrid, dim3(128), 0, s, t);                         \
+    hipLaunchKernelGGL(k_spec_rerun<E>, rgrid, dim3(64), 0, s, t);
+    if (events16) { LC_SPECQ(true) } else { LC_SPECQ(false) }
+#undef LC_SPECQ
     return hipGetLastError();
 }
 
