@@ -363,9 +363,7 @@ typedef struct lc_opts {
                                       are given (lc_batch.events16)                 */
 #define LC_PATH_SPEC_NOPRIO  0x400 /* speculative walks: issue priority by wave age
                                       alone, not by progress                        */
-#define LC_PATH_SPEC_QUEUE   0x800 /* speculative segments as queued walks
-                                      (k_specq_*), not a workgroup per key          */
-#define LC_PATH_ALL          0xFFF
+#define LC_PATH_ALL          0x7FF
 
 /* lc_opts.flags */
 #define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,
@@ -424,7 +422,6 @@ typedef struct lc_stats {
 #define LC_T0_PATH_LATTICE   1  /* k_search_lattice: one wave per key            */
 #define LC_T0_PATH_SPEC      2  /* k_spec: speculative key segments              */
 #define LC_T0_PATH_SEGMENTS  3  /* k_search_segments: quiescent-point segments    */
-#define LC_T0_PATH_SPECQ     4  /* k_specq_walks: speculative segments, queued    */
 
 typedef struct lc_ctx lc_ctx;
 typedef struct lc_dev_batch lc_dev_batch;

@@ -335,8 +335,6 @@ struct Dev {
     size_t spec_ws_words = 0;
     int32_t *spec_rr = nullptr;    // two rerun counts (used in turn), then the rerun list
     int64_t spec_rr_cap = 0;
-    uint32_t *specq = nullptr;     // queued speculative segments: item records, queue ticket
-    size_t specq_words = 0;
     int spec_parity = 0;
     // node records (lc_check_node): this rank's block and the gathered node
     uint64_t *send = nullptr, *node = nullptr;
@@ -373,7 +371,7 @@ struct Dev {
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(lws.base); dfree(dargs); dfree(send); dfree(node);
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
-        dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr); dfree(specq);
+        dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr);
         if (hargs) (void)hipHostFree(hargs);
         if (hnode) (void)hipHostFree(hnode);
         for (hipEvent_t &e : args_ev)
@@ -1081,24 +1079,17 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     //
     // Large batches too (C3 shards: 2 segments per key; 12,500 x 2,000 4.44
     // ms against 5.51 unsegmented, the whole C3 key space 33.2 against 38.0).
-    // LC_PATH_SPEC_QUEUE (measuring): the TOP walks of every (key, segment)
-    // item taken from one queue by independent waves, so a SIMD keeps as many
-    // walks as its registers allow to the end of the launch; segments per key
-    // for about two items per resident wave (C2: 8 per key), at least 2.
-    const bool queued = (o.path_flags & LC_PATH_SPEC_QUEUE) != 0;
-    const int64_t slots = (int64_t)c->cu_count * 24;  // ~6 walk waves per SIMD
-    int segs = 0;
-    if (K > 0 && queued) {
-        segs = K * 2 >= 2 * slots ? 2 : K * 4 >= 2 * slots ? 4 : 8;
-    } else if (K > 0) {
-        segs = (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1));
-        segs = segs >= 8 ? 8 : segs >= 4 ? 4 : 2;
-    }
+    // More segments than waves (a key's waves taking its segments from a
+    // block-local queue, see k_spec) measured slower: C2 8 segments on 4 waves
+    // 0.302 ms, 12 on 4 0.332, against 0.273 for 4 on 4; a C3 shard 4 on 2
+    // 4.75 ms, 8 on 2 5.30, against 4.40 for 2 on 2.
+    int segs = K > 0 ? (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1)) : 0;
+    segs = segs >= 8 ? 8 : segs >= 4 ? 4 : K > 0 ? 2 : 0;
     if (o.spec_segs) segs = o.spec_segs;
-    if (queued && segs != 2 && segs != 4 && segs != 8) segs = segs < 4 ? 2 : segs < 8 ? 4 : 8;
+    const int waves = segs;
     const bool spec = !split && t0_step && fast && segs >= 2 && !(o.path_flags & LC_PATH_SPEC_OFF);
     if (spec) {
-        const size_t need = lcd::spec_ws_words(K, segs);
+        const size_t need = lcd::spec_ws_words(K, waves);
         if (need > c->spec_ws_words) {
             if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
             dfree(c->spec_ws);
@@ -1116,22 +1107,13 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             HIPCHK(hipMemsetAsync(c->spec_rr, 0, 2 * sizeof(int32_t), c->stream));
             c->spec_rr_cap = K + 2;
         }
-        const size_t qneed = queued ? lcd::specq_words(K, segs) : 0;
-        if (qneed > c->specq_words) {
-            if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
-            dfree(c->specq);
-            c->specq = nullptr;
-            c->specq_words = 0;
-            HIPCHK(dalloc(&c->specq, qneed));
-            c->specq_words = qneed;
-        }
     }
     // The speculative segments read 16-bit event words in place; every other
     // kernel reads the 32-bit form, widened here once per upload.
     const uint16_t *ev16 = (spec && d->events16) ? d->events16 : nullptr;
     const uint32_t t0_path = K == 0 || d->table ? LC_T0_PATH_NONE
                              : split            ? LC_T0_PATH_SEGMENTS
-                             : spec             ? (queued ? LC_T0_PATH_SPECQ : LC_T0_PATH_SPEC)
+                             : spec             ? LC_T0_PATH_SPEC
                                                 : LC_T0_PATH_LATTICE;
     if (!ev16 && !d->ev32_ready && d->n_events) {
         const uint64_t n4 = (d->n_events + 3) / 4;
@@ -1222,16 +1204,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         // the validation of a host-unchecked batch runs in extra blocks of
         // the same launch (a second stream cost ~40 us of cross-stream waits)
         const int vblocks = a.strict ? (int)std::min<int64_t>(K, c->cu_count) : 0;
-        if (queued) {
-            HIPCHK(lcd::launch_specq(a0, dargs, segs, c->specq, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2,
-                                     c->cu_count * 8, ev16, c->stream));
-        } else {
-            HIPCHK(lcd::launch_spec(a0, dargs, segs, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2,
-                                    c->cu_count * 8, vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
-                                    !(o.path_flags & LC_PATH_SPEC_NOPRIO),
-                                    K * segs > (int64_t)c->cu_count * 16,  // more keys than one resident round
-                                    c->stream));
-        }
+        HIPCHK(lcd::launch_spec(a0, dargs, segs, waves, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2,
+                                c->cu_count * 8, vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
+                                !(o.path_flags & LC_PATH_SPEC_NOPRIO),
+                                K * waves > (int64_t)c->cu_count * 16,  // more keys than one resident round
+                                c->stream));
         c->spec_parity ^= 1;
         if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0 && !d->table) {

@@ -270,16 +270,6 @@ struct T0Args {
     int32_t *spec_rr;            // speculative segments: keys left to the unsegmented search,
     int32_t *spec_nrr;           //   their count (zero at the launch)
     int32_t *spec_nrr_next;      //   and the next launch's count (zeroed by k_spec_rerun)
-    // queued speculative segments (k_specq_*): per item (LPT position x
-    // segs + segment) a header, the cut's pending :invoke words, the end
-    // set's op-index map, the end set and the two checkpoint sets
-    int32_t *q_hdr;              // 8 per item: cut, end, np, n0, top, ck_e[2], -
-    uint32_t *q_words;           // 8 per item (6 used)
-    uint64_t *q_map;             // 1 per item
-    uint32_t *q_end;             // 64 per item
-    uint32_t *q_ck;              // 128 per item
-    int32_t *q_ticket;           // the walks' queue (zeroed by k_specq_cuts)
-    int32_t q_segs;              // segments per key
 };
 
 template <bool E16>
@@ -2130,28 +2120,34 @@ __device__ unsigned long long lc_spec_stamps[4096 * 8 * 12];
 extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(lc_spec_stamps), (size_t)n * 8 * 12 * 8, 0, hipMemcpyDeviceToHost);
 }
-#define SPEC_STAMP(k, v) \
-    if (lane == 0 && blk < 4096) lc_spec_stamps[((size_t)blk * 8 + wv) * 12 + (k)] = (v);
+#define SPEC_STAMP(s, k, v) \
+    if (lane == 0 && blk < 4096 && (s) < 8) lc_spec_stamps[((size_t)blk * 8 + (s)) * 12 + (k)] = (v);
 #else
-#define SPEC_STAMP(k, v)
+#define SPEC_STAMP(s, k, v)
 #endif
 
-// One workgroup of S waves per key (blockIdx = LPT position).  Results go
-// through a.full like T0's; a.lat_ws holds each wave's 9-10-pending
-// workspace (global memory: with LDS for it, fewer segments fit a CU).
-template <int S, bool E16>
-__global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
+// One workgroup of W waves per key (blockIdx = LPT position), the key cut into
+// up to S segments; the waves take the segments' TOP walks, then their
+// verifying runs, from two block-local queues (launched with S = W: more
+// segments than waves, a wave taking another walk instead of waiting at the
+// barrier for the slowest, measured slower -- every extra cut costs a
+// verifying run and a walk's start-up).  Results go through a.full like
+// T0's; a.lat_ws holds each wave's 9-10-pending fallback workspace (global
+// memory: the workgroup's LDS workspaces are shared, NWS of them).
+template <int S, int W, bool E16>
+__global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
     __shared__ uint32_t s_ck[S][2][64];   // TOP run's checkpoint sets
     __shared__ uint32_t s_pend[S][8];     // ops pending at the cut ([0..5] words, [6] count)
     __shared__ uint64_t s_map[S];         // end: byte i = 0x80 | slot of live op index i
     __shared__ int32_t s_ck_e[S][2];      // checkpoint events (-1: none)
     __shared__ int32_t s_cut[S], s_segend[S];  // segment [cut, end); cut -1: no segment
-    __shared__ int32_t s_top[S];          // TOP run: -1 alive, -2 does not fit, else its failing event
+    __shared__ int32_t s_top[S];          // TOP run: -1 alive, -2 does not fit, -3 lost, else its failing event
     __shared__ int32_t s_ver[S], s_vfev[S];
     __shared__ int32_t s_net[S];          // cut search: pending-count change over each part
     __shared__ int32_t s_cand[S], s_ncand[S];  // each target's cut (-1: none) and ops pending there
-    constexpr int NWS = spec_lds_ws<S>();
+    __shared__ int32_t s_next[2];         // the block's queues: TOP walks, verifying runs
+    constexpr int NWS = spec_lds_ws<W>();
     __shared__ uint32_t s_ws[NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
     __shared__ int32_t s_ws_busy[NWS];
     const uint32_t lane = lane_id(), wv = uni((uint32_t)threadIdx.x >> 6);  // uniform per wave
@@ -2163,11 +2159,11 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     const uint32_t blk = vfirst ? blockIdx.x - nb : blockIdx.x;  // the key block's LPT position
     if (vfirst ? blockIdx.x < nb : blockIdx.x >= (uint32_t)a.n_order) {
         const uint32_t vb = vfirst ? blockIdx.x : blockIdx.x - (uint32_t)a.n_order;
-        for (int64_t k = (int64_t)vb * S + wv; k < a.n_order; k += (int64_t)nb * S) validate_key<false, E16>(a, k);
+        for (int64_t k = (int64_t)vb * W + wv; k < a.n_order; k += (int64_t)nb * W) validate_key<false, E16>(a, k);
         return;  // the whole block: no barrier below is reached by half of it
     }
     const int32_t key = a.order[blk];
-    uint32_t *ws = a.lat_ws + ((size_t)blk * S + wv) * (3 * T0_RMEM * 64);
+    uint32_t *ws = a.lat_ws + ((size_t)blk * W + wv) * (3 * T0_RMEM * 64);
     const uint64_t eb = a.ev_off[key];
     const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
     const EvSrc<E16> evp = ev_src<E16>(a) + eb;
@@ -2184,155 +2180,179 @@ __global__ __launch_bounds__(64 * S) void k_spec(T0Args a) {
     const uint32_t topmask = nstates >= 32 ? ~0u : (1u << nstates) - 1u;
 
     if (threadIdx.x < NWS) s_ws_busy[threadIdx.x] = 0;
+    if (threadIdx.x < 2) s_next[threadIdx.x] = 0;
     __syncthreads();
-    SPEC_STAMP(0, __builtin_amdgcn_s_memtime())
-    SPEC_STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
-                      ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32))
-    SPEC_STAMP(9, (unsigned long long)key)
+    if (wv == 0) {
+        for (uint32_t s = 0; s < (uint32_t)S; ++s) { SPEC_STAMP(s, 0, __builtin_amdgcn_s_memtime()) }
+    }
     // 0. the cuts.  Targets at s/eff of the key's events (T0_SPEC_COST: of its
     // estimated cost, each wave computing every target); each moved to the
     // boundary with the fewest ops pending within 64 events.  Equal event
-    // counts: wave w counts the pending-count change over its own part
-    // [t_w, t_w+1), the parts' prefix gives the count at each target, and
-    // wave w places cut w -- a quarter of the scan each, two barriers.
-    uint32_t cut = 0, end = nev, n0 = 0;
+    // counts: the waves count the pending-count change over the parts
+    // [t_p, t_p+1) (part p on wave p mod W), the parts' prefix gives the count
+    // at each target, and the waves place the cuts likewise -- two barriers.
     const bool cost = (a.flags & T0_SPEC_COST) != 0;
-    if (!plain && !cost && wv + 1 < eff) {
-        const uint32_t t0 = (uint32_t)((uint64_t)nev * wv / eff), t1 = (uint32_t)((uint64_t)nev * (wv + 1) / eff);
-        const int32_t d = spec_net(evp, t0, t1);
-        if (lane == 0) s_net[wv] = d;
+    if (!plain && !cost) {
+        for (uint32_t p = wv; p + 1 < eff; p += W) {
+            const uint32_t t0 = (uint32_t)((uint64_t)nev * p / eff), t1 = (uint32_t)((uint64_t)nev * (p + 1) / eff);
+            const int32_t d = spec_net(evp, t0, t1);
+            if (lane == 0) s_net[p] = d;
+        }
     }
     __syncthreads();
-    if (!plain && !cost && wv >= 1 && wv < eff) {
-        int32_t pend = 0;
-        for (uint32_t q = 0; q < wv; ++q) pend += uni(s_net[q]);
-        const uint32_t t = (uint32_t)((uint64_t)nev * wv / eff);
-        const uint32_t w = t + lane < nev ? evp[t + lane] : 0u;
-        uint32_t n2 = 0;
-        const uint32_t c2 = spec_cut_at(w, nev, t, pend, n2);
-        if (lane == 0) {
-            s_cand[wv] = c2 == SPEC_NONE ? -1 : (int32_t)c2;
-            s_ncand[wv] = (int32_t)n2;
+    if (!plain && !cost) {
+        for (uint32_t s = wv; s < eff; s += W) {
+            if (s == 0) continue;
+            int32_t pend = 0;
+            for (uint32_t q = 0; q < s; ++q) pend += uni(s_net[q]);
+            const uint32_t t = (uint32_t)((uint64_t)nev * s / eff);
+            const uint32_t w = t + lane < nev ? evp[t + lane] : 0u;
+            uint32_t n2 = 0;
+            const uint32_t c2 = spec_cut_at(w, nev, t, pend, n2);
+            if (lane == 0) {
+                s_cand[s] = c2 == SPEC_NONE ? -1 : (int32_t)c2;
+                s_ncand[s] = (int32_t)n2;
+            }
         }
     }
     if (!plain && cost && wv < eff) {
         uint32_t pos_v;
         int32_t pend_v;
         spec_targets_cost(evp, nev, eff, pos_v, pend_v);
-        if (wv >= 1) {  // every wave has every target: each places its own cut
-            const uint32_t t = uni(__builtin_amdgcn_readlane(pos_v, wv));
+        for (uint32_t s = wv; s < eff; s += W) {  // every wave has every target: each places its own cuts
+            if (s == 0) continue;
+            const uint32_t t = uni(__builtin_amdgcn_readlane(pos_v, s));
             const uint32_t w = t + lane < nev ? evp[t + lane] : 0u;
             uint32_t n2 = 0;
-            const uint32_t c2 = spec_cut_at(w, nev, t, uni(__builtin_amdgcn_readlane(pend_v, wv)), n2);
+            const uint32_t c2 = spec_cut_at(w, nev, t, uni(__builtin_amdgcn_readlane(pend_v, s)), n2);
             if (lane == 0) {
-                s_cand[wv] = c2 == SPEC_NONE ? -1 : (int32_t)c2;
-                s_ncand[wv] = (int32_t)n2;
+                s_cand[s] = c2 == SPEC_NONE ? -1 : (int32_t)c2;
+                s_ncand[s] = (int32_t)n2;
             }
         }
     }
     __syncthreads();
-    // 1. every segment from TOP (segment 0 exactly)
-    if (!plain && wv < eff) {
-        // a cut is kept if it lies past the last kept one (every wave reads
-        // the same candidates, so all agree); a segment ends at the next kept cut
-        uint32_t last = 0;
-        cut = 0;
-        end = nev;
-        n0 = 0;
-        for (uint32_t s2 = 1; s2 < eff; ++s2) {
-            const int32_t cc = uni(s_cand[s2]);
-            uint32_t c2 = cc < 0 ? SPEC_NONE : (uint32_t)cc;
-            if (c2 != SPEC_NONE && c2 <= last) c2 = SPEC_NONE;
-            if (c2 != SPEC_NONE) last = c2;
-            if (s2 == wv) {
-                cut = c2;
-                n0 = (uint32_t)uni(s_ncand[s2]);
-            }
-            if (s2 > wv && c2 != SPEC_NONE && end == nev) end = c2;
+    // the kept cuts (each past the last kept one; a segment ends at the next
+    // kept cut), by one thread
+    if (threadIdx.x == 0 && !plain) {
+        int32_t last = 0;
+        s_cut[0] = 0;
+        for (uint32_t s = 1; s < eff; ++s) {
+            int32_t c2 = s_cand[s];
+            if (c2 >= 0 && c2 <= last) c2 = -1;
+            if (c2 >= 0) last = c2;
+            s_cut[s] = c2;
         }
-        if (lane == 0) {
-            s_cut[wv] = cut == SPEC_NONE ? -1 : (int32_t)cut;
-            s_segend[wv] = (int32_t)end;
-            s_ck_e[wv][0] = s_ck_e[wv][1] = -1;
-            s_top[wv] = -1;
+        int32_t end = (int32_t)nev;
+        for (uint32_t s = eff; s-- > 0;) {
+            s_segend[s] = end;
+            if (s_cut[s] >= 0) end = s_cut[s];
+            s_ck_e[s][0] = s_ck_e[s][1] = -1;
+            s_top[s] = -1;
         }
-        SPEC_STAMP(1, __builtin_amdgcn_s_memtime())
-        SPEC_STAMP(6, ((unsigned long long)end << 32) | cut)
-        if (cut != SPEC_NONE) {
+    }
+    __syncthreads();
+    // 1. every segment from TOP (segment 0 exactly), from the block's queue.
+    // (A fixed trip count, no break: with `for (;;) ... break` the compiler
+    // built an exec-masked loop whose exit hung the wave after its first walk.)
+    if (!plain) {
+#pragma unroll 1
+        for (uint32_t k = 0; k < (uint32_t)S; ++k) {
+            uint32_t s = 0;
+            if (lane == 0) s = (uint32_t)atomicAdd(&s_next[0], 1);
+            s = uni(s);
+            if (s >= eff || uni(s_cut[s]) < 0) continue;
+            const int32_t cut_i = uni(s_cut[s]);
+            const uint32_t cut = (uint32_t)cut_i, end = (uint32_t)uni(s_segend[s]);
+            const uint32_t n0 = s == 0 ? 0u : (uint32_t)uni(s_ncand[s]);
+            SPEC_STAMP(s, 1, __builtin_amdgcn_s_memtime())
+            SPEC_STAMP(s, 6, ((unsigned long long)end << 32) | cut)
+            SPEC_STAMP(s, 8, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                 ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32))
+            SPEC_STAMP(s, 9, (unsigned long long)key)
             SpecState st{};
             uint32_t words = 0, np = 0;
-            if (wv == 0) {
+            if (s == 0) {
                 st.W0 = lane == 0 ? 1u << a.init_state : 0u;
             } else {
                 words = spec_pending(evp, cut, n0, np);
                 spec_setup(st, words, np, trp, ntr);
                 st.W0 = lane < (1u << np) ? topmask : 0u;
             }
-            if (lane < 6) s_pend[wv][lane] = words;
-            if (lane == 6) s_pend[wv][6] = np;
+            if (lane < 6) s_pend[s][lane] = words;
+            if (lane == 6) s_pend[s][6] = np;
             uint32_t fev = 0;
             // the ops found pending must be as many as the count says (else
             // the event stream is malformed): the key is searched unsegmented
-            const bool lost = wv != 0 && np != n0;
-            const int r = lost ? 6 : spec_walk<0, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[wv],
-                                                        s_ck_e[wv], a.spec_ck1, a.spec_ck2, fev,
+            const bool lost = s != 0 && np != n0;
+            const int r = lost ? 6 : spec_walk<0, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[s],
+                                                        s_ck_e[s], a.spec_ck1, a.spec_ck2, fev,
                                                         !(a.flags & T0_SPEC_NOPRIO));
-            s_end[wv][lane] = st.W0;
+            s_end[s][lane] = st.W0;
             uint64_t map = 0;
             for (uint32_t q = 0; q < 6; ++q) {
                 const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, q);
                 if ((st.live >> q) & 1u) map |= (uint64_t)(0x80u | sl) << (8 * q);
             }
-            SPEC_STAMP(2, __builtin_amdgcn_s_memtime())
+            SPEC_STAMP(s, 2, __builtin_amdgcn_s_memtime())
             if (lane == 0) {
-                s_map[wv] = map;
-                s_top[wv] = r == 1 ? (int32_t)fev : r == 3 ? -2 : r == 6 ? -3 : -1;
+                s_map[s] = map;
+                s_top[s] = r == 1 ? (int32_t)fev : r == 3 ? -2 : r == 6 ? -3 : -1;
             }
         }
     }
     __syncthreads();
-    SPEC_STAMP(3, __builtin_amdgcn_s_memtime())
     // 2. every segment s >= 1 again, from the set segment s - 1 ended with,
-    // until the runs meet
-    if (!plain && wv >= 1 && wv < eff && uni(s_cut[wv]) >= 0 && uni(s_top[wv]) != -3) {
-        uint32_t pw = wv - 1;
-        while (uni(s_cut[pw]) < 0) --pw;  // s_cut[0] = 0
-        int32_t ver = 0, vfev = -1;
-        if (uni(s_top[pw]) == -1) {
-            const uint32_t cut = (uint32_t)uni(s_cut[wv]), end = (uint32_t)uni(s_segend[wv]);
-            const uint32_t np = uni(s_pend[wv][6]);
-            SpecState st{};
-            spec_setup(st, lane < 6 ? s_pend[wv][lane] : 0u, np, trp, ntr);
-            // the predecessor's end set, relabelled from its op indices to these
-            const uint64_t map = uni(s_map[pw]);
-            uint32_t src = 0;
-            for (uint32_t j = 0; j < np; ++j) {
-                const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, j);
-                uint32_t at = 31;
-                for (uint32_t q = 0; q < 6; ++q)
-                    if (((map >> (8 * q)) & 0xFFu) == (0x80u | sl)) at = q;
-                src |= ((lane >> j) & 1u) << at;
+    // until the runs meet (from the block's second queue)
+    if (!plain) {
+#pragma unroll 1
+        for (uint32_t k = 1; k < (uint32_t)S; ++k) {
+            uint32_t s = 0;
+            if (lane == 0) s = (uint32_t)atomicAdd(&s_next[1], 1) + 1u;
+            s = uni(s);
+            if (s >= eff || uni(s_cut[s]) < 0 || uni(s_top[s]) == -3) continue;
+            SPEC_STAMP(s, 3, __builtin_amdgcn_s_memtime())
+            uint32_t pw = s - 1;
+            while (uni(s_cut[pw]) < 0) --pw;  // s_cut[0] = 0
+            int32_t ver = 0, vfev = -1;
+            if (uni(s_top[pw]) == -1) {
+                const uint32_t cut = (uint32_t)uni(s_cut[s]), end = (uint32_t)uni(s_segend[s]);
+                const uint32_t np = uni(s_pend[s][6]);
+                SpecState st{};
+                spec_setup(st, lane < 6 ? s_pend[s][lane] : 0u, np, trp, ntr);
+                // the predecessor's end set, relabelled from its op indices to these
+                const uint64_t map = uni(s_map[pw]);
+                uint32_t src = 0;
+                for (uint32_t j = 0; j < np; ++j) {
+                    const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, j);
+                    uint32_t at = 31;
+                    for (uint32_t q = 0; q < 6; ++q)
+                        if (((map >> (8 * q)) & 0xFFu) == (0x80u | sl)) at = q;
+                    src |= ((lane >> j) & 1u) << at;
+                }
+                const uint32_t E = (uint32_t)__shfl((int)s_end[pw][lane], (int)(src & 63u));
+                st.W0 = lane < (1u << np) ? E : 0u;
+                uint32_t fev = 0;
+                const int r = spec_walk<1, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[s], s_ck_e[s],
+                                                0, 0, fev);
+                bool last = true;
+                for (uint32_t q = s + 1; q < eff; ++q) last = last && uni(s_cut[q]) < 0;
+                if (r == 4) ver = 1;                        // met the TOP run
+                else if (r == 1) { ver = 2; vfev = (int32_t)fev; }  // died before meeting it
+                else if (r == 3) ver = 6;                   // does not fit
+                else if (r == 5) ver = 3;                   // never met
+                else if (last) ver = 5;                     // the last segment, searched exactly to its end
+                else ver = (st.n <= 6 && !__any(st.W0 != s_end[s][lane])) ? 1 : 3;
+                SPEC_STAMP(s, 7, ((unsigned long long)ver << 32) | (fev - cut))
             }
-            const uint32_t E = (uint32_t)__shfl((int)s_end[pw][lane], (int)(src & 63u));
-            st.W0 = lane < (1u << np) ? E : 0u;
-            uint32_t fev = 0;
-            const int r = spec_walk<1, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[wv], s_ck_e[wv], 0, 0,
-                                       fev);
-            bool last = true;
-            for (uint32_t q = wv + 1; q < eff; ++q) last = last && uni(s_cut[q]) < 0;
-            if (r == 4) ver = 1;                        // met the TOP run
-            else if (r == 1) { ver = 2; vfev = (int32_t)fev; }  // died before meeting it
-            else if (r == 3) ver = 6;                   // does not fit
-            else if (r == 5) ver = 3;                   // never met
-            else if (last) ver = 5;                     // the last segment, searched exactly to its end
-            else ver = (st.n <= 6 && !__any(st.W0 != s_end[wv][lane])) ? 1 : 3;
-            SPEC_STAMP(7, ((unsigned long long)ver << 32) | (fev - cut))
+            SPEC_STAMP(s, 4, __builtin_amdgcn_s_memtime())
+            if (lane == 0) { s_ver[s] = ver; s_vfev[s] = vfev; }
         }
-        SPEC_STAMP(4, __builtin_amdgcn_s_memtime())
-        if (lane == 0) { s_ver[wv] = ver; s_vfev[wv] = vfev; }
     }
     __syncthreads();
-    SPEC_STAMP(5, __builtin_amdgcn_s_memtime())
+    if (wv == 0) {
+        for (uint32_t s = 0; s < (uint32_t)S; ++s) { SPEC_STAMP(s, 5, __builtin_amdgcn_s_memtime()) }
+    }
     // 3. the key's verdict: the first segment whose real run dies
     if (wv == 0) {
         const Args &f = *a.full;
@@ -2394,271 +2414,6 @@ __global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
     }
 }
 
-// ---- Queued speculative segments (k_specq_cuts, k_specq_walks, k_specq_join)
-//
-// The same search as k_spec, scheduled differently.  k_spec gives every key a
-// workgroup of S waves and ends when the slowest of its 4,000 walks ends: on
-// C2 the median TOP walk took 423k cycles, the slowest 578k, and a SIMD's
-// waves issue at 26 % of its VALU rate while they wait on their own chains.
-// A wave's chain is latency-bound, so a SIMD does more work with more waves
-// (the fit's +18 cycles per event per co-resident wave), and shorter walks
-// end the launch sooner.  Here:
-//   k_specq_cuts  -- one wave per key: the cuts (segs per key at equal event
-//                    counts, each moved to the fewest ops pending within 64
-//                    events), the pending ops at each, into the item headers;
-//   k_specq_walks -- independent waves, each taking one item (key x
-//                    segment, LPT key order) from a queue: every TOP walk
-//                    (segment 0 exactly), then the T0_STRICT validation of
-//                    the keys as the queue's last items, which fill the
-//                    walks' tail.  Small workgroups (SPECQ_WPB waves sharing
-//                    a 9-10-pending LDS workspace) free their slots as their
-//                    walks end, so the dispatcher keeps every SIMD full.  (A
-//                    persistent grid looping over the queue needs ~20 more
-//                    VGPRs: 4 waves per SIMD instead of 6.)
-//   k_specq_join  -- one workgroup of segs waves per key: the verifying runs
-//                    from each predecessor's end set (to the checkpoints the
-//                    TOP walk recorded) and the key's verdict, as k_spec.
-// Items live in HBM (840 B each); k_spec_rerun follows for keys whose runs
-// never met.
-#ifndef LC_SPECQ_WPB
-#define LC_SPECQ_WPB 2
-#endif
-constexpr int SPECQ_WPB = LC_SPECQ_WPB;  // independent waves per k_specq_walks workgroup
-constexpr int SPECQ_NWS = SPECQ_WPB >= 4 ? SPECQ_WPB / 2 : 1;  // their shared LDS workspaces
-
-__device__ __forceinline__ bool spec_plain(const T0Args &a, int32_t key, uint32_t nev, uint32_t &nstates) {
-    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
-    (void)tb;
-    nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
-    const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;
-    return (a.key_error && a.key_error[key]) || nstates > T0_MAX_STATES || nstates == 0 || width > T0_MAX_WIDTH ||
-           a.init_state >= T0_MAX_STATES || nev < 2 * SPEC_MIN_LEN;
-}
-
-template <bool E16>
-__global__ __launch_bounds__(256) void k_specq_cuts(T0Args a) {
-    const uint32_t lane = lane_id();
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.q_ticket = 0;  // the walks' queue
-    const int64_t kp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (kp >= a.n_order) return;
-    const uint32_t S = (uint32_t)a.q_segs;
-    const int32_t key = a.order[kp];
-    const uint64_t eb = a.ev_off[key];
-    const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
-    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
-    uint32_t nstates;
-    const bool plain = spec_plain(a, key, nev, nstates);
-    const uint32_t eff = plain ? 0u : min(S, nev / SPEC_MIN_LEN);
-    int32_t *const hdr = a.q_hdr + (size_t)kp * S * 8;
-    // candidate cut s (lane s) and the ops pending there
-    uint32_t cand_v = SPEC_NONE, ncand_v = 0;
-    int32_t pend = 0;
-    uint32_t prev = 0;
-    for (uint32_t s = 1; s < eff; ++s) {
-        const uint32_t t = (uint32_t)((uint64_t)nev * s / eff);
-        pend += spec_net(evp, prev, t);
-        prev = t;
-        const uint32_t w = t + lane < nev ? evp[t + lane] : 0u;
-        uint32_t n2 = 0;
-        const uint32_t c2 = spec_cut_at(w, nev, t, pend, n2);
-        cand_v = lane == s ? c2 : cand_v;
-        ncand_v = lane == s ? n2 : ncand_v;
-    }
-    // kept cuts: each past the last kept one
-    uint32_t kept_v = SPEC_NONE, last = 0;
-    for (uint32_t s = 1; s < eff; ++s) {
-        uint32_t c2 = uni((uint32_t)__builtin_amdgcn_readlane(cand_v, s));
-        if (c2 != SPEC_NONE && c2 <= last) c2 = SPEC_NONE;
-        if (c2 != SPEC_NONE) last = c2;
-        kept_v = lane == s ? c2 : kept_v;
-    }
-    if (eff > 0) kept_v = lane == 0 ? 0u : kept_v;  // segment 0 from the key's start
-    // headers: cut (-1: no segment), end (the next kept cut), pending ops
-    uint32_t end_v = nev;
-    for (uint32_t s = eff; s-- > 1;) {
-        const uint32_t c2 = uni((uint32_t)__builtin_amdgcn_readlane(kept_v, s));
-        end_v = lane < s && c2 != SPEC_NONE ? c2 : end_v;
-    }
-    if (lane < S) {
-        const bool on = lane < eff && kept_v != SPEC_NONE;
-        int32_t *h = hdr + lane * 8;
-        h[0] = on ? (int32_t)kept_v : -1;
-        h[1] = (int32_t)end_v;
-        h[3] = lane == 0 ? 0 : (int32_t)ncand_v;
-        h[4] = -1;
-        h[5] = h[6] = -1;
-    }
-    for (uint32_t s = 0; s < eff; ++s) {
-        const uint32_t c2 = uni((uint32_t)__builtin_amdgcn_readlane(kept_v, s));
-        if (c2 == SPEC_NONE) continue;
-        uint32_t words = 0, np = 0;
-        if (s > 0) words = spec_pending(evp, c2, uni((uint32_t)__builtin_amdgcn_readlane(ncand_v, s)), np);
-        const size_t it = (size_t)kp * S + s;
-        if (lane < 8) a.q_words[it * 8 + lane] = lane < 6 ? words : 0u;
-        if (lane == 0) a.q_hdr[it * 8 + 2] = (int32_t)np;
-    }
-}
-
-// One item's TOP walk (segment 0 exactly from the initial state): its status
-// into the header, its end set and op-index map, its checkpoints.
-template <bool E16>
-__device__ __forceinline__ void specq_walk_item(const T0Args &a, int64_t it, uint32_t *ws, uint32_t *lds_ws,
-                                                int32_t *lds_busy) {
-    const uint32_t lane = lane_id();
-    const uint32_t S = (uint32_t)a.q_segs;
-    int32_t *const h = a.q_hdr + it * 8;
-    const int32_t cut_i = uni(h[0]);
-    if (cut_i < 0) return;
-    const uint32_t s = (uint32_t)(it % S);
-    const int32_t key = a.order[it / S];
-    const uint64_t eb = a.ev_off[key];
-    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
-    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
-    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
-    const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
-    const uint32_t nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
-    const uint32_t topmask = nstates >= 32 ? ~0u : (1u << nstates) - 1u;
-    const uint32_t cut = (uint32_t)cut_i, end = (uint32_t)uni(h[1]);
-    const uint32_t np = (uint32_t)uni(h[2]), n0 = (uint32_t)uni(h[3]);
-    SpecState st{};
-    if (s == 0) {
-        st.W0 = lane == 0 ? 1u << a.init_state : 0u;
-    } else {
-        spec_setup(st, lane < 6 ? a.q_words[it * 8 + lane] : 0u, np, trp, ntr);
-        st.W0 = lane < (1u << np) ? topmask : 0u;
-    }
-    // the ops found pending must be as many as the count says (else the
-    // event stream is malformed): the key is searched unsegmented
-    const bool lost = s != 0 && np != n0;
-    uint32_t fev = 0;
-    const int r = lost ? 6 : spec_walk<0, SPECQ_NWS>(evp, trp, ntr, cut, end, st, ws, lds_ws, lds_busy,
-                                             (uint32_t(*)[64])(a.q_ck + it * 128), h + 5, a.spec_ck1, a.spec_ck2, fev);
-    a.q_end[it * 64 + lane] = st.W0;
-    uint64_t map = 0;
-    for (uint32_t q = 0; q < 6; ++q) {
-        const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, q);
-        if ((st.live >> q) & 1u) map |= (uint64_t)(0x80u | sl) << (8 * q);
-    }
-    if (lane == 0) {
-        a.q_map[it] = map;
-        h[4] = r == 1 ? (int32_t)fev : r == 3 ? -2 : r == 6 ? -3 : -1;
-    }
-}
-
-template <bool E16>
-__global__ __launch_bounds__(64 * SPECQ_WPB) void k_specq_walks(T0Args a) {
-    __shared__ uint32_t s_ws[SPECQ_NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
-    __shared__ int32_t s_ws_busy[SPECQ_NWS];
-    if (threadIdx.x < SPECQ_NWS) s_ws_busy[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t lane = lane_id();
-    const int64_t n_items = (int64_t)a.n_order * a.q_segs;
-    const int64_t n_val = (a.flags & T0_STRICT) ? a.n_order : 0;
-    int32_t t = 0;
-    if (lane == 0) t = atomicAdd(a.q_ticket, 1);
-    t = uni(t);
-    if ((int64_t)t >= n_items + n_val) return;
-    if ((int64_t)t >= n_items) {
-        validate_key<false, E16>(a, (int64_t)t - n_items);
-    } else {
-        uint32_t *const ws = a.lat_ws + (size_t)t * (3 * T0_RMEM * 64);  // the item's global workspace
-        specq_walk_item<E16>(a, t, ws, s_ws, s_ws_busy);
-    }
-}
-
-template <int S, bool E16>
-__global__ __launch_bounds__(64 * S) void k_specq_join(T0Args a) {
-    __shared__ int32_t s_ver[S], s_vfev[S];
-    __shared__ uint32_t s_ws[3 * T0_RMEM * 64];
-    __shared__ int32_t s_ws_busy[1];
-    const uint32_t lane = lane_id(), wv = uni((uint32_t)threadIdx.x >> 6);
-    const int64_t kp = blockIdx.x;
-    const int32_t key = a.order[kp];
-    const uint64_t eb = a.ev_off[key];
-    const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
-    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
-    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
-    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
-    const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
-    uint32_t nstates;
-    const bool plain = spec_plain(a, key, nev, nstates);
-    const uint32_t eff = plain ? 0u : min((uint32_t)S, nev / SPEC_MIN_LEN);
-    const size_t it0 = (size_t)kp * S;
-    const int32_t *const hk = a.q_hdr + it0 * 8;  // the key's item headers
-    uint32_t *const ws = a.lat_ws + (it0 + wv) * (3 * T0_RMEM * 64);
-    if (threadIdx.x == 0) s_ws_busy[0] = 0;
-    __syncthreads();
-    if (wv >= 1 && wv < eff && uni(hk[wv * 8 + 0]) >= 0 && uni(hk[wv * 8 + 4]) != -3) {
-        uint32_t pw = wv - 1;
-        while (uni(hk[pw * 8 + 0]) < 0) --pw;  // segment 0 always exists
-        int32_t ver = 0, vfev = -1;
-        if (uni(hk[pw * 8 + 4]) == -1) {
-            const size_t it = it0 + wv;
-            const uint32_t cut = (uint32_t)uni(hk[wv * 8 + 0]), end = (uint32_t)uni(hk[wv * 8 + 1]);
-            const uint32_t np = (uint32_t)uni(hk[wv * 8 + 2]);
-            SpecState st{};
-            spec_setup(st, lane < 6 ? a.q_words[it * 8 + lane] : 0u, np, trp, ntr);
-            // the predecessor's end set, relabelled from its op indices to these
-            const uint64_t map = uni(a.q_map[it0 + pw]);
-            uint32_t src = 0;
-            for (uint32_t j = 0; j < np; ++j) {
-                const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, j);
-                uint32_t at = 31;
-                for (uint32_t q = 0; q < 6; ++q)
-                    if (((map >> (8 * q)) & 0xFFu) == (0x80u | sl)) at = q;
-                src |= ((lane >> j) & 1u) << at;
-            }
-            const uint32_t E = (uint32_t)__shfl((int)a.q_end[(it0 + pw) * 64 + lane], (int)(src & 63u));
-            st.W0 = lane < (1u << np) ? E : 0u;
-            uint32_t fev = 0;
-            const int r = spec_walk<1, 1>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
-                                          (uint32_t(*)[64])(a.q_ck + it * 128), a.q_hdr + it * 8 + 5, 0, 0, fev);
-            bool last = true;
-            for (uint32_t q = wv + 1; q < eff; ++q) last = last && uni(hk[q * 8 + 0]) < 0;
-            if (r == 4) ver = 1;                                // met the TOP run
-            else if (r == 1) { ver = 2; vfev = (int32_t)fev; }  // died before meeting it
-            else if (r == 3) ver = 6;                           // does not fit
-            else if (r == 5) ver = 3;                           // never met
-            else if (last) ver = 5;                             // the last segment, searched exactly to its end
-            else ver = (st.n <= 6 && !__any(st.W0 != a.q_end[it * 64 + lane])) ? 1 : 3;
-        }
-        if (lane == 0) { s_ver[wv] = ver; s_vfev[wv] = vfev; }
-    }
-    __syncthreads();
-    if (wv != 0) return;
-    // the key's verdict: the first segment whose real run dies
-    const Args &f = *a.full;
-    bool rerun = plain, bad = false;
-    int32_t fv = -1;
-    for (uint32_t s = 0; s < eff && fv < 0 && !rerun && !bad; ++s) {
-        if (uni(hk[s * 8 + 0]) < 0) continue;
-        const int32_t top = uni(hk[s * 8 + 4]);
-        if (top == -2) { bad = true; break; }
-        if (top == -3) { rerun = true; break; }
-        if (s == 0) { fv = top; continue; }
-        const int32_t ver = uni(s_ver[s]);
-        if (ver == 1) fv = top;
-        else if (ver == 2) fv = uni(s_vfev[s]);
-        else if (ver == 6) bad = true;
-        else if (ver != 5) rerun = true;  // never met (or nothing to start from): unsegmented
-    }
-    if (rerun) {
-        if (lane == 0) a.spec_rr[atomicAdd(a.spec_nrr, 1)] = key;
-    } else if (bad) {
-        if (a.flags & T0_STRICT) {
-            t0_malformed(a, key, LC_BATCH_E_FIT);
-            finish_key(f, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
-        } else {
-            const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
-            push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key, f.list_cap);
-        }
-    } else if (fv >= 0) {
-        finish_key(f, key, LC_INVALID, LC_CAUSE_NONLIN, fv, 0, 0, (uint64_t)fv + 1u);
-    } else {
-        finish_key(f, key, LC_VALID, LC_CAUSE_NONE, -1, 0, 0, nev);
-    }
-}
-
 size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * lat_ws_words(); }
 
 // Keys order[0 .. n_order) in workgroups of `segs` segments (2, 3, 4, 6 or
@@ -2666,7 +2421,7 @@ size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t
 // rerun counts used in turn -- `parity` picks this launch's, which must be
 // zero, and k_spec_rerun zeroes the other -- then the rerun list).
 // validate: add the T0_STRICT validation blocks.
-hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws, int32_t *rr, int parity,
+hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
                        bool cost_cuts, bool prio, bool vfirst, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
@@ -2682,65 +2437,23 @@ hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, uint32_t *ws,
     t.spec_rr = rr + 2;
     const dim3 grid((unsigned)std::max(1, a.n_order + std::max(0, validate_blocks)));
     const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid)));
-    if (events16) {
-        if (segs >= 8) hipLaunchKernelGGL((k_spec<8, true>), grid, dim3(512), 0, s, t);
-        else if (segs >= 6) hipLaunchKernelGGL((k_spec<6, true>), grid, dim3(384), 0, s, t);
-        else if (segs >= 4) hipLaunchKernelGGL((k_spec<4, true>), grid, dim3(256), 0, s, t);
-        else if (segs >= 3) hipLaunchKernelGGL((k_spec<3, true>), grid, dim3(192), 0, s, t);
-        else hipLaunchKernelGGL((k_spec<2, true>), grid, dim3(128), 0, s, t);
-    } else {
-        if (segs >= 8) hipLaunchKernelGGL((k_spec<8, false>), grid, dim3(512), 0, s, t);
-        else if (segs >= 6) hipLaunchKernelGGL((k_spec<6, false>), grid, dim3(384), 0, s, t);
-        else if (segs >= 4) hipLaunchKernelGGL((k_spec<4, false>), grid, dim3(256), 0, s, t);
-        else if (segs >= 3) hipLaunchKernelGGL((k_spec<3, false>), grid, dim3(192), 0, s, t);
-        else hipLaunchKernelGGL((k_spec<2, false>), grid, dim3(128), 0, s, t);
-    }
+    // one wave per segment: more segments than waves (8, 12 or 16 on 4
+    // waves, 4 or 8 on 2) measured slower (device_api.hip)
+    (void)waves;
+#define LC_SPEC_L(SS, WW, E) hipLaunchKernelGGL((k_spec<SS, WW, E>), grid, dim3(64 * WW), 0, s, t)
+#define LC_SPEC_ALL(E)                                                   \
+    if (segs >= 8) LC_SPEC_L(8, 8, E);                                  \
+    else if (segs >= 6) LC_SPEC_L(6, 6, E);                             \
+    else if (segs >= 4) LC_SPEC_L(4, 4, E);                             \
+    else if (segs >= 3) LC_SPEC_L(3, 3, E);                             \
+    else LC_SPEC_L(2, 2, E);
+    if (events16) { LC_SPEC_ALL(true) } else { LC_SPEC_ALL(false) }
+#undef LC_SPEC_ALL
+#undef LC_SPEC_L
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (events16) hipLaunchKernelGGL(k_spec_rerun<true>, rgrid, dim3(64), 0, s, t);
     else hipLaunchKernelGGL(k_spec_rerun<false>, rgrid, dim3(64), 0, s, t);
-    return hipGetLastError();
-}
-
-size_t specq_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * 210 + 2; }
-
-// Queued speculative segments: k_specq_cuts, k_specq_walks (one wave per
-// queue ticket: items, then validation), k_specq_join, k_spec_rerun.
-// q: specq_words(n_order, segs) words; ws: spec_ws_words(n_order, segs)
-// (12 KB per item); rr as for launch_spec.
-hipError_t launch_specq(const Args &a, const Args *a_dev, int segs, uint32_t *q, uint32_t *ws, int32_t *rr,
-                        int parity, uint32_t ck1, uint32_t ck2, int rerun_grid, const uint16_t *events16,
-                        hipStream_t s) {
-    T0Args t = make_t0(a, a_dev);
-    t.events16 = events16;
-    t.lat_ws = ws;
-    t.spec_ck1 = ck1;
-    t.spec_ck2 = ck2;
-    t.spec_nrr = rr + (parity & 1);
-    t.spec_nrr_next = rr + ((parity & 1) ^ 1);
-    t.spec_rr = rr + 2;
-    const size_t ni = (size_t)std::max<int64_t>(a.n_order, 1) * segs;
-    t.q_segs = segs;
-    t.q_hdr = (int32_t *)q;
-    t.q_words = q + ni * 8;
-    t.q_map = (uint64_t *)(q + ni * 16);
-    t.q_end = q + ni * 18;
-    t.q_ck = q + ni * 82;
-    t.q_ticket = (int32_t *)(q + ni * 210);
-    const int K = std::max(1, a.n_order);
-    const dim3 cgrid((unsigned)((K + 3) / 4)), jgrid((unsigned)K);
-    const int64_t tickets = (int64_t)K * segs + (a.strict ? K : 0);
-    const dim3 wgrid((unsigned)((tickets + SPECQ_WPB - 1) / SPECQ_WPB));
-    const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid)));
-#define LC_SPECQ(E)                                                                                   \
-    hipLaunchKernelGGL(k_specq_cuts<E>, cgrid, dim3(256), 0, s, t);                                   \
-    hipLaunchKernelGGL(k_specq_walks<E>, wgrid, dim3(64 * SPECQ_WPB), 0, s, t);                       \
-    if (segs >= 8) hipLaunchKernelGGL((k_specq_join<8, E>), jgrid, dim3(512), 0, s, t);               \
-    else if (segs >= 4) hipLaunchKernelGGL((k_specq_join<4, E>), jgrid, dim3(256), 0, s, t);          \
-    else hipLaunchKernelGGL((k_specq_join<2, E>), jgrid, dim3(128), 0, s, t);                         \
-    hipLaunchKernelGGL(k_spec_rerun<E>, rgrid, dim3(64), 0, s, t);
-    if (events16) { LC_SPECQ(true) } else { LC_SPECQ(false) }
-#undef LC_SPECQ
     return hipGetLastError();
 }
 

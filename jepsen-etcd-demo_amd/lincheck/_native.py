@@ -24,9 +24,9 @@ LC_OPT_COUNT_PROBES = 0x1
 # lc_opts.path_flags (ABI 9): pinned search-path choices for A/B runs and tests
 LC_PATH_SPLIT_ON, LC_PATH_SPLIT_OFF, LC_PATH_SPEC_OFF, LC_PATH_LAYERS_OFF = 0x01, 0x02, 0x04, 0x08
 LC_PATH_NODE_SYNC, LC_PATH_NODE_STAGED, LC_PATH_CHUNKS_ON, LC_PATH_CHUNKS_OFF = 0x10, 0x20, 0x40, 0x80
-LC_PATH_SPEC_COST, LC_PATH_EV32, LC_PATH_SPEC_NOPRIO, LC_PATH_SPEC_QUEUE = 0x100, 0x200, 0x400, 0x800
-LC_T0_PATH_NONE, LC_T0_PATH_LATTICE, LC_T0_PATH_SPEC, LC_T0_PATH_SEGMENTS, LC_T0_PATH_SPECQ = 0, 1, 2, 3, 4
-T0_PATH_NAMES = {0: "none", 1: "k_search_lattice", 2: "k_spec", 3: "k_search_segments", 4: "k_specq_walks"}
+LC_PATH_SPEC_COST, LC_PATH_EV32, LC_PATH_SPEC_NOPRIO = 0x100, 0x200, 0x400
+LC_T0_PATH_NONE, LC_T0_PATH_LATTICE, LC_T0_PATH_SPEC, LC_T0_PATH_SEGMENTS = 0, 1, 2, 3
+T0_PATH_NAMES = {0: "none", 1: "k_search_lattice", 2: "k_spec", 3: "k_search_segments"}
 LC_DEV_RESULT, LC_DEV_ASYNC = 1, 2
 LC_INVOKE, LC_OK_T, LC_FAIL, LC_INFO = 0, 1, 2, 3
 LC_F_READ, LC_F_WRITE, LC_F_CAS, LC_F_OTHER, LC_F_ACQUIRE, LC_F_RELEASE, LC_F_TXN = 0, 1, 2, 3, 4, 5, 6
