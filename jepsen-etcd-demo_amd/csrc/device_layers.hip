@@ -52,7 +52,10 @@ namespace {
 
 extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
 
-constexpr int LWG = 1024;               // threads per key
+#ifndef LC_T3L_LWG
+#define LC_T3L_LWG 1024
+#endif
+constexpr int LWG = LC_T3L_LWG;         // threads per key (A/B: make variant VFLAGS=-DLC_T3L_LWG=n)
 constexpr uint32_t TS = 16384;          // LDS table slots (128 KB): two halves, or one table
 constexpr uint32_t TSH = TS / 2;        // a half (the fused step's I and S' tables)
 constexpr uint32_t CLAIM_MAX = 12288;   // entries per full-table pass (75 % load)
