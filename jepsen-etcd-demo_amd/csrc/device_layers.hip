@@ -618,9 +618,17 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
                 }
             }
             o.xp = sh.sxf[p];
+            // the config set's lowest and highest non-empty layers: one
+            // ballot over the layer offsets (every wave; NLAY <= 64)
             uint32_t smin = NLAY, smax = 0;
-            for (uint32_t k = 0; k < NLAY; ++k)
-                if (o.so[k + 1] > o.so[k]) { smin = smin < k ? smin : k; smax = k; }
+            {
+                const uint32_t l = lane_id();
+                const uint64_t ne = __ballot(l < NLAY && o.so[l + 1] > o.so[l]);
+                if (ne) {
+                    smin = (uint32_t)__builtin_ctzll(ne);
+                    smax = 63u - (uint32_t)__builtin_clzll(ne);
+                }
+            }
             if (tid == 0 && a.count_probes) probes += nScfg;  // |S| (oracle: probes += S.n)
             uint64_t nIcfg = 0, nSncfg = 0;
             bool over = false;
@@ -725,8 +733,7 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
                 __syncthreads();
                 return K_DONE;
             }
-            if (tid == 0)
-                for (int j = k < 0 ? 0 : k; j <= (int)NLAY; ++j) sn[j] = sh.n_sn;
+            if ((int)tid >= (k < 0 ? 0 : k) && tid <= NLAY) sn[tid] = sh.n_sn;
             __syncthreads();
             if (nSncfg == 0) {
                 write_final_layers(a, key, o.S, o.so[NLAY]);

@@ -23,6 +23,8 @@ K = pk.n_keys
 ref = None
 for setting in sys.argv[4:]:
     kw = {} if setting == "default" else {k: int(v, 0) for k, v in (kv.split("=") for kv in setting.split(","))}
+    if "spec_ck" in kw:  # (ck1 + 1) | (ck2 + 1) << 16, as lc_opts.spec_ck
+        kw["spec_ck"] = ((kw["spec_ck"] & 0xFFFF) - 1, (kw["spec_ck"] >> 16) - 1)
     dev = Device(0, **kw)
     db = dev.upload(pk)
     for _ in range(10):
