@@ -370,7 +370,42 @@ __device__ __forceinline__ void step_inserts(LayShared &sh, const OkCtx &o, uint
     const uint64_t s0 = pre.s0, s1 = pre.s1;
     const bool h0 = sb + tid < se, h1 = sb + LWG + tid < se;
     uint32_t claims = 0;
-    if (ta && o.nc) {
+// LC_T3L_PAIR2 (default): each thread keeps one candidate and walks entries;
+// 0: pairs by index, the entry from a corrected float quotient (C4 at 2^16:
+// 15.1 ms against 14.2 with the candidate per thread)
+#ifndef LC_T3L_PAIR2
+#define LC_T3L_PAIR2 1
+#endif
+    if (LC_T3L_PAIR2 && ta && o.nc) {
+        // thread t takes candidate t mod nc of entries t / nc, t / nc + LWG /
+        // nc, ...: the candidate's slot and transfer are loaded once, and no
+        // pair index is divided
+        const uint32_t nc = o.nc, cidx = tid % nc, stride = LWG / nc;
+        const uint32_t j0 = tid / nc;
+        const bool lane_on = j0 < stride;  // the last tid % nc lanes of the block idle
+        const uint32_t q = lane_on ? sh.cq[cidx] : 0u, xq = lane_on ? sh.cx[cidx] : 0u;
+        for (uint32_t jb = 0; jb < nk; jb += stride * UP) {
+            uint64_t L2[UP];
+            uint32_t M2[UP], h[UP];
+            bool act[UP];
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const uint32_t j = jb + (uint32_t)u * stride + j0;
+                act[u] = false;
+                L2[u] = 0;
+                M2[u] = 0;
+                h[u] = 0;
+                if (lane_on && j < nk) {
+                    const uint64_t en = Ik[j];
+                    M2[u] = ((en >> q) & 1ull) ? 0u : xfer8((uint32_t)(en >> 56), xq);
+                    L2[u] = (en & LMASK) | 1ull << q;
+                    h[u] = hash64(L2[u]);
+                    act[u] = M2[u] != 0 && pt.mine(h[u]);
+                }
+            }
+            claims += tab_merge_n<UP>(ta, tsma, L2, M2, h, act, &c->ovf);
+        }
+    } else if (ta && o.nc) {
         // pair i = (entry i / nc, candidate i % nc); the quotient from a float
         // reciprocal, corrected
         const uint32_t npairs = nk * o.nc;
