@@ -186,6 +186,53 @@ def test_t0_validates_events():
         np.testing.assert_array_equal(again["fail_event"][:K], good["fail_event"][:K])
 
 
+def test_spec_validates_large_batch():
+    """The speculative segments' own validation (T0_STRICT blocks in the
+    search launch) on a batch of more keys than one resident round of
+    workgroups, where those blocks go first in the grid: every per-event
+    malformation is refused naming its key, and between refusals the same
+    context gives the oracle's records for the good batch."""
+    h = H.synth(n_keys=3000, ops_per_key=300, concurrency=6, anomaly_rate=0.05, seed=81)
+    pk = Packed(h)
+    K = pk.n_keys
+    dev = Device(0)
+    arrs, b = _batch_copy(pk)
+    ev = arrs["events"]
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+
+    def node():
+        out = np.zeros(K, np.uint64)
+        st = N.LcStats()
+        N.check(N.lib().lc_check_node(dev.handle, C.byref(b), K, N.ptr(out, C.c_uint64), C.byref(st)))
+        return out, st
+
+    rec, st = node()
+    assert N.T0_PATH_NAMES.get(int(st.t0_path)) == "k_spec"
+    v, c, fe = _decode(rec, K)
+    np.testing.assert_array_equal(v, orc["valid"])
+    np.testing.assert_array_equal(fe, orc["fail_event"])
+
+    def at(key, pred):
+        lo, hi = int(pk.ev_off[key]), int(pk.ev_off[key + 1])
+        return lo + int(np.flatnonzero(pred(ev[lo:hi]))[0])
+
+    cases = [
+        (211, at(211, lambda e: np.ones(len(e), bool)), lambda w: w | N.LC_EV_OK_BIT),
+        (1057, at(1057, lambda e: (e & N.LC_EV_OK_BIT) != 0), lambda w: (w & 0x7F000000)),
+        (2123, at(2123, lambda e: (e & N.LC_EV_OK_BIT) == 0), lambda w: (w & 0xFF000000) | 0xFFFFF),
+        (2890, at(2890, lambda e: (e & N.LC_EV_OK_BIT) == 0), lambda w: (w & 0x80FFFFFF) | (70 << 24)),
+    ]
+    for key, j, mutate in cases:
+        saved = int(ev[j])
+        ev[j] = mutate(saved)
+        with pytest.raises(N.LincheckError) as ei:
+            node()
+        assert ei.value.code == -1 and f"key {key}" in str(ei.value), str(ei.value)
+        ev[j] = saved
+        again, _ = node()
+        np.testing.assert_array_equal(again, rec)
+
+
 def test_t0_refuses_understated_width():
     """key_width claims fewer ops pending at once than a key has: the batch is
     declared register-tier-only, T0 meets the 11th pending op, and the key is
