@@ -52,6 +52,22 @@ struct Delims {
 };
 const Delims DELIM;
 
+// A token of up to 8 bytes as one little-endian word (longer: ~0), so that
+// keyword and symbol comparisons are integer compares, not library calls.
+inline uint64_t pack8(std::string_view t) {
+    if (t.size() > 8) return ~0ull;
+    uint64_t x = 0;
+    for (size_t i = 0; i < t.size(); ++i) x |= (uint64_t)(unsigned char)t[i] << (8 * i);
+    return x;
+}
+template <size_t N>
+constexpr uint64_t P8(const char (&s)[N]) {
+    static_assert(N - 1 <= 8, "P8: at most 8 bytes");
+    uint64_t x = 0;
+    for (size_t i = 0; i + 1 < N; ++i) x |= (uint64_t)(unsigned char)s[i] << (8 * i);
+    return x;
+}
+
 struct Parser {
     const char *p, *end, *base;
     std::string err;
@@ -104,11 +120,30 @@ struct Parser {
     }
     // Read one scalar token (number / nil / true / false / symbol).
     bool scalar(uint8_t &kind, int64_t &v) {
+        // the common case first: a decimal integer of at most 18 digits
+        // followed by a delimiter (no overflow possible)
+        {
+            const char *q = p;
+            const bool neg = q < end && *q == '-';
+            if (q < end && (*q == '-' || *q == '+')) ++q;
+            const char *d0 = q;
+            uint64_t acc = 0;
+            while (q < end && q - d0 < 18 && (unsigned)(*q - '0') < 10u) acc = acc * 10 + (uint64_t)(*q++ - '0');
+            if (q > d0 && (q == end || DELIM.d[(unsigned char)*q])) {
+                const int64_t val = neg ? -(int64_t)acc : (int64_t)acc;
+                if (val != LC_NIL) {
+                    p = q;
+                    kind = K_INT;
+                    v = val;
+                    return true;
+                }
+            }
+        }
         const char c = *p;
         std::string_view t = token();
         kind = K_OTHER;
         if (t.empty()) return fail(std::string("unexpected character '") + c + "'");
-        if (t == "nil") { kind = K_NIL; return true; }
+        if (pack8(t) == P8("nil")) { kind = K_NIL; return true; }
         const char f0 = t[0];
         const bool num = (f0 >= '0' && f0 <= '9') || ((f0 == '-' || f0 == '+') && t.size() > 1 && t[1] >= '0' && t[1] <= '9');
         if (!num) return true;  // true / false / symbol
@@ -234,11 +269,12 @@ bool txn_tuple(const Top &v) { return v.kind == K_VEC && v.n == 2 && v.e[0].kind
 // The op-map keys read, by length and spelling (one compare per key).
 enum Field { FLD_OTHER, FLD_TYPE, FLD_F, FLD_PROCESS, FLD_INDEX, FLD_VALUE };
 inline Field field_of(std::string_view k) {
-    switch (k.size()) {
-        case 1: return k[0] == 'f' ? FLD_F : FLD_OTHER;
-        case 4: return k == std::string_view("type", 4) ? FLD_TYPE : FLD_OTHER;
-        case 5: return k == std::string_view("value", 5) ? FLD_VALUE : k == std::string_view("index", 5) ? FLD_INDEX : FLD_OTHER;
-        case 7: return k == std::string_view("process", 7) ? FLD_PROCESS : FLD_OTHER;
+    switch (pack8(k)) {
+        case P8("f"): return FLD_F;
+        case P8("type"): return FLD_TYPE;
+        case P8("value"): return FLD_VALUE;
+        case P8("index"): return FLD_INDEX;
+        case P8("process"): return FLD_PROCESS;
         default: return FLD_OTHER;
     }
 }
@@ -263,23 +299,28 @@ bool read_op(Parser &ps, RawOp &op) {
             if (!ps.keyword(v, vk)) return false;
             if (fld == FLD_TYPE) {
                 if (!vk) return ps.fail(":type is not a keyword");
-                if (v == "invoke") op.type = LC_INVOKE;
-                else if (v == "ok") op.type = LC_OK_T;
-                else if (v == "fail") op.type = LC_FAIL;
-                else if (v == "info") op.type = LC_INFO;
-                else return ps.fail("unknown :type :" + std::string(v));
+                switch (pack8(v)) {
+                    case P8("invoke"): op.type = LC_INVOKE; break;
+                    case P8("ok"): op.type = LC_OK_T; break;
+                    case P8("fail"): op.type = LC_FAIL; break;
+                    case P8("info"): op.type = LC_INFO; break;
+                    default: return ps.fail("unknown :type :" + std::string(v));
+                }
             } else {
                 op.f = LC_F_OTHER;
                 op.nem = -1;
                 if (vk) {
-                    if (v == "read") op.f = LC_F_READ;
-                    else if (v == "write") op.f = LC_F_WRITE;
-                    else if (v == "cas") op.f = LC_F_CAS;
-                    else if (v == "acquire") op.f = LC_F_ACQUIRE;  // (model/mutex)
-                    else if (v == "release") op.f = LC_F_RELEASE;
-                    else if (v == "txn") op.f = LC_F_TXN;           // (model/multi-register)
-                    else if (v == "start") op.nem = 1;              // nemesis
-                    else if (v == "stop") op.nem = 0;
+                    switch (pack8(v)) {
+                        case P8("read"): op.f = LC_F_READ; break;
+                        case P8("write"): op.f = LC_F_WRITE; break;
+                        case P8("cas"): op.f = LC_F_CAS; break;
+                        case P8("acquire"): op.f = LC_F_ACQUIRE; break;  // (model/mutex)
+                        case P8("release"): op.f = LC_F_RELEASE; break;
+                        case P8("txn"): op.f = LC_F_TXN; break;          // (model/multi-register)
+                        case P8("start"): op.nem = 1; break;             // nemesis
+                        case P8("stop"): op.nem = 0; break;
+                        default: break;
+                    }
                 }
             }
         } else if (fld == FLD_PROCESS || fld == FLD_INDEX) {
