@@ -333,6 +333,8 @@ struct Dev {
     // speculative segments: each wave's 9-10-pending workspace, the rerun list
     uint32_t *spec_ws = nullptr;
     size_t spec_ws_words = 0;
+    uint32_t *spec_fin = nullptr;  // exact speculative segments: each run's saved set
+    size_t spec_fin_words = 0;
     int32_t *spec_rr = nullptr;    // two rerun counts (used in turn), then the rerun list
     int64_t spec_rr_cap = 0;
     int spec_parity = 0;
@@ -371,7 +373,7 @@ struct Dev {
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(lws.base); dfree(dargs); dfree(send); dfree(node);
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
-        dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr);
+        dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr); dfree(spec_fin);
         if (hargs) (void)hipHostFree(hargs);
         if (hnode) (void)hipHostFree(hnode);
         for (hipEvent_t &e : args_ev)
@@ -1086,8 +1088,15 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     int segs = K > 0 ? (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1)) : 0;
     segs = segs >= 8 ? 8 : segs >= 4 ? 4 : K > 0 ? 2 : 0;
     if (o.spec_segs) segs = o.spec_segs;
+    // Final configs wanted and no set sizes (the Jepsen-shaped checkers):
+    // the segments with exact sets (Knossos's S, not its closure), each run
+    // saving its set at its end or death, the true run's written as the
+    // key's final configs (k_spec<.., EX>).
+    const bool exact_spec = !a.peak && a.final_cfg && a.n_final && o.max_configs >= 16ull * 64 * 32;
+    if (exact_spec && !fast) segs = segs >= 8 ? 8 : segs >= 4 ? 4 : 2;  // the exact builds
     const int waves = segs;
-    const bool spec = !split && t0_step && fast && segs >= 2 && !(o.path_flags & LC_PATH_SPEC_OFF);
+    const bool spec =
+        !split && t0_step && (fast || exact_spec) && segs >= 2 && !(o.path_flags & LC_PATH_SPEC_OFF);
     if (spec) {
         const size_t need = lcd::spec_ws_words(K, waves);
         if (need > c->spec_ws_words) {
@@ -1097,6 +1106,15 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             c->spec_ws_words = 0;
             HIPCHK(dalloc(&c->spec_ws, need));
             c->spec_ws_words = need;
+        }
+        const size_t fneed = exact_spec && !fast ? lcd::spec_fin_words(K, segs) : 0;
+        if (fneed > c->spec_fin_words) {
+            if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
+            dfree(c->spec_fin);
+            c->spec_fin = nullptr;
+            c->spec_fin_words = 0;
+            HIPCHK(dalloc(&c->spec_fin, fneed));
+            c->spec_fin_words = fneed;
         }
         if (K + 2 > c->spec_rr_cap) {
             if (c->n_async) HIPCHK(hipStreamSynchronize(c->stream));
@@ -1208,7 +1226,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
                                 c->cu_count * 8, vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
                                 !(o.path_flags & LC_PATH_SPEC_NOPRIO),
                                 K * waves > (int64_t)c->cu_count * 16,  // more keys than one resident round
-                                c->stream));
+                                exact_spec && !fast ? c->spec_fin : nullptr, c->stream));
         c->spec_parity ^= 1;
         if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0 && !d->table) {

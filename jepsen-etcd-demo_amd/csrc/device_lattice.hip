@@ -270,6 +270,7 @@ struct T0Args {
     int32_t *spec_rr;            // speculative segments: keys left to the unsegmented search,
     int32_t *spec_nrr;           //   their count (zero at the launch)
     int32_t *spec_nrr_next;      //   and the next launch's count (zeroed by k_spec_rerun)
+    uint32_t *spec_fin;          // exact segments: each run's saved set (2 per segment, SPEC_SAVE_WORDS each)
 };
 
 template <bool E16>
@@ -743,45 +744,71 @@ __device__ __forceinline__ int ok_event_mem_gs(const LatMem &m, uint32_t p, uint
     return 0;
 }
 
-// First max_final configs of the lattice held in m.W (register lattices are
-// stored there first), in (register, lane, state) order, with op indices
-// translated back to window slots (slot_v: lane j holds the slot of the op at
-// index j; `live` = the occupied indices).
+// The max_final smallest configs of the lattice held in m.W (register
+// lattices are stored there first) in (slot mask, state) order, op indices
+// translated back to window slots (slot_v: lane j holds the slot of the op
+// at index j; `live` = the occupied indices).  The order is the window's, not
+// the op indices', so every run that holds the same set -- the unsegmented
+// search, a speculative segment's that assigned its own indices -- writes
+// the same records (Knossos's truncation to 10 is of an unordered set; any
+// fixed choice matches it).  Selection: max_final rounds of a wave minimum.
 __device__ __forceinline__ void write_final_mem(const Args &a, int32_t key, const LatMem &m, uint32_t lane,
                                                 uint32_t slot_v, uint32_t live_ops) {
     if (!a.final_cfg) return;
     const uint32_t mf = (uint32_t)a.max_final;
     const uint32_t top = live_ops ? 32u - (uint32_t)__clz(live_ops) : 0u;  // index bits in use
     const int live = top <= 6 ? 1 : (1 << (top - 6));
-    uint32_t base = 0;
-#pragma unroll 1
-    for (int k = 0; k < live; ++k) {
-        const uint32_t w = m.W[k * 64 + lane];
-        const uint32_t c = (uint32_t)__popc(w);
-        uint32_t x = c;  // inclusive prefix over lanes
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        const uint32_t tot = __shfl(x, 63);
-        uint32_t r = base + x - c;
-        uint64_t smask = 0;
-        const uint32_t L = lane + 64u * (uint32_t)k;
-        for (uint32_t j = 0; j < top; ++j) {
-            const uint32_t sj = __builtin_amdgcn_readlane(slot_v, j);
-            if (((L & live_ops) >> j) & 1u) smask |= 1ull << sj;
-        }
-        uint32_t mm = w;
-        while (mm && r < mf) {
-            const uint32_t st = (uint32_t)__ffs(mm) - 1;
-            mm &= mm - 1;
-            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 0] = smask;
-            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 1] = (uint64_t)st << 48;
-            ++r;
-        }
-        base += tot;
+    // slot mask of subset L = lane + 64 k: the lane's bits (indices 0..5)
+    // and the row's (6..), the latter uniform
+    uint64_t lo = 0;
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; j < top && j < 6u; ++j) {
+        const uint32_t sj = __builtin_amdgcn_readlane(slot_v, j);
+        if (((lane & live_ops) >> j) & 1u) lo |= 1ull << sj;
     }
-    if (lane == 0 && a.n_final) a.n_final[key] = base < mf ? base : mf;
+#pragma unroll 1
+    for (int k = 0; k < live; ++k) cnt += (uint32_t)__popc(m.W[k * 64 + lane]);
+    const uint32_t tot = __ockl_wfred_add_u32(cnt);
+    const uint32_t nw = tot < mf ? tot : mf;
+    uint64_t last_m = 0;
+    int last_s = -1;
+#pragma unroll 1
+    for (uint32_t r = 0; r < nw; ++r) {
+        const uint32_t above = last_s < 0 ? ~0u : last_s >= 31 ? 0u : ~((2u << last_s) - 1u);
+        uint64_t bm = ~0ull;
+        uint32_t bs = 32;
+#pragma unroll 1
+        for (int k = 0; k < live; ++k) {
+            uint32_t w = m.W[k * 64 + lane];
+            uint64_t hi = 0;
+            for (uint32_t j = 6; j < top; ++j)
+                if ((((uint32_t)k << 6) & live_ops) >> j & 1u) hi |= 1ull << __builtin_amdgcn_readlane(slot_v, j);
+            const uint64_t sm = lo | hi;
+            if (sm == last_m) w &= above;
+            if (w && sm >= last_m && sm < bm) {
+                bm = sm;
+                bs = (uint32_t)__ffs(w) - 1;
+            }
+        }
+        uint64_t mn = bm;
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t l2 = (uint32_t)__shfl_xor((int)(uint32_t)mn, o), h2 = (uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), o);
+            const uint64_t v = ((uint64_t)h2 << 32) | l2;
+            mn = v < mn ? v : mn;
+        }
+        uint32_t st = bm == mn ? bs : 32u;
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t v = (uint32_t)__shfl_xor((int)st, o);
+            st = v < st ? v : st;
+        }
+        if (lane == 0) {
+            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 0] = mn;
+            a.final_cfg[((size_t)key * a.max_final + r) * 2 + 1] = (uint64_t)st << 48;
+        }
+        last_m = mn;
+        last_s = (int)st;
+    }
+    if (lane == 0 && a.n_final) a.n_final[key] = nw;
 }
 
 // Op indices: an invoke takes the lowest free index.  While at most 6 ops are
@@ -1917,11 +1944,20 @@ __device__ __forceinline__ void spec_prio(uint32_t quarter) {
     else __builtin_amdgcn_s_setprio(0);
 }
 
-template <int MODE, int NWS, class EvT>
+// Words of a run's saved set (EX): T0_RMEM lattice rows, the slot of each op
+// index (one row), the live op indices.
+constexpr uint32_t SPEC_SAVE_WORDS = (T0_RMEM + 2) * 64;
+
+// EX: Knossos's exact sets (ok_lane) instead of closed ones in the lane
+// phase, for steps that report final configs; `save` (EX, may be null)
+// receives the run's set at its end or before its failing :ok, in the
+// LatMem row layout write_final_mem reads, with its slots and live indices.
+template <int MODE, int NWS, class EvT, bool EX = false>
 __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
                                          uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
                                          int32_t *lds_busy, uint32_t (*ck_w)[64], int32_t *ck_e, uint32_t ck1,
-                                         uint32_t ck2, uint32_t &fev_out, bool prio = false) {
+                                         uint32_t ck2, uint32_t &fev_out, bool prio = false,
+                                         uint32_t *save = nullptr) {
     constexpr int RM = T0_RSMALL;
     const uint32_t lane = lane_id();
     LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
@@ -2003,11 +2039,28 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                 // sweeps specialised to the highest live index (one body for
                 // every live set measured 4 % slower per event here)
                 const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
-                if (top >= 6) r = ok_lane_closed<6>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
-                else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
-                else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
-                dirty = false;
-                k_v = setl(k_v, p, 0u);
+                if constexpr (EX) {
+                    // exact sets: p's transfer, then its lane cleared (as in lattice_key)
+                    const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
+                                   pb = __builtin_amdgcn_readlane(b_v, p);
+                    k_v = setl(k_v, p, 0u);
+                    uint32_t probes = 0, nSn = 0;
+                    if (top >= 6)
+                        r = ok_lane<6>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
+                                       false);
+                    else if (top == 5)
+                        r = ok_lane<5>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
+                                       false);
+                    else
+                        r = ok_lane<4>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
+                                       false);
+                } else {
+                    if (top >= 6) r = ok_lane_closed<6>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                    else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                    else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                    dirty = false;
+                    k_v = setl(k_v, p, 0u);
+                }
                 live = r ? live : live & ~(1u << p);
                 n = r ? n : n - 1;
                 status = r;
@@ -2105,6 +2158,29 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
         W0 = W[0];
         dirty = true;
     }
+    if constexpr (EX) {
+        if (save) {
+            // the set standing at the end (or before the failing :ok): the
+            // dense lattice (registers or the workspace) from 7 ops pending on
+            if (n > 6) {
+#pragma unroll 1
+                for (int k = 0; k < T0_RMEM; ++k) {
+                    uint32_t x = 0;
+                    if (in_mem) x = m.W[k * 64 + lane];
+                    else {
+#pragma unroll
+                        for (int q = 0; q < RM; ++q)
+                            if (q == k) x = W[q];
+                    }
+                    save[k * 64 + lane] = x;
+                }
+            } else {
+                save[lane] = W0;
+            }
+            save[T0_RMEM * 64 + lane] = slot_v;
+            if (lane == 0) save[(T0_RMEM + 1) * 64] = live;
+        }
+    }
     if (held >= 0 && lane == 0) atomicExch(&lds_busy[held], 0);
     if (MODE == 0 && prio) __builtin_amdgcn_s_setprio(0);
     st.W0 = W0;
@@ -2134,7 +2210,7 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 // verifying run and a walk's start-up).  Results go through a.full like
 // T0's; a.lat_ws holds each wave's 9-10-pending fallback workspace (global
 // memory: the workgroup's LDS workspaces are shared, NWS of them).
-template <int S, int W, bool E16>
+template <int S, int W, bool E16, bool EX = false>
 __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
     __shared__ uint32_t s_ck[S][2][64];   // TOP run's checkpoint sets
@@ -2285,9 +2361,11 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
             // the ops found pending must be as many as the count says (else
             // the event stream is malformed): the key is searched unsegmented
             const bool lost = s != 0 && np != n0;
-            const int r = lost ? 6 : spec_walk<0, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[s],
-                                                        s_ck_e[s], a.spec_ck1, a.spec_ck2, fev,
-                                                        !(a.flags & T0_SPEC_NOPRIO));
+            uint32_t *const sv = EX ? a.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS : nullptr;
+            const int r = lost ? 6
+                               : spec_walk<0, NWS, EvSrc<E16>, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
+                                                                   s_ck[s], s_ck_e[s], a.spec_ck1, a.spec_ck2, fev,
+                                                                   !(a.flags & T0_SPEC_NOPRIO), sv);
             s_end[s][lane] = st.W0;
             uint64_t map = 0;
             for (uint32_t q = 0; q < 6; ++q) {
@@ -2333,8 +2411,10 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
                 const uint32_t E = (uint32_t)__shfl((int)s_end[pw][lane], (int)(src & 63u));
                 st.W0 = lane < (1u << np) ? E : 0u;
                 uint32_t fev = 0;
-                const int r = spec_walk<1, NWS>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy, s_ck[s], s_ck_e[s],
-                                                0, 0, fev);
+                uint32_t *const sv =
+                    EX ? a.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS + SPEC_SAVE_WORDS : nullptr;
+                const int r = spec_walk<1, NWS, EvSrc<E16>, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
+                                                                s_ck[s], s_ck_e[s], 0, 0, fev, false, sv);
                 bool last = true;
                 for (uint32_t q = s + 1; q < eff; ++q) last = last && uni(s_cut[q]) < 0;
                 if (r == 4) ver = 1;                        // met the TOP run
@@ -2358,18 +2438,24 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
         const Args &f = *a.full;
         bool rerun = plain, bad = false;
         int32_t fv = -1;
+        // EX: the run whose set is the key's final one -- 2 x segment, + 1 for
+        // the verifying run: the run that truly died, or the last segment's
+        // true run
+        uint32_t fin_run = 0;
         if (!plain) {
             for (uint32_t s = 0; s < eff && fv < 0 && !rerun && !bad; ++s) {
                 if (uni(s_cut[s]) < 0) continue;
                 const int32_t top = uni(s_top[s]);
                 if (top == -2) { bad = true; break; }
                 if (top == -3) { rerun = true; break; }
+                fin_run = 2 * s;
                 if (s == 0) { fv = top; continue; }
                 const int32_t ver = uni(s_ver[s]);
                 if (ver == 1) fv = top;
-                else if (ver == 2) fv = uni(s_vfev[s]);
+                else if (ver == 2) { fv = uni(s_vfev[s]); fin_run = 2 * s + 1; }
+                else if (ver == 5) fin_run = 2 * s + 1;
                 else if (ver == 6) bad = true;
-                else if (ver != 5) rerun = true;  // never met (or nothing to start from): unsegmented
+                else rerun = true;  // never met (or nothing to start from): unsegmented
             }
         }
         int kr = K_DONE;
@@ -2380,6 +2466,13 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
         } else if (bad) kr = K_SPILL;
         else if (fv >= 0) finish_key(f, key, LC_INVALID, LC_CAUSE_NONLIN, fv, 0, 0, (uint64_t)fv + 1u);
         else finish_key(f, key, LC_VALID, LC_CAUSE_NONE, -1, 0, 0, nev);
+        if constexpr (EX) {
+            if (!rerun && !bad) {
+                uint32_t *const sv = a.spec_fin + ((size_t)blk * S * 2 + fin_run) * SPEC_SAVE_WORDS;
+                const LatMem fm{sv, sv, sv};
+                write_final_mem(f, key, fm, lane, sv[T0_RMEM * 64 + lane], uni(sv[(T0_RMEM + 1) * 64]));
+            }
+        }
         if (kr == K_SPILL) {
             if (a.flags & T0_STRICT) {
                 t0_malformed(a, key, LC_BATCH_E_FIT);
@@ -2393,14 +2486,14 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
 }
 
 // The keys k_spec left to the unsegmented search (compact T0, FAST).
-template <bool E16>
+template <bool E16, bool EX = false>
 __global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
     __shared__ uint32_t ws[3 * T0_RMEM * 64];
     const int32_t n = *a.spec_nrr;
     if (blockIdx.x == 0 && lane_id() == 0) *a.spec_nrr_next = 0;  // two counters in turn: no memset per step
     for (int32_t w = blockIdx.x; w < n; w += gridDim.x) {
         const int32_t key = a.spec_rr[w];
-        const int kr = lattice_key<T0_RSMALL, true, E16>(a, key, ws);
+        const int kr = lattice_key<T0_RSMALL, !EX, E16>(a, key, ws);
         if (kr == K_SPILL) {
             const Args &f = *a.full;
             if (a.flags & T0_STRICT) {
@@ -2421,9 +2514,14 @@ size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t
 // rerun counts used in turn -- `parity` picks this launch's, which must be
 // zero, and k_spec_rerun zeroes the other -- then the rerun list).
 // validate: add the T0_STRICT validation blocks.
+// fin: exact segments (final configs wanted, no peaks): spec_fin_words(n_order,
+// segs) words for the runs' saved sets, segs 2, 4 or 8; null: closed sets.
+size_t spec_fin_words(int64_t n_keys, int segs) {
+    return (size_t)std::max<int64_t>(n_keys, 1) * segs * 2 * SPEC_SAVE_WORDS;
+}
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
-                       bool cost_cuts, bool prio, bool vfirst, hipStream_t s) {
+                       bool cost_cuts, bool prio, bool vfirst, uint32_t *fin, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
     t.events16 = events16;
     if (cost_cuts) t.flags |= T0_SPEC_COST;
@@ -2435,25 +2533,35 @@ hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, ui
     t.spec_nrr = rr + (parity & 1);
     t.spec_nrr_next = rr + ((parity & 1) ^ 1);
     t.spec_rr = rr + 2;
+    t.spec_fin = fin;
     const dim3 grid((unsigned)std::max(1, a.n_order + std::max(0, validate_blocks)));
     const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid)));
     // one wave per segment: more segments than waves (8, 12 or 16 on 4
     // waves, 4 or 8 on 2) measured slower (device_api.hip)
     (void)waves;
-#define LC_SPEC_L(SS, WW, E) hipLaunchKernelGGL((k_spec<SS, WW, E>), grid, dim3(64 * WW), 0, s, t)
+#define LC_SPEC_L(SS, WW, E, X) hipLaunchKernelGGL((k_spec<SS, WW, E, X>), grid, dim3(64 * WW), 0, s, t)
 #define LC_SPEC_ALL(E)                                                   \
-    if (segs >= 8) LC_SPEC_L(8, 8, E);                                  \
-    else if (segs >= 6) LC_SPEC_L(6, 6, E);                             \
-    else if (segs >= 4) LC_SPEC_L(4, 4, E);                             \
-    else if (segs >= 3) LC_SPEC_L(3, 3, E);                             \
-    else LC_SPEC_L(2, 2, E);
+    if (fin) {                                                           \
+        if (segs >= 8) LC_SPEC_L(8, 8, E, true);                         \
+        else if (segs >= 4) LC_SPEC_L(4, 4, E, true);                    \
+        else LC_SPEC_L(2, 2, E, true);                                   \
+    } else if (segs >= 8) LC_SPEC_L(8, 8, E, false);                    \
+    else if (segs >= 6) LC_SPEC_L(6, 6, E, false);                       \
+    else if (segs >= 4) LC_SPEC_L(4, 4, E, false);                       \
+    else if (segs >= 3) LC_SPEC_L(3, 3, E, false);                       \
+    else LC_SPEC_L(2, 2, E, false);
     if (events16) { LC_SPEC_ALL(true) } else { LC_SPEC_ALL(false) }
 #undef LC_SPEC_ALL
 #undef LC_SPEC_L
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (events16) hipLaunchKernelGGL(k_spec_rerun<true>, rgrid, dim3(64), 0, s, t);
-    else hipLaunchKernelGGL(k_spec_rerun<false>, rgrid, dim3(64), 0, s, t);
+    if (events16) {
+        if (fin) hipLaunchKernelGGL((k_spec_rerun<true, true>), rgrid, dim3(64), 0, s, t);
+        else hipLaunchKernelGGL((k_spec_rerun<true, false>), rgrid, dim3(64), 0, s, t);
+    } else {
+        if (fin) hipLaunchKernelGGL((k_spec_rerun<false, true>), rgrid, dim3(64), 0, s, t);
+        else hipLaunchKernelGGL((k_spec_rerun<false, false>), rgrid, dim3(64), 0, s, t);
+    }
     return hipGetLastError();
 }
 

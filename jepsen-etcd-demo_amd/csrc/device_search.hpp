@@ -132,9 +132,10 @@ size_t spec_ws_words(int64_t n_keys, int segs);
 // 32-bit words); cost_cuts: cuts at equal estimated cost instead of equal
 // event counts;
 // prio: TOP walks' issue priority by progress (s_setprio).
+size_t spec_fin_words(int64_t n_keys, int segs);
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
-                       bool cost_cuts, bool prio, bool vfirst, hipStream_t s);
+                       bool cost_cuts, bool prio, bool vfirst, uint32_t *fin, hipStream_t s);
 uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);

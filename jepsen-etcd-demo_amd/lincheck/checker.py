@@ -217,14 +217,19 @@ class Device:
                                keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events,
                                t0_path=N.T0_PATH_NAMES.get(st.t0_path, st.t0_path), ev_word_bytes=st.ev_word_bytes))
 
-    def check(self, packed: Packed, verdicts_only: bool = False) -> KeyResults:
+    def check(self, packed: Packed, verdicts_only: bool = False, peaks: bool = True) -> KeyResults:
         """lc_check_batch: H2D, search, D2H.  verdicts_only: no peak sizes and
         no final configs are requested (the library's fast path; `peak`,
-        `final` and `n_final` come back zero)."""
+        `final` and `n_final` come back zero).  peaks=False: final configs
+        but no peak sizes (what a Knossos-shaped result needs: the library
+        then runs the segmented search with exact sets; `peak` comes back
+        zero)."""
         K = packed.n_keys
         arrs, r = self._alloc(K)
         if verdicts_only:
             r = N.LcResult(r.valid, r.fail_event, r.cause, None, None, None)
+        elif not peaks:
+            r = N.LcResult(r.valid, r.fail_event, r.cause, None, r.final_configs, r.n_final)
         st = N.LcStats()
         N.check(N.lib().lc_check_batch(self.handle, C.byref(packed.view), C.byref(r), C.byref(st)))
         return self._results(arrs, K, st)
@@ -469,7 +474,7 @@ class Linearizable:
         packed = Packed(hist, self.model)
         if packed.n_keys == 0:
             return {"valid?": True, "configs": [], "final-paths": [], "analyzer": self.analyzer}
-        res = self._dev().check(packed)
+        res = self._dev().check(packed, peaks=False)
         return _render_key(packed, 0, res, None, self.analyzer)
 
     # batched form, used by independent.checker
@@ -477,7 +482,7 @@ class Linearizable:
         from .independent import merge_results, subhistory
         hist = history if isinstance(history, History) else History.from_ops(history)
         packed = Packed(hist, self.model)
-        res = self._dev().check(packed) if packed.n_keys else None
+        res = self._dev().check(packed, peaks=False) if packed.n_keys else None
         results = {}
         ops_cache = None
         for i, k in enumerate(packed.keys):

@@ -77,3 +77,38 @@ def test_spec_resident_async():
     _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
     np.testing.assert_array_equal((rec & 0xFF) - 1, orc["valid"])
     np.testing.assert_array_equal((rec >> 16) - 1, orc["fail_event"])
+
+
+def _finals(r, k):
+    n = min(int(r.n_final[k]), r.final.shape[1])
+    return sorted(map(tuple, r.final[k, :n].tolist()))
+
+
+@pytest.mark.parametrize("shape", ["c5", "crashed", "two_values", "think20", "short_keys"])
+def test_exact_spec_final_configs(shape):
+    """Final configs without peak sizes (the Knossos-shaped checkers) run the
+    segments with exact sets (k_spec<.., EX>): verdicts, causes, failing
+    events, final-config counts and the final config records equal the
+    unsegmented exact search's, whatever the segment count and checkpoints
+    (records are the smallest in (slot mask, state) order, so a run's own
+    op-index assignment does not change which ones are kept)."""
+    h = H.synth(**SHAPES[shape])
+    pk = Packed(h)
+    _, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)
+    for mf in (10, 16):
+        ref = Device(0, path_flags=N.LC_PATH_SPLIT_OFF | N.LC_PATH_SPEC_OFF, max_final=mf).check(pk, peaks=False)
+        np.testing.assert_array_equal(ref.valid, orc["valid"])
+        np.testing.assert_array_equal(ref.fail_event, orc["fail_event"])
+        runs = [("default", dict())]
+        runs += [(f"segs {s} ck {ck}", dict(path_flags=N.LC_PATH_SPLIT_OFF, spec_segs=s, spec_ck=ck))
+                 for s in (2, 4, 8) for ck in ((32, 120), (1, 2))] if mf == 10 else []
+        for what, kw in runs:
+            r = Device(0, max_final=mf, **kw).check(pk, peaks=False)
+            assert r.stats["t0_path"] == "k_spec", what
+            for f in ("valid", "cause", "fail_event", "n_final"):
+                np.testing.assert_array_equal(getattr(r, f), getattr(ref, f), err_msg=f"{what}, max_final {mf}: {f}")
+            # the records written, in order (the rest of each row is not written)
+            bad = [k for k in range(pk.n_keys) if r.final[k, :r.n_final[k]].tolist() != ref.final[k, :ref.n_final[k]].tolist()]
+            assert not bad, f"{what}, max_final {mf}: final configs differ on keys {bad[:8]}"
+    if SHAPES[shape].get("anomaly_rate"):
+        assert (ref.valid == 0).any()
