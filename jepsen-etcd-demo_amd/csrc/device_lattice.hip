@@ -2486,12 +2486,17 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
 }
 
 // The keys k_spec left to the unsegmented search (compact T0, FAST).
+constexpr int SPEC_RERUN_WAVES = 4;
 template <bool E16, bool EX = false>
-__global__ __launch_bounds__(64) void k_spec_rerun(T0Args a) {
-    __shared__ uint32_t ws[3 * T0_RMEM * 64];
+__global__ __launch_bounds__(64 * SPEC_RERUN_WAVES) void k_spec_rerun(T0Args a) {
+    // a few workgroups of several waves: the launch is in every step and
+    // usually finds no key, so its dispatch is what it costs
+    __shared__ uint32_t ws_all[SPEC_RERUN_WAVES][3 * T0_RMEM * 64];
+    uint32_t *const ws = ws_all[threadIdx.x >> 6];
     const int32_t n = *a.spec_nrr;
-    if (blockIdx.x == 0 && lane_id() == 0) *a.spec_nrr_next = 0;  // two counters in turn: no memset per step
-    for (int32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.spec_nrr_next = 0;  // two counters in turn: no memset per step
+    for (int32_t w = blockIdx.x * SPEC_RERUN_WAVES + (int32_t)(threadIdx.x >> 6); w < n;
+         w += gridDim.x * SPEC_RERUN_WAVES) {
         const int32_t key = a.spec_rr[w];
         const int kr = lattice_key<T0_RSMALL, !EX, E16>(a, key, ws);
         if (kr == K_SPILL) {
@@ -2535,7 +2540,7 @@ hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, ui
     t.spec_rr = rr + 2;
     t.spec_fin = fin;
     const dim3 grid((unsigned)std::max(1, a.n_order + std::max(0, validate_blocks)));
-    const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid)));
+    const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid) / SPEC_RERUN_WAVES));
     // one wave per segment: more segments than waves (8, 12 or 16 on 4
     // waves, 4 or 8 on 2) measured slower (device_api.hip)
     (void)waves;
@@ -2556,11 +2561,11 @@ hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, ui
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (events16) {
-        if (fin) hipLaunchKernelGGL((k_spec_rerun<true, true>), rgrid, dim3(64), 0, s, t);
-        else hipLaunchKernelGGL((k_spec_rerun<true, false>), rgrid, dim3(64), 0, s, t);
+        if (fin) hipLaunchKernelGGL((k_spec_rerun<true, true>), rgrid, dim3(64 * SPEC_RERUN_WAVES), 0, s, t);
+        else hipLaunchKernelGGL((k_spec_rerun<true, false>), rgrid, dim3(64 * SPEC_RERUN_WAVES), 0, s, t);
     } else {
-        if (fin) hipLaunchKernelGGL((k_spec_rerun<false, true>), rgrid, dim3(64), 0, s, t);
-        else hipLaunchKernelGGL((k_spec_rerun<false, false>), rgrid, dim3(64), 0, s, t);
+        if (fin) hipLaunchKernelGGL((k_spec_rerun<false, true>), rgrid, dim3(64 * SPEC_RERUN_WAVES), 0, s, t);
+        else hipLaunchKernelGGL((k_spec_rerun<false, false>), rgrid, dim3(64 * SPEC_RERUN_WAVES), 0, s, t);
     }
     return hipGetLastError();
 }
