@@ -23,9 +23,12 @@
   NOT EXERCISED IN THIS REPOSITORY: the build container has no JVM, no
   Clojure and no Leiningen.  The same ABI and the same report decoding are
   exercised from Python (jepsen-etcd-demo_amd/lincheck/, tests/)."
-  (:require [jepsen [checker :as checker]
-                    [independent :as independent]]
+  (:require [clojure.tools.logging :refer [warn]]
+            [jepsen [checker :as checker]
+                    [independent :as independent]
+                    [store :as store]]
             [jepsen.checker.timeline :as timeline]
+            [knossos.linear.report :as linear.report]
             [knossos.model :as model])
   (:import (com.sun.jna Memory Pointer)
            (jepsen.etcdemo LincheckNative)))
@@ -303,6 +306,21 @@
         (LincheckNative/lc_packed_free packed)
         (identity [held init-mem])))))
 
+(defn- render!
+  "jepsen.checker/linearizable's counterexample drawing, SURVEY.md 8(f) F-2:
+  for a key whose analysis is not valid (`when-not`, so :unknown is not drawn,
+  as there), Knossos's own knossos.linear.report/render-analysis! draws the
+  decoded analysis -- :op, :previous-ok and :final-paths, the last already
+  truncated to 10 -- into linear.svg under the key's store directory.  An
+  error while drawing is logged, never raised, as linearizable does."
+  [jepsen-test sub lin subdirectory]
+  (when-not (:valid? lin)
+    (try
+      (linear.report/render-analysis!
+        sub lin (.getCanonicalPath (store/path! jepsen-test subdirectory "linear.svg")))
+      (catch Throwable e
+        (warn e "Error rendering linearizability analysis")))))
+
 (defn checker
   "independent/checker over compose{:linear linearizable(cas-register),
   :timeline html}, with the :linear part batched on the GPU.  opts:
@@ -320,10 +338,12 @@
              results (into {}
                            (for [[k lin] linear]
                              (let [sub (independent/subhistory k history)
+                                   dir ["independent" k]
                                    t   (checker/check-safe tl test sub
                                                            (assoc check-opts
-                                                                  :subdirectory ["independent" k]
+                                                                  :subdirectory dir
                                                                   :history-key k))]
+                               (render! test sub lin dir)
                                [k {:valid?   (checker/merge-valid [(:valid? lin) (:valid? t)])
                                    :linear   lin
                                    :timeline t}])))]

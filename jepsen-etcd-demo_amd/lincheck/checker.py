@@ -18,8 +18,10 @@ Jepsen's check-safe would.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 import traceback
+import warnings
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence
 
@@ -445,6 +447,21 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
 
 
 # ---------------------------------------------------------------- checkers
+def _draw(test: Optional[Dict], sub: Sequence[dict], lin: Dict, subdirectory: Sequence) -> None:
+    """jepsen.checker/linearizable's drawing of an analysis that is not valid
+    (`when-not (:valid? a)`: :unknown is not drawn): linear.svg under the
+    key's directory of the test's store, here `test["store-path"]` (the
+    Python mirror has no store layout of its own; without it nothing is
+    drawn).  An error while drawing is a warning, never raised, as there."""
+    if lin.get("valid?") is not False or not (test or {}).get("store-path"):
+        return
+    try:
+        from .report import render_analysis
+        render_analysis(sub, lin, os.path.join(test["store-path"], *[str(d) for d in subdirectory], "linear.svg"))
+    except Exception as e:  # noqa: BLE001 -- linearizable logs and goes on
+        warnings.warn(f"Error rendering linearizability analysis: {e!r}")
+
+
 class Linearizable:
     """jepsen.checker/linearizable (etcdemo.clj:117-118) on the device."""
 
@@ -475,7 +492,10 @@ class Linearizable:
         if packed.n_keys == 0:
             return {"valid?": True, "configs": [], "final-paths": [], "analyzer": self.analyzer}
         res = self._dev().check(packed, peaks=False)
-        return _render_key(packed, 0, res, None, self.analyzer)
+        out = _render_key(packed, 0, res, None, self.analyzer)
+        _draw(test, history if not isinstance(history, History) else history.to_ops(), out,
+              (opts or {}).get("subdirectory") or [])
+        return out
 
     # batched form, used by independent.checker
     def check_independent(self, test, history, opts, inner) -> Dict:
@@ -487,6 +507,10 @@ class Linearizable:
         ops_cache = None
         for i, k in enumerate(packed.keys):
             lin = _render_key(packed, i, res, None, self.analyzer)
+            if lin.get("valid?") is False and (test or {}).get("store-path"):
+                if ops_cache is None:
+                    ops_cache = history if not isinstance(history, History) else history.to_ops()
+                _draw(test, subhistory(ops_cache, k), lin, ["independent", str(k)])
             if inner is self:
                 results[k] = lin
                 continue

@@ -45,12 +45,19 @@ def _kats():
 
 
 @pytest.mark.parametrize("case", _kats(), ids=lambda c: c["name"])
-def test_known_answers_on_device(case):
-    """etcdemo.clj:115-119 on the device against the hand-derived answers."""
+def test_known_answers_on_device(case, tmp_path):
+    """etcdemo.clj:115-119 on the device against the hand-derived answers;
+    with a store path, linear.svg is drawn for exactly the invalid keys
+    (jepsen.checker/linearizable's render-analysis!, lincheck/report.py)."""
+    import xml.etree.ElementTree as ET
     mdl = MODELS[case.get("model", "cas-register")]()
     lin = ck.linearizable({"model": mdl, "algorithm": "linear"})
     chk = independent.checker(ck.compose({"linear": lin, "timeline": ck.unbridled_optimism()}))
-    out = chk.check({}, case["history"], {})
+    out = chk.check({"store-path": str(tmp_path)}, case["history"], {})
+    drawn = sorted(int(d) for d in os.listdir(tmp_path / "independent")) if (tmp_path / "independent").exists() else []
+    assert drawn == sorted(out["failures"])
+    for k in drawn:
+        ET.parse(tmp_path / "independent" / str(k) / "linear.svg")
     exp = {int(k): v for k, v in case["expect"].items()}
     assert set(out["results"]) == set(exp)
     bad = sorted(k for k, e in exp.items() if e["valid?"] is False)
