@@ -346,6 +346,14 @@ struct Part {
 #ifndef LC_T3L_UP
 #define LC_T3L_UP 2
 #endif
+// the fused step's table sizes: I_{k+1}'s at least TSA/2 x its estimate, S'_k's
+// at least (1 + 1/TSB) x its bound (A/B: make variant VFLAGS=-DLC_T3L_TSA=n)
+#ifndef LC_T3L_TSA
+#define LC_T3L_TSA 4u
+#endif
+#ifndef LC_T3L_TSB
+#define LC_T3L_TSB 3u
+#endif
 constexpr int UP = LC_T3L_UP;  // successor pairs per thread in flight (A/B: make variant VFLAGS=-DLC_T3L_UP=n)
 // The first two entries per thread of an S layer [sb, se), loaded ahead.
 struct SPre {
@@ -699,8 +707,8 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
                 uint64_t *inext = nullptr;
                 if (fast) {
                     StepCtr *c = &sh.ct[par];
-                    const uint32_t tsa = min(TSH, max(128u, pow2_at_least(2u * est_i)));
-                    const uint32_t tsb = min(TSH, max(64u, pow2_at_least(bound_s + bound_s / 3u + 1u)));
+                    const uint32_t tsa = min(TSH, max(128u, pow2_at_least(LC_T3L_TSA * est_i / 2u)));
+                    const uint32_t tsb = min(TSH, max(64u, pow2_at_least(bound_s + bound_s / LC_T3L_TSB + 1u)));
                     uint64_t *ta = sh.tab, *tbl = sh.tab + TSH;
                     if (Ik == sh.icmp)  // typed LDS reads of the layer (no flat loads)
                         step_inserts(sh, o, sb, se, sh.icmp, nk, want_i ? ta : nullptr, tsa - 1,
