@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 9
+#define LC_ABI_VERSION 10
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -300,10 +300,19 @@ int64_t lc_report_wgl(const lc_packed *p, int64_t i, int32_t valid, int32_t fail
 #define LC_ALGO_LINEAR      0  /* :algorithm :linear (etcdemo.clj:118)              */
 #define LC_ALGO_WGL         1  /* :algorithm :wgl              */
 #define LC_ALGO_COMPETITION 2  /* jepsen.checker/linearizable's default             */
-/* The three run the same device search: :valid? and the first :ok that cannot
- * be linearized are properties of the history, not of the algorithm.  Only
- * the host-side result shaping differs (:analyzer; :configs of :wgl through
- * lc_report_wgl). */
+/* LC_ALGO_LINEAR: knossos.linear's config-set search (the tiers T0-T3).
+ * LC_ALGO_WGL (ABI 10): knossos.wgl's own search on the device -- the Wing &
+ * Gong depth-first walk with Lowe's cache of (linearized set, state) pairs,
+ * one wavefront per key; max_configs bounds the cache (more pairs: :unknown,
+ * cause budget), so a key the :linear budget gives up on may still be decided
+ * (and the other way round).  final_configs of an invalid key are the WGL
+ * frontier at the return entry the walk is stuck on (the first max_final the
+ * walk reaches), shaped by lc_report_wgl.  Restated in oracle/wgl_ref.py and
+ * oracle/wgl_ref.c; parity with Knossos unpinned.
+ * LC_ALGO_COMPETITION (knossos.competition races the two and takes the first
+ * answer): the :linear search, then WGL for the keys :linear left :unknown at
+ * its budget; lc_result.analyzer names the analysis each key's answer came
+ * from. */
 
 #define LC_MAX_DEVICES   8    /* devices one context drives (one node)        */
 #define LC_COMM_ID_BYTES 128  /* an RCCL unique id (ncclUniqueId)             */
@@ -363,7 +372,10 @@ typedef struct lc_opts {
                                       are given (lc_batch.events16)                 */
 #define LC_PATH_SPEC_NOPRIO  0x400 /* speculative walks: issue priority by wave age
                                       alone, not by progress                        */
-#define LC_PATH_ALL          0x7FF
+#define LC_PATH_WGL_SMALL    0x800 /* WGL: Lowe's caches start in 2^14-entry tables
+                                      (keys outgrowing them are searched again with a
+                                      table the budget fits)                        */
+#define LC_PATH_ALL          0xFFF
 
 /* lc_opts.flags */
 #define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,
@@ -389,11 +401,14 @@ typedef struct lc_result {
     int32_t  *fail_event;    /* [n_keys] event ordinal (within the key's stream) of
                                 the :ok that could not be linearized, else -1       */
     uint8_t  *cause;         /* [n_keys] LC_CAUSE_*                                  */
-    uint32_t *peak_configs;  /* [n_keys] max config-set size seen (may be NULL)      */
+    uint32_t *peak_configs;  /* [n_keys] max config-set size seen (may be NULL); a
+                                key WGL answered: its cache size at the end       */
     uint64_t *final_configs; /* [n_keys * max_final * 2] (may be NULL): for invalid
                                 keys, up to max_final configs of the last non-empty
                                 set, as {state, slot mask lo} / {slot mask hi}      */
     uint32_t *n_final;       /* [n_keys] configs written to final_configs (may be NULL) */
+    uint8_t  *analyzer;      /* [n_keys] LC_ALGO_LINEAR / LC_ALGO_WGL: the analysis
+                                whose answer the key carries (may be NULL; ABI 10) */
 } lc_result;
 
 typedef struct lc_stats {
@@ -415,6 +430,11 @@ typedef struct lc_stats {
                                  LC_T0_PATH_*                                   */
     uint32_t ev_word_bytes;   /* bytes per event word it read: 2 (lc_batch.events16
                                  read in place) or 4                            */
+    double   wgl_ms;          /* device time of the WGL launches (ABI 10)       */
+    uint64_t wgl_keys;        /* keys the WGL search answered                   */
+    uint64_t wgl_spilled;     /* of those, keys searched again with a table the
+                                 budget fits (they outgrew the shared tables)   */
+    uint64_t wgl_steps;       /* WGL walk steps (linearizations + backtracks)   */
 } lc_stats;
 
 /* lc_stats.t0_path */

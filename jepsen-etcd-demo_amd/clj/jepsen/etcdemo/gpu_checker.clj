@@ -57,7 +57,10 @@
         (let [id (+ named-reg-base (count @names))] (vswap! names assoc r id) id))))
 
 ;; LC_ALGO_*: jepsen.checker/linearizable's :algorithm (:linear, :wgl, else
-;; competition).  All three run the same device search; only :analyzer differs.
+;; competition).  :linear runs knossos.linear's config-set search, :wgl
+;; knossos.wgl's own walk (ABI 10), competition :linear and then WGL for the
+;; keys :linear gave up on at the budget; lc_result.analyzer (offset 48) says
+;; which analysis answered each key.
 (defn- algo-code [algorithm] (case algorithm :linear 0 :wgl 1 2))
 
 (def ^:private max-final 10)  ; jepsen.checker/linearizable truncates to 10
@@ -187,13 +190,14 @@
                       (let [y (aget xs j)] (when-not (= y nil-long) y))])))))))
 
 (defn- report
-  "Decodes lc_report's words for packed key i into the :linear map."
-  [history model algorithm packed i valid fail-ev cause ^Memory finals n-final names]
+  "Decodes lc_report's words for packed key i into the :linear map;
+  analyzer is the analysis that answered the key (:linear or :wgl)."
+  [history model analyzer packed i valid fail-ev cause ^Memory finals n-final names]
   (let [words (long-array 256)
         fin   (.share finals (* i max-final 16))
         ;; :wgl's :configs are the Wing-Gong frontier at the stuck :ok (lc_report_wgl)
         render (fn [^longs w cap]
-                 (if (= algorithm :wgl)
+                 (if (= analyzer :wgl)
                    (LincheckNative/lc_report_wgl packed i valid fail-ev fin n-final max-final w cap)
                    (LincheckNative/lc_report packed i valid fail-ev fin n-final max-final w cap)))
         need  (check-rc (render words 256) "lc_report")
@@ -231,7 +235,7 @@
                                          bad   (model/step (state-model (take!)) fail-op)]
                                      (into [{:op prev :model m0}]
                                            (conj steps {:op fail-op :model {:msg (:msg bad)}}))))))
-        base    {:analyzer (if (= algorithm :wgl) :wgl :linear)
+        base    {:analyzer analyzer
                  :configs  configs}]
     (case (int valid)
       1 (assoc base :valid? true :final-paths [])
@@ -273,20 +277,23 @@
             cause    (Memory. n1)
             finals   (Memory. (* 16 max-final n1))
             n-final  (Memory. (* 4 n1))
-            result   (Memory. 48)]               ; sizeof(lc_result)
+            analyzer (Memory. n1)
+            result   (Memory. 56)]               ; sizeof(lc_result), ABI 10
         (.clear result)
         (.setPointer result 0 valid)
         (.setPointer result 8 fail-ev)
         (.setPointer result 16 cause)
         (.setPointer result 32 finals)
         (.setPointer result 40 n-final)
+        (.setPointer result 48 analyzer)
         (check-rc (LincheckNative/lc_check_batch ctx batch result nil) "lc_check_batch")
         (persistent!
           (reduce
             (fn [m i]
               (let [k  (aget key-ids i)
                     v  (.getByte valid i)
-                    c  (.getByte cause i)]
+                    c  (.getByte cause i)
+                    an (if (= 1 (.getByte analyzer i)) :wgl :linear)]
                 (assoc! m k
                         (cond
                           ;; the key's sub-history could not be prepared:
@@ -295,10 +302,10 @@
                           {:valid? :unknown :error (LincheckNative/lc_packed_key_error packed i)}
                           ;; valid keys: no counterexample to render
                           (= 1 v)
-                          {:valid? true :analyzer (if (= algorithm :wgl) :wgl :linear)
+                          {:valid? true :analyzer an
                            :configs [] :final-paths []}
                           :else
-                          (report history model algorithm packed i v (.getInt fail-ev (* 4 i)) c
+                          (report history model an packed i v (.getInt fail-ev (* 4 i)) c
                                   finals (.getInt n-final (* 4 i)) @names)))))
             (transient {})
             (range n-keys))))

@@ -365,6 +365,17 @@ struct Dev {
         int slots = 0;
         lcd::LayWs w{};
     } lws;
+    // knossos.wgl workspaces (device_wgl.hip): [0] tables sized to share at
+    // most WGL_SMALL_BYTES among the resident waves, [1] tables the budget
+    // fits, for the keys that outgrow [0]; zeroed once (entries are stamped)
+    struct WWs {
+        char *base = nullptr;
+        size_t bytes = 0;
+        size_t slot_bytes = 0;
+        int slots = 0;
+    } wws[2];
+    uint32_t wgl_seq = 0;     // launches so far (the high half of every cache stamp)
+    uint8_t *analyzer = nullptr;  // [cap_keys] LC_ALGO_* that answered each key
     ~Dev() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -372,6 +383,7 @@ struct Dev {
         if (hctl) (void)hipHostFree(hctl);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
         dfree(ws[0].base); dfree(ws[1].base); dfree(lws.base); dfree(dargs); dfree(send); dfree(node);
+        dfree(wws[0].base); dfree(wws[1].base); dfree(analyzer);
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
         dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr); dfree(spec_fin);
         if (hargs) (void)hipHostFree(hargs);
@@ -429,8 +441,9 @@ static int ensure_capacity(Dev *c, int64_t n_keys) {
     if (n_keys <= c->cap_keys) return LC_OK;
     int64_t cap = std::max<int64_t>(n_keys, 1024);
     dfree(c->lists); dfree(c->valid); dfree(c->fail_event); dfree(c->cause);
-    dfree(c->peak); dfree(c->final_cfg); dfree(c->n_final);
+    dfree(c->peak); dfree(c->final_cfg); dfree(c->n_final); dfree(c->analyzer);
     HIPCHK(dalloc(&c->lists, (size_t)cap * 5));
+    HIPCHK(dalloc(&c->analyzer, (size_t)cap));
     HIPCHK(dalloc(&c->valid, (size_t)cap));
     HIPCHK(dalloc(&c->fail_event, (size_t)cap));
     HIPCHK(dalloc(&c->cause, (size_t)cap));
@@ -1003,6 +1016,108 @@ static int ensure_segments(Dev *c, int64_t n_keys) {
     return LC_OK;
 }
 
+// ---- knossos.wgl (device_wgl.hip) ---------------------------------------------
+
+// Lowe's caches of the resident waves share at most this many bytes; a key
+// whose cache outgrows its share is searched again with a table the budget
+// fits (fewer waves at once).
+constexpr size_t WGL_SMALL_BYTES = 4ull << 30;
+constexpr uint32_t WGL_LDS_EVENTS = 8192;  // events (+ slot history) per key held in LDS
+
+// Allocate (or reuse) WGL workspace `which` for `slots` waves of layout w.
+static int ensure_wgl_ws(Dev *c, int which, const lcd::WglWs &w, int want, int *slots_out) {
+    Dev::WWs &W = c->wws[which];
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    int slots = std::max(want, 1);
+    const size_t limit = W.bytes + free_b / 2;
+    while (slots > 1 && (size_t)slots * w.slot_bytes > limit) slots /= 2;
+    if ((size_t)slots * w.slot_bytes > limit)
+        return lc::fail(LC_E_NOMEM, "WGL workspace: one wave needs %zu bytes (budget %llu)", w.slot_bytes,
+                        (unsigned long long)c->o->max_configs);
+    if (!W.base || W.slot_bytes != w.slot_bytes || W.slots < slots) {
+        if (W.base) HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(W.base);
+        W.bytes = 0; W.slots = 0; W.slot_bytes = 0;
+        HIPCHK(hipMalloc((void **)&W.base, (size_t)slots * w.slot_bytes));
+        HIPCHK(hipMemsetAsync(W.base, 0, (size_t)slots * w.slot_bytes, c->stream));  // stamp 0: never a key's
+        W.bytes = (size_t)slots * w.slot_bytes;
+        W.slots = slots;
+        W.slot_bytes = w.slot_bytes;
+    }
+    *slots_out = std::min(slots, W.slots);
+    return LC_OK;
+}
+
+// knossos.wgl over keys order[0 .. n): n = n_order, or *n_in (a device
+// count) when n_in is given (n_hint bounds it).  Results through a's arrays;
+// analyzer (device, may be null) gets LC_ALGO_WGL per key searched.
+static int run_wgl(Dev *c, const DevBatch *d, const lcd::Args &a, const int32_t *order, int32_t n_order,
+                   const int32_t *n_in, int64_t n_hint, uint8_t *analyzer, lc_stats *st) {
+    if (n_hint <= 0 || d->n_keys == 0) return LC_OK;
+    const lc_opts &o = *c->o;
+    // the longest key (LPT order: the first), for the frame stack and slot history
+    uint64_t max_ev = 1;
+    if (!d->order_of.empty()) {
+        const int32_t k0 = d->order_of[0];
+        max_ev = std::max<uint64_t>(1, d->order_off[(size_t)k0 + 1] - d->order_off[(size_t)k0]);
+    }
+    if (max_ev > 0x7FFFFFFFull) return lc::fail(LC_E_INVALID, "WGL: a key with more than 2^31 events");
+    const uint64_t need = lcd::wgl_table_entries(o.max_configs);
+    const int slots_a = (int)std::min<int64_t>(n_hint, (int64_t)c->cu_count * 4);
+    uint64_t t_a = 1ull << 14;
+    while (t_a * 2 <= need && t_a * 2 * 32 * (uint64_t)slots_a <= WGL_SMALL_BYTES) t_a *= 2;
+    if (o.path_flags & LC_PATH_WGL_SMALL) t_a = 1ull << 14;
+    t_a = std::min(t_a, need);
+    const lcd::WglWs wa = lcd::wgl_layout(o.max_configs, (uint32_t)max_ev, (uint32_t)t_a);
+    int slots = 0;
+    int rc = ensure_wgl_ws(c, 0, wa, slots_a, &slots);
+    if (rc) return rc;
+    int32_t *const ctl = c->counters + 16;  // [0] -, [1] ticket, [2] spill count, [3] spill ticket
+    int32_t *const spill = c->lists + 4 * c->cap_keys;
+    HIPCHK(hipMemsetAsync(ctl, 0, 4 * sizeof(int32_t), c->stream));
+    lcd::WglArgs w{};
+    w.ev_off = a.ev_off; w.events = a.events; w.trans = a.trans; w.trans_off = a.trans_off;
+    w.key_states = a.key_states; w.key_error = a.key_error; w.table = a.table;
+    w.init_state = a.init_state; w.n_trans = a.n_trans; w.budget = o.max_configs; w.max_final = o.max_final;
+    w.lds_events = (uint32_t)std::min<uint64_t>(max_ev, WGL_LDS_EVENTS);
+    w.order = order; w.n_order = n_order; w.n_in = n_in;
+    w.ticket = ctl + 1;
+    w.err = a.err;
+    w.gen_base = (uint64_t)(++c->wgl_seq) << 32;
+    w.spill_at = t_a < need ? (uint32_t)(t_a / 2 - 1) : 0u;
+    w.spill = spill; w.n_spill = ctl + 2;
+    w.ws = wa;
+    w.ws.base = c->wws[0].base;
+    w.valid = a.valid; w.fail_event = a.fail_event; w.cause = a.cause; w.peak = a.peak;
+    w.final_cfg = a.final_cfg; w.n_final = a.n_final; w.analyzer = analyzer; w.rec = a.rec;
+    w.ev_count = a.ev_count; w.keys_done = a.keys_done;
+    HIPCHK(hipEventRecord(c->et3a, c->stream));
+    HIPCHK(lcd::launch_wgl(w, slots, c->stream));
+    int32_t n_spill = 0;
+    if (w.spill_at) {
+        int32_t *h = (int32_t *)(c->hctl + 4) + 18;
+        HIPCHK(hipMemcpyAsync(h, ctl + 2, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        n_spill = *h;
+        if (n_spill > 0) {
+            const lcd::WglWs wb = lcd::wgl_layout(o.max_configs, (uint32_t)max_ev, 0);
+            rc = ensure_wgl_ws(c, 1, wb, (int)std::min<int64_t>(n_spill, (int64_t)c->cu_count * 4), &slots);
+            if (rc) return rc;
+            w.order = spill; w.n_order = 0; w.n_in = ctl + 2;
+            w.ticket = ctl + 3;
+            w.gen_base = (uint64_t)(++c->wgl_seq) << 32;
+            w.spill_at = 0;
+            w.ws = wb;
+            w.ws.base = c->wws[1].base;
+            HIPCHK(lcd::launch_wgl(w, slots, c->stream));
+        }
+    }
+    HIPCHK(hipEventRecord(c->et3b, c->stream));
+    if (st) st->wgl_spilled += (uint64_t)n_spill;
+    return LC_OK;
+}
+
 enum ResMode { RES_HOST = 0, RES_DEV = 1, RES_CTX = 2 };
 
 // Search d on c.  RES_HOST: r's arrays are host memory and receive the
@@ -1048,6 +1163,71 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     a.err = c->counters + 4;
     a.err_base = (int32_t)key0;  // malformed keys are reported by their index in the caller's batch
     a.list_cap = (int32_t)c->cap_keys;
+    // which analysis answered each key (lc_result.analyzer)
+    uint8_t *const analyzer = mode == RES_DEV ? r->analyzer : (mode == RES_HOST && r->analyzer) ? c->analyzer : nullptr;
+    if (analyzer && K > 0 && o.algorithm != LC_ALGO_WGL)
+        HIPCHK(hipMemsetAsync(analyzer, LC_ALGO_LINEAR, (size_t)K, c->stream));
+    if (o.algorithm == LC_ALGO_WGL) {
+        // knossos.wgl's own search (device_wgl.hip) for every key
+        if (enqueued) *enqueued = false;
+        HIPCHK(hipMemsetAsync(c->ctl, 0, 4 * sizeof(unsigned long long) + 4 * sizeof(int32_t), c->stream));
+        HIPCHK(hipMemsetAsync(c->counters + 6, 0, 10 * sizeof(int32_t), c->stream));
+        c->ticket_live = false;
+        if (!d->ev32_ready && d->n_events) {
+            const uint64_t n4 = (d->n_events + 3) / 4;
+            const int blocks = (int)std::min<uint64_t>((n4 + 255) / 256, (uint64_t)c->cu_count * 8);
+            hipLaunchKernelGGL(k_widen16, dim3(std::max(blocks, 1)), dim3(256), 0, c->stream, d->events16, d->events,
+                               d->n_events);
+            HIPCHK(hipGetLastError());
+            d->ev32_ready = true;
+        }
+        if (a.n_final && K > 0) HIPCHK(hipMemsetAsync(a.n_final, 0, (size_t)K * 4, c->stream));
+        HIPCHK(hipEventRecord(c->e0, c->stream));
+        if (!d->validated && K > 0) {  // the per-event checks the host skipped, ahead of the walk
+            lcd::Args av = a;
+            av.n_order = (int32_t)K;
+            HIPCHK(lcd::launch_validate(av, c->stream, true));
+        }
+        lc_stats ws{};
+        rc = run_wgl(c, d, a, d->order, (int32_t)K, nullptr, K, analyzer, &ws);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(c->e1, c->stream));
+        HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
+        if (mode == RES_HOST && K > 0) {
+            HIPCHK(hipMemcpyAsync(r->valid, c->valid, (size_t)K, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(r->fail_event, c->fail_event, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(r->cause, c->cause, (size_t)K, hipMemcpyDeviceToHost, c->stream));
+            if (r->peak_configs)
+                HIPCHK(hipMemcpyAsync(r->peak_configs, c->peak, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+            if (r->final_configs)
+                HIPCHK(hipMemcpyAsync(r->final_configs, c->final_cfg, (size_t)K * o.max_final * 16,
+                                      hipMemcpyDeviceToHost, c->stream));
+            if (r->n_final)
+                HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+            if (r->analyzer)
+                HIPCHK(hipMemcpyAsync(r->analyzer, c->analyzer, (size_t)K, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        rc = take_error(c);
+        if (rc) return rc;
+        float ms = 0, msw = 0;
+        HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+        if (K > 0) HIPCHK(hipEventElapsedTime(&msw, c->et3a, c->et3b));
+        if (st) {
+            *st = lc_stats{};
+            st->kernel_ms = ms;
+            st->wgl_ms = msw;
+            st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            st->lds_keys = c->hctl[2];
+            st->wgl_keys = c->hctl[2];
+            st->wgl_steps = c->hctl[1];
+            st->events = c->hctl[1];
+            st->wgl_spilled = ws.wgl_spilled;
+        }
+        return LC_OK;
+    }
+    const bool competition = o.algorithm == LC_ALGO_COMPETITION;
+    if (competition) allow_async = false;  // the WGL step needs the :linear step's causes
     int32_t *spill0 = c->lists, *spill1 = c->lists + c->cap_keys, *spill2 = c->lists + 2 * c->cap_keys;
     int32_t *wide = c->lists + 3 * c->cap_keys, *old_narrow = c->lists + 4 * c->cap_keys;
     int32_t *n_spill0 = c->counters + 0, *n_spill1 = c->counters + 1, *n_spill2 = c->counters + 2;
@@ -1142,7 +1322,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         d->ev32_ready = true;
     }
     uint32_t ticket_base = 0;
-    if (t0_step && c->ticket_live) {
+    if (t0_step && c->ticket_live && !competition) {
         ticket_base = c->ticket_next;
     } else {
         // zero everything but the error words (a malformed batch reported at
@@ -1284,6 +1464,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
                                       hipMemcpyDeviceToHost, c->stream));
             if (r->n_final)
                 HIPCHK(hipMemcpyAsync(r->n_final, c->n_final, (size_t)K * 4, hipMemcpyDeviceToHost, c->stream));
+            if (r->analyzer)
+                HIPCHK(hipMemcpyAsync(r->analyzer, c->analyzer, (size_t)K, hipMemcpyDeviceToHost, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
         return take_error(c);
@@ -1358,6 +1540,33 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
     if (K > 0) HIPCHK(hipEventElapsedTime(&ms0, c->e0, c->et0));
     if (t3) HIPCHK(hipEventElapsedTime(&ms3, c->et3a, c->et3b));
+    // knossos.competition: the keys :linear left :unknown at its budget are
+    // answered by WGL's search (the analysis that could still finish)
+    uint64_t wgl_keys = 0, wgl_steps = 0, wgl_spilled = 0;
+    float msw = 0;
+    if (competition && K > 0) {
+        int32_t *const list = c->lists, *const count = c->counters + 16;
+        HIPCHK(hipMemsetAsync(count, 0, sizeof(int32_t), c->stream));
+        HIPCHK(lcd::launch_collect_budget(a.cause, (int32_t)K, list, count, c->stream));
+        int32_t *h = (int32_t *)(c->hctl + 4) + 16;
+        HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h, count, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const int32_t n_b = *h;
+        const uint64_t ev0 = acc[1];
+        if (n_b > 0) {
+            lc_stats ws{};
+            rc = run_wgl(c, d, a, list, 0, count, n_b, analyzer, &ws);
+            if (rc) return rc;
+            rc = readback();
+            if (rc) return rc;
+            HIPCHK(hipEventElapsedTime(&msw, c->et3a, c->et3b));
+            HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+            wgl_keys = (uint64_t)n_b;
+            wgl_steps = acc[1] - ev0;
+            wgl_spilled = ws.wgl_spilled;
+        }
+    }
     if (st) {
         st->kernel_ms = ms;
         st->tier0_ms = ms0;
@@ -1371,6 +1580,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         st->deep_keys = (uint64_t)(n_deep + n_widek);  // keys the HBM tier (re)searched
         st->t0_path = t0_path;
         st->ev_word_bytes = t0_path ? (ev16 ? 2u : 4u) : 0u;
+        st->wgl_ms = msw;
+        st->wgl_keys = wgl_keys;
+        st->wgl_steps = wgl_steps;
+        st->wgl_spilled = wgl_spilled;
     }
     return LC_OK;
 }

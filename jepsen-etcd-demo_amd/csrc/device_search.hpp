@@ -157,4 +157,53 @@ int t3_block();
 size_t cfg_bytes_narrow();
 size_t cfg_bytes_wide();
 
+// knossos.wgl on the device (device_wgl.hip): one wave per key walks the
+// Wing & Gong search with Lowe's cache in HBM.  Per resident wave a slot of
+// slot_bytes: the cache table (tab_mask + 1 entries of 32 B), the frame
+// stack, the per-event slot history.
+struct WglWs {
+    char *base;
+    size_t slot_bytes;
+    uint32_t tab_mask;
+    size_t off_frames, off_prev;
+};
+struct WglArgs {
+    const uint64_t *ev_off;
+    const uint32_t *events;
+    const uint32_t *trans;
+    const uint32_t *trans_off;   // may be null
+    const uint16_t *key_states;  // may be null
+    const uint8_t *key_error;    // may be null
+    const uint16_t *table;       // may be null: a table model's rows
+    uint32_t init_state;
+    uint32_t n_trans;
+    uint64_t budget;             // Lowe's cache holds at most this many pairs
+    int32_t max_final;
+    uint32_t lds_events;         // events (and their slot history) per key kept in LDS
+    const int32_t *order;        // keys order[0 .. n) with n = n_in ? *n_in : n_order
+    int32_t n_order;
+    const int32_t *n_in;
+    int32_t *ticket;             // zeroed before the launch
+    const int32_t *err;          // validation error words: a refused batch is not searched
+    uint64_t gen_base;           // launch << 32: a table entry is the key's when its stamp is gen_base | ticket + 1
+    uint32_t spill_at;           // > 0: a key whose cache would pass this many pairs goes to spill (a larger table)
+    int32_t *spill;
+    int32_t *n_spill;
+    WglWs ws;
+    int8_t *valid;
+    int32_t *fail_event;
+    uint8_t *cause;
+    uint32_t *peak;              // may be null: the cache size at the end
+    uint64_t *final_cfg;         // may be null: the frontier at the stuck :ok (first max_final, walk order)
+    uint32_t *n_final;           // may be null
+    uint8_t *analyzer;           // may be null: LC_ALGO_WGL written for every key searched here
+    uint64_t *rec;               // may be null: LC_REC_* records
+    unsigned long long *ev_count;   // search steps
+    unsigned long long *keys_done;
+};
+WglWs wgl_layout(uint64_t budget, uint32_t max_events, uint32_t table_entries);
+size_t wgl_table_entries(uint64_t budget);
+hipError_t launch_wgl(const WglArgs &a, int grid, hipStream_t s);
+hipError_t launch_collect_budget(const uint8_t *cause, int32_t n, int32_t *list, int32_t *count, hipStream_t s);
+
 }  // namespace lcd

@@ -1,0 +1,476 @@
+// device_wgl.hip -- knossos.wgl on the device: the Wing & Gong depth-first
+// linearization search with Lowe's cache of (linearized set, model state)
+// pairs, one wavefront per key (:algorithm :wgl, the slot at etcdemo.clj:118;
+// SURVEY.md 8(f) F-3; the search north_star names).  Restated in
+// oracle/wgl_ref.py (the list walk as knossos.wgl writes it) and
+// oracle/wgl_ref.c; parity against Knossos itself is unpinned.
+//
+// The search is sequential by definition -- its :unknown (a cache of more
+// than `budget` pairs) depends on the order it explores -- so a key's walk is
+// the walk the restatement makes, step for step, and the parallelism is over
+// keys (one wave each) and, within a key, over the ops pending at once (one
+// lane per window slot: the candidates of a step are evaluated together).
+//
+// Representation (the same as oracle/wgl_ref.c):
+//   a search node is (R, X, s): R the first return entry still in the list
+//   (the :ok of the earliest op not linearized yet; every op returning before
+//   R is linearized), X the window slots of the linearized ops pending at R,
+//   s the model state.  (R, X) names the linearized set exactly, so Lowe's
+//   cache is a set of (R, X, s).
+//   The list walk from the head visits the call entries of the ops pending at
+//   R and not linearized, in invoke order, then stops at R.  A node's
+//   candidates are therefore those slots (pending mask minus X), tried in
+//   order of their :invoke; a candidate is taken when the model can step it
+//   and its child (R', X', s') is not cached.  Taking the op of R itself
+//   moves R to the next :ok whose op is not linearized (the ops returning in
+//   between leave X).
+//
+// One probe round per node.  The cache status of a node's candidates is read
+// once, when the node is first reached (every candidate probed at once, one
+// lane each), and kept in its frame: while the subtree of a candidate c is
+// searched, every pair cached there has c in its linearized set, and no
+// other candidate's child has, so the remaining candidates' status cannot
+// change before the walk comes back.  A backtrack therefore costs a frame
+// load and no probe; a step down costs one probe round (plus, when resuming
+// a node, one coalesced read of 64 consecutive table entries to find the
+// insertion slot, which the subtree may have taken).
+//
+// Memory per resident wave (lcd::WglWs): Lowe's cache, an open-addressed
+// table of 32-byte entries {X lo, X hi, R, s, stamp} in HBM, at most half
+// full (sized from the budget); an entry belongs to the current key when its
+// stamp is the key's (launch << 32 | ticket + 1), so tables are never
+// cleared between keys or launches.  The frame stack (64 B per level; depth
+// <= ops of the key) in HBM.  The key's event words and, per :invoke event,
+// the :invoke that held its window slot before it (to undo a move of R) in
+// LDS for the first `lds_events` events, in HBM beyond.
+
+#include "device_common.hpp"
+
+namespace lcd {
+namespace {
+
+constexpr uint32_t WGL_END = 0xFFFFFFFFu;  // R past the last return: every :ok passed
+constexpr uint32_t WGL_NONE = 0xFFFFFFFFu; // no :invoke (prev of a slot's first op)
+
+extern "C" __device__ int lc_wgl_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t wsetl(uint32_t v, uint32_t l, uint32_t x) {
+    return (uint32_t)lc_wgl_writelane((int)x, (int)l, (int)v);
+}
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return (uint64_t)uni((uint32_t)x) | (uint64_t)uni((uint32_t)(x >> 32)) << 32;
+}
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+__device__ __forceinline__ bool mbit(uint64_t lo, uint64_t hi, uint32_t s) {
+    return ((s < 64 ? lo : hi) >> (s & 63)) & 1ull;
+}
+__device__ __forceinline__ void mset(uint64_t &lo, uint64_t &hi, uint32_t s) {
+    if (s < 64) lo |= 1ull << s; else hi |= 1ull << (s - 64);
+}
+__device__ __forceinline__ void mclr(uint64_t &lo, uint64_t &hi, uint32_t s) {
+    if (s < 64) lo &= ~(1ull << s); else hi &= ~(1ull << (s - 64));
+}
+
+__device__ __forceinline__ uint32_t wgl_hash(uint32_t R, uint32_t s, uint64_t lo, uint64_t hi) {
+    uint64_t h = lo * 0x9E3779B97F4A7C15ull;
+    h ^= (hi + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+    h ^= ((uint64_t)R << 17 ^ (uint64_t)s) * 0x165667B19E3779F9ull;
+    h ^= h >> 29;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 32;
+    return (uint32_t)h;
+}
+
+struct Frame {  // one level of the walk: the node a step down left (64 B)
+    uint32_t R, s, pad0, pad1;
+    uint64_t xlo, xhi;   // linearized pending ops (slots)
+    uint64_t plo, phi;   // ops pending at R (slots)
+    uint64_t clo, chi;   // candidates still to try: legal and not cached when the node was reached
+};
+
+struct KeyIo {
+    const uint32_t *gev;   // the key's event words (HBM)
+    uint32_t *gprev;       // per :invoke event: the :invoke that held its slot before (HBM part)
+    uint32_t *lev;         // LDS copies of the first lds_n of each
+    uint32_t *lprev;
+    uint32_t lds_n;
+    __device__ __forceinline__ uint32_t ev(uint32_t j) const { return uni(j < lds_n ? lev[j] : gev[j]); }
+    __device__ __forceinline__ uint32_t prev(uint32_t j) const { return uni(j < lds_n ? lprev[j] : gprev[j]); }
+    __device__ __forceinline__ void set_prev(uint32_t j, uint32_t v) const {
+        if (__lane_id() == 0) {
+            if (j < lds_n) lprev[j] = v; else gprev[j] = v;
+        }
+    }
+};
+
+__device__ __forceinline__ void wgl_finish(const WglArgs &a, int32_t key, int verdict, int cause, int32_t fev,
+                                           uint32_t cache_n, uint32_t n_front, uint64_t steps) {
+    if (__lane_id() == 0) {
+        a.valid[key] = (int8_t)verdict;
+        a.cause[key] = (uint8_t)cause;
+        a.fail_event[key] = fev;
+        if (a.peak) a.peak[key] = cache_n;
+        if (a.n_final) a.n_final[key] = verdict == LC_INVALID ? n_front : 0u;
+        if (a.analyzer) a.analyzer[key] = (uint8_t)LC_ALGO_WGL;
+        if (a.rec)
+            a.rec[key] = (uint64_t)(uint8_t)(verdict + 1) | (uint64_t)(uint8_t)cause << 8 |
+                         (uint64_t)(uint32_t)(fev + 1) << 16;
+        atomicAdd(a.ev_count, (unsigned long long)steps);
+        atomicAdd(a.keys_done, 1ull);
+    }
+}
+
+// Search one key (the whole wave).  Every lane runs the same control flow:
+// every branch below is on a wave-uniform value.
+__device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t *lds, char *slot_ws) {
+    const uint32_t lane = __lane_id();
+    const uint64_t eb = a.ev_off[key];
+    const uint32_t n = (uint32_t)(a.ev_off[key + 1] - eb);
+    if (a.key_error && a.key_error[key]) {
+        wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+        return;
+    }
+    if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
+        wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 0, 0, 0);
+        return;
+    }
+    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
+    const uint64_t gen = a.gen_base | (uint64_t)(ticket + 1u);
+    uint4 *tab = (uint4 *)slot_ws;  // 2 x uint4 per entry
+    Frame *frames = (Frame *)(slot_ws + a.ws.off_frames);
+    KeyIo io;
+    io.gev = a.events + eb;
+    io.gprev = (uint32_t *)(slot_ws + a.ws.off_prev);
+    io.lds_n = n < a.lds_events ? n : a.lds_events;
+    io.lev = lds;
+    io.lprev = lds + a.lds_events;
+    // Stage the events (LDS part) and look for an :invoke the window cannot
+    // hold (slot >= LC_WIDE_MAX_SLOTS): the key is then :unknown "window" at
+    // the first such :invoke, before any search (as the restatement).
+    uint32_t win_ev = WGL_END;
+    for (uint32_t base = 0; base < n; base += 64) {
+        const uint32_t j = base + lane;
+        uint32_t w = 0;
+        if (j < n) w = io.gev[j];
+        if (j < io.lds_n) io.lev[j] = w;
+        const bool wide = j < n && !(w & LC_EV_OK_BIT) && LC_EV_SLOT(w) >= LC_WIDE_MAX_SLOTS;
+        const uint64_t m = ballot(wide);
+        if (m && win_ev == WGL_END) win_ev = base + (uint32_t)__builtin_ctzll(m);
+    }
+    __syncthreads();
+    if (win_ev != WGL_END) {
+        wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_WINDOW, (int32_t)win_ev, 0, 0, 0);
+        return;
+    }
+    auto desc_of = [&](uint32_t w) -> uint32_t {
+        const uint32_t t = LC_EV_TRANS(w);
+        return t < a.n_trans - tb ? uni(a.trans[tb + t]) : 0u;
+    };
+    // per lane: the op holding window slot `lane` (occ0, dsc0) and `lane + 64`
+    // (occ1, dsc1) at R -- its :invoke event and its transition descriptor
+    uint32_t occ0 = WGL_NONE, occ1 = WGL_NONE, dsc0 = 0, dsc1 = 0;
+    uint64_t xlo = 0, xhi = 0, plo = 0, phi = 0;
+    uint32_t s = a.init_state;
+    uint32_t R = WGL_END;
+    // Move R forward from `from` (the op of R already in X): the :oks of ops
+    // in X leave X and the pending set; the :invokes passed become pending.
+    auto advance = [&](uint32_t from) {
+        R = WGL_END;
+        for (uint32_t j = from; j < n; ++j) {
+            const uint32_t w = io.ev(j);
+            const uint32_t sl = LC_EV_SLOT(w);
+            if (w & LC_EV_OK_BIT) {
+                if (mbit(xlo, xhi, sl)) {
+                    mclr(xlo, xhi, sl);
+                    mclr(plo, phi, sl);
+                    continue;
+                }
+                R = j;
+                break;
+            }
+            const uint32_t d = desc_of(w);
+            const uint32_t l = sl & 63u;
+            if (sl < 64) { io.set_prev(j, rdl(occ0, l)); occ0 = wsetl(occ0, l, j); dsc0 = wsetl(dsc0, l, d); }
+            else { io.set_prev(j, rdl(occ1, l)); occ1 = wsetl(occ1, l, j); dsc1 = wsetl(dsc1, l, d); }
+            mset(plo, phi, sl);
+        }
+    };
+    advance(0);
+    uint32_t depth = 0, cache_n = 0, n_front = 0;
+    uint32_t deepest = 0;
+    bool have_deepest = false;
+    uint64_t steps = 0;
+    uint64_t clo = 0, chi = 0;
+    bool fresh = true;       // the current node has not been probed yet
+    bool have_pos = false;   // ipos0/1 are insertion slots (nothing inserted since the probe)
+    uint32_t ipos0 = 0, ipos1 = 0;
+    const uint32_t mask = a.ws.tab_mask;
+    // hard bound on the loop: every step down inserts a new pair, so a walk
+    // takes at most 2 (budget + 1) steps; the bound only guards the kernel
+    const uint64_t max_it = 2 * (a.budget + 2) + 4;
+    for (uint64_t it = 0; it < max_it; ++it) {
+        // ---- candidates of the current node ----
+        const bool has_R = R != WGL_END;
+        const uint32_t rs = has_R ? LC_EV_SLOT(io.ev(R)) : 0xFFu;
+        // the child reached by taking the op of R: R moves on (tentatively)
+        uint32_t R2 = WGL_END;
+        uint64_t x2lo = 0, x2hi = 0;
+        auto child_of_R = [&]() {
+            x2lo = xlo; x2hi = xhi;
+            mset(x2lo, x2hi, rs);
+            R2 = WGL_END;
+            for (uint32_t j = R; j < n; ++j) {
+                const uint32_t w = io.ev(j);
+                if (!(w & LC_EV_OK_BIT)) continue;
+                const uint32_t sl = LC_EV_SLOT(w);
+                if (mbit(x2lo, x2hi, sl)) { mclr(x2lo, x2hi, sl); continue; }
+                R2 = j;
+                break;
+            }
+        };
+        if (fresh) {
+            fresh = false;
+            const uint32_t sl0 = lane, sl1 = lane + 64u;
+            uint32_t s20 = 0, s21 = 0;
+            const bool ok0 = mbit(plo, phi, sl0) && !mbit(xlo, xhi, sl0) && step(a.table, s, dsc0, s20);
+            const bool ok1 = mbit(plo, phi, sl1) && !mbit(xlo, xhi, sl1) && step(a.table, s, dsc1, s21);
+            const bool r_ok = has_R && ((ballot(rs < 64 ? ok0 : ok1) >> (rs & 63)) & 1ull);
+            if (r_ok) child_of_R();
+            // each candidate's child key
+            uint64_t k0lo = xlo, k0hi = xhi, k1lo = xlo, k1hi = xhi;
+            mset(k0lo, k0hi, sl0);
+            mset(k1lo, k1hi, sl1);
+            uint32_t kR0 = R, kR1 = R;
+            if (sl0 == rs) { kR0 = R2; k0lo = x2lo; k0hi = x2hi; }
+            if (sl1 == rs) { kR1 = R2; k1lo = x2lo; k1hi = x2hi; }
+            uint32_t p0 = wgl_hash(kR0, s20, k0lo, k0hi) & mask, p1 = wgl_hash(kR1, s21, k1lo, k1hi) & mask;
+            bool act0 = ok0, act1 = ok1, hit0 = false, hit1 = false;
+            for (uint32_t probe = 0; probe <= mask; ++probe) {
+                if (!ballot(act0 || act1)) break;
+                uint4 e00 = {}, e01 = {}, e10 = {}, e11 = {};
+                if (act0) { e00 = tab[2 * (size_t)p0]; e01 = tab[2 * (size_t)p0 + 1]; }
+                if (act1) { e10 = tab[2 * (size_t)p1]; e11 = tab[2 * (size_t)p1 + 1]; }
+                if (act0) {
+                    const uint64_t g = (uint64_t)e01.z | (uint64_t)e01.w << 32;
+                    if (g != gen) { act0 = false; }
+                    else if (e01.x == kR0 && e01.y == s20 && ((uint64_t)e00.x | (uint64_t)e00.y << 32) == k0lo &&
+                             ((uint64_t)e00.z | (uint64_t)e00.w << 32) == k0hi) { act0 = false; hit0 = true; }
+                    else p0 = (p0 + 1) & mask;
+                }
+                if (act1) {
+                    const uint64_t g = (uint64_t)e11.z | (uint64_t)e11.w << 32;
+                    if (g != gen) { act1 = false; }
+                    else if (e11.x == kR1 && e11.y == s21 && ((uint64_t)e10.x | (uint64_t)e10.y << 32) == k1lo &&
+                             ((uint64_t)e10.z | (uint64_t)e10.w << 32) == k1hi) { act1 = false; hit1 = true; }
+                    else p1 = (p1 + 1) & mask;
+                }
+            }
+            clo = ballot(ok0 && !hit0);
+            chi = ballot(ok1 && !hit1);
+            ipos0 = p0;
+            ipos1 = p1;
+            have_pos = true;
+        }
+        if ((clo | chi) == 0) {
+            // ---- no candidate left ----
+            if (!has_R) {  // the walk runs off the end of the list: linearizable
+                wgl_finish(a, key, LC_VALID, LC_CAUSE_NONE, -1, cache_n, 0, steps);
+                return;
+            }
+            // stuck on the return entry R: the deepest such entries' nodes
+            // are the frontier (the first max_final of them, in walk order)
+            if (!have_deepest || R >= deepest) {
+                if (!have_deepest || R > deepest) { deepest = R; n_front = 0; have_deepest = true; }
+                if (a.final_cfg && n_front < (uint32_t)a.max_final && lane == 0) {
+                    uint64_t *f = a.final_cfg + ((size_t)key * a.max_final + n_front) * 2;
+                    f[0] = xlo;
+                    f[1] = (xhi & ((1ull << 48) - 1)) | (uint64_t)s << 48;
+                }
+                if (n_front < (uint32_t)a.max_final) ++n_front;
+            }
+            if (depth == 0) {
+                wgl_finish(a, key, LC_INVALID, LC_CAUSE_NONLIN, (int32_t)deepest, cache_n, n_front, steps);
+                return;
+            }
+            // backtrack: the frame of the node above, and the slots of the
+            // :invokes the step down passed restored (newest first)
+            --depth;
+            ++steps;
+            const uint32_t *fw = (const uint32_t *)(frames + depth);
+            const uint32_t word = lane < 16 ? fw[lane] : 0u;
+            const uint32_t fR = rdl(word, 0), fs = rdl(word, 1);
+            const uint64_t fxlo = (uint64_t)rdl(word, 4) | (uint64_t)rdl(word, 5) << 32;
+            const uint64_t fxhi = (uint64_t)rdl(word, 6) | (uint64_t)rdl(word, 7) << 32;
+            const uint64_t fplo = (uint64_t)rdl(word, 8) | (uint64_t)rdl(word, 9) << 32;
+            const uint64_t fphi = (uint64_t)rdl(word, 10) | (uint64_t)rdl(word, 11) << 32;
+            const uint64_t fclo = (uint64_t)rdl(word, 12) | (uint64_t)rdl(word, 13) << 32;
+            const uint64_t fchi = (uint64_t)rdl(word, 14) | (uint64_t)rdl(word, 15) << 32;
+            if (fR != R) {
+                for (uint32_t j = (R == WGL_END ? n : R); j-- > fR;) {
+                    const uint32_t w = io.ev(j);
+                    if (w & LC_EV_OK_BIT) continue;
+                    const uint32_t sl = LC_EV_SLOT(w), l = sl & 63u;
+                    const uint32_t pj = io.prev(j);
+                    const uint32_t d = pj == WGL_NONE ? 0u : desc_of(io.ev(pj));
+                    if (sl < 64) { occ0 = wsetl(occ0, l, pj); dsc0 = wsetl(dsc0, l, d); }
+                    else { occ1 = wsetl(occ1, l, pj); dsc1 = wsetl(dsc1, l, d); }
+                }
+            }
+            R = fR; s = fs; xlo = fxlo; xhi = fxhi; plo = fplo; phi = fphi; clo = fclo; chi = fchi;
+            have_pos = false;
+            continue;
+        }
+        // ---- step down: the candidate with the earliest :invoke ----
+        const uint32_t v0 = ((clo >> lane) & 1ull) ? occ0 : WGL_NONE;
+        const uint32_t v1 = ((chi >> lane) & 1ull) ? occ1 : WGL_NONE;
+        uint32_t v = v0 < v1 ? v0 : v1;
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+            v = u < v ? u : v;
+        }
+        const uint32_t inv = uni(v);
+        const uint64_t m0 = ballot(v0 == inv), m1 = ballot(v1 == inv);
+        const uint32_t c = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
+        const uint32_t cl = c & 63u;
+        const uint32_t cd = c < 64 ? rdl(dsc0, cl) : rdl(dsc1, cl);
+        uint32_t sc = 0;
+        (void)step(a.table, s, cd, sc);
+        sc = uni(sc);
+        uint32_t cR = R;
+        uint64_t cxlo = xlo, cxhi = xhi;
+        mset(cxlo, cxhi, c);
+        if (c == rs) {
+            child_of_R();
+            cR = R2; cxlo = x2lo; cxhi = x2hi;
+        }
+        // insertion slot: from the probe, or the first free entry from the
+        // key's home slot (the key is known not to be there)
+        uint32_t pos;
+        if (have_pos) {
+            pos = c < 64 ? rdl(ipos0, cl) : rdl(ipos1, cl);
+        } else {
+            uint32_t home = wgl_hash(cR, sc, cxlo, cxhi) & mask;
+            pos = home;
+            for (uint32_t probe = 0; probe <= mask; probe += 64) {
+                const uint32_t q = (home + probe + lane) & mask;
+                const uint4 e1 = tab[2 * (size_t)q + 1];
+                const uint64_t free_m = ballot(((uint64_t)e1.z | (uint64_t)e1.w << 32) != gen);
+                if (free_m) { pos = (home + probe + (uint32_t)__builtin_ctzll(free_m)) & mask; break; }
+            }
+        }
+        if (a.spill_at && cache_n + 1 > a.spill_at) {
+            // the table would pass half full: the key is searched again with
+            // a table the budget fits (no result written here)
+            if (lane == 0) {
+                const int32_t i = atomicAdd(a.n_spill, 1);
+                a.spill[i] = key;
+            }
+            return;
+        }
+        if (lane == 0) {
+            tab[2 * (size_t)pos] = make_uint4((uint32_t)cxlo, (uint32_t)(cxlo >> 32), (uint32_t)cxhi,
+                                              (uint32_t)(cxhi >> 32));
+            tab[2 * (size_t)pos + 1] = make_uint4(cR, sc, (uint32_t)gen, (uint32_t)(gen >> 32));
+        }
+        ++cache_n;
+        ++steps;
+        if ((uint64_t)cache_n > a.budget) {
+            wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_BUDGET, -1, cache_n, 0, steps);
+            return;
+        }
+        // the node's frame, with c no longer to try
+        uint64_t nclo = clo, nchi = chi;
+        mclr(nclo, nchi, c);
+        if (lane < 16) {
+            uint32_t wv;
+            switch (lane) {
+                case 0: wv = R; break;
+                case 1: wv = s; break;
+                case 4: wv = (uint32_t)xlo; break;
+                case 5: wv = (uint32_t)(xlo >> 32); break;
+                case 6: wv = (uint32_t)xhi; break;
+                case 7: wv = (uint32_t)(xhi >> 32); break;
+                case 8: wv = (uint32_t)plo; break;
+                case 9: wv = (uint32_t)(plo >> 32); break;
+                case 10: wv = (uint32_t)phi; break;
+                case 11: wv = (uint32_t)(phi >> 32); break;
+                case 12: wv = (uint32_t)nclo; break;
+                case 13: wv = (uint32_t)(nclo >> 32); break;
+                case 14: wv = (uint32_t)nchi; break;
+                case 15: wv = (uint32_t)(nchi >> 32); break;
+                default: wv = 0; break;
+            }
+            ((uint32_t *)(frames + depth))[lane] = wv;
+        }
+        ++depth;
+        // apply the step
+        s = sc;
+        mset(xlo, xhi, c);
+        if (c == rs) advance(R);
+        fresh = true;
+    }
+    // not reached: the walk ends within max_it steps
+    wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, cache_n, 0, steps);
+}
+
+__global__ __launch_bounds__(64) void k_wgl(WglArgs a) {
+    extern __shared__ uint32_t lds[];
+    if (a.err && __builtin_amdgcn_readfirstlane(*(volatile const int32_t *)a.err) != 0) return;  // refused batch
+    char *slot_ws = a.ws.base + (size_t)blockIdx.x * a.ws.slot_bytes;
+    const int32_t n_work = a.n_in ? *a.n_in : a.n_order;
+    for (;;) {
+        int32_t w = 0;
+        if (__lane_id() == 0) w = atomicAdd(a.ticket, 1);
+        w = (int32_t)uni((uint32_t)w);
+        if (w >= n_work) break;
+        wgl_key(a, a.order[w], (uint32_t)w, lds, slot_ws);
+        __syncthreads();  // the next key's staging overwrites the LDS copies
+    }
+}
+
+// Keys a :linear step left :unknown at the budget (knossos.competition: the
+// other analysis answers them).
+__global__ void k_collect_budget(const uint8_t *cause, int32_t n, int32_t *list, int32_t *count) {
+    for (int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < n; i += (int32_t)(gridDim.x * blockDim.x))
+        if (cause[i] == LC_CAUSE_BUDGET) list[atomicAdd(count, 1)] = i;
+}
+
+}  // namespace
+
+WglWs wgl_layout(uint64_t budget, uint32_t max_events, uint32_t table_entries) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    WglWs w{};
+    uint64_t T = table_entries ? table_entries : wgl_table_entries(budget);
+    w.tab_mask = (uint32_t)(T - 1);
+    size_t off = al(T * 32);
+    w.off_frames = off;
+    off += al(((size_t)max_events + 2) * sizeof(Frame));
+    w.off_prev = off;
+    off += al(((size_t)max_events + 1) * 4);
+    w.slot_bytes = off;
+    return w;
+}
+
+size_t wgl_table_entries(uint64_t budget) {
+    uint64_t T = 1;
+    while (T < 2 * (budget + 2)) T <<= 1;
+    return (size_t)T;
+}
+
+hipError_t launch_wgl(const WglArgs &a, int grid, hipStream_t s) {
+    const size_t lds = (size_t)a.lds_events * 2 * sizeof(uint32_t);
+    hipLaunchKernelGGL(k_wgl, dim3(grid), dim3(64), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_collect_budget(const uint8_t *cause, int32_t n, int32_t *list, int32_t *count, hipStream_t s) {
+    const int blocks = (int)std::min<int64_t>(((int64_t)n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_collect_budget, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, cause, n, list, count);
+    return hipGetLastError();
+}
+
+}  // namespace lcd

@@ -17,14 +17,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 9
+LC_ABI_VERSION = 10
 LC_MAX_DEVICES = 8
 LC_COMM_ID_BYTES = 128
 LC_OPT_COUNT_PROBES = 0x1
 # lc_opts.path_flags (ABI 9): pinned search-path choices for A/B runs and tests
 LC_PATH_SPLIT_ON, LC_PATH_SPLIT_OFF, LC_PATH_SPEC_OFF, LC_PATH_LAYERS_OFF = 0x01, 0x02, 0x04, 0x08
 LC_PATH_NODE_SYNC, LC_PATH_NODE_STAGED, LC_PATH_CHUNKS_ON, LC_PATH_CHUNKS_OFF = 0x10, 0x20, 0x40, 0x80
-LC_PATH_SPEC_COST, LC_PATH_EV32, LC_PATH_SPEC_NOPRIO = 0x100, 0x200, 0x400
+LC_PATH_SPEC_COST, LC_PATH_EV32, LC_PATH_SPEC_NOPRIO, LC_PATH_WGL_SMALL = 0x100, 0x200, 0x400, 0x800
 LC_T0_PATH_NONE, LC_T0_PATH_LATTICE, LC_T0_PATH_SPEC, LC_T0_PATH_SEGMENTS = 0, 1, 2, 3
 T0_PATH_NAMES = {0: "none", 1: "k_search_lattice", 2: "k_spec", 3: "k_search_segments"}
 LC_DEV_RESULT, LC_DEV_ASYNC = 1, 2
@@ -34,6 +34,7 @@ LC_MOP_READ, LC_MOP_WRITE = 0, 1
 LC_MODEL_CAS_REGISTER, LC_MODEL_REGISTER, LC_MODEL_MUTEX, LC_MODEL_MULTI_REGISTER = 0, 1, 2, 3
 LC_TABLE_NONE = 0xFFFF
 LC_ALGO_LINEAR, LC_ALGO_WGL, LC_ALGO_COMPETITION = 0, 1, 2
+ANALYZERS = {LC_ALGO_LINEAR: "linear", LC_ALGO_WGL: "wgl"}
 LC_NIL = -(1 << 63)
 LC_NO_KEY = LC_NIL
 LC_NO_PROCESS = LC_NIL
@@ -82,7 +83,7 @@ class LcOpts(C.Structure):
 class LcResult(C.Structure):
     _fields_ = [("valid", P(C.c_int8)), ("fail_event", P(C.c_int32)), ("cause", P(C.c_uint8)),
                 ("peak_configs", P(C.c_uint32)), ("final_configs", P(C.c_uint64)),
-                ("n_final", P(C.c_uint32))]
+                ("n_final", P(C.c_uint32)), ("analyzer", P(C.c_uint8))]
 
 
 class LcStats(C.Structure):
@@ -90,7 +91,9 @@ class LcStats(C.Structure):
                 ("lds_keys", C.c_uint64), ("deep_keys", C.c_uint64), ("events", C.c_uint64),
                 ("tier0_ms", C.c_double), ("tier3_ms", C.c_double),
                 ("probes_t3", C.c_uint64), ("t3_bytes", C.c_uint64),
-                ("t0_path", C.c_uint32), ("ev_word_bytes", C.c_uint32)]
+                ("t0_path", C.c_uint32), ("ev_word_bytes", C.c_uint32),
+                ("wgl_ms", C.c_double), ("wgl_keys", C.c_uint64), ("wgl_spilled", C.c_uint64),
+                ("wgl_steps", C.c_uint64)]
 
 
 class LcSynthOpts(C.Structure):

@@ -125,6 +125,7 @@ class KeyResults:
     final: np.ndarray        # uint64 [K, max_final, 2]
     n_final: np.ndarray      # uint32
     stats: Dict[str, float]
+    analyzer: Optional[np.ndarray] = None  # uint8 LC_ALGO_LINEAR / LC_ALGO_WGL per key
 
 
 def comm_id() -> bytes:
@@ -205,10 +206,12 @@ class Device:
         K1 = max(K, 1)
         arrs = dict(valid=np.zeros(K1, np.int8), fail_event=np.zeros(K1, np.int32),
                     cause=np.zeros(K1, np.uint8), peak=np.zeros(K1, np.uint32),
-                    final=np.zeros((K1, self.max_final, 2), np.uint64), n_final=np.zeros(K1, np.uint32))
+                    final=np.zeros((K1, self.max_final, 2), np.uint64), n_final=np.zeros(K1, np.uint32),
+                    analyzer=np.zeros(K1, np.uint8))
         r = N.LcResult(N.ptr(arrs["valid"], C.c_int8), N.ptr(arrs["fail_event"], C.c_int32),
                        N.ptr(arrs["cause"], C.c_uint8), N.ptr(arrs["peak"], C.c_uint32),
-                       N.ptr(arrs["final"], C.c_uint64), N.ptr(arrs["n_final"], C.c_uint32))
+                       N.ptr(arrs["final"], C.c_uint64), N.ptr(arrs["n_final"], C.c_uint32),
+                       N.ptr(arrs["analyzer"], C.c_uint8))
         return arrs, r
 
     def _results(self, arrs, K, st) -> KeyResults:
@@ -217,7 +220,10 @@ class Device:
                           dict(kernel_ms=st.kernel_ms, tier0_ms=st.tier0_ms, tier3_ms=st.tier3_ms, total_ms=st.total_ms,
                                probes=st.probes, probes_t3=st.probes_t3, t3_bytes=st.t3_bytes,
                                keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events,
-                               t0_path=N.T0_PATH_NAMES.get(st.t0_path, st.t0_path), ev_word_bytes=st.ev_word_bytes))
+                               t0_path=N.T0_PATH_NAMES.get(st.t0_path, st.t0_path), ev_word_bytes=st.ev_word_bytes,
+                               wgl_ms=st.wgl_ms, wgl_keys=st.wgl_keys, wgl_spilled=st.wgl_spilled,
+                               wgl_steps=st.wgl_steps),
+                          arrs["analyzer"][:K])
 
     def check(self, packed: Packed, verdicts_only: bool = False, peaks: bool = True) -> KeyResults:
         """lc_check_batch: H2D, search, D2H.  verdicts_only: no peak sizes and
@@ -229,9 +235,9 @@ class Device:
         K = packed.n_keys
         arrs, r = self._alloc(K)
         if verdicts_only:
-            r = N.LcResult(r.valid, r.fail_event, r.cause, None, None, None)
+            r = N.LcResult(r.valid, r.fail_event, r.cause, None, None, None, r.analyzer)
         elif not peaks:
-            r = N.LcResult(r.valid, r.fail_event, r.cause, None, r.final_configs, r.n_final)
+            r = N.LcResult(r.valid, r.fail_event, r.cause, None, r.final_configs, r.n_final, r.analyzer)
         st = N.LcStats()
         N.check(N.lib().lc_check_batch(self.handle, C.byref(packed.view), C.byref(r), C.byref(st)))
         return self._results(arrs, K, st)
@@ -302,7 +308,7 @@ class DevBatch:
         st = N.LcStats()
         r = self.r
         if not peak:  # peak config-set sizes cost a wave reduction per event
-            r = N.LcResult(r.valid, r.fail_event, r.cause, None, r.final_configs, r.n_final)
+            r = N.LcResult(r.valid, r.fail_event, r.cause, None, r.final_configs, r.n_final, r.analyzer)
         N.check(N.lib().lc_check_device(self.dev.handle, self.handle, C.byref(r), 0, C.byref(st)))
         return self.dev._results({k: v.copy() for k, v in self.arrs.items()}, self.n_keys, st)
 
@@ -447,6 +453,11 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
 
 
 # ---------------------------------------------------------------- checkers
+def _analyzer_of(res: KeyResults, i: int) -> str:
+    """:analyzer of key i: the analysis whose answer it carries."""
+    return N.ANALYZERS.get(int(res.analyzer[i]), "linear") if res.analyzer is not None else "linear"
+
+
 def _draw(test: Optional[Dict], sub: Sequence[dict], lin: Dict, subdirectory: Sequence) -> None:
     """jepsen.checker/linearizable's drawing of an analysis that is not valid
     (`when-not (:valid? a)`: :unknown is not drawn): linear.svg under the
@@ -475,8 +486,9 @@ class Linearizable:
         # jepsen.checker/linearizable: :linear, :wgl, anything else -> competition
         algo = str(opts.get("algorithm", "competition")).lstrip(":")
         self.algorithm = {"linear": N.LC_ALGO_LINEAR, "wgl": N.LC_ALGO_WGL}.get(algo, N.LC_ALGO_COMPETITION)
-        # knossos.competition returns whichever analysis finishes first; here
-        # the device's :linear search always answers
+        # knossos.competition returns whichever analysis finishes first: here
+        # the :linear search, and WGL's for the keys :linear leaves :unknown at
+        # the budget (lc_result.analyzer says which answered each key)
         self.analyzer = "wgl" if self.algorithm == N.LC_ALGO_WGL else "linear"
         self.model = model
         self.budget = int(opts.get("max-configs", DEFAULT_BUDGET))
@@ -492,7 +504,7 @@ class Linearizable:
         if packed.n_keys == 0:
             return {"valid?": True, "configs": [], "final-paths": [], "analyzer": self.analyzer}
         res = self._dev().check(packed, peaks=False)
-        out = _render_key(packed, 0, res, None, self.analyzer)
+        out = _render_key(packed, 0, res, None, _analyzer_of(res, 0))
         _draw(test, history if not isinstance(history, History) else history.to_ops(), out,
               (opts or {}).get("subdirectory") or [])
         return out
@@ -506,7 +518,7 @@ class Linearizable:
         results = {}
         ops_cache = None
         for i, k in enumerate(packed.keys):
-            lin = _render_key(packed, i, res, None, self.analyzer)
+            lin = _render_key(packed, i, res, None, _analyzer_of(res, i))
             if lin.get("valid?") is False and (test or {}).get("store-path"):
                 if ops_cache is None:
                     ops_cache = history if not isinstance(history, History) else history.to_ops()

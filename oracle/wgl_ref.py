@@ -37,7 +37,10 @@ Independent of the device and of linear_ref's config-set search: it is a
 different algorithm (a backtracking walk over a linked entry list), so
 agreeing with it on verdicts, failing ops and frontiers is evidence, not a
 restatement of the same code.  A key whose search caches more than `budget`
-pairs is "unknown" (cause "budget").
+pairs is "unknown" (cause "budget").  The representation limits of the packed
+form apply as in linear_ref, before the search: a key whose :invoke needs
+window slot >= 112 (lowest free at invoke, freed at :ok) is "unknown"
+("window"), one with more than 32767 register values "unknown" ("states").
 """
 
 from __future__ import annotations
@@ -69,6 +72,25 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET, model: str =
     step, init = L.model_step(model)
     state = init if initial is None else initial
     res = WglAnalysis(valid=True, ops=ops)
+    if model == "multi-register":
+        if L.reachable_maps(ops, state, L.WIDE_MAX_STATES) > L.WIDE_MAX_STATES:
+            res.valid, res.cause = "unknown", "states"
+            return res
+    elif len(L.register_values(ops)) + 1 > L.WIDE_MAX_STATES:
+        res.valid, res.cause = "unknown", "states"
+        return res
+    free = list(range(128))
+    slot_of = {}
+    for kind, oid, pos in events:
+        if kind == "invoke":
+            s = min(free)
+            if s >= L.WIDE_MAX_SLOTS:
+                res.valid, res.cause = "unknown", "window"
+                return res
+            free.remove(s)
+            slot_of[oid] = s
+        else:
+            free.append(slot_of[oid])
     # the entry list: ("call" | "ret", op id, position), history order
     E = [("call" if kind == "invoke" else "ret", oid, pos) for kind, oid, pos in events]
     n = len(E)
@@ -104,6 +126,7 @@ def analysis(history: Sequence[dict], budget: int = DEFAULT_BUDGET, model: str =
     deepest = -1
     while True:
         if entry == END:
+            res.cache_size = len(cache)
             return res  # every return passed: linearizable
         kind, oid, pos = E[entry]
         if kind == "call":

@@ -266,7 +266,7 @@ def test_lc_history_and_result_offsets_match_header():
     assert int(re.search(r"\(Memory\. (\d+)\)[^;\n]*; sizeof\(lc_result\)", src).group(1)) == C_sizeof(N.LcResult)
     res = dict((f, int(o)) for o, f in re.findall(r"\(\.setPointer result (\d+) ([\w-]+)\)", src))
     want = {"valid": "valid", "fail-ev": "fail_event", "cause": "cause", "finals": "final_configs",
-            "n-final": "n_final"}
+            "n-final": "n_final", "analyzer": "analyzer"}
     assert set(res) == set(want)
     for local, field in want.items():
         assert getattr(N.LcResult, field).offset == res[local], (local, field)

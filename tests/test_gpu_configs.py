@@ -77,30 +77,41 @@ def test_known_answers_on_device(case, tmp_path):
 
 def _wgl_cases():
     """KATs, random multi-key histories (crashes, failures, unmatched
-    invocations, nemesis ops) and a C5-shaped synthetic one."""
-    out = [(c["name"], c.get("model", "cas-register"), c["history"]) for c in _kats()]
+    invocations, nemesis ops), a C5-shaped synthetic one, and VERDICT r3's
+    C4-shaped keys: 30 clients, 2 % crashed write/cas, seed 4, 4 keys each at
+    300, 600 and 1,200 ops, budget 2^16 -- where :linear gives up on every
+    key and WGL's walk decides 7 of 12."""
+    out = [(c["name"], c.get("model", "cas-register"), c["history"], 1 << 20) for c in _kats()]
     for seed in range(12):
         out.append((f"random-{seed}", "cas-register",
-                    random_history(500 + seed, n_keys=6, max_ops=24, procs=5, p_info=0.05, p_garbage_read=0.15)))
+                    random_history(500 + seed, n_keys=6, max_ops=24, procs=5, p_info=0.05, p_garbage_read=0.15),
+                    1 << 20))
     h = H.synth(n_keys=40, ops_per_key=120, concurrency=6, anomaly_rate=0.3, seed=55)
-    out.append(("c5-shape", "cas-register", h.to_ops()))
+    out.append(("c5-shape", "cas-register", h.to_ops(), 1 << 20))
+    for n in (300, 600, 1200):
+        h = H.synth(n_keys=4, ops_per_key=n, concurrency=30, info_rate=0.02, seed=4)
+        out.append((f"c4-shape-{n}", "cas-register", h.to_ops(), 1 << 16))
     return out
 
 
 def test_wgl_on_device_against_wgl_restatement():
     """:algorithm :wgl (the slot at etcdemo.clj:118) on the
-    device against oracle/wgl_ref.py, a restatement of knossos.wgl's own
-    search (Wing & Gong with Lowe's cache: a backtracking walk over call /
-    return entries, independent of the device's config sets).  Per key:
-    :valid?, the :ok the search is stuck on (:op :index), :previous-ok, and
-    :configs -- the frontier at that :ok (lc_report_wgl) -- equal to WGL's
-    frontier as a set when it has at most 10 configs (jepsen's truncation),
-    a subset of it otherwise.  Parity with Knossos itself is unpinned."""
-    n_cfg = n_bad = 0
-    for name, mname, hist in _wgl_cases():
+    device -- knossos.wgl's own walk (device_wgl.hip) -- against
+    oracle/wgl_ref.py, the restatement written as knossos.wgl's list walk
+    (Wing & Gong with Lowe's cache: a backtracking walk over call / return
+    entries).  Per key: :valid? (an :unknown at the cache budget included),
+    the :ok the search is stuck on (:op :index), :previous-ok, and :configs
+    -- the frontier at that :ok (lc_report_wgl) -- equal to WGL's frontier as
+    a set when it has at most 10 configs (jepsen's truncation), a subset of it
+    otherwise.  Parity with Knossos itself is unpinned."""
+    n_cfg = n_bad = n_c4 = 0
+    for name, mname, hist, budget in _wgl_cases():
         mdl = MODELS[mname]()
-        out = independent.checker(ck.linearizable({"model": mdl, "algorithm": "wgl"})).check({}, hist, {})
-        ref = W.check_independent(hist, model=mname)
+        lin = ck.linearizable({"model": mdl, "algorithm": "wgl", "max-configs": budget})
+        out = independent.checker(lin).check({}, hist, {})
+        ref = W.check_independent(hist, budget=budget, model=mname)
+        if name.startswith("c4-shape"):
+            n_c4 += sum(w.valid is True for w in ref.values())
         assert set(out["results"]) == set(ref), name
         for k, w in ref.items():
             g = out["results"][k]
@@ -125,6 +136,7 @@ def test_wgl_on_device_against_wgl_restatement():
                 assert got == want, (name, k)
             n_cfg += len(got)
     assert n_bad > 20 and n_cfg > n_bad
+    assert n_c4 >= 7  # decided where :linear gives up
 
 
 def _state_of(mname, st):

@@ -99,3 +99,106 @@ def test_wgl_budget():
     sub = LR.subhistory(ops, LR.history_keys(ops)[0])
     assert W.analysis(sub, budget=3).valid in ("unknown", True, False)
     assert W.analysis(sub, budget=1).valid == "unknown"
+
+
+# ---- the C restatement (oracle/wgl_ref.c) against the Python one ------------
+import numpy as np  # noqa: E402
+
+import cref  # noqa: E402
+from lincheck import history as H  # noqa: E402
+
+CAUSE = {"none": 0, "nonlin": 1, "budget": 2, "window": 3, "states": 4, "error": 5}
+
+
+def _slots(events):
+    """Window slot of every op (lowest free at :invoke, freed at :ok), as
+    lc_pack and wgl_ref.c assign them."""
+    free, slot = list(range(128)), {}
+    for kind, oid, _ in events:
+        if kind == "invoke":
+            slot[oid] = min(free)
+            free.remove(slot[oid])
+        else:
+            free.append(slot[oid])
+    return slot
+
+
+def c_vs_python(ops, budget, model="cas-register"):
+    """Per key: verdict, cause, failing event, cache size and frontier of
+    wgl_ref.c equal to wgl_ref.py's (the C frontier is the first 10 the walk
+    reaches: a subset of the Python set, all of it when that has <= 10)."""
+    h = H.History.from_ops(ops)
+    keys, r, fin, nf = cref.check_history_wgl(h.as_c(), budget=budget, threads=2, model=model)
+    assert list(keys) == LR.history_keys(ops)
+    out = []
+    for i, k in enumerate(keys):
+        sub = LR.subhistory(ops, k)
+        try:
+            w = W.analysis(sub, budget=budget, model=model)
+        except LR.HistoryError:
+            assert r["valid"][i] == -1 and r["cause"][i] == CAUSE["error"]
+            continue
+        assert r["valid"][i] == {True: 1, False: 0, "unknown": -1}[w.valid], (k, w.valid, w.cause)
+        assert r["cause"][i] == CAUSE[w.cause], (k, w.cause)
+        ops_k, events = LR.complete(sub, model)
+        if w.cause in ("none", "nonlin"):
+            assert r["peak"][i] == w.cache_size, (k, r["peak"][i], w.cache_size)
+        if w.valid is False:
+            assert events[r["fail_event"][i]][2] == w.fail_pos
+            slot = _slots(events)
+            want = set()
+            for st_, lin in w.frontier:
+                m = 0
+                for q in lin:
+                    m |= 1 << slot[q]
+                val = (1 if st_ else None) if model == "mutex" else st_
+                want.add((m, val))
+            got = set()
+            for j in range(nf[i]):
+                lo, hi, val = (int(x) for x in fin[i, j])
+                got.add(((lo & (2**64 - 1)) | ((hi & (2**64 - 1)) << 64), None if val == -(1 << 63) else val))
+            assert nf[i] == min(10, len(want)) and len(got) == nf[i], (k, nf[i], len(want))
+            assert got <= want
+        out.append((k, w))
+    return out
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.integers(0, 2**31 - 1), st.sampled_from([1 << 20, 3, 7]),
+       st.sampled_from(["cas-register", "register", "mutex"]))
+def test_c_wgl_matches_python(seed, budget, model):
+    c_vs_python(random_history(seed, n_keys=3, max_ops=12, procs=4, p_info=0.1, model=model), budget, model)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(n_keys=3, ops_per_key=200, concurrency=8, anomaly_rate=1.0, seed=5),
+    dict(n_keys=2, ops_per_key=120, concurrency=6, info_rate=0.05, seed=4),
+    dict(n_keys=3, ops_per_key=60, concurrency=5, interleave=True, nemesis_period=3.0, seed=1),
+])
+def test_c_wgl_matches_python_on_synthetic(kw):
+    c_vs_python(H.synth(**kw).to_ops(), 1 << 14)
+
+
+def test_c_wgl_c4_shaped_keys():
+    """VERDICT r3's C4-shaped keys (30 clients, 2 % crashed write/cas, seed 4,
+    budget 2^16), the 300-op ones: :linear gives up on every key at the
+    budget, WGL's walk decides most of them; C and Python agree step for
+    step (same verdicts, same cache sizes)."""
+    h = H.synth(n_keys=4, ops_per_key=300, concurrency=30, info_rate=0.02, seed=4)
+    res = c_vs_python(h.to_ops(), 1 << 16)
+    _, lin = cref.check_history(h.as_c(), budget=1 << 16, threads=4)
+    assert (lin["valid"] == -1).all()
+    assert sum(w.valid is True for _, w in res) >= 3
+
+
+def test_wgl_window_limit():
+    """More than 112 ops pending at once (crashed writes pile up): :unknown
+    "window" before any search, in both restatements, at the same :invoke."""
+    ops = []
+    for p in range(115):
+        ops.append({"type": "invoke", "f": "write", "value": Tuple(0, 1), "process": p, "index": len(ops)})
+        ops.append({"type": "info", "f": "write", "value": Tuple(0, 1), "process": p, "index": len(ops)})
+    w = W.analysis(LR.subhistory(ops, 0))
+    assert w.valid == "unknown" and w.cause == "window"
+    _, r, _, _ = cref.check_history_wgl(H.History.from_ops(ops).as_c())
+    assert r["valid"][0] == -1 and r["cause"][0] == CAUSE["window"] and r["fail_event"][0] == 112
