@@ -34,7 +34,18 @@ Also reported (one JSON line on rank 0):
                 profiles/*pmc*.json when committed for this workload.
   cpu_baseline  the C restatement of knossos.linear (oracle/linear_ref.c,
                 kind "port") on this host's cores and on one core, on a
-                bounded sample of the same workload (rank 0, N = 1).
+                bounded sample of the same workload (rank 0, N = 1); `wgl`
+                beside it: the C restatement of knossos.wgl
+                (oracle/wgl_ref.c) on the same cores and sample.
+
+--algorithm wgl|competition runs the step with lc_opts.algorithm
+LC_ALGO_WGL (knossos.wgl's walk on the device: device_wgl.hip) or
+LC_ALGO_COMPETITION (:linear, then WGL for its budget keys); the line then
+names k_wgl as the dominant kernel where it is.  --jepsen times the drop-in's
+real call instead: independent/checker(compose {:linear linearizable,
+:timeline}) from the packed history to Knossos-shaped result maps (exact-set
+search with final configs, counterexamples for the invalid keys), with the
+pack / search / shaping split reported.
 """
 
 import argparse
@@ -51,6 +62,10 @@ for p in (os.path.join(ROOT, "jepsen-etcd-demo_amd"), os.path.join(ROOT, "oracle
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# profiles/*.json summaries (rocprofv3 --pmc / SQ) are used for `traffic` /
+# `issue` only when they were taken of this round's build
+PROFILE_ROUND = 4
+ALGORITHMS = {"linear": 0, "wgl": 1, "competition": 2}
 SHADER_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 METRIC = "history ops linearizability-checked/sec (whole node)"
 
@@ -84,6 +99,10 @@ def parse():
     ap.add_argument("--no-probes", action="store_true", help="skip the probe-counting pass")
     ap.add_argument("--no-c3", action="store_true", help="N = 1: skip the C3-on-one-GPU block (c3_strong)")
     ap.add_argument("--c3-steps", type=int, default=10, help="timed pipelined steps of the c3_strong block")
+    ap.add_argument("--algorithm", default="linear", choices=sorted(ALGORITHMS),
+                    help="lc_opts.algorithm of the step (jepsen.checker/linearizable's :algorithm)")
+    ap.add_argument("--jepsen", action="store_true",
+                    help="time independent/checker(compose{linearizable, timeline}) -> result maps")
     ap.add_argument("--keys", type=int, default=0, help="override keys (exploration only)")
     ap.add_argument("--ops", type=int, default=0, help="override ops per key (exploration only)")
     return ap.parse_args()
@@ -165,6 +184,71 @@ def bench_c1(args):
     print(json.dumps(line, default=str), flush=True)
 
 
+def bench_jepsen(args):
+    """The drop-in's real call (etcdemo.clj:115-119): independent/checker over
+    compose {:linear (linearizable {:model cas-register}) :timeline} from the
+    history to Knossos-shaped result maps -- lc_pack, lc_check_batch with
+    final configs (the exact-set segmented search), then every key's result
+    map and the counterexamples (lc_report, :final-paths) of the invalid
+    ones.  A step is that whole call; the split into packing, search and
+    shaping is reported beside it (Linearizable.last_timing)."""
+    import numpy as np
+    import torch
+
+    from lincheck import checker as CK
+    from lincheck import history as H
+    from lincheck import independent as IND
+    from lincheck import model as M
+
+    if args.config is None:
+        args.config = "C5"
+    cfg = dict(CONFIGS[args.config])
+    if args.keys or args.ops:
+        cfg["keys"] = args.keys or cfg["keys"]
+        cfg["ops"] = args.ops or cfg["ops"]
+    K, ops = cfg["keys"], cfg["ops"]
+    hist = H.synth(n_keys=K, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
+                   anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"])
+    lin = CK.linearizable({"model": M.cas_register(), "algorithm": args.algorithm, "max-configs": args.budget})
+    chk = IND.checker(CK.compose({"linear": lin, "timeline": CK.unbridled_optimism()}))
+    for _ in range(args.warmup):
+        out = chk.check({}, hist, {})
+    torch.cuda.synchronize()
+    ts, parts = [], []
+    for _ in range(args.steps):
+        t = time.perf_counter()
+        out = chk.check({}, hist, {})
+        ts.append(time.perf_counter() - t)
+        parts.append(lin.last_timing)
+    torch.cuda.synchronize()
+    elapsed = float(np.sum(ts))
+    split = {k: float(np.mean([p[k] for p in parts])) for k in parts[0]}
+    res = out["results"]
+    n_valid = sum(r["valid?"] is True for r in res.values())
+    n_bad = sum(r["valid?"] is False for r in res.values())
+    parity = None
+    if not args.no_cpu:
+        import cref
+        keys, orc = cref.check_history(hist.as_c(), budget=args.budget, threads=16)
+        fails = sorted(int(k) for k, r in zip(keys, orc) if r["valid"] == 0)
+        parity = bool(sorted(out["failures"]) == fails)
+    line = {
+        "metric": METRIC, "value": (n_valid + n_bad) * ops * args.steps / elapsed, "unit": "ops/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": cfg["desc"], "keys": K, "ops_per_key": ops, "concurrency": cfg["concurrency"],
+                   "budget": args.budget, "algorithm": args.algorithm, "parallelism": "1 GPU"},
+        "step": "independent/checker(compose {:linear linearizable, :timeline}) on the packed history -> "
+                "result maps (lc_pack, lc_check_batch with final configs, lc_report for invalid keys)",
+        "split_ms": split,
+        "search_stats": {k: out["stats"].get(k) for k in ("kernel_ms", "tier0_ms", "t0_path", "wgl_ms", "wgl_keys")},
+        "verdicts": {"valid": n_valid, "invalid": n_bad, "unknown": len(res) - n_valid - n_bad},
+        "failures_equal_oracle": parity,
+        "roofline": None, "cpu_baseline": None,
+    }
+    print(json.dumps(line, default=str), flush=True)
+
+
 def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quota):
     """oracle/linear_ref.c with a pthread pool over keys (independent/
     checker's pmap) on this host: all usable cores, then one core, each on a
@@ -215,9 +299,40 @@ def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quo
            "host": {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota},
            "one_thread": {"value": k1 * ops / t1, "cores": 1,
                           "sample": f"first {k1} keys of the batch, 1 thread, {t1:.2f} s"}}
-    parity = bool(np.array_equal(orc["valid"], v_host[:ks]) and np.array_equal(orc["fail_event"], fe_host[:ks]))
+    if args.algorithm == "linear":
+        parity = bool(np.array_equal(orc["valid"], v_host[:ks]) and np.array_equal(orc["fail_event"], fe_host[:ks]))
+    else:
+        parity = None
     if ks < K:
         cpu["parity_sample_keys"] = ks
+    # knossos.wgl's search (the other analysis jepsen.checker/linearizable
+    # offers, north_star's "CPU :linear/:wgl"): oracle/wgl_ref.c on the same
+    # cores, on as many of the batch's first keys as ~8 s allow
+    kw = min(K, threads)
+    tw = time.perf_counter()
+    _, worc, _, _ = cref.check_history_wgl(first_keys(kw).as_c(), budget=args.budget, threads=threads)
+    twc = time.perf_counter() - tw
+    if kw < K:
+        kw2 = K if twc * K / kw <= 8.0 else min(K, max(kw, int(kw * 8.0 / max(twc, 1e-6)) // kw * kw))
+        if kw2 > kw:
+            kw = kw2
+            tw = time.perf_counter()
+            _, worc, _, _ = cref.check_history_wgl(first_keys(kw).as_c(), budget=args.budget, threads=threads)
+            twc = time.perf_counter() - tw
+    wreps = 1
+    if kw == K and twc < 0.6:
+        wreps = min(20, int(math.ceil(0.6 / max(twc, 1e-6))))
+        tw = time.perf_counter()
+        for _ in range(wreps):
+            _, worc, _, _ = cref.check_history_wgl(hist.as_c(), budget=args.budget, threads=threads)
+        twc = (time.perf_counter() - tw) / wreps
+    wwhat = (f"full {args.config} batch" if kw == K else f"first {kw} of the {K} keys of the {args.config} batch")
+    cpu["wgl"] = {"value": kw * ops / twc, "unit": "ops/s", "cores": threads, "kind": "port",
+                  "sample": f"{wwhat}, oracle/wgl_ref.c (knossos.wgl), {threads} threads, "
+                            + (f"{wreps} runs of {twc:.3f} s" if wreps > 1 else f"{twc:.2f} s"),
+                  "keys_decided": int((worc["valid"] != -1).sum()), "keys": kw}
+    if args.algorithm == "wgl":
+        parity = bool(np.array_equal(worc["valid"], v_host[:kw]) and np.array_equal(worc["fail_event"], fe_host[:kw]))
     return cpu, parity
 
 
@@ -285,6 +400,8 @@ def main():
         args.config = "C2" if world == 1 else "C3"
     if args.config == "C1":
         return bench_c1(args)
+    if args.jepsen:
+        return bench_jepsen(args)
 
     import numpy as np
     # torch first: liblincheck then binds the same HIP runtime (and RCCL), so
@@ -343,8 +460,9 @@ def main():
         else:
             cid = obj[0]
     torch.cuda.set_device(local)
+    algo = ALGORITHMS[args.algorithm]
     try:
-        dev = Device(local, budget=args.budget, comm=(rank, world, cid) if cid is not None else None)
+        dev = Device(local, budget=args.budget, comm=(rank, world, cid) if cid is not None else None, algorithm=algo)
     except Exception as e:
         if cid is None:
             raise
@@ -361,7 +479,7 @@ def main():
             print(f"[rank {rank}] RCCL unavailable ({rccl_error}); records gathered over gloo",
                   file=sys.stderr, flush=True)
             del dev
-            dev = Device(local, budget=args.budget)
+            dev = Device(local, budget=args.budget, algorithm=algo)
     n_node = block * (1 if host_gather else world)
     node_buf = np.zeros(max(n_node, 1), np.uint64)
 
@@ -385,7 +503,7 @@ def main():
     # search of the step before, records land in page-locked memory); the
     # synchronous call (lc_check_node, one step at a time) runs after them
     # for its own rate and for the per-launch kernel times of the roofline.
-    d1_t0, d1_t3, d1_t3b = [], [], []
+    d1_t0, d1_t3, d1_t3b, d1_wgl = [], [], [], []
     d1_path = {}  # the register tier's kernel and event word width (lc_stats, synchronous steps)
     pipelined = not args.d1_sync
     node_pin = PinnedRecords(n_node) if pipelined else None
@@ -396,6 +514,8 @@ def main():
         if st.tier3_ms > 0:
             d1_t3.append(st.tier3_ms)
             d1_t3b.append(st.t3_bytes)
+        if st.wgl_ms > 0:
+            d1_wgl.append(st.wgl_ms)
 
     def d1_step():
         rec, st = dev.check_node(packed, block, out=node_buf)
@@ -416,7 +536,7 @@ def main():
         for _ in range(args.warmup):
             step()
         sync(); barrier(); sync()
-        del d1_t0[:], d1_t3[:], d1_t3b[:]
+        del d1_t0[:], d1_t3[:], d1_t3b[:], d1_wgl[:]
         n_enq[0] = 0
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -469,7 +589,7 @@ def main():
         del db
 
     probes = probes_t3 = None
-    if rank == 0 and not args.no_probes:
+    if rank == 0 and not args.no_probes and args.algorithm == "linear":
         # probe count from one extra pass with
         # LC_OPT_COUNT_PROBES: the timed steps skip the per-event popcounts
         dev_c = Device(local, budget=args.budget, count_probes=True)
@@ -478,14 +598,10 @@ def main():
         del dev_c
 
     if rank == 0:
-        gv, gc, gfe = P.unpack_records(node.astype(np.int64))
         shard_keys = [P.shard_range(cfg["keys"], world, r) for r in range(world)] if strong else \
             [(r * K, (r + 1) * K) for r in range(world)]
-        parts_v, parts_fe = [], []
-        for r, (lo, hi) in enumerate(shard_keys):
-            parts_v.append(gv[r * block: r * block + (hi - lo)])
-            parts_fe.append(gfe[r * block: r * block + (hi - lo)])
-        nv, nfe = np.concatenate(parts_v), np.concatenate(parts_fe)
+        # the node's verdicts from its gathered blocks (rank order, padding 0)
+        nv, _, nfe = P.node_verdicts(node, [hi - lo for lo, hi in shard_keys], block)
         v_host, fe_host = nv[:K], nfe[:K]  # rank 0's own shard
         n_keys_total = int(nv.size)
         decided = int(((nv == 1) | (nv == 0)).sum())
@@ -531,11 +647,36 @@ def main():
             kt = avg_t3
             if probes_t3:
                 d4_t3 = 64 * probes_t3 / (kt * 1e-3) / 1e9
+        wgl = None
+        avg_wgl = float(np.mean(d1_wgl)) if d1_wgl else 0.0
+        if args.algorithm != "linear":
+            # knossos.wgl's walk (k_wgl) and what it moved: one batch check
+            # for the per-key cache sizes and the walk's steps
+            wres = dev.check(packed) if world == 1 else None
+            wsel = (wres.analyzer == 1) if wres is not None else None
+            cache_entries = int(wres.peak[wsel].sum()) if wres is not None else None
+            wsteps = int(wres.stats["wgl_steps"]) if wres is not None else None
+            wgl = {"ms_per_launch": avg_wgl, "launches": len(d1_wgl),
+                   "keys_answered": int(wsel.sum()) if wsel is not None else None,
+                   "keys_decided": int(((wres.valid != -1) & wsel).sum()) if wsel is not None else None,
+                   "keys_spilled": int(wres.stats["wgl_spilled"]) if wres is not None else None,
+                   "steps": wsteps, "cache_entries": cache_entries,
+                   "steps_per_s": (wsteps / (avg_wgl * 1e-3)) if wsteps and avg_wgl > 0 else None}
+            if avg_wgl >= max(avg_t0, avg_t3):
+                # Algorithmic bytes of a WGL launch: the event words (4 B),
+                # each cache entry written once (32 B), a 64-B frame written
+                # or read per step, the records -- the probes' reads come on
+                # top (up to a window of 32-B entries per step).
+                dominant = "k_wgl (knossos.wgl walk)"
+                kt = avg_wgl
+                alg_bytes = 4 * n_events + 32 * (cache_entries or 0) + 64 * (wsteps or 0) + 8 * K
+                tags = ("k_wgl",)
         achieved = alg_bytes / (kt * 1e-3) / 1e9 if kt > 0 else 0.0
         # measured HBM traffic and VALU issue of the same kernel on the same
         # workload, from the committed rocprofv3 --pmc summaries (profiles/)
         traffic = traffic_src = issue = None
-        tags = (t0_name,) if "T0" in dominant else ("k_search_layers",)
+        if "k_wgl" not in dominant:
+            tags = (t0_name,) if "T0" in dominant else ("k_search_layers",)
         for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*.json"))):
             try:
                 d = json.load(open(fpath))
@@ -545,6 +686,7 @@ def main():
                 continue
             kname = d.get("kernel") or ""
             if (d.get("workload") != args.config or d.get("budget", args.budget) != args.budget
+                    or d.get("round") != PROFILE_ROUND or d.get("algorithm", "linear") != args.algorithm
                     or not any(t in kname for t in tags)):
                 continue
             if d.get("bytes_per_launch"):
@@ -579,7 +721,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": cfg["desc"], "keys_total": n_keys_total, "keys_per_gpu": K, "ops_per_key": ops,
-                       "concurrency": cfg["concurrency"], "budget": args.budget,
+                       "concurrency": cfg["concurrency"], "budget": args.budget, "algorithm": args.algorithm,
                        "parallelism": f"keys sharded over {world} GPU(s), records all-gathered "
                                       f"({('host/gloo, RCCL unavailable: ' + rccl_error) if rccl_error else 'host/gloo rehearsal' if host_gather else 'RCCL' if world > 1 else 'one rank'})"},
             "step": ("lc_check_node_async (two steps in flight)" if pipelined else "lc_check_node") +
@@ -601,6 +743,7 @@ def main():
             "resident": resident,
             "tier0_ms": avg_t0,
             "tier3_ms": avg_t3,
+            "wgl": wgl,
             "probes": probes,
             "probes_t3": probes_t3,
             "ns_per_event_critical_path": avg_t0 * 1e6 / max(max_events, 1),

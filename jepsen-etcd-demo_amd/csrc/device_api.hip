@@ -115,6 +115,18 @@ __global__ void k_widen16(const uint16_t *in, uint32_t *out, uint64_t n) {
         out[i] = LC_EV16_WIDE(in[i]);
 }
 
+// Read and clear the error words of the ring slots in `mask` (one atomic
+// exchange per word, so an error a still-running step raises meanwhile is
+// never lost, only reported by the next read).
+__global__ void k_take_err(int32_t *words, uint32_t mask, int32_t *out) {
+    if (threadIdx.x != 0) return;
+    for (int q = 0; q < 4; ++q) {
+        const bool on = (mask >> q) & 1u;
+        out[2 * q] = on ? atomicExch(&words[2 * q], 0) : 0;
+        out[2 * q + 1] = on ? atomicExch(&words[2 * q + 1], 0) : 0;
+    }
+}
+
 // Verdict record of one key (include/lincheck.h LC_REC_*), 0 for padding.
 __global__ void k_pack_records(const int8_t *valid, const uint8_t *cause, const int32_t *fail_event, int64_t n,
                                int64_t block, uint64_t *out) {
@@ -274,6 +286,13 @@ static hipError_t grow(DevBatch::Mem &m, T *&p, size_t n) {
 }
 
 constexpr size_t CTL_BYTES = 4 * sizeof(unsigned long long) + 16 * sizeof(int32_t);
+// Beyond CTL_BYTES in the 256-byte control block: counters[16..19] the WGL
+// step's, [24..31] the error words of the last 4 LC_DEV_ASYNC steps (slot =
+// the step's sequence number mod 4: a refusal is reported by the wait for
+// that step), [32..39] where k_take_err leaves what it read.
+constexpr int ERR_RING = 24, ERR_TAKEN = 32;
+// Most device memory the speculative segments' per-key workspaces may take.
+constexpr uint64_t SPEC_WS_MAX_BYTES = 8ull << 30;
 
 // One device of a context: its stream, scratch and result arrays.
 struct Dev {
@@ -283,6 +302,7 @@ struct Dev {
     hipStream_t stream = nullptr;
     hipStream_t vstream = nullptr;  // validation of host-unchecked batches, beside T0
     hipStream_t cstream = nullptr;  // lc_check_node's chunked uploads, ahead of the searches
+    hipStream_t estream = nullptr;  // lc_wait_step's error reads (behind no upload or step)
     static constexpr int NODE_CHUNKS = 4;
     DevBatch *chunk[NODE_CHUNKS] = {};
     hipEvent_t chunk_ready[NODE_CHUNKS] = {};
@@ -402,6 +422,8 @@ struct Dev {
         }
         if (cstream) (void)hipStreamSynchronize(cstream);
         if (cstream) (void)hipStreamDestroy(cstream);
+        if (estream) (void)hipStreamSynchronize(estream);
+        if (estream) (void)hipStreamDestroy(estream);
         if (vstream) (void)hipStreamSynchronize(vstream);
         for (hipEvent_t e : {e0, e1, et0, et3a, et3b, ea0, ea1, vin, vdone})
             if (e) (void)hipEventDestroy(e);
@@ -551,16 +573,17 @@ static int dev_init(Dev *c, int device) {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->vstream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->estream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->vin, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->vdone, hipEventDisableTiming));
     for (hipEvent_t *e : {&c->e0, &c->e1, &c->et0, &c->et3a, &c->et3b, &c->ea0, &c->ea1}) HIPCHK(hipEventCreate(e));
     for (hipEvent_t &e : c->ring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(dalloc(&c->ctl, 16));
+    HIPCHK(dalloc(&c->ctl, 32));
     c->acc = c->ctl;
     c->counters = (int32_t *)(c->ctl + 4);
-    HIPCHK(hipMemset(c->ctl, 0, CTL_BYTES));
-    HIPCHK(hipHostMalloc((void **)&c->hctl, 16 * sizeof(unsigned long long), hipHostMallocDefault));
-    std::memset(c->hctl, 0, 16 * sizeof(unsigned long long));
+    HIPCHK(hipMemset(c->ctl, 0, 32 * sizeof(unsigned long long)));
+    HIPCHK(hipHostMalloc((void **)&c->hctl, 32 * sizeof(unsigned long long), hipHostMallocDefault));
+    std::memset(c->hctl, 0, 32 * sizeof(unsigned long long));
     HIPCHK(dalloc(&c->dargs, Dev::ARGS_RING));
     HIPCHK(hipHostMalloc((void **)&c->hargs, sizeof(lcd::Args) * Dev::ARGS_RING, hipHostMallocDefault));
     for (hipEvent_t &e : c->args_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -981,8 +1004,16 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
 
 // ---- one device's search ----------------------------------------------------
 
-// After a readback of the control block: a malformed batch T0 found.  The
-// kernels name the key by its index in the caller's batch (Args::err_base).
+static int batch_error(int why, int64_t key) {
+    return lc::fail(LC_E_INVALID, "batch: key %lld: %s", (long long)key,
+                    (why & lcd::LC_BATCH_E_SLOTS)   ? "an :ok of a slot with no pending op, or an :invoke into an occupied slot"
+                    : (why & lcd::LC_BATCH_E_TRANS) ? "transition id out of range, or a state beyond key_states"
+                                                    : "key_width / key_states understate the key");
+}
+
+// After a readback of the control block: a malformed batch a synchronous
+// step found.  The kernels name the key by its index in the caller's batch
+// (Args::err_base).
 static int take_error(Dev *c) {
     int32_t *cnt = (int32_t *)(c->hctl + 4);
     if (!cnt[4]) return LC_OK;
@@ -991,10 +1022,22 @@ static int take_error(Dev *c) {
     cnt[4] = cnt[5] = 0;
     HIPCHK(hipMemsetAsync(c->counters + 4, 0, 2 * sizeof(int32_t), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    return lc::fail(LC_E_INVALID, "batch: key %lld: %s", (long long)key,
-                    (why & lcd::LC_BATCH_E_SLOTS)   ? "an :ok of a slot with no pending op, or an :invoke into an occupied slot"
-                    : (why & lcd::LC_BATCH_E_TRANS) ? "transition id out of range, or a state beyond key_states"
-                                                    : "key_width / key_states understate the key");
+    return batch_error(why, key);
+}
+
+// The error words of the LC_DEV_ASYNC steps in ring slots `mask` (first
+// `first`, when it is one of them), read and cleared on stream s.
+static int take_ring(Dev *c, uint32_t mask, int first, hipStream_t s) {
+    hipLaunchKernelGGL(k_take_err, dim3(1), dim3(64), 0, s, c->counters + ERR_RING, mask, c->counters + ERR_TAKEN);
+    HIPCHK(hipGetLastError());
+    int32_t *h = (int32_t *)(c->hctl + 16);
+    HIPCHK(hipMemcpyAsync(h, c->counters + ERR_TAKEN, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int q = first >= 0 && h[2 * first] ? first : -1;
+    for (int i = 0; i < 4 && q < 0; ++i)
+        if (h[2 * i]) q = i;
+    if (q < 0) return LC_OK;
+    return batch_error(h[2 * q], (int64_t)h[2 * q + 1] - 1);
 }
 
 // Segment arrays for n_keys keys (grown on demand).
@@ -1238,6 +1281,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // result download when the results go to host memory).
     const bool t0_step = K > 0 && d->t0_only && !(o.flags & LC_OPT_COUNT_PROBES);
     const bool async = t0_step && allow_async && mode != RES_HOST;
+    // an enqueued step reports a malformed batch through its own error words
+    if (async) a.err = c->counters + ERR_RING + 2 * (int)(c->async_seq % 4);
     // Key segments (device_lattice.hip): verdicts only, a batch of about one
     // key per SIMD or fewer (where each key's serial chain is exposed), and
     // quiescent points close enough for the cuts to pay (segments_pay: on
@@ -1275,8 +1320,13 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     const bool exact_spec = !a.peak && a.final_cfg && a.n_final && o.max_configs >= 16ull * 64 * 32;
     if (exact_spec && !fast) segs = segs >= 8 ? 8 : segs >= 4 ? 4 : 2;  // the exact builds
     const int waves = segs;
-    const bool spec =
-        !split && t0_step && (fast || exact_spec) && segs >= 2 && !(o.path_flags & LC_PATH_SPEC_OFF);
+    bool spec = !split && t0_step && (fast || exact_spec) && segs >= 2 && !(o.path_flags & LC_PATH_SPEC_OFF);
+    // The segments' workspaces are per key: a batch whose keys
+    // would need more than SPEC_WS_MAX_BYTES of them takes the unsegmented
+    // register tier, whose workspace is per resident wave.
+    if (spec && (uint64_t)(lcd::spec_ws_words(K, waves) + (exact_spec && !fast ? lcd::spec_fin_words(K, segs) : 0)) * 4 >
+                    SPEC_WS_MAX_BYTES)
+        spec = false;
     if (spec) {
         const size_t need = lcd::spec_ws_words(K, waves);
         if (need > c->spec_ws_words) {
@@ -1388,7 +1438,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         if (o.seg_len > 0) sa.seg_len = (uint32_t)o.seg_len;
         sa.seg_cnt = c->seg_cnt; sa.seg_end = c->seg_end; sa.seg_out = c->seg_out; sa.seg0_fev = c->seg0_fev;
         sa.work = c->seg_work; sa.rerun = c->seg_rerun; sa.rerun_init = c->seg_rerun_init; sa.ctl = c->seg_ctl;
-        sa.err = c->counters + 4; sa.valid = a.valid; sa.fail_event = a.fail_event; sa.cause = a.cause;
+        sa.err = a.err; sa.valid = a.valid; sa.fail_event = a.fail_event; sa.cause = a.cause;
         sa.rec = a.rec;
         sa.strict = a.strict;
         sa.err_base = a.err_base;
@@ -1599,7 +1649,9 @@ static int dev_wait(Dev *c, int *n_async, float *span_ms) {
     *span_ms = 0;
     if (c->n_async) HIPCHK(hipEventElapsedTime(span_ms, c->ea0, c->ea1));
     c->n_async = 0;
-    return take_error(c);
+    const int rs = take_error(c);
+    const int rr = take_ring(c, 0xFu, -1, c->stream);  // every step has finished: all slots
+    return rs ? rs : rr;
 }
 
 static void merge_stats(lc_stats &t, const lc_stats &s) {
@@ -1614,6 +1666,10 @@ static void merge_stats(lc_stats &t, const lc_stats &s) {
     t.events += s.events;
     t.t0_path = std::max(t.t0_path, s.t0_path);
     t.ev_word_bytes = std::max(t.ev_word_bytes, s.ev_word_bytes);
+    t.wgl_ms = std::max(t.wgl_ms, s.wgl_ms);
+    t.wgl_keys += s.wgl_keys;
+    t.wgl_spilled += s.wgl_spilled;
+    t.wgl_steps += s.wgl_steps;
 }
 
 // Run fn(g) for every device g of c at once (one driver thread per device
@@ -1768,18 +1824,20 @@ extern "C" int lc_wait_step(lc_ctx *c, int back) {
     for (int p = 0; p < c->n_dev; ++p) {
         Dev *d = c->dev[p];
         HIPCHK(hipSetDevice(d->device));
+        int r;
         if (back < 0 || back >= 4 || (uint64_t)back >= d->async_seq) {
             HIPCHK(hipStreamSynchronize(d->stream));  // no such step on record: everything
+            r = take_ring(d, 0xFu, -1, d->stream);
         } else {
-            HIPCHK(hipEventSynchronize(d->ring[(d->async_seq - 1 - (uint64_t)back) % 4]));
+            // Errors of the finished step surface here (include/lincheck.h):
+            // its own error words, read and cleared atomically on a stream of
+            // their own, so the later steps still running keep theirs (one 4
+            // steps later shares the slot: an error it has raised already is
+            // reported now too)
+            const int q = (int)((d->async_seq - 1 - (uint64_t)back) % 4);
+            HIPCHK(hipEventSynchronize(d->ring[q]));
+            r = take_ring(d, 1u << q, q, d->estream);
         }
-        // Errors of the finished steps surface here (include/lincheck.h): the
-        // error words are read on the copy stream, which does not wait for
-        // the later steps still running (an error one of them has already
-        // raised is reported now too, and cleared).
-        HIPCHK(hipMemcpyAsync(d->hctl + 6, d->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, d->cstream));
-        HIPCHK(hipStreamSynchronize(d->cstream));
-        const int r = take_error(d);
         if (r && !rc) rc = r;
     }
     return rc;
@@ -1819,6 +1877,7 @@ extern "C" int lc_check_batch(lc_ctx *c, const lc_batch *b, lc_result *r, lc_sta
         if (r->peak_configs) rp.peak_configs = r->peak_configs + k0;
         if (r->final_configs) rp.final_configs = r->final_configs + (size_t)k0 * mf * 2;
         if (r->n_final) rp.n_final = r->n_final + k0;
+        if (r->analyzer) rp.analyzer = r->analyzer + k0;
         return dev_search(d, d->staged, &rp, RES_HOST, false, k0, &ps[(size_t)p]);
     });
     if (std::getenv("LC_TIMING")) {

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
+import time
 import traceback
 import warnings
 from dataclasses import dataclass
@@ -390,6 +391,10 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
         # the key's sub-history could not be prepared: what check-safe makes
         # of the exception knossos would throw (etcdemo.clj:115)
         return {"valid?": "unknown", "error": packed.key_error(i) or "error"}
+    if v == N.LC_VALID:
+        # nothing to render: the device keeps final configs of invalid keys
+        # only (as gpu_checker.clj, which skips lc_report here too)
+        return {"analyzer": analyzer, "configs": [], "final-paths": [], "valid?": True}
     w = _report(packed, i, res, analyzer)
     ops: Dict[tuple, Dict] = {}
 
@@ -512,9 +517,12 @@ class Linearizable:
     # batched form, used by independent.checker
     def check_independent(self, test, history, opts, inner) -> Dict:
         from .independent import merge_results, subhistory
+        t0 = time.perf_counter()
         hist = history if isinstance(history, History) else History.from_ops(history)
         packed = Packed(hist, self.model)
+        t1 = time.perf_counter()
         res = self._dev().check(packed, peaks=False) if packed.n_keys else None
+        t2 = time.perf_counter()
         results = {}
         ops_cache = None
         for i, k in enumerate(packed.keys):
@@ -544,6 +552,10 @@ class Linearizable:
         out = merge_results(results)
         if res is not None:
             out["stats"] = res.stats
+        # where the call went (bench.py --jepsen): history -> packed SoA,
+        # lc_check_batch (H2D, search, D2H), result maps + counterexamples
+        self.last_timing = {"pack_ms": (t1 - t0) * 1e3, "search_ms": (t2 - t1) * 1e3,
+                            "shape_ms": (time.perf_counter() - t2) * 1e3}
         return out
 
 

@@ -6,7 +6,10 @@ are split over ranks (one process per GPU), each rank searches its shard,
 and the fixed-size per-key verdict records are all-gathered -- over RCCL
 (torch.distributed "nccl") on MI355X, over gloo in CPU tests.
 
-Record (int64): bits 0..7 valid+1, 8..15 cause, 16..47 failing event + 1.
+Record (int64): bits 0..7 valid+1, 8..15 cause, 16..47 failing event + 1
+(include/lincheck.h LC_REC_*; 0 = padding).  A node step (lc_check_node)
+lays the records out in blocks of `block` per rank, each rank's shard first
+in its block and the rest padded with 0, blocks in rank order.
 """
 
 from __future__ import annotations
@@ -80,3 +83,44 @@ def gather_records(keys, records, group=None):
         c = int(sizes[r].item())
         ks.append(out[r, 0, :c]); rs.append(out[r, 1, :c])
     return np.concatenate(ks), np.concatenate(rs)
+
+
+def node_block(valid, cause, fail_event, block: int) -> np.ndarray:
+    """This rank's block of node records as lc_check_node lays it out: the
+    shard's records, padded with 0 (never a record: an :unknown key, the one
+    whose valid + 1 is 0, always has a cause, LC_CAUSE_BUDGET or above)."""
+    rec = np.asarray(pack_records(valid, cause, fail_event), np.int64)
+    if rec.size > block:
+        raise ValueError(f"a shard of {rec.size} keys does not fit a block of {block}")
+    out = np.zeros(block, np.int64)
+    out[:rec.size] = rec
+    return out
+
+
+def gather_blocks(block_rec, group=None) -> np.ndarray:
+    """All-gather every rank's equal-size block in rank order: what
+    lc_check_node's ncclAllGather does over RCCL, here over the process
+    group's backend (gloo on the host)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(block_rec, dtype=np.int64))
+    world = dist.get_world_size(group)
+    out = torch.empty(world * t.numel(), dtype=torch.int64)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return out.numpy()
+
+
+def node_verdicts(node, shard_sizes: Sequence[int], block: int):
+    """Per-key (valid, cause, fail_event) of the node's key space, in key
+    order, from the gathered blocks: rank r's shard is the first
+    shard_sizes[r] records of block r.  The padding must be all 0."""
+    node = np.asarray(node, np.int64)
+    if node.size < block * len(shard_sizes):
+        raise ValueError("node records shorter than the blocks")
+    parts = []
+    for r, n in enumerate(shard_sizes):
+        blk = node[r * block:(r + 1) * block]
+        if (blk[n:] != 0).any():
+            raise ValueError(f"rank {r}'s block has records past its shard")
+        parts.append(blk[:n])
+    return unpack_records(np.concatenate(parts) if parts else np.zeros(0, np.int64))

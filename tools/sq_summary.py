@@ -17,7 +17,9 @@ for path in sys.argv[6:]:
             name = r["Kernel_Name"]
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 med = {k: statistics.median(v) for k, v in vals.items()}
-d = {"workload": workload, "kernel": name, "round": 3, "budget": int(budget), "command": cmd,
+import os
+d = {"workload": workload, "kernel": name, "round": int(os.environ.get("LC_ROUND", "4")), "budget": int(budget),
+     "command": cmd, "algorithm": os.environ.get("LC_ALGORITHM", "linear"),
      "dispatches": {k: len(v) for k, v in vals.items()}, "per_launch_median": med}
 if "SQ_INSTS_VALU" in med:
     d["sq_insts_valu_per_launch"] = med["SQ_INSTS_VALU"]
