@@ -287,7 +287,7 @@ static hipError_t grow(DevBatch::Mem &m, T *&p, size_t n) {
 
 constexpr size_t CTL_BYTES = 4 * sizeof(unsigned long long) + 16 * sizeof(int32_t);
 // Beyond CTL_BYTES in the 256-byte control block: counters[16..19] the WGL
-// step's, [24..31] the error words of the last 4 LC_DEV_ASYNC steps (slot =
+// step's, [20] the keys a competition step hands to WGL, [24..31] the error words of the last 4 LC_DEV_ASYNC steps (slot =
 // the step's sequence number mod 4: a refusal is reported by the wait for
 // that step), [32..39] where k_take_err leaves what it read.
 constexpr int ERR_RING = 24, ERR_TAKEN = 32;
@@ -1595,10 +1595,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     uint64_t wgl_keys = 0, wgl_steps = 0, wgl_spilled = 0;
     float msw = 0;
     if (competition && K > 0) {
-        int32_t *const list = c->lists, *const count = c->counters + 16;
+        int32_t *const list = c->lists, *const count = c->counters + 20;  // (run_wgl zeroes [16..19])
         HIPCHK(hipMemsetAsync(count, 0, sizeof(int32_t), c->stream));
         HIPCHK(lcd::launch_collect_budget(a.cause, (int32_t)K, list, count, c->stream));
-        int32_t *h = (int32_t *)(c->hctl + 4) + 16;
+        int32_t *h = (int32_t *)(c->hctl + 4) + 20;
         HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(h, count, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));

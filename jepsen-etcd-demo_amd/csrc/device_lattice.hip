@@ -2202,6 +2202,18 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 #define SPEC_STAMP(s, k, v)
 #endif
 
+// Checked builds only (LC_SPEC_CHECK_UNIFORM): a queue index that is not
+// wave-uniform refuses the batch instead of walking on a divergent index.
+#ifdef LC_SPEC_CHECK_UNIFORM
+#define SPEC_CHECK_UNIFORM(x)                                                        \
+    if (__any((x) != (uint32_t)__builtin_amdgcn_readfirstlane(x)) && lane == 0) {  \
+        atomicOr(&a.err[0], (int32_t)LC_BATCH_E_FIT);                              \
+        atomicMax(&a.err[1], a.err_base + key + 1);                                \
+    }
+#else
+#define SPEC_CHECK_UNIFORM(x)
+#endif
+
 // One workgroup of W waves per key (blockIdx = LPT position), the key cut into
 // up to S segments; the waves take the segments' TOP walks, then their
 // verifying runs, from two block-local queues (launched with S = W: more
@@ -2329,14 +2341,21 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     }
     __syncthreads();
     // 1. every segment from TOP (segment 0 exactly), from the block's queue.
-    // (A fixed trip count, no break: with `for (;;) ... break` the compiler
-    // built an exec-masked loop whose exit hung the wave after its first walk.)
+    // INVARIANT (both queue loops below): a fixed trip count (S, S - 1) and a
+    // queue index made wave-uniform by uni() before any branch on it.  With
+    // `for (;;) ... break` the compiler built an exec-masked loop whose exit
+    // hung the wave after its first walk (round 3).  tests/test_pack.py::
+    // test_spec_queue_loops_keep_fixed_trip_counts checks the shape of these
+    // loops in this file; the LC_SPEC_CHECK_UNIFORM build (make variant
+    // NAME=specchk VFLAGS=-DLC_SPEC_CHECK_UNIFORM) also checks at run time that
+    // the index is uniform, refusing the batch (LC_BATCH_E_FIT) if it is not.
     if (!plain) {
 #pragma unroll 1
         for (uint32_t k = 0; k < (uint32_t)S; ++k) {
             uint32_t s = 0;
             if (lane == 0) s = (uint32_t)atomicAdd(&s_next[0], 1);
             s = uni(s);
+            SPEC_CHECK_UNIFORM(s);
             if (s >= eff || uni(s_cut[s]) < 0) continue;
             const int32_t cut_i = uni(s_cut[s]);
             const uint32_t cut = (uint32_t)cut_i, end = (uint32_t)uni(s_segend[s]);
@@ -2388,6 +2407,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
             uint32_t s = 0;
             if (lane == 0) s = (uint32_t)atomicAdd(&s_next[1], 1) + 1u;
             s = uni(s);
+            SPEC_CHECK_UNIFORM(s);
             if (s >= eff || uni(s_cut[s]) < 0 || uni(s_top[s]) == -3) continue;
             SPEC_STAMP(s, 3, __builtin_amdgcn_s_memtime())
             uint32_t pw = s - 1;

@@ -422,7 +422,10 @@ __global__ __launch_bounds__(64) void k_wgl(WglArgs a) {
     if (a.err && __builtin_amdgcn_readfirstlane(*(volatile const int32_t *)a.err) != 0) return;  // refused batch
     char *slot_ws = a.ws.base + (size_t)blockIdx.x * a.ws.slot_bytes;
     const int32_t n_work = a.n_in ? *a.n_in : a.n_order;
-    for (;;) {
+    // a fixed trip count over a uni()-uniform ticket (the loop shape
+    // device_lattice.hip's k_spec had to adopt: an open `for (;;) ... break`
+    // once compiled into an exec-masked loop that never exited)
+    for (int32_t guard = 0; guard <= n_work; ++guard) {
         int32_t w = 0;
         if (__lane_id() == 0) w = atomicAdd(a.ticket, 1);
         w = (int32_t)uni((uint32_t)w);
