@@ -224,6 +224,7 @@ struct DevBatch {
     bool taggable = false;     // keys may be cut into segments (shared table, states 0..5, no op installs nil)
     bool seg_pays = false;     // sampled keys have quiescent points close enough for segments to pay
     bool validated = false;    // the host checked every event (else the device does: T0_STRICT or k_validate<true>)
+    int64_t narrow_keys = 0;   // keys with at most 24 window slots (key_width): the WGL walk's LDS cache tier
     // Device storage behind the arrays above, grown on demand: a batch that is
     // re-uploaded (a context's staging batch for lc_check_batch) keeps it, so
     // a host-to-host check allocates nothing once its sizes have been seen.
@@ -921,6 +922,9 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     d->taggable = sh.taggable;
     d->seg_pays = sh.seg_pays;
     d->validated = validated;
+    d->narrow_keys = 0;
+    if (b->key_width && c->o->algorithm != LC_ALGO_LINEAR)
+        for (int64_t k = 0; k < K; ++k) d->narrow_keys += b->key_width[k] <= 24;
     HIPCHK(hipSetDevice(c->device));
     // The event words first: their copy (the bulk of the bytes) runs while
     // the host stages the per-key arrays below.  A register-tier batch with
@@ -1123,7 +1127,19 @@ static int run_wgl(Dev *c, const DevBatch *d, const lcd::Args &a, const int32_t 
     w.ev_off = a.ev_off; w.events = a.events; w.trans = a.trans; w.trans_off = a.trans_off;
     w.key_states = a.key_states; w.key_error = a.key_error; w.table = a.table;
     w.init_state = a.init_state; w.n_trans = a.n_trans; w.budget = o.max_configs; w.max_final = o.max_final;
+    // LDS per block: the first events of the key and their slot history (8 B
+    // per event), the LDS tier of the cache (8 B per entry; narrow keys), the
+    // frame ring -- within a fourth of the CU's 160 KB when the launch has
+    // four keys per CU (one wave each), up to 64 KB otherwise
+    const int64_t per_cu = std::min<int64_t>(4, std::max<int64_t>(1, (n_hint + c->cu_count - 1) / c->cu_count));
+    const size_t lds_cap = std::min<size_t>(64u << 10, (160u << 10) / (size_t)per_cu);
     w.lds_events = (uint32_t)std::min<uint64_t>(max_ev, WGL_LDS_EVENTS);
+    w.lds_tab = d->narrow_keys > 0 ? 4096u : 0u;
+    while (lcd::wgl_lds_bytes(w.lds_events, w.lds_tab) > lds_cap) {
+        if (w.lds_tab > 1024) w.lds_tab /= 2;
+        else w.lds_events = w.lds_events > 1024 ? w.lds_events - 256 : w.lds_events / 2;
+    }
+    w.key_width = a.key_width;
     w.order = order; w.n_order = n_order; w.n_in = n_in;
     w.ticket = ctl + 1;
     w.err = a.err;

@@ -180,6 +180,8 @@ struct WglArgs {
     uint64_t budget;             // Lowe's cache holds at most this many pairs
     int32_t max_final;
     uint32_t lds_events;         // events (and their slot history) per key kept in LDS
+    uint32_t lds_tab;            // entries of the LDS tier of Lowe's cache (power of 2; 0: none)
+    const uint8_t *key_width;    // may be null (then no key takes the LDS tier)
     const int32_t *order;        // keys order[0 .. n) with n = n_in ? *n_in : n_order
     int32_t n_order;
     const int32_t *n_in;
@@ -204,6 +206,7 @@ struct WglArgs {
 WglWs wgl_layout(uint64_t budget, uint32_t max_events, uint32_t table_entries);
 size_t wgl_table_entries(uint64_t budget);
 hipError_t launch_wgl(const WglArgs &a, int grid, hipStream_t s);
+size_t wgl_lds_bytes(uint32_t lds_events, uint32_t lds_tab);  // dynamic LDS of a k_wgl block
 hipError_t launch_collect_budget(const uint8_t *cause, int32_t n, int32_t *list, int32_t *count, hipStream_t s);
 
 }  // namespace lcd

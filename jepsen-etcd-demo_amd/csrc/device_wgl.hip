@@ -51,6 +51,7 @@ namespace {
 
 constexpr uint32_t WGL_END = 0xFFFFFFFFu;  // R past the last return: every :ok passed
 constexpr uint32_t WGL_NONE = 0xFFFFFFFFu; // no :invoke (prev of a slot's first op)
+constexpr uint32_t WGL_RING = 32;          // frames of the walk's top levels kept in LDS
 
 extern "C" __device__ int lc_wgl_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ uint32_t wsetl(uint32_t v, uint32_t l, uint32_t x) {
@@ -68,11 +69,17 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_bal
 __device__ __forceinline__ bool mbit(uint64_t lo, uint64_t hi, uint32_t s) {
     return ((s < 64 ? lo : hi) >> (s & 63)) & 1ull;
 }
+// (written as selects of both words: a branch between the two references
+// made the compiler keep the pair in scratch memory, indexed by s >> 6)
 __device__ __forceinline__ void mset(uint64_t &lo, uint64_t &hi, uint32_t s) {
-    if (s < 64) lo |= 1ull << s; else hi |= 1ull << (s - 64);
+    const uint64_t b = 1ull << (s & 63u);
+    lo |= s < 64 ? b : 0ull;
+    hi |= s < 64 ? 0ull : b;
 }
 __device__ __forceinline__ void mclr(uint64_t &lo, uint64_t &hi, uint32_t s) {
-    if (s < 64) lo &= ~(1ull << s); else hi &= ~(1ull << (s - 64));
+    const uint64_t b = 1ull << (s & 63u);
+    lo &= s < 64 ? ~b : ~0ull;
+    hi &= s < 64 ? ~0ull : ~b;
 }
 
 __device__ __forceinline__ uint32_t wgl_hash(uint32_t R, uint32_t s, uint64_t lo, uint64_t hi) {
@@ -200,7 +207,55 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
         }
     };
     advance(0);
+    // ---- Lowe's cache ----
+    // Narrow keys (<= 24 window slots, < 2^24 - 1 events) start in an LDS
+    // table of 8-byte entries, X | s << 24 | R << 39 (R = n for the end of
+    // the list; all ones = empty), and move to the HBM table when it is half
+    // full; other keys use the HBM table from the start.
+    const uint32_t mask = a.ws.tab_mask;
+    const bool narrow = a.lds_tab != 0 && a.key_width && a.key_width[key] <= 24u && n < (1u << 24) - 1u;
+    bool in_lds = narrow;
+    uint64_t *const ltab = (uint64_t *)(lds + 2 * a.lds_events);
+    uint32_t *const lfr = lds + 2 * a.lds_events + 2 * a.lds_tab;  // frame ring: WGL_RING x 16 words
+    const uint32_t lmask = a.lds_tab - 1u;
+    if (in_lds) {
+        for (uint32_t i = lane; i < a.lds_tab; i += 64) ltab[i] = ~0ull;
+        __syncthreads();
+    }
+    auto lkey = [&](uint32_t R_, uint32_t s_, uint64_t x_) -> uint64_t {
+        return (x_ & 0xFFFFFFull) | (uint64_t)s_ << 24 | (uint64_t)(R_ == WGL_END ? n : R_) << 39;
+    };
+    // Move every LDS entry to the HBM table (the LDS tier is half full):
+    // lanes insert at once, a slot claimed by raising its stamp to this key's
+    // (stamps only grow, so a larger old stamp is impossible and an equal one
+    // is another entry of this key).
+    auto migrate = [&]() {
+        for (uint32_t i = lane; i < a.lds_tab; i += 64) {
+            const uint64_t e = ltab[i];
+            if (e == ~0ull) continue;
+            const uint32_t eR0 = (uint32_t)(e >> 39), es = (uint32_t)(e >> 24) & 0x7FFFu;
+            const uint32_t eR = eR0 == n ? WGL_END : eR0;
+            const uint64_t ex = e & 0xFFFFFFull;
+            uint32_t h = wgl_hash(eR, es, ex, 0) & mask;
+            for (uint32_t probe = 0; probe <= mask; ++probe) {
+                unsigned long long *g = (unsigned long long *)(tab + 2 * (size_t)h + 1) + 1;
+                const unsigned long long old = atomicMax(g, (unsigned long long)gen);
+                if (old != gen) {
+                    tab[2 * (size_t)h] = make_uint4((uint32_t)ex, 0u, 0u, 0u);
+                    uint32_t *w1 = (uint32_t *)(tab + 2 * (size_t)h + 1);
+                    w1[0] = eR;
+                    w1[1] = es;
+                    break;
+                }
+                h = (h + 1) & mask;
+            }
+        }
+        // the lines this CU's L1 may hold were written at the memory side
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        in_lds = false;
+    };
     uint32_t depth = 0, cache_n = 0, n_front = 0;
+    uint32_t ring_lo = 0;  // frames [ring_lo, depth) are in the LDS ring too
     uint32_t deepest = 0;
     bool have_deepest = false;
     uint64_t steps = 0;
@@ -208,7 +263,12 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
     bool fresh = true;       // the current node has not been probed yet
     bool have_pos = false;   // ipos0/1 are insertion slots (nothing inserted since the probe)
     uint32_t ipos0 = 0, ipos1 = 0;
-    const uint32_t mask = a.ws.tab_mask;
+    // the last step down's pair, inserted during the next probe round (its
+    // slot search shares that round's wait); pend_pos known when the probe
+    // that chose it found its slot
+    bool pend = false, pend_known = false;
+    uint32_t pend_R = 0, pend_s = 0, pend_pos = 0;
+    uint64_t pend_xlo = 0, pend_xhi = 0;
     // hard bound on the loop: every step down inserts a new pair, so a walk
     // takes at most 2 (budget + 1) steps; the bound only guards the kernel
     const uint64_t max_it = 2 * (a.budget + 2) + 4;
@@ -247,26 +307,58 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
             uint32_t kR0 = R, kR1 = R;
             if (sl0 == rs) { kR0 = R2; k0lo = x2lo; k0hi = x2hi; }
             if (sl1 == rs) { kR1 = R2; k1lo = x2lo; k1hi = x2hi; }
-            uint32_t p0 = wgl_hash(kR0, s20, k0lo, k0hi) & mask, p1 = wgl_hash(kR1, s21, k1lo, k1hi) & mask;
+            const uint32_t h0 = wgl_hash(kR0, s20, k0lo, k0hi), h1 = wgl_hash(kR1, s21, k1lo, k1hi);
             bool act0 = ok0, act1 = ok1, hit0 = false, hit1 = false;
-            for (uint32_t probe = 0; probe <= mask; ++probe) {
-                if (!ballot(act0 || act1)) break;
-                uint4 e00 = {}, e01 = {}, e10 = {}, e11 = {};
-                if (act0) { e00 = tab[2 * (size_t)p0]; e01 = tab[2 * (size_t)p0 + 1]; }
-                if (act1) { e10 = tab[2 * (size_t)p1]; e11 = tab[2 * (size_t)p1 + 1]; }
-                if (act0) {
-                    const uint64_t g = (uint64_t)e01.z | (uint64_t)e01.w << 32;
-                    if (g != gen) { act0 = false; }
-                    else if (e01.x == kR0 && e01.y == s20 && ((uint64_t)e00.x | (uint64_t)e00.y << 32) == k0lo &&
-                             ((uint64_t)e00.z | (uint64_t)e00.w << 32) == k0hi) { act0 = false; hit0 = true; }
-                    else p0 = (p0 + 1) & mask;
+            uint32_t p0, p1;
+            // the pending pair's slot search: 64 entries from its home, read
+            // beside the first probes
+            const uint32_t ph = wgl_hash(pend_R, pend_s, pend_xlo, pend_xhi);
+            bool pfree = false;
+            if (in_lds) {
+                const uint64_t q0 = lkey(kR0, s20, k0lo), q1 = lkey(kR1, s21, k1lo);
+                p0 = h0 & lmask;
+                p1 = h1 & lmask;
+                if (pend && !pend_known) pfree = ltab[(ph + lane) & lmask] == ~0ull;
+                for (uint32_t probe = 0; probe <= lmask; ++probe) {
+                    if (!ballot(act0 || act1)) break;
+                    const uint64_t e0 = act0 ? ltab[p0] : 0ull, e1 = act1 ? ltab[p1] : 0ull;
+                    if (act0) {
+                        if (e0 == ~0ull) act0 = false;
+                        else if (e0 == q0) { act0 = false; hit0 = true; }
+                        else p0 = (p0 + 1) & lmask;
+                    }
+                    if (act1) {
+                        if (e1 == ~0ull) act1 = false;
+                        else if (e1 == q1) { act1 = false; hit1 = true; }
+                        else p1 = (p1 + 1) & lmask;
+                    }
                 }
-                if (act1) {
-                    const uint64_t g = (uint64_t)e11.z | (uint64_t)e11.w << 32;
-                    if (g != gen) { act1 = false; }
-                    else if (e11.x == kR1 && e11.y == s21 && ((uint64_t)e10.x | (uint64_t)e10.y << 32) == k1lo &&
-                             ((uint64_t)e10.z | (uint64_t)e10.w << 32) == k1hi) { act1 = false; hit1 = true; }
-                    else p1 = (p1 + 1) & mask;
+            } else {
+                p0 = h0 & mask;
+                p1 = h1 & mask;
+                if (pend && !pend_known) {
+                    const uint4 pe = tab[2 * (size_t)((ph + lane) & mask) + 1];
+                    pfree = ((uint64_t)pe.z | (uint64_t)pe.w << 32) != gen;
+                }
+                for (uint32_t probe = 0; probe <= mask; ++probe) {
+                    if (!ballot(act0 || act1)) break;
+                    uint4 e00 = {}, e01 = {}, e10 = {}, e11 = {};
+                    if (act0) { e00 = tab[2 * (size_t)p0]; e01 = tab[2 * (size_t)p0 + 1]; }
+                    if (act1) { e10 = tab[2 * (size_t)p1]; e11 = tab[2 * (size_t)p1 + 1]; }
+                    if (act0) {
+                        const uint64_t g = (uint64_t)e01.z | (uint64_t)e01.w << 32;
+                        if (g != gen) { act0 = false; }
+                        else if (e01.x == kR0 && e01.y == s20 && ((uint64_t)e00.x | (uint64_t)e00.y << 32) == k0lo &&
+                                 ((uint64_t)e00.z | (uint64_t)e00.w << 32) == k0hi) { act0 = false; hit0 = true; }
+                        else p0 = (p0 + 1) & mask;
+                    }
+                    if (act1) {
+                        const uint64_t g = (uint64_t)e11.z | (uint64_t)e11.w << 32;
+                        if (g != gen) { act1 = false; }
+                        else if (e11.x == kR1 && e11.y == s21 && ((uint64_t)e10.x | (uint64_t)e10.y << 32) == k1lo &&
+                                 ((uint64_t)e10.z | (uint64_t)e10.w << 32) == k1hi) { act1 = false; hit1 = true; }
+                        else p1 = (p1 + 1) & mask;
+                    }
                 }
             }
             clo = ballot(ok0 && !hit0);
@@ -274,6 +366,44 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
             ipos0 = p0;
             ipos1 = p1;
             have_pos = true;
+            if (pend) {
+                // the pending pair goes in now (nothing looked for it: every
+                // pair probed here has the pending step's op linearized too)
+                const uint32_t tm = in_lds ? lmask : mask;
+                if (!pend_known) {
+                    const uint64_t fm = ballot(pfree);
+                    if (fm) {
+                        pend_pos = (ph + (uint32_t)__builtin_ctzll(fm)) & tm;
+                    } else {  // 64 taken in a row (a table at most half full: rare)
+                        pend_pos = ph & tm;
+                        for (uint32_t probe = 64; probe <= tm; probe += 64) {
+                            const uint32_t q = (ph + probe + lane) & tm;
+                            bool fr;
+                            if (in_lds) fr = ltab[q] == ~0ull;
+                            else {
+                                const uint4 e1 = tab[2 * (size_t)q + 1];
+                                fr = ((uint64_t)e1.z | (uint64_t)e1.w << 32) != gen;
+                            }
+                            const uint64_t f2 = ballot(fr);
+                            if (f2) { pend_pos = (ph + probe + (uint32_t)__builtin_ctzll(f2)) & tm; break; }
+                        }
+                    }
+                }
+                if (lane == 0) {
+                    if (in_lds) {
+                        ltab[pend_pos] = lkey(pend_R, pend_s, pend_xlo);
+                    } else {
+                        tab[2 * (size_t)pend_pos] = make_uint4((uint32_t)pend_xlo, (uint32_t)(pend_xlo >> 32),
+                                                               (uint32_t)pend_xhi, (uint32_t)(pend_xhi >> 32));
+                        tab[2 * (size_t)pend_pos + 1] = make_uint4(pend_R, pend_s, (uint32_t)gen, (uint32_t)(gen >> 32));
+                    }
+                }
+                pend = false;
+                // a candidate whose probe ended at that slot (then empty) has
+                // no insertion slot now: it searches again if chosen
+                if (ipos0 == pend_pos) ipos0 = WGL_NONE;
+                if (ipos1 == pend_pos) ipos1 = WGL_NONE;
+            }
         }
         if ((clo | chi) == 0) {
             // ---- no candidate left ----
@@ -296,12 +426,18 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
                 wgl_finish(a, key, LC_INVALID, LC_CAUSE_NONLIN, (int32_t)deepest, cache_n, n_front, steps);
                 return;
             }
-            // backtrack: the frame of the node above, and the slots of the
-            // :invokes the step down passed restored (newest first)
+            // backtrack: the frame of the node above (the LDS ring holds the
+            // last WGL_RING levels), and the slots of the :invokes the step
+            // down passed restored (newest first)
             --depth;
             ++steps;
-            const uint32_t *fw = (const uint32_t *)(frames + depth);
-            const uint32_t word = lane < 16 ? fw[lane] : 0u;
+            uint32_t word;
+            if (depth >= ring_lo) {
+                word = lane < 16 ? lfr[(depth % WGL_RING) * 16 + lane] : 0u;
+            } else {
+                word = lane < 16 ? ((const uint32_t *)(frames + depth))[lane] : 0u;
+                ring_lo = depth;
+            }
             const uint32_t fR = rdl(word, 0), fs = rdl(word, 1);
             const uint64_t fxlo = (uint64_t)rdl(word, 4) | (uint64_t)rdl(word, 5) << 32;
             const uint64_t fxhi = (uint64_t)rdl(word, 6) | (uint64_t)rdl(word, 7) << 32;
@@ -347,21 +483,6 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
             child_of_R();
             cR = R2; cxlo = x2lo; cxhi = x2hi;
         }
-        // insertion slot: from the probe, or the first free entry from the
-        // key's home slot (the key is known not to be there)
-        uint32_t pos;
-        if (have_pos) {
-            pos = c < 64 ? rdl(ipos0, cl) : rdl(ipos1, cl);
-        } else {
-            uint32_t home = wgl_hash(cR, sc, cxlo, cxhi) & mask;
-            pos = home;
-            for (uint32_t probe = 0; probe <= mask; probe += 64) {
-                const uint32_t q = (home + probe + lane) & mask;
-                const uint4 e1 = tab[2 * (size_t)q + 1];
-                const uint64_t free_m = ballot(((uint64_t)e1.z | (uint64_t)e1.w << 32) != gen);
-                if (free_m) { pos = (home + probe + (uint32_t)__builtin_ctzll(free_m)) & mask; break; }
-            }
-        }
         if (a.spill_at && cache_n + 1 > a.spill_at) {
             // the table would pass half full: the key is searched again with
             // a table the budget fits (no result written here)
@@ -371,18 +492,25 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
             }
             return;
         }
-        if (lane == 0) {
-            tab[2 * (size_t)pos] = make_uint4((uint32_t)cxlo, (uint32_t)(cxlo >> 32), (uint32_t)cxhi,
-                                              (uint32_t)(cxhi >> 32));
-            tab[2 * (size_t)pos + 1] = make_uint4(cR, sc, (uint32_t)gen, (uint32_t)(gen >> 32));
-        }
         ++cache_n;
         ++steps;
         if ((uint64_t)cache_n > a.budget) {
             wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_BUDGET, -1, cache_n, 0, steps);
             return;
         }
-        // the node's frame, with c no longer to try
+        // the pair joins the cache in the next probe round; at the slot this
+        // round's probe found for it, unless the round was an earlier one
+        // (the subtree may have taken it) or the table changes tier now
+        pend = true;
+        pend_R = cR; pend_s = sc; pend_xlo = cxlo; pend_xhi = cxhi;
+        pend_pos = have_pos ? (c < 64 ? rdl(ipos0, cl) : rdl(ipos1, cl)) : WGL_NONE;
+        pend_known = pend_pos != WGL_NONE;
+        if (in_lds && cache_n > a.lds_tab / 2) {
+            migrate();
+            pend_known = false;
+        }
+        have_pos = false;
+        // the node's frame, with c no longer to try (HBM, and the LDS ring)
         uint64_t nclo = clo, nchi = chi;
         mclr(nclo, nchi, c);
         if (lane < 16) {
@@ -405,8 +533,10 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
                 default: wv = 0; break;
             }
             ((uint32_t *)(frames + depth))[lane] = wv;
+            lfr[(depth % WGL_RING) * 16 + lane] = wv;
         }
         ++depth;
+        if (depth - ring_lo > WGL_RING) ring_lo = depth - WGL_RING;
         // apply the step
         s = sc;
         mset(xlo, xhi, c);
@@ -464,8 +594,12 @@ size_t wgl_table_entries(uint64_t budget) {
     return (size_t)T;
 }
 
+size_t wgl_lds_bytes(uint32_t lds_events, uint32_t lds_tab) {
+    return (size_t)lds_events * 2 * sizeof(uint32_t) + (size_t)lds_tab * 8 + (size_t)WGL_RING * 64;
+}
+
 hipError_t launch_wgl(const WglArgs &a, int grid, hipStream_t s) {
-    const size_t lds = (size_t)a.lds_events * 2 * sizeof(uint32_t);
+    const size_t lds = wgl_lds_bytes(a.lds_events, a.lds_tab);
     hipLaunchKernelGGL(k_wgl, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
 }
