@@ -375,7 +375,9 @@ typedef struct lc_opts {
 #define LC_PATH_WGL_SMALL    0x800 /* WGL: Lowe's caches start in 2^14-entry tables
                                       (keys outgrowing them are searched again with a
                                       table the budget fits)                        */
-#define LC_PATH_ALL          0xFFF
+#define LC_PATH_SPEC_NOSTAGE 0x1000 /* speculative segments: event words read from HBM
+                                      by every run, not staged in LDS once per key  */
+#define LC_PATH_ALL          0x1FFF
 
 /* lc_opts.flags */
 #define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,

@@ -1127,17 +1127,23 @@ static int run_wgl(Dev *c, const DevBatch *d, const lcd::Args &a, const int32_t 
     w.ev_off = a.ev_off; w.events = a.events; w.trans = a.trans; w.trans_off = a.trans_off;
     w.key_states = a.key_states; w.key_error = a.key_error; w.table = a.table;
     w.init_state = a.init_state; w.n_trans = a.n_trans; w.budget = o.max_configs; w.max_final = o.max_final;
-    // LDS per block: the first events of the key and their slot history (8 B
-    // per event), the LDS tier of the cache (8 B per entry; narrow keys), the
+    // LDS per block: the first events of the key, their slot history and
+    // descriptors (12 B per event), the LDS tier of the cache (8 B per entry; narrow keys), the
     // frame ring -- within a fourth of the CU's 160 KB when the launch has
     // four keys per CU (one wave each), up to 64 KB otherwise
+    // (a key whose events do not all fit is searched from HBM; more than 64
+    // KB per block when the launch has about one key per CU: C4's 10,000
+    // events take 120 KB)
     const int64_t per_cu = std::min<int64_t>(4, std::max<int64_t>(1, (n_hint + c->cu_count - 1) / c->cu_count));
-    const size_t lds_cap = std::min<size_t>(64u << 10, (160u << 10) / (size_t)per_cu);
+    size_t lds_cap = (160u << 10) / (size_t)per_cu - 1024;
+    if (!lcd::wgl_allow_lds(lds_cap)) lds_cap = std::min<size_t>(lds_cap, 64u << 10);
     w.lds_events = (uint32_t)std::min<uint64_t>(max_ev, WGL_LDS_EVENTS);
+    if (d->narrow_keys == 0) w.lds_events = (uint32_t)std::min<uint64_t>(max_ev, 3 * WGL_LDS_EVENTS / 2);
     w.lds_tab = d->narrow_keys > 0 ? 4096u : 0u;
+    w.lds_events = (w.lds_events + 1u) & ~1u;  // even: the cache tier after it is 8-byte aligned
     while (lcd::wgl_lds_bytes(w.lds_events, w.lds_tab) > lds_cap) {
         if (w.lds_tab > 1024) w.lds_tab /= 2;
-        else w.lds_events = w.lds_events > 1024 ? w.lds_events - 256 : w.lds_events / 2;
+        else w.lds_events = w.lds_events > 1024 ? w.lds_events - 256 : (w.lds_events / 2 + 1u) & ~1u;
     }
     w.key_width = a.key_width;
     w.order = order; w.n_order = n_order; w.n_in = n_in;
@@ -1472,7 +1478,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
                                 c->cu_count * 4, vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
                                 !(o.path_flags & LC_PATH_SPEC_NOPRIO),
                                 K * waves > (int64_t)c->cu_count * 16,  // more keys than one resident round
-                                exact_spec && !fast ? c->spec_fin : nullptr, c->stream));
+                                exact_spec && !fast ? c->spec_fin : nullptr,
+                                !(o.path_flags & LC_PATH_SPEC_NOSTAGE), c->stream));
         c->spec_parity ^= 1;
         if (!async) HIPCHK(hipEventRecord(c->et0, c->stream));
     } else if (K > 0 && !d->table) {

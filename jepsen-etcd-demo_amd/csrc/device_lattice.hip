@@ -39,6 +39,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cstdint>
 
@@ -80,6 +82,23 @@ template <> struct EvSrc<true> {
     const uint16_t *p;
     __device__ __forceinline__ uint32_t operator[](uint64_t j) const { return LC_EV16_WIDE(p[j]); }
     __device__ __forceinline__ EvSrc operator+(uint64_t o) const { return {p + o}; }
+};
+// A key's 16-bit event words staged in its workgroup's LDS (k_spec): the
+// first n_lds words from there, the rest from HBM.  The cut search, every
+// segment's TOP walk and its verifying run then read HBM once between them.
+struct EvStaged {
+    const uint16_t *l;  // the LDS copy
+    const uint16_t *g;  // the words in HBM
+    uint32_t n_lds;
+    __device__ __forceinline__ uint32_t operator[](uint64_t j) const {
+        uint32_t w;
+        if (j < n_lds) w = l[j];
+        else w = g[j];
+        return LC_EV16_WIDE(w);
+    }
+    __device__ __forceinline__ EvStaged operator+(uint64_t o) const {
+        return {l + o, g + o, n_lds > o ? n_lds - (uint32_t)o : 0u};
+    }
 };
 
 __device__ __forceinline__ Xfer xfer_of(uint32_t d) {
@@ -246,6 +265,8 @@ constexpr uint32_t T0_SPEC_NOPRIO = 128;
 // more keys than the chip holds at once: dispatched last, they would run
 // after the last round of keys, alone)
 constexpr uint32_t T0_SPEC_VFIRST = 256;
+// k_spec: events read from HBM, not staged in LDS (A/B)
+constexpr uint32_t T0_SPEC_NOSTAGE = 512;
 struct T0Args {
     const uint64_t *ev_off;
     const uint32_t *events;
@@ -2222,8 +2243,16 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 // verifying run and a walk's start-up).  Results go through a.full like
 // T0's; a.lat_ws holds each wave's 9-10-pending fallback workspace (global
 // memory: the workgroup's LDS workspaces are shared, NWS of them).
+// 16-bit event words of a key k_spec stages in LDS: none for 2-segment
+// workgroups (the many-key batches, where 6 KB more per block would cost
+// occupancy), 4,096 (8 KB) otherwise -- C2's keys have ~1,470.
+template <int S, bool E16>
+constexpr uint32_t spec_ev_lds() { return (E16 && S > 2) ? 4096u : 0u; }
+
 template <int S, int W, bool E16, bool EX = false>
 __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
+    constexpr uint32_t EVC = spec_ev_lds<S, E16>();
+    __shared__ uint16_t s_ev[EVC ? EVC : 1];  // the key's event words (EvStaged)
     __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
     __shared__ uint32_t s_ck[S][2][64];   // TOP run's checkpoint sets
     __shared__ uint32_t s_pend[S][8];     // ops pending at the cut ([0..5] words, [6] count)
@@ -2254,7 +2283,32 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     uint32_t *ws = a.lat_ws + ((size_t)blk * W + wv) * (3 * T0_RMEM * 64);
     const uint64_t eb = a.ev_off[key];
     const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
-    const EvSrc<E16> evp = ev_src<E16>(a) + eb;
+    // the key's words: staged in LDS (8 loads in flight per thread, then the
+    // stores; made visible by the barrier below), else read from HBM
+    uint32_t n_lds = 0;
+    if constexpr (EVC > 0) {
+        if (!(a.flags & T0_SPEC_NOSTAGE)) {
+            n_lds = nev < EVC ? nev : EVC;
+            const uint16_t *g = a.events16 + eb;
+            for (uint32_t base = 0; base < n_lds; base += 64u * W * 8u) {
+                uint16_t v[8];
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) {
+                    const uint32_t j = base + q * 64u * W + threadIdx.x;
+                    v[q] = j < n_lds ? g[j] : (uint16_t)0;
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) {
+                    const uint32_t j = base + q * 64u * W + threadIdx.x;
+                    if (j < n_lds) s_ev[j] = v[q];
+                }
+            }
+        }
+    }
+    using EvK = typename std::conditional<(EVC > 0), EvStaged, EvSrc<E16>>::type;
+    EvK evp;
+    if constexpr (EVC > 0) evp = EvStaged{s_ev, a.events16 + eb, n_lds};
+    else evp = ev_src<E16>(a) + eb;
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
     const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
@@ -2382,7 +2436,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
             const bool lost = s != 0 && np != n0;
             uint32_t *const sv = EX ? a.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS : nullptr;
             const int r = lost ? 6
-                               : spec_walk<0, NWS, EvSrc<E16>, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
+                               : spec_walk<0, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
                                                                    s_ck[s], s_ck_e[s], a.spec_ck1, a.spec_ck2, fev,
                                                                    !(a.flags & T0_SPEC_NOPRIO), sv);
             s_end[s][lane] = st.W0;
@@ -2433,7 +2487,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
                 uint32_t fev = 0;
                 uint32_t *const sv =
                     EX ? a.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS + SPEC_SAVE_WORDS : nullptr;
-                const int r = spec_walk<1, NWS, EvSrc<E16>, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
+                const int r = spec_walk<1, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
                                                                 s_ck[s], s_ck_e[s], 0, 0, fev, false, sv);
                 bool last = true;
                 for (uint32_t q = s + 1; q < eff; ++q) last = last && uni(s_cut[q]) < 0;
@@ -2546,10 +2600,11 @@ size_t spec_fin_words(int64_t n_keys, int segs) {
 }
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
-                       bool cost_cuts, bool prio, bool vfirst, uint32_t *fin, hipStream_t s) {
+                       bool cost_cuts, bool prio, bool vfirst, uint32_t *fin, bool stage, hipStream_t s) {
     T0Args t = make_t0(a, a_dev);
     t.events16 = events16;
     if (cost_cuts) t.flags |= T0_SPEC_COST;
+    if (!stage) t.flags |= T0_SPEC_NOSTAGE;
     if (vfirst && validate_blocks > 0) t.flags |= T0_SPEC_VFIRST;
     if (!prio) t.flags |= T0_SPEC_NOPRIO;
     t.lat_ws = ws;

@@ -135,7 +135,7 @@ size_t spec_ws_words(int64_t n_keys, int segs);
 size_t spec_fin_words(int64_t n_keys, int segs);
 hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, uint32_t *ws, int32_t *rr, int parity,
                        uint32_t ck1, uint32_t ck2, int rerun_grid, int validate_blocks, const uint16_t *events16,
-                       bool cost_cuts, bool prio, bool vfirst, uint32_t *fin, hipStream_t s);
+                       bool cost_cuts, bool prio, bool vfirst, uint32_t *fin, bool stage, hipStream_t s);
 uint32_t t0_max_width();   // most ops pending at once that T0 holds
 uint32_t t0_max_states();  // most register states T0 holds
 hipError_t launch_t1(const Args &a, int grid, hipStream_t s);
@@ -207,6 +207,7 @@ WglWs wgl_layout(uint64_t budget, uint32_t max_events, uint32_t table_entries);
 size_t wgl_table_entries(uint64_t budget);
 hipError_t launch_wgl(const WglArgs &a, int grid, hipStream_t s);
 size_t wgl_lds_bytes(uint32_t lds_events, uint32_t lds_tab);  // dynamic LDS of a k_wgl block
+bool wgl_allow_lds(size_t bytes);  // lets k_wgl blocks take `bytes` of dynamic LDS (false: not granted)
 hipError_t launch_collect_budget(const uint8_t *cause, int32_t n, int32_t *list, int32_t *count, hipStream_t s);
 
 }  // namespace lcd

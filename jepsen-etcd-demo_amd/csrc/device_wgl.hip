@@ -99,18 +99,40 @@ struct Frame {  // one level of the walk: the node a step down left (64 B)
     uint64_t clo, chi;   // candidates still to try: legal and not cached when the node was reached
 };
 
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
+// The block's dynamic LDS (one wave per block): from word 0, the key's first
+// E = lds_events event words, then per event the :invoke that held its slot
+// before it (prev), then per event its transition descriptor (0 for an :ok);
+// the LDS tier of the cache (lds_tab u64); the frame ring (WGL_RING x 16
+// words).  Declared here, not passed as a pointer, so its accesses are LDS
+// instructions rather than flat ones.
+extern __shared__ uint32_t wgl_lds[];
+
+// The key's events, their slot history and descriptors: all in LDS (LDS:
+// the key fits lds_events), else all in HBM.  (One source per key: written
+// as a per-event choice, the compiler merged the two loads into one flat
+// load through a selected pointer.)
+template <bool LDS>
 struct KeyIo {
     const uint32_t *gev;   // the key's event words (HBM)
-    uint32_t *gprev;       // per :invoke event: the :invoke that held its slot before (HBM part)
-    uint32_t *lev;         // LDS copies of the first lds_n of each
-    uint32_t *lprev;
-    uint32_t lds_n;
-    __device__ __forceinline__ uint32_t ev(uint32_t j) const { return uni(j < lds_n ? lev[j] : gev[j]); }
-    __device__ __forceinline__ uint32_t prev(uint32_t j) const { return uni(j < lds_n ? lprev[j] : gprev[j]); }
+    uint32_t *gprev;       // prev (HBM form)
+    const uint32_t *trans; // the key's transition descriptors (HBM form)
+    uint32_t ntr;          // entries of trans
+    uint32_t E;            // LDS layout stride (lds_events)
+    __device__ __forceinline__ uint32_t ev(uint32_t j) const { return uni(LDS ? wgl_lds[j] : gev[j]); }
+    __device__ __forceinline__ uint32_t prev(uint32_t j) const { return uni(LDS ? wgl_lds[E + j] : gprev[j]); }
     __device__ __forceinline__ void set_prev(uint32_t j, uint32_t v) const {
         if (__lane_id() == 0) {
-            if (j < lds_n) lprev[j] = v; else gprev[j] = v;
+            if (LDS) wgl_lds[E + j] = v;
+            else gprev[j] = v;
         }
+    }
+    // the descriptor of :invoke event j
+    __device__ __forceinline__ uint32_t dsc(uint32_t j) const {
+        if (LDS) return uni(wgl_lds[2 * E + j]);
+        const uint32_t t = LC_EV_TRANS(uni(gev[j]));
+        return t < ntr ? uni(trans[t]) : 0u;
     }
 };
 
@@ -132,8 +154,10 @@ __device__ __forceinline__ void wgl_finish(const WglArgs &a, int32_t key, int ve
 }
 
 // Search one key (the whole wave).  Every lane runs the same control flow:
-// every branch below is on a wave-uniform value.
-__device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t *lds, char *slot_ws) {
+// every branch below is on a wave-uniform value.  LDS: the key's events fit
+// the block's LDS (lds_events).
+template <bool LDS>
+__device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *slot_ws) {
     const uint32_t lane = __lane_id();
     const uint64_t eb = a.ev_off[key];
     const uint32_t n = (uint32_t)(a.ev_off[key + 1] - eb);
@@ -149,21 +173,26 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
     const uint64_t gen = a.gen_base | (uint64_t)(ticket + 1u);
     uint4 *tab = (uint4 *)slot_ws;  // 2 x uint4 per entry
     Frame *frames = (Frame *)(slot_ws + a.ws.off_frames);
-    KeyIo io;
+    KeyIo<LDS> io;
     io.gev = a.events + eb;
     io.gprev = (uint32_t *)(slot_ws + a.ws.off_prev);
-    io.lds_n = n < a.lds_events ? n : a.lds_events;
-    io.lev = lds;
-    io.lprev = lds + a.lds_events;
-    // Stage the events (LDS part) and look for an :invoke the window cannot
-    // hold (slot >= LC_WIDE_MAX_SLOTS): the key is then :unknown "window" at
-    // the first such :invoke, before any search (as the restatement).
+    io.ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
+    io.trans = a.trans + (io.ntr ? tb : 0u);
+    io.E = a.lds_events;
+    // Stage the events and their descriptors (LDS part), and look for an
+    // :invoke the window cannot hold (slot >= LC_WIDE_MAX_SLOTS): the key is
+    // then :unknown "window" at the first such :invoke, before any search
+    // (as the restatement).
     uint32_t win_ev = WGL_END;
     for (uint32_t base = 0; base < n; base += 64) {
         const uint32_t j = base + lane;
         uint32_t w = 0;
         if (j < n) w = io.gev[j];
-        if (j < io.lds_n) io.lev[j] = w;
+        if (LDS && j < n) {
+            const uint32_t t = LC_EV_TRANS(w);
+            wgl_lds[j] = w;
+            wgl_lds[2 * io.E + j] = (!(w & LC_EV_OK_BIT) && t < io.ntr) ? io.trans[t] : 0u;
+        }
         const bool wide = j < n && !(w & LC_EV_OK_BIT) && LC_EV_SLOT(w) >= LC_WIDE_MAX_SLOTS;
         const uint64_t m = ballot(wide);
         if (m && win_ev == WGL_END) win_ev = base + (uint32_t)__builtin_ctzll(m);
@@ -173,10 +202,6 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
         wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_WINDOW, (int32_t)win_ev, 0, 0, 0);
         return;
     }
-    auto desc_of = [&](uint32_t w) -> uint32_t {
-        const uint32_t t = LC_EV_TRANS(w);
-        return t < a.n_trans - tb ? uni(a.trans[tb + t]) : 0u;
-    };
     // per lane: the op holding window slot `lane` (occ0, dsc0) and `lane + 64`
     // (occ1, dsc1) at R -- its :invoke event and its transition descriptor
     uint32_t occ0 = WGL_NONE, occ1 = WGL_NONE, dsc0 = 0, dsc1 = 0;
@@ -199,7 +224,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
                 R = j;
                 break;
             }
-            const uint32_t d = desc_of(w);
+            const uint32_t d = io.dsc(j);
             const uint32_t l = sl & 63u;
             if (sl < 64) { io.set_prev(j, rdl(occ0, l)); occ0 = wsetl(occ0, l, j); dsc0 = wsetl(dsc0, l, d); }
             else { io.set_prev(j, rdl(occ1, l)); occ1 = wsetl(occ1, l, j); dsc1 = wsetl(dsc1, l, d); }
@@ -215,8 +240,8 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
     const uint32_t mask = a.ws.tab_mask;
     const bool narrow = a.lds_tab != 0 && a.key_width && a.key_width[key] <= 24u && n < (1u << 24) - 1u;
     bool in_lds = narrow;
-    uint64_t *const ltab = (uint64_t *)(lds + 2 * a.lds_events);
-    uint32_t *const lfr = lds + 2 * a.lds_events + 2 * a.lds_tab;  // frame ring: WGL_RING x 16 words
+    uint64_t *const ltab = (uint64_t *)(wgl_lds + 3 * a.lds_events);
+    uint32_t *const lfr = wgl_lds + 3 * a.lds_events + 2 * a.lds_tab;  // frame ring: WGL_RING x 16 words
     const uint32_t lmask = a.lds_tab - 1u;
     if (in_lds) {
         for (uint32_t i = lane; i < a.lds_tab; i += 64) ltab[i] = ~0ull;
@@ -451,7 +476,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
                     if (w & LC_EV_OK_BIT) continue;
                     const uint32_t sl = LC_EV_SLOT(w), l = sl & 63u;
                     const uint32_t pj = io.prev(j);
-                    const uint32_t d = pj == WGL_NONE ? 0u : desc_of(io.ev(pj));
+                    const uint32_t d = pj == WGL_NONE ? 0u : io.dsc(pj);
                     if (sl < 64) { occ0 = wsetl(occ0, l, pj); dsc0 = wsetl(dsc0, l, d); }
                     else { occ1 = wsetl(occ1, l, pj); dsc1 = wsetl(dsc1, l, d); }
                 }
@@ -463,12 +488,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
         // ---- step down: the candidate with the earliest :invoke ----
         const uint32_t v0 = ((clo >> lane) & 1ull) ? occ0 : WGL_NONE;
         const uint32_t v1 = ((chi >> lane) & 1ull) ? occ1 : WGL_NONE;
-        uint32_t v = v0 < v1 ? v0 : v1;
-        for (int o = 32; o >= 1; o >>= 1) {
-            const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
-            v = u < v ? u : v;
-        }
-        const uint32_t inv = uni(v);
+        const uint32_t inv = uni(__ockl_wfred_min_u32(v0 < v1 ? v0 : v1));
         const uint64_t m0 = ballot(v0 == inv), m1 = ballot(v1 == inv);
         const uint32_t c = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
         const uint32_t cl = c & 63u;
@@ -476,13 +496,6 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
         uint32_t sc = 0;
         (void)step(a.table, s, cd, sc);
         sc = uni(sc);
-        uint32_t cR = R;
-        uint64_t cxlo = xlo, cxhi = xhi;
-        mset(cxlo, cxhi, c);
-        if (c == rs) {
-            child_of_R();
-            cR = R2; cxlo = x2lo; cxhi = x2hi;
-        }
         if (a.spill_at && cache_n + 1 > a.spill_at) {
             // the table would pass half full: the key is searched again with
             // a table the budget fits (no result written here)
@@ -502,7 +515,6 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
         // round's probe found for it, unless the round was an earlier one
         // (the subtree may have taken it) or the table changes tier now
         pend = true;
-        pend_R = cR; pend_s = sc; pend_xlo = cxlo; pend_xhi = cxhi;
         pend_pos = have_pos ? (c < 64 ? rdl(ipos0, cl) : rdl(ipos1, cl)) : WGL_NONE;
         pend_known = pend_pos != WGL_NONE;
         if (in_lds && cache_n > a.lds_tab / 2) {
@@ -537,10 +549,12 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
         }
         ++depth;
         if (depth - ring_lo > WGL_RING) ring_lo = depth - WGL_RING;
-        // apply the step
+        // apply the step (taking R's op moves R: the child's R and X are then
+        // what the probe round's tentative scan found), and name the pair
         s = sc;
         mset(xlo, xhi, c);
         if (c == rs) advance(R);
+        pend_R = R; pend_s = s; pend_xlo = xlo; pend_xhi = xhi;
         fresh = true;
     }
     // not reached: the walk ends within max_it steps
@@ -548,7 +562,6 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, uint32_t
 }
 
 __global__ __launch_bounds__(64) void k_wgl(WglArgs a) {
-    extern __shared__ uint32_t lds[];
     if (a.err && __builtin_amdgcn_readfirstlane(*(volatile const int32_t *)a.err) != 0) return;  // refused batch
     char *slot_ws = a.ws.base + (size_t)blockIdx.x * a.ws.slot_bytes;
     const int32_t n_work = a.n_in ? *a.n_in : a.n_order;
@@ -560,7 +573,10 @@ __global__ __launch_bounds__(64) void k_wgl(WglArgs a) {
         if (__lane_id() == 0) w = atomicAdd(a.ticket, 1);
         w = (int32_t)uni((uint32_t)w);
         if (w >= n_work) break;
-        wgl_key(a, a.order[w], (uint32_t)w, lds, slot_ws);
+        const int32_t key = a.order[w];
+        const uint64_t nev = a.ev_off[key + 1] - a.ev_off[key];
+        if (nev <= a.lds_events) wgl_key<true>(a, key, (uint32_t)w, slot_ws);
+        else wgl_key<false>(a, key, (uint32_t)w, slot_ws);
         __syncthreads();  // the next key's staging overwrites the LDS copies
     }
 }
@@ -595,7 +611,13 @@ size_t wgl_table_entries(uint64_t budget) {
 }
 
 size_t wgl_lds_bytes(uint32_t lds_events, uint32_t lds_tab) {
-    return (size_t)lds_events * 2 * sizeof(uint32_t) + (size_t)lds_tab * 8 + (size_t)WGL_RING * 64;
+    return (size_t)lds_events * 3 * sizeof(uint32_t) + (size_t)lds_tab * 8 + (size_t)WGL_RING * 64;
+}
+
+bool wgl_allow_lds(size_t bytes) {
+    if (bytes <= (64u << 10)) return true;
+    return hipFuncSetAttribute((const void *)k_wgl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
+           hipSuccess;
 }
 
 hipError_t launch_wgl(const WglArgs &a, int grid, hipStream_t s) {
