@@ -105,6 +105,8 @@ def parse():
                     help="time independent/checker(compose{linearizable, timeline}) -> result maps")
     ap.add_argument("--keys", type=int, default=0, help="override keys (exploration only)")
     ap.add_argument("--ops", type=int, default=0, help="override ops per key (exploration only)")
+    ap.add_argument("--path-flags", type=lambda x: int(x, 0), default=0,
+                    help="lc_opts.path_flags (LC_PATH_*) of the step: pinned path choices for A/B runs only")
     return ap.parse_args()
 
 
@@ -462,7 +464,8 @@ def main():
     torch.cuda.set_device(local)
     algo = ALGORITHMS[args.algorithm]
     try:
-        dev = Device(local, budget=args.budget, comm=(rank, world, cid) if cid is not None else None, algorithm=algo)
+        dev = Device(local, budget=args.budget, comm=(rank, world, cid) if cid is not None else None, algorithm=algo,
+                     path_flags=args.path_flags)
     except Exception as e:
         if cid is None:
             raise
@@ -479,7 +482,7 @@ def main():
             print(f"[rank {rank}] RCCL unavailable ({rccl_error}); records gathered over gloo",
                   file=sys.stderr, flush=True)
             del dev
-            dev = Device(local, budget=args.budget, algorithm=algo)
+            dev = Device(local, budget=args.budget, algorithm=algo, path_flags=args.path_flags)
     n_node = block * (1 if host_gather else world)
     node_buf = np.zeros(max(n_node, 1), np.uint64)
 

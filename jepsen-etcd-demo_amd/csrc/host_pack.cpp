@@ -34,6 +34,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <chrono>
 #include <cstdio>
@@ -105,12 +107,31 @@ struct KeyOut {
     std::string msg;
 };
 
-// Pairing + event emission for one key (rows in history order).
-void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model, KeyOut &out) {
+// A3 pairing of one key (rows in history order): `ops` in invoke order and
+// `row_op[i]` = the op invoked or completed :ok/:fail at row i (-1: none).
+// false (err/msg set, ops cleared) on a sub-history complete rejects.
+bool pair_rows(const lc_history &h, const int64_t *rows, int64_t nrows, int model, std::vector<KOp> &ops,
+               std::vector<int32_t> &row_op, int &err, std::string &msg) {
+    // process -> outstanding op: a direct table over the key's process range
+    // when it is narrow (Jepsen numbers processes densely), else ProcMap
     ProcMap pm;
-    out.ops.clear();
-    out.ops.reserve((size_t)nrows / 2 + 1);
-    std::vector<int32_t> row_op((size_t)nrows, -1);  // op created/completed at this row
+    int64_t pmin = INT64_MAX, pmax = INT64_MIN;
+    for (int64_t i = 0; i < nrows; ++i) {
+        const int64_t p = h.process[rows[i]];
+        pmin = std::min(pmin, p);
+        pmax = std::max(pmax, p);
+    }
+    const bool direct = nrows > 0 && (uint64_t)(pmax - pmin) < 4096;
+    static thread_local std::vector<int32_t> dmap;
+    if (direct) dmap.assign((size_t)(pmax - pmin + 1), -1);
+    auto pfind = [&](int64_t p) -> int32_t * {
+        if (!direct) return pm.find(p);
+        int32_t &x = dmap[(size_t)(p - pmin)];
+        return x >= 0 ? &x : nullptr;
+    };
+    ops.clear();
+    ops.reserve((size_t)nrows / 2 + 1);
+    row_op.assign((size_t)nrows, -1);
     for (int64_t i = 0; i < nrows; ++i) {
         int64_t r = rows[i];
         uint8_t t = h.type[r];
@@ -118,24 +139,25 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
         if (t == LC_INVOKE) {
             if (!is_client_f(h.f[r], model)) {
                 static const char *names[] = {"cas-register", "register", "mutex", "multi-register"};
-                out.err = LC_E_UNSUPPORTED;
-                out.msg = "row " + std::to_string(r) + ": " + names[model] + " cannot step this :f";
-                out.ops.clear();
-                return;
+                err = LC_E_UNSUPPORTED;
+                msg = "row " + std::to_string(r) + ": " + names[model] + " cannot step this :f";
+                ops.clear();
+                return false;
             }
-            int32_t id = (int32_t)out.ops.size();
-            out.ops.push_back({r, -1, h.f[r], 0, h.v0[r], h.v1[r], r});
-            pm.set(p, id);
+            int32_t id = (int32_t)ops.size();
+            ops.push_back({r, -1, h.f[r], 0, h.v0[r], h.v1[r], r});
+            if (direct) dmap[(size_t)(p - pmin)] = id;
+            else pm.set(p, id);
             row_op[(size_t)i] = id;
         } else if (t == LC_OK_T || t == LC_FAIL) {
-            int32_t *pid = pm.find(p);
+            int32_t *pid = pfind(p);
             if (!pid) {
-                out.err = LC_E_INVALID;
-                out.msg = "row " + std::to_string(r) + ": process completed an operation without a prior invocation";
-                out.ops.clear();
-                return;
+                err = LC_E_INVALID;
+                msg = "row " + std::to_string(r) + ": process completed an operation without a prior invocation";
+                ops.clear();
+                return false;
             }
-            KOp &op = out.ops[(size_t)*pid];
+            KOp &op = ops[(size_t)*pid];
             if (t == LC_OK_T) {
                 op.fate = 1;
                 op.row_ret = r;
@@ -155,25 +177,34 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
             } else {
                 op.fate = 2;
             }
-            pm.erase(p);
-        } else if (t == LC_INFO) {
-            if (pm.find(p)) pm.erase(p);  // crashed: pending forever
+            if (direct) dmap[(size_t)(p - pmin)] = -1;
+            else pm.erase(p);
+        } else if (t == LC_INFO) {  // crashed: pending forever
+            if (direct) dmap[(size_t)(p - pmin)] = -1;
+            else if (pm.find(p)) pm.erase(p);
         }
     }
-    // Emit events in row order; assign window slots.
+    return true;
+}
+
+// Events of a paired key in row order, failed pairs dropped, each invoke
+// given the lowest free window slot (released at its :ok): ev[j] = slot << 24
+// | op id (invoke) or LC_EV_OK_BIT | slot << 24, ev_row[j] its row, ev_op[j]
+// (may be null) the op id (-1 for :ok).  Returns the event count (<= nrows).
+int64_t emit_events(const int64_t *rows, int64_t nrows, const std::vector<KOp> &ops,
+                    const std::vector<int32_t> &row_op, uint32_t *ev, int64_t *ev_row, int32_t *ev_op, int &width) {
     uint64_t freemask[2] = {~0ull, ~0ull};
-    std::vector<int8_t> slot_of(out.ops.size(), -1);
-    out.ev.reserve((size_t)nrows);
-    out.ev_row.reserve((size_t)nrows);
-    out.ev_op.reserve((size_t)nrows);
+    static thread_local std::vector<int8_t> slot_of;
+    slot_of.assign(ops.size(), -1);
+    int64_t ne = 0;
     int maxslot = -1;
     for (int64_t i = 0; i < nrows; ++i) {
         int32_t id = row_op[(size_t)i];
         if (id < 0) continue;
-        KOp &op = out.ops[(size_t)id];
+        const KOp &op = ops[(size_t)id];
         if (op.fate == 2) continue;  // without-failures
         int64_t r = rows[i];
-        if (h.type[r] == LC_INVOKE) {
+        if (op.row_inv == r) {  // the op's invoke
             int s;
             if (freemask[0]) s = __builtin_ctzll(freemask[0]);
             else if (freemask[1]) s = 64 + __builtin_ctzll(freemask[1]);
@@ -182,18 +213,41 @@ void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model
             int enc = s < 127 ? s : 127;  // >= 127 cannot be encoded; the search stops earlier
             slot_of[(size_t)id] = (int8_t)enc;
             maxslot = std::max(maxslot, s);
-            out.ev.push_back(((uint32_t)enc << 24) | (uint32_t)id);
-            out.ev_op.push_back(id);
+            ev[ne] = ((uint32_t)enc << 24) | (uint32_t)id;
+            if (ev_op) ev_op[ne] = id;
         } else {
             int s = slot_of[(size_t)id];
             if (s < 127) freemask[s >> 6] |= 1ull << (s & 63);
-            out.ev.push_back(LC_EV_OK_BIT | ((uint32_t)s << 24));
-            out.ev_op.push_back(-1);
+            ev[ne] = LC_EV_OK_BIT | ((uint32_t)s << 24);
+            if (ev_op) ev_op[ne] = -1;
         }
-        out.ev_row.push_back(r);
+        ev_row[ne++] = r;
     }
-    out.width = std::min(maxslot + 1, 255);
+    width = std::min(maxslot + 1, 255);
+    return ne;
 }
+
+// Pairing + event emission for one key into a KeyOut (multi-register).
+void pack_key(const lc_history &h, const int64_t *rows, int64_t nrows, int model, KeyOut &out) {
+    static thread_local std::vector<int32_t> row_op;
+    if (!pair_rows(h, rows, nrows, model, out.ops, row_op, out.err, out.msg)) return;
+    out.ev.resize((size_t)nrows);
+    out.ev_row.resize((size_t)nrows);
+    out.ev_op.resize((size_t)nrows);
+    const int64_t ne = emit_events(rows, nrows, out.ops, row_op, out.ev.data(), out.ev_row.data(), out.ev_op.data(),
+                                   out.width);
+    out.ev.resize((size_t)ne);
+    out.ev_row.resize((size_t)ne);
+    out.ev_op.resize((size_t)ne);
+}
+
+// lc_pack's per-event staging (register models), reused across calls.
+struct Staging {
+    lc::uninit_vector<uint32_t> ev;
+    lc::uninit_vector<int64_t> row;
+};
+Staging g_staging;
+std::mutex g_staging_mu;
 
 // (model/multi-register) memo of one key: registers, reachable maps, table.
 constexpr int64_t ABSENT = LC_NIL + 1;  // a register the map lacks (reserved value)
@@ -509,62 +563,8 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         lap("A2 bucketing");
 
         // ---- A3: per-key pairing, fail-drop, slots (parallel over keys) ----
-        std::vector<KeyOut> ko((size_t)K);
         unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         if (K < 64) nt = 1;
-        {
-            auto work = [&](unsigned t) {
-                std::vector<int64_t> merged;  // key rows + shared rows, in history order
-                for (int64_t k = t; k < K; k += nt) {
-                    const int64_t *kr = P->krows.data() + P->krow_off[(size_t)k];
-                    const int64_t nk = (int64_t)(P->krow_off[(size_t)k + 1] - P->krow_off[(size_t)k]);
-                    if (P->shared_rows.empty()) {
-                        pack_key(*h, kr, nk, model, ko[(size_t)k]);
-                        continue;
-                    }
-                    merged.resize((size_t)nk + P->shared_rows.size());
-                    std::merge(kr, kr + nk, P->shared_rows.begin(), P->shared_rows.end(), merged.begin());
-                    pack_key(*h, merged.data(), (int64_t)merged.size(), model, ko[(size_t)k]);
-                }
-            };
-            std::vector<std::thread> pool;
-            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
-            work(0);
-            for (auto &th : pool) th.join();
-        }
-        lap("A3 pairing (parallel)");
-        for (int64_t k = 0; k < K; ++k) {
-            KeyOut &o = ko[(size_t)k];
-            if (!o.err) continue;
-            if (P->key_error.empty()) {
-                P->key_error.assign((size_t)K, 0);
-                P->key_msg.assign((size_t)K, std::string());
-            }
-            P->key_error[(size_t)k] = 1;
-            P->key_msg[(size_t)k] = o.msg;
-            // no events: the search never looks at this key
-            std::vector<uint32_t>().swap(o.ev);
-            std::vector<int64_t>().swap(o.ev_row);
-            std::vector<int32_t>().swap(o.ev_op);
-            std::vector<KOp>().swap(o.ops);
-            o.width = 0;
-        }
-        if (model == LC_MODEL_MULTI_REGISTER) {
-            pack_multi_register(*h, n_init ? opts->init : nullptr, n_init, ko, nt, P);
-            *out = P;
-            return LC_OK;
-        }
-
-        // ---- A4/A5: register states + transition descriptors ----
-        // A state is a value some surviving write / cas could install.  Keys
-        // are independent up to the shared numbering, so: (1) per key, in
-        // parallel, its state values in order of first appearance; (2)
-        // serially, the shared state numbering (or per-key tables past 254
-        // values); (3) per key, in parallel, its distinct descriptors in order
-        // of first appearance and each invoke's index among them; (4)
-        // serially over keys (a few dozen descriptors each), their global
-        // transition ids; (5) per key, in parallel, the event words.  The ids
-        // are those of one serial pass over keys and events.
         auto par_keys = [&](const auto &fn) {
             auto work = [&](unsigned t) {
                 for (int64_t k = t; k < K; k += nt) fn(k);
@@ -574,36 +574,177 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             work(0);
             for (auto &th : pool) th.join();
         };
-        // (1) distinct state values per key, in order of first appearance
-        std::vector<std::vector<int64_t>> kvals((size_t)K);
-        par_keys([&](int64_t k) {
-            std::vector<int64_t> &vals = kvals[(size_t)k];
-            if (model == LC_MODEL_MUTEX) {  // state 1 = locked (state 0, "nil", = unlocked)
-                vals.push_back(1);
+        // key k's rows plus the shared rows, in history order
+        auto key_rows = [&](int64_t k, std::vector<int64_t> &merged, const int64_t *&rows, int64_t &nrows) {
+            const int64_t *kr = P->krows.data() + P->krow_off[(size_t)k];
+            const int64_t nk = (int64_t)(P->krow_off[(size_t)k + 1] - P->krow_off[(size_t)k]);
+            if (P->shared_rows.empty()) {
+                rows = kr;
+                nrows = nk;
                 return;
             }
-            std::unordered_map<int64_t, char> seen;
-            auto add = [&](int64_t v) {
-                if (v == LC_NIL) return;
-                if (vals.size() < 16) {
-                    if (std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
-                    return;
-                }
-                if (seen.empty())
-                    for (int64_t x : vals) seen.emplace(x, 0);
-                if (seen.emplace(v, 0).second) vals.push_back(v);
-            };
-            for (const KOp &op : ko[(size_t)k].ops) {
-                if (op.fate == 2) continue;
-                if (op.f == LC_F_WRITE) add(op.v0);
-                if (op.f == LC_F_CAS) add(op.v1);
+            merged.resize((size_t)nk + P->shared_rows.size());
+            std::merge(kr, kr + nk, P->shared_rows.begin(), P->shared_rows.end(), merged.begin());
+            rows = merged.data();
+            nrows = (int64_t)merged.size();
+        };
+        auto key_error = [&](int64_t k, const std::string &msg) {  // serial
+            if (P->key_error.empty()) {
+                P->key_error.assign((size_t)K, 0);
+                P->key_msg.assign((size_t)K, std::string());
             }
+            P->key_error[(size_t)k] = 1;  // no events: the search never looks at this key
+            P->key_msg[(size_t)k] = msg;
+        };
+        if (model == LC_MODEL_MULTI_REGISTER) {
+            std::vector<KeyOut> ko((size_t)K);
+            par_keys([&](int64_t k) {
+                static thread_local std::vector<int64_t> merged;
+                const int64_t *rows;
+                int64_t nrows;
+                key_rows(k, merged, rows, nrows);
+                pack_key(*h, rows, nrows, model, ko[(size_t)k]);
+            });
+            lap("A3 pairing (parallel)");
+            for (int64_t k = 0; k < K; ++k) {
+                KeyOut &o = ko[(size_t)k];
+                if (!o.err) continue;
+                key_error(k, o.msg);
+                std::vector<uint32_t>().swap(o.ev);
+                std::vector<int64_t>().swap(o.ev_row);
+                std::vector<int32_t>().swap(o.ev_op);
+                std::vector<KOp>().swap(o.ops);
+                o.width = 0;
+            }
+            pack_multi_register(*h, n_init ? opts->init : nullptr, n_init, ko, nt, P);
+            *out = P;
+            return LC_OK;
+        }
+
+        // ---- A3-A5 for the register models ----
+        // A state is a value some surviving write / cas could install.  Keys
+        // are independent up to the shared numbering, so: (1) per key, in
+        // parallel: pairing, its events into a flat staging array (its rows'
+        // span plus the shared rows) with each invoke's index among the key's
+        // distinct (f, value) triples in the trans field, its state values in
+        // order of first appearance; (2) serially, the shared state numbering
+        // (or per-key tables past 254 values); (3) per key, in parallel, the
+        // descriptor of each triple and the key's distinct descriptors in
+        // order of first appearance; (4) serially over keys (a few dozen
+        // descriptors each), their global transition ids; (5) per key, in
+        // parallel, the event words.  The ids are those of one serial pass
+        // over keys and events.  Per key only short lists outlive step (1).
+        struct KeyFlat {
+            std::vector<int64_t> vals;   // state values, order of first appearance
+            std::vector<int64_t> trip;   // distinct (f, v0, v1) of its invokes, order of first appearance
+            std::vector<uint32_t> ud;    // (3) its distinct descriptors; (4) their transition ids
+            std::vector<uint32_t> remap; // (3) triple -> index in ud
+            int64_t n_ev = 0;
+            int width = 0, err = 0;
+            std::string msg;
+        };
+        std::vector<KeyFlat> kf((size_t)K);
+        const uint64_t n_shared = P->shared_rows.size();
+        auto stage_off = [&](int64_t k) { return P->krow_off[(size_t)k] + (uint64_t)k * n_shared; };
+        // staging kept between calls (its pages stay mapped: no fresh page
+        // faults per call); a call that finds it taken allocates its own
+        Staging own;
+        std::unique_lock<std::mutex> lk(g_staging_mu, std::try_to_lock);
+        Staging &stg = lk.owns_lock() ? g_staging : own;
+        stg.ev.resize(std::max<uint64_t>(stage_off(K), 1));
+        stg.row.resize(std::max<uint64_t>(stage_off(K), 1));
+        uint32_t *const st_ev = stg.ev.data();
+        int64_t *const st_row = stg.row.data();
+        par_keys([&](int64_t k) {
+            static thread_local std::vector<int64_t> merged;
+            static thread_local std::vector<KOp> ops;
+            static thread_local std::vector<int32_t> row_op;
+            static thread_local std::vector<uint32_t> tix;
+            static thread_local std::vector<uint64_t> tt;
+            KeyFlat &o = kf[(size_t)k];
+            if (model == LC_MODEL_MUTEX) o.vals.push_back(1);  // state 1 = locked (state 0, "nil", = unlocked)
+            const int64_t *rows;
+            int64_t nrows;
+            key_rows(k, merged, rows, nrows);
+            if (!pair_rows(*h, rows, nrows, model, ops, row_op, o.err, o.msg)) return;
+            uint32_t *ev = st_ev + stage_off(k);
+            o.n_ev = emit_events(rows, nrows, ops, row_op, ev, st_row + stage_off(k), nullptr, o.width);
+            // (1) distinct state values
+            if (model != LC_MODEL_MUTEX) {
+                std::vector<int64_t> &vals = o.vals;
+                std::unordered_map<int64_t, char> seen;
+                auto add = [&](int64_t v) {
+                    if (v == LC_NIL) return;
+                    if (vals.size() < 16) {
+                        if (std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
+                        return;
+                    }
+                    if (seen.empty())
+                        for (int64_t x : vals) seen.emplace(x, 0);
+                    if (seen.emplace(v, 0).second) vals.push_back(v);
+                };
+                for (const KOp &op : ops) {
+                    if (op.fate == 2) continue;
+                    if (op.f == LC_F_WRITE) add(op.v0);
+                    if (op.f == LC_F_CAS) add(op.v1);
+                }
+            }
+            // each surviving op's triple index (the fields its descriptor
+            // reads), distinct triples in invoke order, through an
+            // open-addressing table of index + 1 kept under half full
+            tix.resize(ops.size());
+            size_t tmask = 255;
+            tt.assign(tmask + 1, 0);
+            auto thash = [](int64_t f, int64_t a, int64_t b) {
+                uint64_t x = (uint64_t)f * 0x9E3779B97F4A7C15ull ^ (uint64_t)a * 0xC2B2AE3D27D4EB4Full ^
+                             (uint64_t)b * 0x165667B19E3779F9ull;
+                return (size_t)(x ^ (x >> 29));
+            };
+            for (size_t q = 0; q < ops.size(); ++q) {
+                const KOp &op = ops[q];
+                if (op.fate == 2) continue;
+                const int64_t f = op.f;
+                const int64_t a = (f == LC_F_ACQUIRE || f == LC_F_RELEASE) ? 0 : op.v0;
+                const int64_t b = f == LC_F_CAS ? op.v1 : 0;
+                size_t x = thash(f, a, b) & tmask;
+                for (;; x = (x + 1) & tmask) {
+                    const uint64_t e = tt[x];
+                    if (!e) {
+                        const uint32_t ti = (uint32_t)(o.trip.size() / 3);
+                        o.trip.push_back(f);
+                        o.trip.push_back(a);
+                        o.trip.push_back(b);
+                        tt[x] = ti + 1;
+                        tix[q] = ti;
+                        if ((size_t)(ti + 1) * 2 > tmask) {  // grow
+                            tmask = tmask * 2 + 1;
+                            tt.assign(tmask + 1, 0);
+                            for (uint32_t u = 0; u <= ti; ++u) {
+                                size_t y = thash(o.trip[3 * u], o.trip[3 * u + 1], o.trip[3 * u + 2]) & tmask;
+                                while (tt[y]) y = (y + 1) & tmask;
+                                tt[y] = u + 1;
+                            }
+                        }
+                        break;
+                    }
+                    const uint32_t u = (uint32_t)e - 1;
+                    if (o.trip[3 * u] == f && o.trip[3 * u + 1] == a && o.trip[3 * u + 2] == b) {
+                        tix[q] = u;
+                        break;
+                    }
+                }
+            }
+            for (int64_t j = 0; j < o.n_ev; ++j)
+                if (!(ev[j] & LC_EV_OK_BIT)) ev[j] = (ev[j] & 0xFF000000u) | tix[ev[j] & 0xFFFFFFu];
         });
+        lap("A3/A4 (1) pairing, values, triples");
+        for (int64_t k = 0; k < K; ++k)
+            if (kf[(size_t)k].err) key_error(k, kf[(size_t)k].msg);
         // (2) one numbering shared by every key while the batch has < 255 values
         std::unordered_map<int64_t, uint32_t> gstate;
         bool shared = true;
         for (int64_t k = 0; k < K && shared; ++k)
-            for (int64_t v : kvals[(size_t)k]) {
+            for (int64_t v : kf[(size_t)k].vals) {
                 if (gstate.size() >= LC_NARROW_MAX_STATES - 1 && !gstate.count(v)) { shared = false; break; }
                 gstate.emplace(v, (uint32_t)gstate.size() + 1);
             }
@@ -616,29 +757,20 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         P->key_states.assign((size_t)K, 0);
         P->key_width.assign((size_t)K, 0);
         P->ev_off.assign((size_t)K + 1, 0);
-        for (int64_t k = 0; k < K; ++k) P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + ko[(size_t)k].ev.size();
+        for (int64_t k = 0; k < K; ++k) P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + (uint64_t)kf[(size_t)k].n_ev;
         P->events.resize((size_t)P->ev_off[(size_t)K]);
         P->ev_row.resize((size_t)P->ev_off[(size_t)K]);
-
+        lap("A4 (2) numbering, arrays");
         auto sid = [](const std::unordered_map<int64_t, uint32_t> &m, int64_t v) -> uint32_t {
             if (v == LC_NIL) return 0;
             auto it = m.find(v);
             return it == m.end() ? LC_STATE_NONE : it->second;
         };
-        auto make_desc = [&](const std::unordered_map<int64_t, uint32_t> &m, const KOp &op) -> uint32_t {
-            if (op.f == LC_F_ACQUIRE) return LC_DESC(LC_T_CAS, 0, sid(m, 1));  // unlocked -> locked
-            if (op.f == LC_F_RELEASE) return LC_DESC(LC_T_CAS, sid(m, 1), 0);  // locked -> unlocked
-            if (op.f == LC_F_READ)
-                return op.v0 == LC_NIL ? LC_DESC(LC_T_READ_ANY, 0, 0) : LC_DESC(LC_T_READ, sid(m, op.v0), 0);
-            if (op.f == LC_F_WRITE) return LC_DESC(LC_T_WRITE, 0, sid(m, op.v0));
-            return LC_DESC(LC_T_CAS, sid(m, op.v0), sid(m, op.v1));
-        };
-        // (3) per key: its state table (unshared), distinct descriptors, and
-        // each invoke event's index among them (in the word's trans field)
-        std::vector<std::vector<uint32_t>> kdesc((size_t)K);
+        // (3) per key: its state table (unshared), each triple's descriptor
+        // and the distinct descriptors in order of first appearance
         par_keys([&](int64_t k) {
-            KeyOut &o = ko[(size_t)k];
-            const std::vector<int64_t> &vals = kvals[(size_t)k];
+            KeyFlat &o = kf[(size_t)k];
+            const std::vector<int64_t> &vals = o.vals;
             std::unordered_map<int64_t, uint32_t> lstate;
             if (!shared) {
                 for (int64_t v : vals) lstate.emplace(v, lstate.size() < LC_STATE_NONE - 1 ? (uint32_t)lstate.size() + 1
@@ -646,42 +778,39 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             }
             const std::unordered_map<int64_t, uint32_t> &sm = shared ? gstate : lstate;
             P->key_states[(size_t)k] = (uint16_t)std::min<size_t>(vals.size() + 1, 65535);
-            std::vector<uint32_t> &ud = kdesc[(size_t)k];
+            const size_t nt3 = o.trip.size() / 3;
+            o.remap.resize(nt3);
             std::unordered_map<uint32_t, uint32_t> local;
-            for (size_t j = 0; j < o.ev.size(); ++j) {
-                uint32_t &w = o.ev[j];
-                if (w & LC_EV_OK_BIT) continue;
-                const uint32_t d = make_desc(sm, o.ops[(size_t)o.ev_op[j]]);
-                uint32_t li = (uint32_t)ud.size();
-                if (ud.size() < 48) {
-                    for (uint32_t q = 0; q < ud.size(); ++q)
-                        if (ud[q] == d) { li = q; break; }
-                    if (li == ud.size()) ud.push_back(d);
-                } else {
-                    if (local.empty())
-                        for (uint32_t q = 0; q < ud.size(); ++q) local.emplace(ud[q], q);
-                    auto it = local.emplace(d, (uint32_t)ud.size());
-                    li = it.first->second;
-                    if (it.second) ud.push_back(d);
-                }
-                w = (w & 0xFF000000u) | li;  // (< 2^24: the key's distinct descriptors are fewer)
+            for (size_t u = 0; u < nt3; ++u) {
+                const int64_t f = o.trip[3 * u], a = o.trip[3 * u + 1], b = o.trip[3 * u + 2];
+                uint32_t d;
+                if (f == LC_F_ACQUIRE) d = LC_DESC(LC_T_CAS, 0, sid(sm, 1));  // unlocked -> locked
+                else if (f == LC_F_RELEASE) d = LC_DESC(LC_T_CAS, sid(sm, 1), 0);  // locked -> unlocked
+                else if (f == LC_F_READ) d = a == LC_NIL ? LC_DESC(LC_T_READ_ANY, 0, 0) : LC_DESC(LC_T_READ, sid(sm, a), 0);
+                else if (f == LC_F_WRITE) d = LC_DESC(LC_T_WRITE, 0, sid(sm, a));
+                else d = LC_DESC(LC_T_CAS, sid(sm, a), sid(sm, b));
+                auto it = local.emplace(d, (uint32_t)o.ud.size());
+                if (it.second) o.ud.push_back(d);
+                o.remap[u] = it.first->second;  // (< 2^24: the key's distinct descriptors are fewer)
             }
+            std::vector<int64_t>().swap(o.trip);
             if (!shared) {  // the key's state table, kept in lstate order as state ids
                 std::vector<int64_t> tab(lstate.size() + 1, LC_NIL);
                 for (auto &kv : lstate)
                     if (kv.second != LC_STATE_NONE) tab[kv.second] = kv.first;
-                kvals[(size_t)k].swap(tab);
+                o.vals.swap(tab);
             }
         });
+        lap("A5 (3) descriptors");
         // (4) global transition ids, in key order
         std::unordered_map<uint32_t, uint32_t> gtrans;
         if (!shared) P->trans_off.assign((size_t)K, 0);
         bool too_many = false;
         for (int64_t k = 0; k < K && !too_many; ++k) {
-            std::vector<uint32_t> &ud = kdesc[(size_t)k];
+            std::vector<uint32_t> &ud = kf[(size_t)k].ud;
             if (!shared) {
                 P->state_off[(size_t)k] = P->state_vals.size();
-                P->state_vals.insert(P->state_vals.end(), kvals[(size_t)k].begin(), kvals[(size_t)k].end());
+                P->state_vals.insert(P->state_vals.end(), kf[(size_t)k].vals.begin(), kf[(size_t)k].vals.end());
                 P->trans_off[(size_t)k] = (uint32_t)P->trans.size();
                 P->trans.insert(P->trans.end(), ud.begin(), ud.end());
                 too_many = ud.size() > 0x1000000u;
@@ -699,27 +828,25 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             delete P;
             return lc::fail(LC_E_UNSUPPORTED, "lc_pack: more than 2^24 distinct operations");
         }
+        lap("A5 (4) transition ids");
         // (5) event words with transition ids, rows, widths
         par_keys([&](int64_t k) {
-            KeyOut &o = ko[(size_t)k];
-            const std::vector<uint32_t> &ud = kdesc[(size_t)k];
+            KeyFlat &o = kf[(size_t)k];
+            const uint32_t *src = st_ev + stage_off(k);
+            const int64_t *srow = st_row + stage_off(k);
             const uint64_t base = P->ev_off[(size_t)k];
-            for (size_t j = 0; j < o.ev.size(); ++j) {
-                const uint32_t w = o.ev[j];
-                P->events[base + j] = (w & LC_EV_OK_BIT) ? w : (w & 0xFF000000u) | ud[w & 0xFFFFFFu];
-                P->ev_row[base + j] = o.ev_row[j];
+            for (int64_t j = 0; j < o.n_ev; ++j) {
+                const uint32_t w = src[j];
+                P->events[base + (uint64_t)j] =
+                    (w & LC_EV_OK_BIT) ? w : (w & 0xFF000000u) | o.ud[o.remap[w & 0xFFFFFFu]];
+                P->ev_row[base + (uint64_t)j] = srow[j];
             }
             P->key_width[(size_t)k] = (uint8_t)o.width;
-            std::vector<uint32_t>().swap(o.ev);
-            std::vector<int64_t>().swap(o.ev_row);
-            std::vector<int32_t>().swap(o.ev_op);
-            std::vector<KOp>().swap(o.ops);
-            std::vector<uint32_t>().swap(kdesc[(size_t)k]);
-            std::vector<int64_t>().swap(kvals[(size_t)k]);
+            o = KeyFlat{};
         });
         if (!shared) P->state_off[(size_t)K] = P->state_vals.size();
         if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
-        lap("A4/A5 states, descriptors");
+        lap("A5 (5) event words");
         // 16-bit event words (lc_batch.events16) when every word fits: half
         // the bytes over the host link for the register tier (both passes
         // split over the threads in contiguous ranges)
