@@ -346,12 +346,13 @@ def device_for(device: int = 0, budget: int = DEFAULT_BUDGET, algorithm: int = N
 # ---------------------------------------------------------------- result maps
 def merge_valid(vals: Sequence[Any]) -> Any:
     """jepsen.checker/merge-valid: false > :unknown > true."""
-    vals = list(vals)
-    if any(v is False for v in vals):
-        return False
-    if any(v == "unknown" for v in vals):
-        return "unknown"
-    return True
+    out = True
+    for v in vals:
+        if v is False:
+            return False
+        if v is not True and v == "unknown":
+            out = "unknown"
+    return out
 
 
 def _sub_op(packed: Packed, row: int) -> Dict:
@@ -525,8 +526,18 @@ class Linearizable:
         t2 = time.perf_counter()
         results = {}
         ops_cache = None
+        # the other checkers of a compose, and whether any reads a sub-history
+        parts = [] if inner is self else list(inner.checkers.items())
+        valid = res.valid.tolist() if res is not None else []
+        names = {code: name for code, name in N.ANALYZERS.items()}
+        anl = res.analyzer.tolist() if res is not None and res.analyzer is not None else None
         for i, k in enumerate(packed.keys):
-            lin = _render_key(packed, i, res, None, _analyzer_of(res, i))
+            analyzer = names.get(anl[i], "linear") if anl is not None else "linear"
+            if valid[i] == N.LC_VALID:
+                # nothing to render (as _render_key): the common case, inline
+                lin = {"analyzer": analyzer, "configs": [], "final-paths": [], "valid?": True}
+            else:
+                lin = _render_key(packed, i, res, None, analyzer)
             if lin.get("valid?") is False and (test or {}).get("store-path"):
                 if ops_cache is None:
                     ops_cache = history if not isinstance(history, History) else history.to_ops()
@@ -538,7 +549,7 @@ class Linearizable:
             # sub-history is built only for checkers that read one)
             sub = None
             r = {}
-            for name, ch in inner.checkers.items():
+            for name, ch in parts:
                 if ch is self:
                     r[name] = lin
                     continue

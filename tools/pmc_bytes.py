@@ -24,8 +24,8 @@ import os
 d = {"workload": workload, "kernel": name, "round": rnd, "dispatches": [len(f), len(w)],
      "algorithm": os.environ.get("LC_ALGORITHM", "linear"),
      "fetch_size_kb_raw_median": fk, "write_size_kb_raw_median": wk,
-     "fetch_correction": "x2 (MI355X_MICROARCH.md section HBM: gfx950 FETCH_SIZE reports 1/2 of the bytes of a "
-                         "coalesced streaming read)",
+     "fetch_correction": "x2 (MI355X_MICROARCH.md section HBM; validated on gfx950 at 2, 4, 8 and 16 B/lane: "
+                         "profiles/r04_fetch_calib.json)",
      "bytes_per_launch": int(round((2 * fk + wk) * 1024)), "command": cmd,
      "passes": [fcsv, wcsv], "budget": int(budget)}
 json.dump(d, open(out, "w"), indent=1)
