@@ -82,24 +82,50 @@ __device__ __forceinline__ void mclr(uint64_t &lo, uint64_t &hi, uint32_t s) {
     hi &= s < 64 ? ~0ull : ~b;
 }
 
-__device__ __forceinline__ uint32_t wgl_hash(uint32_t R, uint32_t s, uint64_t lo, uint64_t hi) {
-    uint64_t h = lo * 0x9E3779B97F4A7C15ull;
-    h ^= (hi + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
-    h ^= ((uint64_t)R << 17 ^ (uint64_t)s) * 0x165667B19E3779F9ull;
-    h ^= h >> 29;
-    h *= 0xBF58476D1CE4E5B9ull;
-    h ^= h >> 32;
-    return (uint32_t)h;
+// Table hash of a pair (R, X, s).  X enters through its Zobrist code zx =
+// XOR of zob(slot) over the slots in X, which the walk keeps as X changes
+// (one XOR per slot added or dropped; a frame holds its node's code) -- a
+// candidate's child is then zx ^ zob(its slot), and a pair costs one 32-bit
+// finalizer instead of four 64-bit products per lane.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ uint32_t zob(uint32_t slot) { return fmix32(slot * 0x9E3779B9u + 0x7F4A7C15u); }
+__device__ __forceinline__ uint32_t wgl_hash(uint32_t R, uint32_t s, uint32_t zx) {
+    return fmix32(zx ^ (R * 0x27D4EB2Fu) ^ (s * 0x165667B1u + 0x61C88647u));
 }
 
 struct Frame {  // one level of the walk: the node a step down left (64 B)
-    uint32_t R, s, pad0, pad1;
+    uint32_t R, s, zx, pad1;   // zx: X's Zobrist code
     uint64_t xlo, xhi;   // linearized pending ops (slots)
     uint64_t plo, phi;   // ops pending at R (slots)
     uint64_t clo, chi;   // candidates still to try: legal and not cached when the node was reached
 };
 
 extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
+// Diagnostic build only (make variant NAME=wglprof VFLAGS=-DLC_WGL_PROF):
+// cycles of the walk's phases summed over keys (tools/wgl_prof.py reads them
+// back through lc_debug_wgl_prof): [0] staging, [1] probe rounds, [2] child
+// scans inside them, [3] backtracks, [4] steps down before advance, [5]
+// advances, [6] probe-loop iterations, [7] steps.
+#ifdef LC_WGL_PROF
+__device__ unsigned long long lc_wgl_prof[8];
+#define WP_DECL uint64_t wp[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t wp_t = __builtin_amdgcn_s_memtime();
+#define WP_MARK(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); wp[i] += t_ - wp_t; wp_t = t_; } while (0)
+#define WP_ADD(i, x) do { wp[i] += (x); } while (0)
+#define WP_DUMP() do { if (__lane_id() == 0) for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&lc_wgl_prof[q_], (unsigned long long)wp[q_]); } while (0)
+#else
+#define WP_DECL
+#define WP_MARK(i) do {} while (0)
+#define WP_ADD(i, x) do {} while (0)
+#define WP_DUMP() do {} while (0)
+#endif
 
 // The block's dynamic LDS (one wave per block): from word 0, the key's first
 // E = lds_events event words, then per event the :invoke that held its slot
@@ -159,6 +185,7 @@ __device__ __forceinline__ void wgl_finish(const WglArgs &a, int32_t key, int ve
 template <bool LDS>
 __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *slot_ws) {
     const uint32_t lane = __lane_id();
+    WP_DECL
     const uint64_t eb = a.ev_off[key];
     const uint32_t n = (uint32_t)(a.ev_off[key + 1] - eb);
     if (a.key_error && a.key_error[key]) {
@@ -206,6 +233,8 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     // (occ1, dsc1) at R -- its :invoke event and its transition descriptor
     uint32_t occ0 = WGL_NONE, occ1 = WGL_NONE, dsc0 = 0, dsc1 = 0;
     uint64_t xlo = 0, xhi = 0, plo = 0, phi = 0;
+    uint32_t zx = 0;  // Zobrist code of X
+    const uint32_t zl0 = zob(lane), zl1 = zob(lane + 64u);  // this lane's slots' codes
     uint32_t s = a.init_state;
     uint32_t R = WGL_END;
     // Move R forward from `from` (the op of R already in X): the :oks of ops
@@ -219,6 +248,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 if (mbit(xlo, xhi, sl)) {
                     mclr(xlo, xhi, sl);
                     mclr(plo, phi, sl);
+                    zx ^= zob(sl);
                     continue;
                 }
                 R = j;
@@ -261,7 +291,9 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             const uint32_t eR0 = (uint32_t)(e >> 39), es = (uint32_t)(e >> 24) & 0x7FFFu;
             const uint32_t eR = eR0 == n ? WGL_END : eR0;
             const uint64_t ex = e & 0xFFFFFFull;
-            uint32_t h = wgl_hash(eR, es, ex, 0) & mask;
+            uint32_t ez = 0;
+            for (uint64_t m = ex; m; m &= m - 1) ez ^= zob((uint32_t)__builtin_ctzll(m));
+            uint32_t h = wgl_hash(eR, es, ez) & mask;
             for (uint32_t probe = 0; probe <= mask; ++probe) {
                 unsigned long long *g = (unsigned long long *)(tab + 2 * (size_t)h + 1) + 1;
                 const unsigned long long old = atomicMax(g, (unsigned long long)gen);
@@ -292,27 +324,30 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     // slot search shares that round's wait); pend_pos known when the probe
     // that chose it found its slot
     bool pend = false, pend_known = false;
-    uint32_t pend_R = 0, pend_s = 0, pend_pos = 0;
-    uint64_t pend_xlo = 0, pend_xhi = 0;
+    // (the pending pair is always the node of the probe round that inserts
+    // it -- the node the step down reached -- so it is named by R, X, s)
+    uint32_t pend_pos = 0;
     // hard bound on the loop: every step down inserts a new pair, so a walk
     // takes at most 2 (budget + 1) steps; the bound only guards the kernel
     const uint64_t max_it = 2 * (a.budget + 2) + 4;
+    WP_MARK(0);
     for (uint64_t it = 0; it < max_it; ++it) {
         // ---- candidates of the current node ----
         const bool has_R = R != WGL_END;
         const uint32_t rs = has_R ? LC_EV_SLOT(io.ev(R)) : 0xFFu;
         // the child reached by taking the op of R: R moves on (tentatively)
-        uint32_t R2 = WGL_END;
+        uint32_t R2 = WGL_END, z2 = 0;
         uint64_t x2lo = 0, x2hi = 0;
         auto child_of_R = [&]() {
             x2lo = xlo; x2hi = xhi;
             mset(x2lo, x2hi, rs);
+            z2 = zx ^ zob(rs);
             R2 = WGL_END;
             for (uint32_t j = R; j < n; ++j) {
                 const uint32_t w = io.ev(j);
                 if (!(w & LC_EV_OK_BIT)) continue;
                 const uint32_t sl = LC_EV_SLOT(w);
-                if (mbit(x2lo, x2hi, sl)) { mclr(x2lo, x2hi, sl); continue; }
+                if (mbit(x2lo, x2hi, sl)) { mclr(x2lo, x2hi, sl); z2 ^= zob(sl); continue; }
                 R2 = j;
                 break;
             }
@@ -324,20 +359,24 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             const bool ok0 = mbit(plo, phi, sl0) && !mbit(xlo, xhi, sl0) && step(a.table, s, dsc0, s20);
             const bool ok1 = mbit(plo, phi, sl1) && !mbit(xlo, xhi, sl1) && step(a.table, s, dsc1, s21);
             const bool r_ok = has_R && ((ballot(rs < 64 ? ok0 : ok1) >> (rs & 63)) & 1ull);
-            if (r_ok) child_of_R();
+            if (r_ok) {
+                WP_MARK(1);
+                child_of_R();
+                WP_MARK(2);
+            }
             // each candidate's child key
             uint64_t k0lo = xlo, k0hi = xhi, k1lo = xlo, k1hi = xhi;
             mset(k0lo, k0hi, sl0);
             mset(k1lo, k1hi, sl1);
-            uint32_t kR0 = R, kR1 = R;
-            if (sl0 == rs) { kR0 = R2; k0lo = x2lo; k0hi = x2hi; }
-            if (sl1 == rs) { kR1 = R2; k1lo = x2lo; k1hi = x2hi; }
-            const uint32_t h0 = wgl_hash(kR0, s20, k0lo, k0hi), h1 = wgl_hash(kR1, s21, k1lo, k1hi);
+            uint32_t kR0 = R, kR1 = R, kz0 = zx ^ zl0, kz1 = zx ^ zl1;
+            if (sl0 == rs) { kR0 = R2; k0lo = x2lo; k0hi = x2hi; kz0 = z2; }
+            if (sl1 == rs) { kR1 = R2; k1lo = x2lo; k1hi = x2hi; kz1 = z2; }
+            const uint32_t h0 = wgl_hash(kR0, s20, kz0), h1 = wgl_hash(kR1, s21, kz1);
             bool act0 = ok0, act1 = ok1, hit0 = false, hit1 = false;
             uint32_t p0, p1;
             // the pending pair's slot search: 64 entries from its home, read
             // beside the first probes
-            const uint32_t ph = wgl_hash(pend_R, pend_s, pend_xlo, pend_xhi);
+            const uint32_t ph = wgl_hash(R, s, zx);
             bool pfree = false;
             if (in_lds) {
                 const uint64_t q0 = lkey(kR0, s20, k0lo), q1 = lkey(kR1, s21, k1lo);
@@ -346,6 +385,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 if (pend && !pend_known) pfree = ltab[(ph + lane) & lmask] == ~0ull;
                 for (uint32_t probe = 0; probe <= lmask; ++probe) {
                     if (!ballot(act0 || act1)) break;
+                    WP_ADD(6, 1);
                     const uint64_t e0 = act0 ? ltab[p0] : 0ull, e1 = act1 ? ltab[p1] : 0ull;
                     if (act0) {
                         if (e0 == ~0ull) act0 = false;
@@ -367,6 +407,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 }
                 for (uint32_t probe = 0; probe <= mask; ++probe) {
                     if (!ballot(act0 || act1)) break;
+                    WP_ADD(6, 1);
                     uint4 e00 = {}, e01 = {}, e10 = {}, e11 = {};
                     if (act0) { e00 = tab[2 * (size_t)p0]; e01 = tab[2 * (size_t)p0 + 1]; }
                     if (act1) { e10 = tab[2 * (size_t)p1]; e11 = tab[2 * (size_t)p1 + 1]; }
@@ -416,11 +457,11 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 }
                 if (lane == 0) {
                     if (in_lds) {
-                        ltab[pend_pos] = lkey(pend_R, pend_s, pend_xlo);
+                        ltab[pend_pos] = lkey(R, s, xlo);
                     } else {
-                        tab[2 * (size_t)pend_pos] = make_uint4((uint32_t)pend_xlo, (uint32_t)(pend_xlo >> 32),
-                                                               (uint32_t)pend_xhi, (uint32_t)(pend_xhi >> 32));
-                        tab[2 * (size_t)pend_pos + 1] = make_uint4(pend_R, pend_s, (uint32_t)gen, (uint32_t)(gen >> 32));
+                        tab[2 * (size_t)pend_pos] = make_uint4((uint32_t)xlo, (uint32_t)(xlo >> 32),
+                                                               (uint32_t)xhi, (uint32_t)(xhi >> 32));
+                        tab[2 * (size_t)pend_pos + 1] = make_uint4(R, s, (uint32_t)gen, (uint32_t)(gen >> 32));
                     }
                 }
                 pend = false;
@@ -429,10 +470,12 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 if (ipos0 == pend_pos) ipos0 = WGL_NONE;
                 if (ipos1 == pend_pos) ipos1 = WGL_NONE;
             }
+            WP_MARK(1);
         }
         if ((clo | chi) == 0) {
             // ---- no candidate left ----
             if (!has_R) {  // the walk runs off the end of the list: linearizable
+                WP_DUMP();
                 wgl_finish(a, key, LC_VALID, LC_CAUSE_NONE, -1, cache_n, 0, steps);
                 return;
             }
@@ -448,6 +491,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 if (n_front < (uint32_t)a.max_final) ++n_front;
             }
             if (depth == 0) {
+                WP_DUMP();
                 wgl_finish(a, key, LC_INVALID, LC_CAUSE_NONLIN, (int32_t)deepest, cache_n, n_front, steps);
                 return;
             }
@@ -463,7 +507,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 word = lane < 16 ? ((const uint32_t *)(frames + depth))[lane] : 0u;
                 ring_lo = depth;
             }
-            const uint32_t fR = rdl(word, 0), fs = rdl(word, 1);
+            const uint32_t fR = rdl(word, 0), fs = rdl(word, 1), fz = rdl(word, 2);
             const uint64_t fxlo = (uint64_t)rdl(word, 4) | (uint64_t)rdl(word, 5) << 32;
             const uint64_t fxhi = (uint64_t)rdl(word, 6) | (uint64_t)rdl(word, 7) << 32;
             const uint64_t fplo = (uint64_t)rdl(word, 8) | (uint64_t)rdl(word, 9) << 32;
@@ -481,8 +525,9 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     else { occ1 = wsetl(occ1, l, pj); dsc1 = wsetl(dsc1, l, d); }
                 }
             }
-            R = fR; s = fs; xlo = fxlo; xhi = fxhi; plo = fplo; phi = fphi; clo = fclo; chi = fchi;
+            R = fR; s = fs; zx = fz; xlo = fxlo; xhi = fxhi; plo = fplo; phi = fphi; clo = fclo; chi = fchi;
             have_pos = false;
+            WP_MARK(3);
             continue;
         }
         // ---- step down: the candidate with the earliest :invoke ----
@@ -503,11 +548,13 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 const int32_t i = atomicAdd(a.n_spill, 1);
                 a.spill[i] = key;
             }
+            WP_DUMP();
             return;
         }
         ++cache_n;
         ++steps;
         if ((uint64_t)cache_n > a.budget) {
+            WP_DUMP();
             wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_BUDGET, -1, cache_n, 0, steps);
             return;
         }
@@ -530,6 +577,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             switch (lane) {
                 case 0: wv = R; break;
                 case 1: wv = s; break;
+                case 2: wv = zx; break;
                 case 4: wv = (uint32_t)xlo; break;
                 case 5: wv = (uint32_t)(xlo >> 32); break;
                 case 6: wv = (uint32_t)xhi; break;
@@ -553,8 +601,11 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         // what the probe round's tentative scan found), and name the pair
         s = sc;
         mset(xlo, xhi, c);
+        zx ^= zob(c);
+        WP_ADD(7, 1);
+        WP_MARK(4);
         if (c == rs) advance(R);
-        pend_R = R; pend_s = s; pend_xlo = xlo; pend_xhi = xhi;
+        WP_MARK(5);
         fresh = true;
     }
     // not reached: the walk ends within max_it steps
@@ -589,6 +640,17 @@ __global__ void k_collect_budget(const uint8_t *cause, int32_t n, int32_t *list,
 }
 
 }  // namespace
+
+#ifdef LC_WGL_PROF
+extern "C" int lc_debug_wgl_prof(unsigned long long *host, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(lc_wgl_prof), sizeof(lc_wgl_prof), 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(lc_wgl_prof), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return (int)e;
+}
+#endif
 
 WglWs wgl_layout(uint64_t budget, uint32_t max_events, uint32_t table_entries) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
