@@ -64,7 +64,23 @@ __device__ __forceinline__ bool lds_insert(uint64_t *tab, uint32_t mask, uint64_
     return isnew;
 }
 
-__device__ __forceinline__ void write_final_narrow(const Args &a, int32_t key, const uint64_t *S, uint32_t nS) {
+// A launch's Args as the kernarg segment holds them (the kernel's first
+// parameter), through an opaque pointer: fields read through it are scalar
+// loads where they are used.  Read through the kernel's by-value parameter,
+// every field used anywhere is loaded at the kernel's entry and held in a
+// scalar register for the whole kernel; past the scalar file the compiler
+// spills them into VGPR lanes and reloads them inside the hot loops.  The
+// set tiers read their cold fields (results, work lists, per-key setup)
+// through this.
+using KArgs = const __attribute__((address_space(4))) Args;
+__device__ __forceinline__ KArgs &kargs() {
+    KArgs *p = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
+template <class A>
+__device__ __forceinline__ void write_final_narrow(A &a, int32_t key, const uint64_t *S, uint32_t nS) {
     if (!a.final_cfg) return;
     uint32_t nf = nS < (uint32_t)a.max_final ? nS : (uint32_t)a.max_final;
     for (uint32_t i = lane_id(); i < nf; i += 64) {
@@ -84,7 +100,9 @@ __device__ __forceinline__ void push_list(int32_t *list, int32_t *count, int32_t
     }
 }
 
-__device__ __forceinline__ void finish_key(const Args &a, int32_t key, int verdict, int cause,
+
+template <class A>
+__device__ __forceinline__ void finish_key(A &a, int32_t key, int verdict, int cause,
                                            int32_t fev, uint32_t peak, uint64_t probes, uint64_t nev) {
     if (lane_id() == 0) {
         a.valid[key] = (int8_t)verdict;
@@ -105,13 +123,15 @@ __device__ __forceinline__ void finish_key(const Args &a, int32_t key, int verdi
 // The batch was found malformed by the validation that ran before this
 // launch (err words, stream order): the set tiers trust validated events, so
 // over a refused batch they do nothing (the call returns LC_E_INVALID).
-__device__ __forceinline__ bool batch_refused(const Args &a) {
+template <class A>
+__device__ __forceinline__ bool batch_refused(A &a) {
     return a.err && __builtin_amdgcn_readfirstlane(*(volatile const int32_t *)a.err) != 0;
 }
 
 // Next entry of this launch's work list (dynamic: one atomic ticket per key,
 // so long keys -- listed first by the host's LPT order -- do not serialise).
-__device__ __forceinline__ int32_t next_work(const Args &a) {
+template <class A>
+__device__ __forceinline__ int32_t next_work(A &a) {
     int32_t w = 0;
     if (lane_id() == 0) w = atomicAdd(a.ticket, 1);
     return __builtin_amdgcn_readfirstlane(w);

@@ -264,7 +264,7 @@ __device__ Slot<C> slot_ptrs(const HbmWs &w, uint32_t slot) {
 }
 
 template <class C, int WG>
-__device__ void write_final_hbm(const Args &a, int32_t key, const typename C::T *S, uint32_t nS) {
+__device__ void write_final_hbm(KArgs &a, int32_t key, const typename C::T *S, uint32_t nS) {
     if (!a.final_cfg) return;
     const uint32_t nf = nS < (uint32_t)a.max_final ? nS : (uint32_t)a.max_final;
     for (uint32_t i = threadIdx.x; i < nf; i += WG) {
@@ -516,7 +516,7 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
     uint32_t nstates = a.trans_off ? (a.key_states ? (uint32_t)a.key_states[key] : 256u) : a.shared_states;
     nstates = nstates < 256u ? nstates : 256u;  // narrow configs hold 8-bit states
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
-        if (tid == 0) finish_key(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
+        if (tid == 0) finish_key(kargs(), key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
     }
     if (tid == 0) { sl.S[0][0] = C::init(a.init_state); sl.posS[0][0] = NOPOS; sh.err = 0; sh.probes = 0; }
@@ -543,8 +543,8 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
                 if (slot >= C::MAX_SLOTS) {
                     erase_all<C, WG>(w, sl, sl.posI, nIlast, sl.posS[cur], nSprev);
                     if (C::MAX_SLOTS == LC_NARROW_MAX_SLOTS) return K_WIDE;
-                    write_final_hbm<C, WG>(a, key, sl.S[cur], nS);
-                    if (tid == 0) finish_key(a, key, LC_UNKNOWN, LC_CAUSE_WINDOW, evno, peak, 0, (uint64_t)evno);
+                    write_final_hbm<C, WG>(kargs(), key, sl.S[cur], nS);
+                    if (tid == 0) finish_key(kargs(), key, LC_UNKNOWN, LC_CAUSE_WINDOW, evno, peak, 0, (uint64_t)evno);
                     return K_DONE;
                 }
                 if (slot < 64) pend0 |= 1ull << slot; else pend1 |= 1ull << (slot - 64);
@@ -613,9 +613,9 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
                 const int cause = sh.err ? LC_CAUSE_ERROR : LC_CAUSE_BUDGET;
                 const uint32_t nSn_now = sh.nSn;
                 if (!lds) erase_all<C, WG>(w, sl, sl.posI, nI, posSn, nSn_now);
-                write_final_hbm<C, WG>(a, key, S, nS);
+                write_final_hbm<C, WG>(kargs(), key, S, nS);
                 probes = block_sum<WG>(probes, &sh.probes);
-                if (tid == 0) finish_key(a, key, LC_UNKNOWN, cause, evno, peak, probes, (uint64_t)evno);
+                if (tid == 0) finish_key(kargs(), key, LC_UNKNOWN, cause, evno, peak, probes, (uint64_t)evno);
                 return K_DONE;
             }
 #ifdef LC_T3_PROF
@@ -630,10 +630,10 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
                 const int verdict = nSn_all == 0 ? LC_INVALID : LC_UNKNOWN;
                 const int cause = sh.err ? LC_CAUSE_ERROR : (nSn_all == 0 ? LC_CAUSE_NONLIN : LC_CAUSE_BUDGET);
                 if (!lds) erase_all<C, WG>(w, sl, sl.posI, nI, posSn, nSn);
-                write_final_hbm<C, WG>(a, key, S, nS);
+                write_final_hbm<C, WG>(kargs(), key, S, nS);
                 probes = block_sum<WG>(probes, &sh.probes);
                 if (tid == 0)
-                    finish_key(a, key, verdict, cause, evno, peak, probes, (uint64_t)evno + (verdict == LC_INVALID));
+                    finish_key(kargs(), key, verdict, cause, evno, peak, probes, (uint64_t)evno + (verdict == LC_INVALID));
                 return K_DONE;
             }
             nSprev = lds ? 0u : nSn;
@@ -646,9 +646,9 @@ __device__ int search_key_hbm(const Args &a, const HbmWs &w, int32_t key, Slot<C
     __syncthreads();
     T3P_PRINT();
     erase_all<C, WG>(w, sl, sl.posI, nIlast, sl.posS[cur], nSprev);
-    write_final_hbm<C, WG>(a, key, sl.S[cur], nS);
+    write_final_hbm<C, WG>(kargs(), key, sl.S[cur], nS);
     probes = block_sum<WG>(probes, &sh.probes);
-    if (tid == 0) finish_key(a, key, LC_VALID, LC_CAUSE_NONE, -1, peak, probes, e - b);
+    if (tid == 0) finish_key(kargs(), key, LC_VALID, LC_CAUSE_NONE, -1, peak, probes, e - b);
     return K_DONE;
 }
 
@@ -656,19 +656,25 @@ template <class C, int WG>
 __global__ __launch_bounds__(WG) void k_search_hbm(Args a, HbmWs w) {
     __shared__ HbmShared<C, WG> sh;
     Slot<C> sl = slot_ptrs<C>(w, blockIdx.x);
-    const int32_t n = a.n_in ? min(*a.n_in, a.list_cap) : a.n_order;
-    if (n == 0 || batch_refused(a)) return;  // empty work list / malformed batch
+    // (the work list and results through kargs(): device_common.hpp)
+    int32_t n;
+    {
+        KArgs &ka = kargs();
+        n = ka.n_in ? min(*ka.n_in, ka.list_cap) : ka.n_order;
+        if (n == 0 || batch_refused(ka)) return;  // empty work list / malformed batch
+    }
     for (;;) {
-        if (threadIdx.x == 0) sh.work = atomicAdd(a.ticket, 1);
+        if (threadIdx.x == 0) sh.work = atomicAdd(kargs().ticket, 1);
         __syncthreads();
         const int32_t wi = sh.work;
         __syncthreads();
         if (wi >= n) break;
-        const int32_t key = a.order[wi];
+        const int32_t key = kargs().order[wi];
         const int r = search_key_hbm<C, WG>(a, w, key, sl, sh);
         if (r == K_WIDE && threadIdx.x == 0) {
-            const int32_t i = atomicAdd(a.n_wide, 1);
-            a.wide[i] = key;
+            KArgs &ka = kargs();
+            const int32_t i = atomicAdd(ka.n_wide, 1);
+            ka.wide[i] = key;
         }
         __syncthreads();
     }

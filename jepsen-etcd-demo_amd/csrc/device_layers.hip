@@ -258,7 +258,8 @@ __device__ __forceinline__ void add_sums(StepCtr *c, uint32_t c1, uint32_t c2, u
     }
 }
 
-__device__ void write_final_layers(const Args &a, int32_t key, const uint64_t *S, uint32_t nS) {
+__device__ void write_final_layers(int32_t key, const uint64_t *S, uint32_t nS) {
+    KArgs &a = kargs();
     if (!a.final_cfg || threadIdx.x != 0) return;
     uint32_t nf = 0;
     for (uint32_t j = 0; j < nS && nf < (uint32_t)a.max_final; ++j) {
@@ -282,7 +283,7 @@ enum { K_OLD = 3 };  // more states than a mask holds: the config-keyed narrow t
 #define LC_DECL uint64_t lq[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; uint64_t lq_t = __builtin_amdgcn_s_memtime(), lq_0 = lq_t;
 #define LC_MARK(i) do { if (tid == 0) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); lq[i] += t_ - lq_t; lq_t = t_; } } while (0)
 #define LC_ADD(i, x) do { if (tid == 0) lq[i] += (x); } while (0)
-#define LC_DUMP() do { if (tid == 0 && a.final_cfg) { lq[9] = __builtin_amdgcn_s_memtime() - lq_0; \
+#define LC_DUMP() do { KArgs &a = kargs(); if (tid == 0 && a.final_cfg) { lq[9] = __builtin_amdgcn_s_memtime() - lq_0; \
     for (int q_ = 0; q_ < 10; ++q_) a.final_cfg[(size_t)key * a.max_final * 2 + q_] = lq[q_]; } } while (0)
 #else
 #define LC_DECL
@@ -595,21 +596,24 @@ __device__ bool step_slow(LayShared &sh, const OkCtx &o, uint32_t sb, uint32_t s
 // Search one key with the whole workgroup.
 __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, LayShared &sh) {
     const uint32_t tid = threadIdx.x;
-    const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
-    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
-    const uint32_t nstates = a.trans_off ? (a.key_states ? (uint32_t)a.key_states[key] : 256u) : a.shared_states;
-    if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
-        if (tid == 0) finish_key(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
+    // (the key's setup and results through kargs(): see device_common.hpp)
+    KArgs &ka = kargs();
+    const uint64_t b = ka.ev_off[key], e = ka.ev_off[key + 1];
+    const uint32_t tb = ka.trans_off ? ka.trans_off[key] : 0u;
+    const uint32_t nstates = ka.trans_off ? (ka.key_states ? (uint32_t)ka.key_states[key] : 256u) : ka.shared_states;
+    const uint32_t init_state = ka.init_state;
+    if (ka.key_states && ka.key_states[key] > LC_WIDE_MAX_STATES) {
+        if (tid == 0) finish_key(kargs(), key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
     }
-    if (nstates > LAY_STATES || a.init_state >= LAY_STATES) return K_OLD;
+    if (nstates > LAY_STATES || init_state >= LAY_STATES) return K_OLD;
     char *base = w.base + (size_t)blockIdx.x * w.slot_bytes;
     uint64_t *const S0 = (uint64_t *)(base + w.off_S0), *const S1 = (uint64_t *)(base + w.off_S1);
     uint64_t *const I0 = (uint64_t *)(base + w.off_I0), *const I1 = (uint64_t *)(base + w.off_I1);
     const uint64_t budget = a.budget;
     int cur = 0;
     if (tid == 0) {
-        S0[0] = (uint64_t)(1u << a.init_state) << 56;  // {(init, {})}
+        S0[0] = (uint64_t)(1u << init_state) << 56;  // {(init, {})}
         sh.err = 0;
     }
     if (tid <= NLAY) sh.soff[0][tid] = tid == 0 ? 0u : 1u;
@@ -767,11 +771,11 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
             if (over) {
                 const int cause = sh.err ? LC_CAUSE_ERROR : LC_CAUSE_BUDGET;
                 clear_slots(sh.tab, TS);
-                write_final_layers(a, key, o.S, o.so[NLAY]);
+                write_final_layers(key, o.S, o.so[NLAY]);
                 LC_DUMP();
                 if (tid == 0) {
-                    finish_key(a, key, LC_UNKNOWN, cause, evno, peak, probes, (uint64_t)evno);
-                    atomicAdd(a.stream_bytes, (unsigned long long)sbytes);
+                    finish_key(kargs(), key, LC_UNKNOWN, cause, evno, peak, probes, (uint64_t)evno);
+                    atomicAdd(kargs().stream_bytes, (unsigned long long)sbytes);
                 }
                 __syncthreads();
                 return K_DONE;
@@ -779,10 +783,10 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
             if ((int)tid >= (k < 0 ? 0 : k) && tid <= NLAY) sn[tid] = sh.n_sn;
             __syncthreads();
             if (nSncfg == 0) {
-                write_final_layers(a, key, o.S, o.so[NLAY]);
+                write_final_layers(key, o.S, o.so[NLAY]);
                 if (tid == 0) {
-                    finish_key(a, key, LC_INVALID, LC_CAUSE_NONLIN, evno, peak, probes, (uint64_t)evno + 1);
-                    atomicAdd(a.stream_bytes, (unsigned long long)sbytes);
+                    finish_key(kargs(), key, LC_INVALID, LC_CAUSE_NONLIN, evno, peak, probes, (uint64_t)evno + 1);
+                    atomicAdd(kargs().stream_bytes, (unsigned long long)sbytes);
                 }
                 __syncthreads();
                 return K_DONE;
@@ -794,10 +798,10 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
         }
     }
     __syncthreads();
-    write_final_layers(a, key, cur ? S1 : S0, sh.soff[cur][NLAY]);
+    write_final_layers(key, cur ? S1 : S0, sh.soff[cur][NLAY]);
     if (tid == 0) {
-        finish_key(a, key, LC_VALID, LC_CAUSE_NONE, -1, peak, probes, e - b);
-        atomicAdd(a.stream_bytes, (unsigned long long)sbytes);
+        finish_key(kargs(), key, LC_VALID, LC_CAUSE_NONE, -1, peak, probes, e - b);
+        atomicAdd(kargs().stream_bytes, (unsigned long long)sbytes);
     }
     __syncthreads();
     return K_DONE;
@@ -805,21 +809,28 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
 
 __global__ __launch_bounds__(LWG) void k_search_layers(Args a, LayWs w) {
     __shared__ LayShared sh;
-    const int32_t n = a.n_in ? min(*a.n_in, a.list_cap) : a.n_order;
-    if (n == 0 || batch_refused(a)) return;  // empty work list / malformed batch
+    // (the work list and results through kargs(); the walk keeps only the
+    // fields it reads per event from the by-value parameter)
+    int32_t n;
+    {
+        KArgs &ka = kargs();
+        n = ka.n_in ? min(*ka.n_in, ka.list_cap) : ka.n_order;
+        if (n == 0 || batch_refused(ka)) return;  // empty work list / malformed batch
+    }
     clear_slots(sh.tab, TS);
     for (;;) {
-        if (threadIdx.x == 0) sh.work = atomicAdd(a.ticket, 1);
+        if (threadIdx.x == 0) sh.work = atomicAdd(kargs().ticket, 1);
         __syncthreads();
         const int32_t wi = sh.work;
         __syncthreads();
         if (wi >= n) break;
-        const int32_t key = a.order[wi];
+        const int32_t key = kargs().order[wi];
         const int r = search_key_layers(a, w, key, sh);
         if (threadIdx.x == 0 && (r == K_WIDE || r == K_OLD)) {
-            int32_t *list = r == K_WIDE ? a.wide : a.spill, *count = r == K_WIDE ? a.n_wide : a.n_spill;
+            KArgs &ka = kargs();
+            int32_t *list = r == K_WIDE ? ka.wide : ka.spill, *count = r == K_WIDE ? ka.n_wide : ka.n_spill;
             const int32_t i = atomicAdd(count, 1);
-            if (i < a.list_cap) list[i] = key;
+            if (i < ka.list_cap) list[i] = key;
         }
         __syncthreads();
     }

@@ -59,11 +59,11 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
     const uint64_t b = a.ev_off[key], e = a.ev_off[key + 1];
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     if (a.key_error && a.key_error[key]) {  // a table-model batch starts here, not in T0
-        finish_key(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
+        finish_key(kargs(), key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
         return K_DONE;
     }
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
-        finish_key(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
+        finish_key(kargs(), key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 1, 0, 0);
         return K_DONE;
     }
     // Too many register states for an 8-bit state field: wide configs.  A
@@ -179,8 +179,8 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
             if (overflow) {
                 if (verdict == LC_UNKNOWN) {
                     fev = (int32_t)(base + i - b);
-                    write_final_narrow(a, key, S, nS);
-                    finish_key(a, key, verdict, cause, fev, peak, probes, base + i - b);
+                    write_final_narrow(kargs(), key, S, nS);
+                    finish_key(kargs(), key, verdict, cause, fev, peak, probes, base + i - b);
                     return K_DONE;
                 }
                 return K_SPILL;
@@ -207,14 +207,14 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
             nI_last = nI < CAP_I ? nI : CAP_I;
             if (nSn == 0) {
                 verdict = LC_INVALID; cause = LC_CAUSE_NONLIN; fev = (int32_t)(base + i - b);
-                write_final_narrow(a, key, S, nS);
-                finish_key(a, key, verdict, cause, fev, peak, probes, base + i + 1 - b);
+                write_final_narrow(kargs(), key, S, nS);
+                finish_key(kargs(), key, verdict, cause, fev, peak, probes, base + i + 1 - b);
                 return K_DONE;
             }
             if (nSn > a.budget) {
                 verdict = LC_UNKNOWN; cause = LC_CAUSE_BUDGET; fev = (int32_t)(base + i - b);
-                write_final_narrow(a, key, S, nS);
-                finish_key(a, key, verdict, cause, fev, peak, probes, base + i - b);
+                write_final_narrow(kargs(), key, S, nS);
+                finish_key(kargs(), key, verdict, cause, fev, peak, probes, base + i - b);
                 return K_DONE;
             }
             if (nSn > CAP_S) return K_SPILL;
@@ -227,21 +227,29 @@ __device__ int search_key_lds(const Args &a, int32_t key, LdsTier<CAP_S, CAP_I> 
             pending &= ~pbit;
         }
     }
-    write_final_narrow(a, key, t.S[cur], nS);
-    finish_key(a, key, LC_VALID, LC_CAUSE_NONE, -1, peak, probes, e - b);
+    write_final_narrow(kargs(), key, t.S[cur], nS);
+    finish_key(kargs(), key, LC_VALID, LC_CAUSE_NONE, -1, peak, probes, e - b);
     return K_DONE;
 }
 
 template <int CAP_S, int CAP_I>
 __global__ __launch_bounds__(64) void k_search_lds(Args a) {
     __shared__ LdsTier<CAP_S, CAP_I> t;
-    const int32_t n = a.n_in ? min(*a.n_in, a.list_cap) : a.n_order;
-    if (n == 0 || batch_refused(a)) return;  // empty work list / malformed batch: no ticket traffic
-    for (int32_t w = next_work(a); w < n; w = next_work(a)) {
-        const int32_t key = a.order[w];
+    // (the work list and results through kargs(): device_common.hpp)
+    int32_t n;
+    {
+        KArgs &ka = kargs();
+        n = ka.n_in ? min(*ka.n_in, ka.list_cap) : ka.n_order;
+        if (n == 0 || batch_refused(ka)) return;  // empty work list / malformed batch: no ticket traffic
+    }
+    for (int32_t w = next_work(kargs()); w < n; w = next_work(kargs())) {
+        const int32_t key = kargs().order[w];
         const int r = search_key_lds<CAP_S, CAP_I>(a, key, t);
-        if (r == K_SPILL) push_list(a.spill, a.n_spill, key, a.list_cap);
-        else if (r == K_WIDE) push_list(a.wide, a.n_wide, key, a.list_cap);
+        if (r == K_SPILL || r == K_WIDE) {
+            KArgs &ka = kargs();
+            if (r == K_SPILL) push_list(ka.spill, ka.n_spill, key, ka.list_cap);
+            else push_list(ka.wide, ka.n_wide, key, ka.list_cap);
+        }
         __syncthreads();
     }
 }

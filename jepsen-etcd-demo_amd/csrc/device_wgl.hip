@@ -100,12 +100,24 @@ __device__ __forceinline__ uint32_t wgl_hash(uint32_t R, uint32_t s, uint32_t zx
     return fmix32(zx ^ (R * 0x27D4EB2Fu) ^ (s * 0x165667B1u + 0x61C88647u));
 }
 
-struct Frame {  // one level of the walk: the node a step down left (64 B)
-    uint32_t R, s, zx, pad1;   // zx: X's Zobrist code
-    uint64_t xlo, xhi;   // linearized pending ops (slots)
-    uint64_t plo, phi;   // ops pending at R (slots)
-    uint64_t clo, chi;   // candidates still to try: legal and not cached when the node was reached
+// The walk's slot sets live one bit per lane: lane l holds, for window slots
+// l and l + 64, whether each is linearized (X: bits 0, 1), pending at R (P:
+// bits 2, 3) and still a candidate of the node (C: bits 4, 5) -- one VGPR
+// instead of six 64-bit scalar pairs, which left the kernel's scalar file
+// spilling into VGPR lanes on every step.
+constexpr uint32_t LM_X = 0, LM_P = 2, LM_C = 4;
+__device__ __forceinline__ uint32_t lm_bit(uint32_t lm, uint32_t sl, uint32_t base) {  // sl uniform
+    return (rdl(lm, sl & 63u) >> (base + (sl >> 6))) & 1u;
+}
+__device__ __forceinline__ uint32_t lm_one(uint32_t sl, uint32_t base) {  // this lane's bit of slot sl
+    return __lane_id() == (sl & 63u) ? 1u << (base + (sl >> 6)) : 0u;
+}
+
+struct Frame {  // one level of the walk: the node a step down left (80 B)
+    uint32_t R, s, zx, pad;  // zx: X's Zobrist code
+    uint8_t m[64];           // per lane: its X / P / C bits (C: candidates still to try)
 };
+constexpr uint32_t FRAME_WORDS = sizeof(Frame) / 4;
 
 extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
 
@@ -162,8 +174,22 @@ struct KeyIo {
     }
 };
 
-__device__ __forceinline__ void wgl_finish(const WglArgs &a, int32_t key, int verdict, int cause, int32_t fev,
+// The launch's arguments as the kernarg segment holds them, through an
+// opaque pointer: the result arrays and lists the walk touches once per key
+// are loaded where they are used.  (Read through the kernel's by-value
+// parameter, every field used anywhere is loaded at the kernel's entry and
+// stays in a scalar register for the whole walk: the scalar file spilled into
+// VGPR lanes, and every step paid the reloads.)
+using KargWgl = const __attribute__((address_space(4))) WglArgs;
+__device__ __forceinline__ KargWgl &cold_args() {
+    KargWgl *p = (KargWgl *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
+__device__ __forceinline__ void wgl_finish(const WglArgs &, int32_t key, int verdict, int cause, int32_t fev,
                                            uint32_t cache_n, uint32_t n_front, uint64_t steps) {
+    KargWgl &a = cold_args();
     if (__lane_id() == 0) {
         a.valid[key] = (int8_t)verdict;
         a.cause[key] = (uint8_t)cause;
@@ -232,7 +258,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     // per lane: the op holding window slot `lane` (occ0, dsc0) and `lane + 64`
     // (occ1, dsc1) at R -- its :invoke event and its transition descriptor
     uint32_t occ0 = WGL_NONE, occ1 = WGL_NONE, dsc0 = 0, dsc1 = 0;
-    uint64_t xlo = 0, xhi = 0, plo = 0, phi = 0;
+    uint32_t lm = 0;  // this lane's X / P / C bits
     uint32_t zx = 0;  // Zobrist code of X
     const uint32_t zl0 = zob(lane), zl1 = zob(lane + 64u);  // this lane's slots' codes
     uint32_t s = a.init_state;
@@ -245,9 +271,8 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             const uint32_t w = io.ev(j);
             const uint32_t sl = LC_EV_SLOT(w);
             if (w & LC_EV_OK_BIT) {
-                if (mbit(xlo, xhi, sl)) {
-                    mclr(xlo, xhi, sl);
-                    mclr(plo, phi, sl);
+                if (lm_bit(lm, sl, LM_X)) {
+                    lm &= ~(lm_one(sl, LM_X) | lm_one(sl, LM_P));
                     zx ^= zob(sl);
                     continue;
                 }
@@ -258,7 +283,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             const uint32_t l = sl & 63u;
             if (sl < 64) { io.set_prev(j, rdl(occ0, l)); occ0 = wsetl(occ0, l, j); dsc0 = wsetl(dsc0, l, d); }
             else { io.set_prev(j, rdl(occ1, l)); occ1 = wsetl(occ1, l, j); dsc1 = wsetl(dsc1, l, d); }
-            mset(plo, phi, sl);
+            lm |= lm_one(sl, LM_P);
         }
     };
     advance(0);
@@ -271,7 +296,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     const bool narrow = a.lds_tab != 0 && a.key_width && a.key_width[key] <= 24u && n < (1u << 24) - 1u;
     bool in_lds = narrow;
     uint64_t *const ltab = (uint64_t *)(wgl_lds + 3 * a.lds_events);
-    uint32_t *const lfr = wgl_lds + 3 * a.lds_events + 2 * a.lds_tab;  // frame ring: WGL_RING x 16 words
+    uint32_t *const lfr = wgl_lds + 3 * a.lds_events + 2 * a.lds_tab;  // frame ring: WGL_RING frames
     const uint32_t lmask = a.lds_tab - 1u;
     if (in_lds) {
         for (uint32_t i = lane; i < a.lds_tab; i += 64) ltab[i] = ~0ull;
@@ -313,19 +338,16 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     };
     uint32_t depth = 0, cache_n = 0, n_front = 0;
     uint32_t ring_lo = 0;  // frames [ring_lo, depth) are in the LDS ring too
-    uint32_t deepest = 0;
-    bool have_deepest = false;
+    uint32_t deepest = WGL_NONE;  // the deepest return entry the walk got stuck on
     uint64_t steps = 0;
-    uint64_t clo = 0, chi = 0;
     bool fresh = true;       // the current node has not been probed yet
     bool have_pos = false;   // ipos0/1 are insertion slots (nothing inserted since the probe)
     uint32_t ipos0 = 0, ipos1 = 0;
     // the last step down's pair, inserted during the next probe round (its
     // slot search shares that round's wait); pend_pos known when the probe
-    // that chose it found its slot
+    // that chose it found its slot.  The pending pair is always the node of
+    // the probe round that inserts it (the node the step down reached).
     bool pend = false, pend_known = false;
-    // (the pending pair is always the node of the probe round that inserts
-    // it -- the node the step down reached -- so it is named by R, X, s)
     uint32_t pend_pos = 0;
     // hard bound on the loop: every step down inserts a new pair, so a walk
     // takes at most 2 (budget + 1) steps; the bound only guards the kernel
@@ -335,33 +357,33 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         // ---- candidates of the current node ----
         const bool has_R = R != WGL_END;
         const uint32_t rs = has_R ? LC_EV_SLOT(io.ev(R)) : 0xFFu;
-        // the child reached by taking the op of R: R moves on (tentatively)
-        uint32_t R2 = WGL_END, z2 = 0;
-        uint64_t x2lo = 0, x2hi = 0;
-        auto child_of_R = [&]() {
-            x2lo = xlo; x2hi = xhi;
-            mset(x2lo, x2hi, rs);
-            z2 = zx ^ zob(rs);
-            R2 = WGL_END;
-            for (uint32_t j = R; j < n; ++j) {
-                const uint32_t w = io.ev(j);
-                if (!(w & LC_EV_OK_BIT)) continue;
-                const uint32_t sl = LC_EV_SLOT(w);
-                if (mbit(x2lo, x2hi, sl)) { mclr(x2lo, x2hi, sl); z2 ^= zob(sl); continue; }
-                R2 = j;
-                break;
-            }
-        };
         if (fresh) {
             fresh = false;
+            // X as two scalar words (keys, the pending pair)
+            const uint64_t xlo = ballot(lm & 1u), xhi = ballot(lm & 2u);
             const uint32_t sl0 = lane, sl1 = lane + 64u;
             uint32_t s20 = 0, s21 = 0;
-            const bool ok0 = mbit(plo, phi, sl0) && !mbit(xlo, xhi, sl0) && step(a.table, s, dsc0, s20);
-            const bool ok1 = mbit(plo, phi, sl1) && !mbit(xlo, xhi, sl1) && step(a.table, s, dsc1, s21);
+            const bool ok0 = (lm & 4u) && !(lm & 1u) && step(a.table, s, dsc0, s20);
+            const bool ok1 = (lm & 8u) && !(lm & 2u) && step(a.table, s, dsc1, s21);
             const bool r_ok = has_R && ((ballot(rs < 64 ? ok0 : ok1) >> (rs & 63)) & 1ull);
+            // the child reached by taking the op of R: R moves on (tentatively;
+            // the ops returning in between leave X)
+            uint32_t R2 = WGL_END, z2 = 0;
+            uint64_t x2lo = 0, x2hi = 0;
             if (r_ok) {
                 WP_MARK(1);
-                child_of_R();
+                uint32_t x2 = (lm & 3u) | lm_one(rs, LM_X);
+                z2 = zx ^ zob(rs);
+                for (uint32_t j = R; j < n; ++j) {
+                    const uint32_t w = io.ev(j);
+                    if (!(w & LC_EV_OK_BIT)) continue;
+                    const uint32_t sl = LC_EV_SLOT(w);
+                    if (lm_bit(x2, sl, LM_X)) { x2 &= ~lm_one(sl, LM_X); z2 ^= zob(sl); continue; }
+                    R2 = j;
+                    break;
+                }
+                x2lo = ballot(x2 & 1u);
+                x2hi = ballot(x2 & 2u);
                 WP_MARK(2);
             }
             // each candidate's child key
@@ -427,8 +449,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     }
                 }
             }
-            clo = ballot(ok0 && !hit0);
-            chi = ballot(ok1 && !hit1);
+            lm = (lm & 0xFu) | (ok0 && !hit0 ? 1u << LM_C : 0u) | (ok1 && !hit1 ? 2u << LM_C : 0u);
             ipos0 = p0;
             ipos1 = p1;
             have_pos = true;
@@ -472,7 +493,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             }
             WP_MARK(1);
         }
-        if ((clo | chi) == 0) {
+        if (!ballot((lm >> LM_C) & 3u)) {
             // ---- no candidate left ----
             if (!has_R) {  // the walk runs off the end of the list: linearizable
                 WP_DUMP();
@@ -481,14 +502,18 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             }
             // stuck on the return entry R: the deepest such entries' nodes
             // are the frontier (the first max_final of them, in walk order)
-            if (!have_deepest || R >= deepest) {
-                if (!have_deepest || R > deepest) { deepest = R; n_front = 0; have_deepest = true; }
-                if (a.final_cfg && n_front < (uint32_t)a.max_final && lane == 0) {
-                    uint64_t *f = a.final_cfg + ((size_t)key * a.max_final + n_front) * 2;
-                    f[0] = xlo;
-                    f[1] = (xhi & ((1ull << 48) - 1)) | (uint64_t)s << 48;
+            if (deepest == WGL_NONE || R >= deepest) {
+                if (deepest == WGL_NONE || R > deepest) { deepest = R; n_front = 0; }
+                KargWgl &ca = cold_args();
+                if (ca.final_cfg && n_front < (uint32_t)ca.max_final) {
+                    const uint64_t xlo = ballot(lm & 1u), xhi = ballot(lm & 2u);
+                    if (lane == 0) {
+                        uint64_t *f = ca.final_cfg + ((size_t)key * ca.max_final + n_front) * 2;
+                        f[0] = xlo;
+                        f[1] = (xhi & ((1ull << 48) - 1)) | (uint64_t)s << 48;
+                    }
                 }
-                if (n_front < (uint32_t)a.max_final) ++n_front;
+                if (n_front < (uint32_t)ca.max_final) ++n_front;
             }
             if (depth == 0) {
                 WP_DUMP();
@@ -500,20 +525,18 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             // down passed restored (newest first)
             --depth;
             ++steps;
-            uint32_t word;
+            uint32_t word, mbyte;
             if (depth >= ring_lo) {
-                word = lane < 16 ? lfr[(depth % WGL_RING) * 16 + lane] : 0u;
-            } else {
-                word = lane < 16 ? ((const uint32_t *)(frames + depth))[lane] : 0u;
+                const uint32_t *f = lfr + (depth % WGL_RING) * FRAME_WORDS;
+                word = lane < 4 ? f[lane] : 0u;
+                mbyte = ((const uint8_t *)(f + 4))[lane];
+            } else {  // (the bytes as words here: loads the compiler cannot merge with the LDS ones above)
+                const uint32_t *f = (const uint32_t *)(frames + depth);
+                word = lane < 4 ? f[lane] : 0u;
+                mbyte = (f[4 + (lane >> 2)] >> (8u * (lane & 3u))) & 0xFFu;
                 ring_lo = depth;
             }
             const uint32_t fR = rdl(word, 0), fs = rdl(word, 1), fz = rdl(word, 2);
-            const uint64_t fxlo = (uint64_t)rdl(word, 4) | (uint64_t)rdl(word, 5) << 32;
-            const uint64_t fxhi = (uint64_t)rdl(word, 6) | (uint64_t)rdl(word, 7) << 32;
-            const uint64_t fplo = (uint64_t)rdl(word, 8) | (uint64_t)rdl(word, 9) << 32;
-            const uint64_t fphi = (uint64_t)rdl(word, 10) | (uint64_t)rdl(word, 11) << 32;
-            const uint64_t fclo = (uint64_t)rdl(word, 12) | (uint64_t)rdl(word, 13) << 32;
-            const uint64_t fchi = (uint64_t)rdl(word, 14) | (uint64_t)rdl(word, 15) << 32;
             if (fR != R) {
                 for (uint32_t j = (R == WGL_END ? n : R); j-- > fR;) {
                     const uint32_t w = io.ev(j);
@@ -525,14 +548,14 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     else { occ1 = wsetl(occ1, l, pj); dsc1 = wsetl(dsc1, l, d); }
                 }
             }
-            R = fR; s = fs; zx = fz; xlo = fxlo; xhi = fxhi; plo = fplo; phi = fphi; clo = fclo; chi = fchi;
+            R = fR; s = fs; zx = fz; lm = mbyte;
             have_pos = false;
             WP_MARK(3);
             continue;
         }
         // ---- step down: the candidate with the earliest :invoke ----
-        const uint32_t v0 = ((clo >> lane) & 1ull) ? occ0 : WGL_NONE;
-        const uint32_t v1 = ((chi >> lane) & 1ull) ? occ1 : WGL_NONE;
+        const uint32_t v0 = (lm & (1u << LM_C)) ? occ0 : WGL_NONE;
+        const uint32_t v1 = (lm & (2u << LM_C)) ? occ1 : WGL_NONE;
         const uint32_t inv = uni(__ockl_wfred_min_u32(v0 < v1 ? v0 : v1));
         const uint64_t m0 = ballot(v0 == inv), m1 = ballot(v1 == inv);
         const uint32_t c = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
@@ -545,8 +568,9 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             // the table would pass half full: the key is searched again with
             // a table the budget fits (no result written here)
             if (lane == 0) {
-                const int32_t i = atomicAdd(a.n_spill, 1);
-                a.spill[i] = key;
+                KargWgl &ca = cold_args();
+                const int32_t i = atomicAdd(ca.n_spill, 1);
+                ca.spill[i] = key;
             }
             WP_DUMP();
             return;
@@ -570,37 +594,21 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         }
         have_pos = false;
         // the node's frame, with c no longer to try (HBM, and the LDS ring)
-        uint64_t nclo = clo, nchi = chi;
-        mclr(nclo, nchi, c);
-        if (lane < 16) {
-            uint32_t wv;
-            switch (lane) {
-                case 0: wv = R; break;
-                case 1: wv = s; break;
-                case 2: wv = zx; break;
-                case 4: wv = (uint32_t)xlo; break;
-                case 5: wv = (uint32_t)(xlo >> 32); break;
-                case 6: wv = (uint32_t)xhi; break;
-                case 7: wv = (uint32_t)(xhi >> 32); break;
-                case 8: wv = (uint32_t)plo; break;
-                case 9: wv = (uint32_t)(plo >> 32); break;
-                case 10: wv = (uint32_t)phi; break;
-                case 11: wv = (uint32_t)(phi >> 32); break;
-                case 12: wv = (uint32_t)nclo; break;
-                case 13: wv = (uint32_t)(nclo >> 32); break;
-                case 14: wv = (uint32_t)nchi; break;
-                case 15: wv = (uint32_t)(nchi >> 32); break;
-                default: wv = 0; break;
-            }
-            ((uint32_t *)(frames + depth))[lane] = wv;
-            lfr[(depth % WGL_RING) * 16 + lane] = wv;
+        {
+            const uint32_t wv = lane == 0 ? R : lane == 1 ? s : zx;
+            const uint8_t mb = (uint8_t)(lm & ~lm_one(c, LM_C));
+            uint32_t *f = (uint32_t *)(frames + depth);
+            uint32_t *fl = lfr + (depth % WGL_RING) * FRAME_WORDS;
+            if (lane < 3) { f[lane] = wv; fl[lane] = wv; }
+            ((uint8_t *)(f + 4))[lane] = mb;
+            ((uint8_t *)(fl + 4))[lane] = mb;
         }
         ++depth;
         if (depth - ring_lo > WGL_RING) ring_lo = depth - WGL_RING;
         // apply the step (taking R's op moves R: the child's R and X are then
-        // what the probe round's tentative scan found), and name the pair
+        // what the probe round's tentative scan found)
         s = sc;
-        mset(xlo, xhi, c);
+        lm |= lm_one(c, LM_X);
         zx ^= zob(c);
         WP_ADD(7, 1);
         WP_MARK(4);
@@ -673,7 +681,7 @@ size_t wgl_table_entries(uint64_t budget) {
 }
 
 size_t wgl_lds_bytes(uint32_t lds_events, uint32_t lds_tab) {
-    return (size_t)lds_events * 3 * sizeof(uint32_t) + (size_t)lds_tab * 8 + (size_t)WGL_RING * 64;
+    return (size_t)lds_events * 3 * sizeof(uint32_t) + (size_t)lds_tab * 8 + (size_t)WGL_RING * sizeof(Frame);
 }
 
 bool wgl_allow_lds(size_t bytes) {

@@ -121,12 +121,14 @@ bool pair_rows(const lc_history &h, const int64_t *rows, int64_t nrows, int mode
         pmin = std::min(pmin, p);
         pmax = std::max(pmax, p);
     }
-    const bool direct = nrows > 0 && (uint64_t)(pmax - pmin) < 4096;
+    // (differences in unsigned arithmetic: process ids span all of int64)
+    auto off = [&](int64_t p) { return (size_t)((uint64_t)p - (uint64_t)pmin); };
+    const bool direct = nrows > 0 && (uint64_t)pmax - (uint64_t)pmin < 4096;
     static thread_local std::vector<int32_t> dmap;
-    if (direct) dmap.assign((size_t)(pmax - pmin + 1), -1);
+    if (direct) dmap.assign(off(pmax) + 1, -1);
     auto pfind = [&](int64_t p) -> int32_t * {
         if (!direct) return pm.find(p);
-        int32_t &x = dmap[(size_t)(p - pmin)];
+        int32_t &x = dmap[off(p)];
         return x >= 0 ? &x : nullptr;
     };
     ops.clear();
@@ -146,7 +148,7 @@ bool pair_rows(const lc_history &h, const int64_t *rows, int64_t nrows, int mode
             }
             int32_t id = (int32_t)ops.size();
             ops.push_back({r, -1, h.f[r], 0, h.v0[r], h.v1[r], r});
-            if (direct) dmap[(size_t)(p - pmin)] = id;
+            if (direct) dmap[off(p)] = id;
             else pm.set(p, id);
             row_op[(size_t)i] = id;
         } else if (t == LC_OK_T || t == LC_FAIL) {
@@ -177,10 +179,10 @@ bool pair_rows(const lc_history &h, const int64_t *rows, int64_t nrows, int mode
             } else {
                 op.fate = 2;
             }
-            if (direct) dmap[(size_t)(p - pmin)] = -1;
+            if (direct) dmap[off(p)] = -1;
             else pm.erase(p);
         } else if (t == LC_INFO) {  // crashed: pending forever
-            if (direct) dmap[(size_t)(p - pmin)] = -1;
+            if (direct) dmap[off(p)] = -1;
             else if (pm.find(p)) pm.erase(p);
         }
     }
