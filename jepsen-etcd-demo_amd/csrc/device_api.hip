@@ -621,8 +621,10 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         o.spec_segs != 8)
         return lc::fail(LC_E_INVALID, "lc_create: spec_segs must be 0, 2, 3, 4, 6 or 8");
     if (o.seg_len < 0) return lc::fail(LC_E_INVALID, "lc_create: seg_len < 0");
-    if (o.spec_ck && (((uint32_t)o.spec_ck & 0xFFFFu) == 0 || ((uint32_t)o.spec_ck >> 16) == 0))
-        return lc::fail(LC_E_INVALID, "lc_create: spec_ck must be 0 or (ck1 + 1) | (ck2 + 1) << 16");
+    // (a negative word is a ck2 past 32766 that wrapped: refused, not read as another value)
+    if (o.spec_ck < 0 || (o.spec_ck && (((uint32_t)o.spec_ck & 0xFFFFu) == 0 || ((uint32_t)o.spec_ck >> 16) == 0)))
+        return lc::fail(LC_E_INVALID, "lc_create: spec_ck must be 0 or (ck1 + 1) | (ck2 + 1) << 16, "
+                                      "0 <= ck1 <= 65534, 0 <= ck2 <= 32766");
     if (o.n_devices < 0 || o.n_devices > MAX_DEV)
         return lc::fail(LC_E_INVALID, "lc_create: n_devices must be 0..%d", MAX_DEV);
     if (o.comm_size < 0 || o.comm_size > 4096 || (o.comm_size > 1 && (o.comm_rank < 0 || o.comm_rank >= o.comm_size)))

@@ -172,6 +172,33 @@ struct KeyIo {
         const uint32_t t = LC_EV_TRANS(uni(gev[j]));
         return t < ntr ? uni(trans[t]) : 0u;
     }
+    // per lane: event j (this lane's; j < n) and, for an :invoke, its descriptor
+    __device__ __forceinline__ uint32_t ev_at(uint32_t j) const { return LDS ? wgl_lds[j] : gev[j]; }
+    __device__ __forceinline__ uint32_t dsc_at(uint32_t j, uint32_t w) const {
+        if (LDS) return wgl_lds[2 * E + j];
+        const uint32_t t = LC_EV_TRANS(w);
+        return (!(w & LC_EV_OK_BIT) && t < ntr) ? trans[t] : 0u;
+    }
+};
+
+// A forward scan's window of 64 events (and their descriptors) held one per
+// lane: a scan reads each event with a v_readlane instead of waiting on one
+// memory round trip per event.
+template <bool LDS, bool DSC>
+struct EvWindow {
+    const KeyIo<LDS> &io;
+    uint32_t n, base = 0xFFFFFFFFu, w = 0, d = 0;
+    __device__ __forceinline__ EvWindow(const KeyIo<LDS> &io_, uint32_t n_) : io(io_), n(n_) {}
+    __device__ __forceinline__ void at(uint32_t j) {  // j uniform, < n
+        if (j - base >= 64u) {
+            base = j;
+            const uint32_t k = j + __lane_id();
+            w = k < n ? io.ev_at(k) : 0u;
+            if (DSC) d = k < n ? io.dsc_at(k, w) : 0u;
+        }
+    }
+    __device__ __forceinline__ uint32_t ev(uint32_t j) { at(j); return rdl(w, j - base); }
+    __device__ __forceinline__ uint32_t dsc(uint32_t j) { at(j); return rdl(d, j - base); }
 };
 
 // The launch's arguments as the kernarg segment holds them, through an
@@ -267,8 +294,9 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     // in X leave X and the pending set; the :invokes passed become pending.
     auto advance = [&](uint32_t from) {
         R = WGL_END;
+        EvWindow<LDS, true> win(io, n);
         for (uint32_t j = from; j < n; ++j) {
-            const uint32_t w = io.ev(j);
+            const uint32_t w = win.ev(j);
             const uint32_t sl = LC_EV_SLOT(w);
             if (w & LC_EV_OK_BIT) {
                 if (lm_bit(lm, sl, LM_X)) {
@@ -279,7 +307,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 R = j;
                 break;
             }
-            const uint32_t d = io.dsc(j);
+            const uint32_t d = win.dsc(j);
             const uint32_t l = sl & 63u;
             if (sl < 64) { io.set_prev(j, rdl(occ0, l)); occ0 = wsetl(occ0, l, j); dsc0 = wsetl(dsc0, l, d); }
             else { io.set_prev(j, rdl(occ1, l)); occ1 = wsetl(occ1, l, j); dsc1 = wsetl(dsc1, l, d); }
@@ -374,8 +402,9 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 WP_MARK(1);
                 uint32_t x2 = (lm & 3u) | lm_one(rs, LM_X);
                 z2 = zx ^ zob(rs);
+                EvWindow<LDS, false> win(io, n);
                 for (uint32_t j = R; j < n; ++j) {
-                    const uint32_t w = io.ev(j);
+                    const uint32_t w = win.ev(j);
                     if (!(w & LC_EV_OK_BIT)) continue;
                     const uint32_t sl = LC_EV_SLOT(w);
                     if (lm_bit(x2, sl, LM_X)) { x2 &= ~lm_one(sl, LM_X); z2 ^= zob(sl); continue; }
@@ -394,7 +423,9 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             if (sl0 == rs) { kR0 = R2; k0lo = x2lo; k0hi = x2hi; kz0 = z2; }
             if (sl1 == rs) { kR1 = R2; k1lo = x2lo; k1hi = x2hi; kz1 = z2; }
             const uint32_t h0 = wgl_hash(kR0, s20, kz0), h1 = wgl_hash(kR1, s21, kz1);
-            bool act0 = ok0, act1 = ok1, hit0 = false, hit1 = false;
+            // (0/1 words, not bools: a bool carried around a loop becomes a
+            // lane mask in scalar pairs, merged with EXEC at every step)
+            uint32_t act0 = ok0 ? 1u : 0u, act1 = ok1 ? 1u : 0u, hit0 = 0, hit1 = 0;
             uint32_t p0, p1;
             // the pending pair's slot search: 64 entries from its home, read
             // beside the first probes
@@ -405,20 +436,20 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 p0 = h0 & lmask;
                 p1 = h1 & lmask;
                 if (pend && !pend_known) pfree = ltab[(ph + lane) & lmask] == ~0ull;
+                // (branch-free per lane: every lane reads its two slots, a
+                // finished probe just stops moving -- no EXEC-mask juggling)
                 for (uint32_t probe = 0; probe <= lmask; ++probe) {
-                    if (!ballot(act0 || act1)) break;
+                    if (!ballot((act0 | act1) != 0u)) break;
                     WP_ADD(6, 1);
-                    const uint64_t e0 = act0 ? ltab[p0] : 0ull, e1 = act1 ? ltab[p1] : 0ull;
-                    if (act0) {
-                        if (e0 == ~0ull) act0 = false;
-                        else if (e0 == q0) { act0 = false; hit0 = true; }
-                        else p0 = (p0 + 1) & lmask;
-                    }
-                    if (act1) {
-                        if (e1 == ~0ull) act1 = false;
-                        else if (e1 == q1) { act1 = false; hit1 = true; }
-                        else p1 = (p1 + 1) & lmask;
-                    }
+                    const uint64_t e0 = ltab[p0], e1 = ltab[p1];
+                    const uint32_t eq0 = e0 == q0 ? 1u : 0u, eq1 = e1 == q1 ? 1u : 0u;
+                    const uint32_t em0 = e0 == ~0ull ? 1u : 0u, em1 = e1 == ~0ull ? 1u : 0u;
+                    hit0 |= act0 & eq0;
+                    hit1 |= act1 & eq1;
+                    act0 &= ~(eq0 | em0) & 1u;
+                    act1 &= ~(eq1 | em1) & 1u;
+                    p0 = (p0 + act0) & lmask;
+                    p1 = (p1 + act1) & lmask;
                 }
             } else {
                 p0 = h0 & mask;
@@ -428,28 +459,32 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     pfree = ((uint64_t)pe.z | (uint64_t)pe.w << 32) != gen;
                 }
                 for (uint32_t probe = 0; probe <= mask; ++probe) {
-                    if (!ballot(act0 || act1)) break;
+                    if (!ballot((act0 | act1) != 0u)) break;
                     WP_ADD(6, 1);
+                    // (the loads only where a probe is active: an HBM entry is
+                    // 32 bytes; the updates branch-free)
                     uint4 e00 = {}, e01 = {}, e10 = {}, e11 = {};
                     if (act0) { e00 = tab[2 * (size_t)p0]; e01 = tab[2 * (size_t)p0 + 1]; }
                     if (act1) { e10 = tab[2 * (size_t)p1]; e11 = tab[2 * (size_t)p1 + 1]; }
-                    if (act0) {
-                        const uint64_t g = (uint64_t)e01.z | (uint64_t)e01.w << 32;
-                        if (g != gen) { act0 = false; }
-                        else if (e01.x == kR0 && e01.y == s20 && ((uint64_t)e00.x | (uint64_t)e00.y << 32) == k0lo &&
-                                 ((uint64_t)e00.z | (uint64_t)e00.w << 32) == k0hi) { act0 = false; hit0 = true; }
-                        else p0 = (p0 + 1) & mask;
-                    }
-                    if (act1) {
-                        const uint64_t g = (uint64_t)e11.z | (uint64_t)e11.w << 32;
-                        if (g != gen) { act1 = false; }
-                        else if (e11.x == kR1 && e11.y == s21 && ((uint64_t)e10.x | (uint64_t)e10.y << 32) == k1lo &&
-                                 ((uint64_t)e10.z | (uint64_t)e10.w << 32) == k1hi) { act1 = false; hit1 = true; }
-                        else p1 = (p1 + 1) & mask;
-                    }
+                    const bool own0 = ((uint64_t)e01.z | (uint64_t)e01.w << 32) == gen;
+                    const bool own1 = ((uint64_t)e11.z | (uint64_t)e11.w << 32) == gen;
+                    const bool eq0 = own0 && e01.x == kR0 && e01.y == s20 &&
+                                     ((uint64_t)e00.x | (uint64_t)e00.y << 32) == k0lo &&
+                                     ((uint64_t)e00.z | (uint64_t)e00.w << 32) == k0hi;
+                    const bool eq1 = own1 && e11.x == kR1 && e11.y == s21 &&
+                                     ((uint64_t)e10.x | (uint64_t)e10.y << 32) == k1lo &&
+                                     ((uint64_t)e10.z | (uint64_t)e10.w << 32) == k1hi;
+                    hit0 |= act0 & (eq0 ? 1u : 0u);
+                    hit1 |= act1 & (eq1 ? 1u : 0u);
+                    act0 &= (own0 && !eq0) ? 1u : 0u;
+                    act1 &= (own1 && !eq1) ? 1u : 0u;
+                    p0 = (p0 + act0) & mask;
+                    p1 = (p1 + act1) & mask;
                 }
             }
             lm = (lm & 0xFu) | (ok0 && !hit0 ? 1u << LM_C : 0u) | (ok1 && !hit1 ? 2u << LM_C : 0u);
+            (void)act0;
+            (void)act1;
             ipos0 = p0;
             ipos1 = p1;
             have_pos = true;

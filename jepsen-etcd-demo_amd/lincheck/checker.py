@@ -183,7 +183,10 @@ class Device:
         o.debug_mode = debug_mode  # ablation builds only; 0 = the real search
         o.path_flags, o.spec_segs, o.seg_len = path_flags, spec_segs, seg_len
         if spec_ck is not None:
-            o.spec_ck = (int(spec_ck[0]) + 1) | ((int(spec_ck[1]) + 1) << 16)
+            ck1, ck2 = int(spec_ck[0]), int(spec_ck[1])
+            if not (0 <= ck1 <= 65534 and 0 <= ck2 <= 32766):  # the int32 word holds ck + 1 in 16 / 15 bits
+                raise ValueError(f"spec_ck ({ck1}, {ck2}) out of range: 0 <= ck1 <= 65534, 0 <= ck2 <= 32766")
+            o.spec_ck = (ck1 + 1) | ((ck2 + 1) << 16)
         if devices is not None and len(devices) > 1:
             o.n_devices = len(devices)
             for g, d in enumerate(devices):

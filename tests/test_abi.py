@@ -84,3 +84,18 @@ def test_wgl_and_competition_accepted(algo):
         N.lib().lc_destroy(h)
     else:
         assert b"algorithm" not in N.lib().lc_last_error()
+
+
+def test_spec_ck_range_checked():
+    """spec_ck packs (ck1 + 1) | (ck2 + 1) << 16 into an int32; a
+    ck2 past 32766 wraps the word negative.  lc_create refuses such a word
+    and the Python binding refuses the pair before packing it."""
+    from lincheck.checker import Device
+    o = N.LcOpts()
+    o.spec_ck = -((1 << 31) - 1)  # what (0, 40000) would have wrapped to
+    h = C.c_void_p()
+    assert N.lib().lc_create(C.byref(o), C.byref(h)) == -1
+    assert b"spec_ck" in N.lib().lc_last_error()
+    for bad in [(0, 40000), (-1, 5), (70000, 5)]:
+        with pytest.raises(ValueError, match="spec_ck"):
+            Device(0, spec_ck=bad)
