@@ -172,8 +172,10 @@ struct KeyIo {
         const uint32_t t = LC_EV_TRANS(uni(gev[j]));
         return t < ntr ? uni(trans[t]) : 0u;
     }
-    // per lane: event j (this lane's; j < n) and, for an :invoke, its descriptor
+    // per lane: event j (this lane's; j < n), its slot's previous :invoke and,
+    // for an :invoke, its descriptor
     __device__ __forceinline__ uint32_t ev_at(uint32_t j) const { return LDS ? wgl_lds[j] : gev[j]; }
+    __device__ __forceinline__ uint32_t prev_at(uint32_t j) const { return LDS ? wgl_lds[E + j] : gprev[j]; }
     __device__ __forceinline__ uint32_t dsc_at(uint32_t j, uint32_t w) const {
         if (LDS) return wgl_lds[2 * E + j];
         const uint32_t t = LC_EV_TRANS(w);
@@ -199,6 +201,25 @@ struct EvWindow {
     }
     __device__ __forceinline__ uint32_t ev(uint32_t j) { at(j); return rdl(w, j - base); }
     __device__ __forceinline__ uint32_t dsc(uint32_t j) { at(j); return rdl(d, j - base); }
+};
+
+// A backward scan's window (a backtrack's restore): per lane an event, its
+// slot's previous :invoke and that :invoke's descriptor -- the gather of the
+// descriptors done by all lanes at once.
+template <bool LDS>
+struct EvWindowRev {
+    const KeyIo<LDS> &io;
+    uint32_t base = 0xFFFFFFFFu, w = 0, pv = 0, pd = 0;
+    __device__ __forceinline__ explicit EvWindowRev(const KeyIo<LDS> &io_) : io(io_) {}
+    __device__ __forceinline__ void at(uint32_t j) {  // j uniform, < n
+        if (j - base >= 64u) {
+            base = j >= 63u ? j - 63u : 0u;
+            const uint32_t k = base + __lane_id();  // <= j < n for the lanes read
+            w = k <= j ? io.ev_at(k) : LC_EV_OK_BIT;
+            pv = (!(w & LC_EV_OK_BIT)) ? io.prev_at(k) : WGL_NONE;
+            pd = pv != WGL_NONE ? io.dsc_at(pv, io.ev_at(pv)) : 0u;
+        }
+    }
 };
 
 // The launch's arguments as the kernarg segment holds them, through an
@@ -573,12 +594,13 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             }
             const uint32_t fR = rdl(word, 0), fs = rdl(word, 1), fz = rdl(word, 2);
             if (fR != R) {
+                EvWindowRev<LDS> win(io);
                 for (uint32_t j = (R == WGL_END ? n : R); j-- > fR;) {
-                    const uint32_t w = io.ev(j);
+                    win.at(j);
+                    const uint32_t w = rdl(win.w, j - win.base);
                     if (w & LC_EV_OK_BIT) continue;
                     const uint32_t sl = LC_EV_SLOT(w), l = sl & 63u;
-                    const uint32_t pj = io.prev(j);
-                    const uint32_t d = pj == WGL_NONE ? 0u : io.dsc(pj);
+                    const uint32_t pj = rdl(win.pv, j - win.base), d = rdl(win.pd, j - win.base);
                     if (sl < 64) { occ0 = wsetl(occ0, l, pj); dsc0 = wsetl(dsc0, l, d); }
                     else { occ1 = wsetl(occ1, l, pj); dsc1 = wsetl(dsc1, l, d); }
                 }
