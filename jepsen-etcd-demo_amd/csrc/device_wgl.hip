@@ -189,7 +189,7 @@ struct KeyIo {
 template <bool LDS, bool DSC>
 struct EvWindow {
     const KeyIo<LDS> &io;
-    uint32_t n, base = 0xFFFFFFFFu, w = 0, d = 0;
+    uint32_t n, base = 0x80000000u, w = 0, d = 0;  // (base: no window yet -- j - base >= 64 for every j < 2^31)
     __device__ __forceinline__ EvWindow(const KeyIo<LDS> &io_, uint32_t n_) : io(io_), n(n_) {}
     __device__ __forceinline__ void at(uint32_t j) {  // j uniform, < n
         if (j - base >= 64u) {
@@ -209,7 +209,7 @@ struct EvWindow {
 template <bool LDS>
 struct EvWindowRev {
     const KeyIo<LDS> &io;
-    uint32_t base = 0xFFFFFFFFu, w = 0, pv = 0, pd = 0;
+    uint32_t base = 0x80000000u, w = 0, pv = 0, pd = 0;  // (no window yet, as EvWindow)
     __device__ __forceinline__ explicit EvWindowRev(const KeyIo<LDS> &io_) : io(io_) {}
     __device__ __forceinline__ void at(uint32_t j) {  // j uniform, < n
         if (j - base >= 64u) {
