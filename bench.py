@@ -667,12 +667,12 @@ def main():
                    "steps_per_s": (wsteps / (avg_wgl * 1e-3)) if wsteps and avg_wgl > 0 else None}
             if avg_wgl >= max(avg_t0, avg_t3):
                 # Algorithmic bytes of a WGL launch: the event words (4 B),
-                # each cache entry written once (32 B), a 64-B frame written
+                # each cache entry written once (32 B), an 80-B frame written
                 # or read per step, the records -- the probes' reads come on
                 # top (up to a window of 32-B entries per step).
                 dominant = "k_wgl (knossos.wgl walk)"
                 kt = avg_wgl
-                alg_bytes = 4 * n_events + 32 * (cache_entries or 0) + 64 * (wsteps or 0) + 8 * K
+                alg_bytes = 4 * n_events + 32 * (cache_entries or 0) + 80 * (wsteps or 0) + 8 * K
                 tags = ("k_wgl",)
         achieved = alg_bytes / (kt * 1e-3) / 1e9 if kt > 0 else 0.0
         # measured HBM traffic and VALU issue of the same kernel on the same

@@ -256,19 +256,24 @@ __device__ __forceinline__ void wgl_finish(const WglArgs &, int32_t key, int ver
 // Search one key (the whole wave).  Every lane runs the same control flow:
 // every branch below is on a wave-uniform value.  LDS: the key's events fit
 // the block's LDS (lds_events).
-template <bool LDS>
-__device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *slot_ws) {
+// WIDE: the key's window reaches slot 64 (the second slot of each lane is in
+// use); without, every slot-64-127 term is the constant zero and drops out of
+// the walk (a lone wave per SIMD issues an instruction per 4 cycles, so the
+// walk's time is its instruction count).  Returns false when a narrow walk
+// finds a slot >= 64 its key_width did not declare (the caller walks it wide).
+template <bool LDS, bool WIDE>
+__device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *slot_ws) {
     const uint32_t lane = __lane_id();
     WP_DECL
     const uint64_t eb = a.ev_off[key];
     const uint32_t n = (uint32_t)(a.ev_off[key + 1] - eb);
     if (a.key_error && a.key_error[key]) {
         wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
-        return;
+        return true;
     }
     if (a.key_states && a.key_states[key] > LC_WIDE_MAX_STATES) {
         wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_STATES, -1, 0, 0, 0);
-        return;
+        return true;
     }
     const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
     const uint64_t gen = a.gen_base | (uint64_t)(ticket + 1u);
@@ -285,6 +290,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     // then :unknown "window" at the first such :invoke, before any search
     // (as the restatement).
     uint32_t win_ev = WGL_END;
+    bool past64 = false;  // an :invoke into slot >= 64
     for (uint32_t base = 0; base < n; base += 64) {
         const uint32_t j = base + lane;
         uint32_t w = 0;
@@ -295,13 +301,15 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             wgl_lds[2 * io.E + j] = (!(w & LC_EV_OK_BIT) && t < io.ntr) ? io.trans[t] : 0u;
         }
         const bool wide = j < n && !(w & LC_EV_OK_BIT) && LC_EV_SLOT(w) >= LC_WIDE_MAX_SLOTS;
+        if (!WIDE) past64 = past64 || ballot(j < n && !(w & LC_EV_OK_BIT) && LC_EV_SLOT(w) >= 64u) != 0;
         const uint64_t m = ballot(wide);
         if (m && win_ev == WGL_END) win_ev = base + (uint32_t)__builtin_ctzll(m);
     }
     __syncthreads();
+    if (!WIDE && past64 && win_ev == WGL_END) return false;
     if (win_ev != WGL_END) {
         wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_WINDOW, (int32_t)win_ev, 0, 0, 0);
-        return;
+        return true;
     }
     // per lane: the op holding window slot `lane` (occ0, dsc0) and `lane + 64`
     // (occ1, dsc1) at R -- its :invoke event and its transition descriptor
@@ -330,7 +338,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             }
             const uint32_t d = win.dsc(j);
             const uint32_t l = sl & 63u;
-            if (sl < 64) { io.set_prev(j, rdl(occ0, l)); occ0 = wsetl(occ0, l, j); dsc0 = wsetl(dsc0, l, d); }
+            if (!WIDE || sl < 64) { io.set_prev(j, rdl(occ0, l)); occ0 = wsetl(occ0, l, j); dsc0 = wsetl(dsc0, l, d); }
             else { io.set_prev(j, rdl(occ1, l)); occ1 = wsetl(occ1, l, j); dsc1 = wsetl(dsc1, l, d); }
             lm |= lm_one(sl, LM_P);
         }
@@ -409,11 +417,11 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         if (fresh) {
             fresh = false;
             // X as two scalar words (keys, the pending pair)
-            const uint64_t xlo = ballot(lm & 1u), xhi = ballot(lm & 2u);
+            const uint64_t xlo = ballot(lm & 1u), xhi = WIDE ? ballot(lm & 2u) : 0ull;
             const uint32_t sl0 = lane, sl1 = lane + 64u;
             uint32_t s20 = 0, s21 = 0;
             const bool ok0 = (lm & 4u) && !(lm & 1u) && step(a.table, s, dsc0, s20);
-            const bool ok1 = (lm & 8u) && !(lm & 2u) && step(a.table, s, dsc1, s21);
+            const bool ok1 = WIDE && (lm & 8u) && !(lm & 2u) && step(a.table, s, dsc1, s21);
             const bool r_ok = has_R && ((ballot(rs < 64 ? ok0 : ok1) >> (rs & 63)) & 1ull);
             // the child reached by taking the op of R: R moves on (tentatively;
             // the ops returning in between leave X)
@@ -433,7 +441,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     break;
                 }
                 x2lo = ballot(x2 & 1u);
-                x2hi = ballot(x2 & 2u);
+                x2hi = WIDE ? ballot(x2 & 2u) : 0ull;
                 WP_MARK(2);
             }
             // each candidate's child key
@@ -554,7 +562,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             if (!has_R) {  // the walk runs off the end of the list: linearizable
                 WP_DUMP();
                 wgl_finish(a, key, LC_VALID, LC_CAUSE_NONE, -1, cache_n, 0, steps);
-                return;
+                return true;
             }
             // stuck on the return entry R: the deepest such entries' nodes
             // are the frontier (the first max_final of them, in walk order)
@@ -574,7 +582,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             if (depth == 0) {
                 WP_DUMP();
                 wgl_finish(a, key, LC_INVALID, LC_CAUSE_NONLIN, (int32_t)deepest, cache_n, n_front, steps);
-                return;
+                return true;
             }
             // backtrack: the frame of the node above (the LDS ring holds the
             // last WGL_RING levels), and the slots of the :invokes the step
@@ -601,7 +609,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     if (w & LC_EV_OK_BIT) continue;
                     const uint32_t sl = LC_EV_SLOT(w), l = sl & 63u;
                     const uint32_t pj = rdl(win.pv, j - win.base), d = rdl(win.pd, j - win.base);
-                    if (sl < 64) { occ0 = wsetl(occ0, l, pj); dsc0 = wsetl(dsc0, l, d); }
+                    if (!WIDE || sl < 64) { occ0 = wsetl(occ0, l, pj); dsc0 = wsetl(dsc0, l, d); }
                     else { occ1 = wsetl(occ1, l, pj); dsc1 = wsetl(dsc1, l, d); }
                 }
             }
@@ -612,12 +620,12 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         }
         // ---- step down: the candidate with the earliest :invoke ----
         const uint32_t v0 = (lm & (1u << LM_C)) ? occ0 : WGL_NONE;
-        const uint32_t v1 = (lm & (2u << LM_C)) ? occ1 : WGL_NONE;
+        const uint32_t v1 = (WIDE && (lm & (2u << LM_C))) ? occ1 : WGL_NONE;
         const uint32_t inv = uni(__ockl_wfred_min_u32(v0 < v1 ? v0 : v1));
-        const uint64_t m0 = ballot(v0 == inv), m1 = ballot(v1 == inv);
-        const uint32_t c = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
+        const uint64_t m0 = ballot(v0 == inv), m1 = WIDE ? ballot(v1 == inv) : 0ull;
+        const uint32_t c = (!WIDE || m0) ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
         const uint32_t cl = c & 63u;
-        const uint32_t cd = c < 64 ? rdl(dsc0, cl) : rdl(dsc1, cl);
+        const uint32_t cd = (!WIDE || c < 64) ? rdl(dsc0, cl) : rdl(dsc1, cl);
         uint32_t sc = 0;
         (void)step(a.table, s, cd, sc);
         sc = uni(sc);
@@ -630,20 +638,20 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 ca.spill[i] = key;
             }
             WP_DUMP();
-            return;
+            return true;
         }
         ++cache_n;
         ++steps;
         if ((uint64_t)cache_n > a.budget) {
             WP_DUMP();
             wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_BUDGET, -1, cache_n, 0, steps);
-            return;
+            return true;
         }
         // the pair joins the cache in the next probe round; at the slot this
         // round's probe found for it, unless the round was an earlier one
         // (the subtree may have taken it) or the table changes tier now
         pend = true;
-        pend_pos = have_pos ? (c < 64 ? rdl(ipos0, cl) : rdl(ipos1, cl)) : WGL_NONE;
+        pend_pos = have_pos ? ((!WIDE || c < 64) ? rdl(ipos0, cl) : rdl(ipos1, cl)) : WGL_NONE;
         pend_known = pend_pos != WGL_NONE;
         if (in_lds && cache_n > a.lds_tab / 2) {
             migrate();
@@ -675,6 +683,7 @@ __device__ void wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     }
     // not reached: the walk ends within max_it steps
     wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, cache_n, 0, steps);
+    return true;
 }
 
 __global__ __launch_bounds__(64) void k_wgl(WglArgs a) {
@@ -691,8 +700,17 @@ __global__ __launch_bounds__(64) void k_wgl(WglArgs a) {
         if (w >= n_work) break;
         const int32_t key = a.order[w];
         const uint64_t nev = a.ev_off[key + 1] - a.ev_off[key];
-        if (nev <= a.lds_events) wgl_key<true>(a, key, (uint32_t)w, slot_ws);
-        else wgl_key<false>(a, key, (uint32_t)w, slot_ws);
+        const bool lds = nev <= a.lds_events;
+        // narrow walk unless key_width says the window reaches slot 64 (or
+        // the walk finds it does)
+        const bool wide = !a.key_width || a.key_width[key] > 64u;
+        bool done = false;
+        if (!wide) done = lds ? wgl_key<true, false>(a, key, (uint32_t)w, slot_ws)
+                              : wgl_key<false, false>(a, key, (uint32_t)w, slot_ws);
+        if (!done) {
+            if (lds) wgl_key<true, true>(a, key, (uint32_t)w, slot_ws);
+            else wgl_key<false, true>(a, key, (uint32_t)w, slot_ws);
+        }
         __syncthreads();  // the next key's staging overwrites the LDS copies
     }
 }
