@@ -474,7 +474,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             work(0);
             for (auto &th : pool) th.join();
         };
-        std::vector<int32_t> row_key((size_t)n);
+        lc::uninit_vector<int32_t> row_key((size_t)n);  // every row written below
         std::vector<std::vector<int64_t>> rkeys(nr), rshared(nr);
         std::vector<int64_t> bad_row(nr, -1), bad_mop(nr, -1);
         range_rows([&](unsigned t, int64_t r0, int64_t r1) {
@@ -561,7 +561,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             for (int64_t r = r0; r < r1; ++r)
                 if (row_key[(size_t)r] >= 0) P->krows[cur[(size_t)row_key[(size_t)r]]++] = r;
         });
-        std::vector<int32_t>().swap(row_key);
+        lc::uninit_vector<int32_t>().swap(row_key);
         lap("A2 bucketing");
 
         // ---- A3: per-key pairing, fail-drop, slots (parallel over keys) ----
@@ -671,29 +671,39 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             if (!pair_rows(*h, rows, nrows, model, ops, row_op, o.err, o.msg)) return;
             uint32_t *ev = st_ev + stage_off(k);
             o.n_ev = emit_events(rows, nrows, ops, row_op, ev, st_row + stage_off(k), nullptr, o.width);
-            // (1) distinct state values
-            if (model != LC_MODEL_MUTEX) {
-                std::vector<int64_t> &vals = o.vals;
-                std::unordered_map<int64_t, char> seen;
-                auto add = [&](int64_t v) {
-                    if (v == LC_NIL) return;
-                    if (vals.size() < 16) {
-                        if (std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
-                        return;
-                    }
-                    if (seen.empty())
-                        for (int64_t x : vals) seen.emplace(x, 0);
-                    if (seen.emplace(v, 0).second) vals.push_back(v);
-                };
-                for (const KOp &op : ops) {
-                    if (op.fate == 2) continue;
-                    if (op.f == LC_F_WRITE) add(op.v0);
-                    if (op.f == LC_F_CAS) add(op.v1);
+            // (1) distinct state values, and each surviving op's triple
+            // index (the fields its descriptor reads), distinct triples in
+            // invoke order.  Small values (0 .. 14, and nil) -- what Jepsen
+            // register tests write -- go through direct tables stamped per
+            // key; others through a set / an open-addressing table of index +
+            // 1 kept under half full.
+            constexpr int64_t SMALL = 15;  // values 0 .. 14, plus nil as 15
+            auto small = [](int64_t v) -> int64_t { return v == LC_NIL ? SMALL : (v >= 0 && v < SMALL ? v : -1); };
+            static thread_local std::vector<uint32_t> dstamp, dtrip;  // (f, a, b) small -> stamp, index
+            static thread_local uint32_t kstamp = 0;
+            if (dstamp.empty()) { dstamp.assign(8 * 16 * 16, 0); dtrip.assign(8 * 16 * 16, 0); }
+            if (++kstamp == 0) { std::fill(dstamp.begin(), dstamp.end(), 0u); kstamp = 1; }
+            uint32_t vseen = 0;  // small state values seen
+            std::vector<int64_t> &vals = o.vals;
+            std::unordered_map<int64_t, char> seen;
+            auto add = [&](int64_t v) {
+                if (v == LC_NIL) return;
+                const int64_t sv = small(v);
+                if (sv >= 0) {
+                    if (vseen >> sv & 1u) return;
+                    vseen |= 1u << sv;
+                    vals.push_back(v);
+                    if (!seen.empty()) seen.emplace(v, 0);
+                    return;
                 }
-            }
-            // each surviving op's triple index (the fields its descriptor
-            // reads), distinct triples in invoke order, through an
-            // open-addressing table of index + 1 kept under half full
+                if (vals.size() < 16) {
+                    if (std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
+                    return;
+                }
+                if (seen.empty())
+                    for (int64_t x : vals) seen.emplace(x, 0);
+                if (seen.emplace(v, 0).second) vals.push_back(v);
+            };
             tix.resize(ops.size());
             size_t tmask = 255;
             tt.assign(tmask + 1, 0);
@@ -702,20 +712,38 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
                              (uint64_t)b * 0x165667B19E3779F9ull;
                 return (size_t)(x ^ (x >> 29));
             };
+            auto new_trip = [&](int64_t f, int64_t a, int64_t b) -> uint32_t {
+                const uint32_t ti = (uint32_t)(o.trip.size() / 3);
+                o.trip.push_back(f);
+                o.trip.push_back(a);
+                o.trip.push_back(b);
+                return ti;
+            };
             for (size_t q = 0; q < ops.size(); ++q) {
                 const KOp &op = ops[q];
                 if (op.fate == 2) continue;
+                if (model != LC_MODEL_MUTEX) {
+                    if (op.f == LC_F_WRITE) add(op.v0);
+                    if (op.f == LC_F_CAS) add(op.v1);
+                }
                 const int64_t f = op.f;
                 const int64_t a = (f == LC_F_ACQUIRE || f == LC_F_RELEASE) ? 0 : op.v0;
                 const int64_t b = f == LC_F_CAS ? op.v1 : 0;
+                const int64_t sa = small(a), sb = small(b);
+                if (sa >= 0 && sb >= 0 && f < 8) {
+                    const size_t di = (size_t)f * 256 + (size_t)sa * 16 + (size_t)sb;
+                    if (dstamp[di] != kstamp) {
+                        dstamp[di] = kstamp;
+                        dtrip[di] = new_trip(f, a, b);
+                    }
+                    tix[q] = dtrip[di];
+                    continue;
+                }
                 size_t x = thash(f, a, b) & tmask;
                 for (;; x = (x + 1) & tmask) {
                     const uint64_t e = tt[x];
                     if (!e) {
-                        const uint32_t ti = (uint32_t)(o.trip.size() / 3);
-                        o.trip.push_back(f);
-                        o.trip.push_back(a);
-                        o.trip.push_back(b);
+                        const uint32_t ti = new_trip(f, a, b);
                         tt[x] = ti + 1;
                         tix[q] = ti;
                         if ((size_t)(ti + 1) * 2 > tmask) {  // grow
