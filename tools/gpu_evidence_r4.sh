@@ -62,5 +62,9 @@ timeout -k 10 400 python -u bench.py --config C2 --algorithm wgl --steps 10 --wa
 prof c2wgl --config C2 --algorithm wgl --steps 10 --warmup 2 $PROF || exit 1
 step bench_c5_jepsen
 timeout -k 10 400 python -u bench.py --config C5 --jepsen --steps 10 --warmup 2 > $O/bench_c5_jepsen.json 2> $O/bench_c5_jepsen.err || { tail -5 $O/bench_c5_jepsen.err; exit 1; }
+step wgl_phases
+( export LINCHECK_LIB_OVERRIDE=jepsen-etcd-demo_amd/lincheck/liblincheck_wglprof.so
+  timeout -k 10 300 python -u tools/wgl_prof.py C2 > $O/wglprof_C2.json 2> $O/wglprof_C2.err &&
+  timeout -k 10 300 python -u tools/wgl_prof.py C4 65536 > $O/wglprof_C4.json 2> $O/wglprof_C4.err ) || { tail -5 $O/wglprof_C2.err $O/wglprof_C4.err; exit 1; }
 fi
 echo ALL_OK
