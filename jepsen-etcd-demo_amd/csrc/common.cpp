@@ -5,6 +5,8 @@
 
 #include <cstdarg>
 #include <cstdlib>
+#include <map>
+#include <unordered_map>
 #include <mutex>
 #include <unordered_set>
 
@@ -59,9 +61,15 @@ void range_pop() {
 
 // Page-locked host memory for arrays the device reads whole (lc_pack's event
 // words): the DMA engine reads them directly instead of through a bounce
-// buffer.  Without a visible GPU (or for small arrays) plain malloc.
+// buffer.  Without a visible GPU (or for small arrays) plain malloc.  Freed
+// blocks are kept (up to 1 GB) and handed to the next request they fit
+// within 2x: pinning and unpinning cost milliseconds per call (hipHostFree
+// synchronises), and a Jepsen-shaped caller packs a history per check.
 static std::mutex g_pin_mu;
-static std::unordered_set<void *> g_pinned;
+static std::unordered_map<void *, size_t> g_pinned;  // live and cached blocks -> size
+static std::multimap<size_t, void *> g_pin_free;     // cached blocks by size
+static size_t g_pin_cached = 0;
+constexpr size_t PIN_CACHE_MAX = 1ull << 30;
 
 void *pinned_alloc(size_t bytes) {
     static const bool gpu = [] {
@@ -71,10 +79,20 @@ void *pinned_alloc(size_t bytes) {
         return ok;
     }();
     if (gpu && bytes >= (64u << 10) && bytes <= (2ull << 30)) {
+        {
+            std::lock_guard<std::mutex> g(g_pin_mu);
+            auto it = g_pin_free.lower_bound(bytes);
+            if (it != g_pin_free.end() && it->first <= 2 * bytes) {
+                void *p = it->second;
+                g_pin_cached -= it->first;
+                g_pin_free.erase(it);
+                return p;
+            }
+        }
         void *p = nullptr;
         if (hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess && p) {
             std::lock_guard<std::mutex> g(g_pin_mu);
-            g_pinned.insert(p);
+            g_pinned[p] = bytes;
             return p;
         }
         (void)hipGetLastError();
@@ -88,8 +106,14 @@ void pinned_free(void *p) {
         std::lock_guard<std::mutex> g(g_pin_mu);
         auto it = g_pinned.find(p);
         if (it != g_pinned.end()) {
-            g_pinned.erase(it);
-            (void)hipHostFree(p);
+            const size_t sz = it->second;
+            if (g_pin_cached + sz <= PIN_CACHE_MAX) {
+                g_pin_free.emplace(sz, p);
+                g_pin_cached += sz;
+            } else {
+                g_pinned.erase(it);
+                (void)hipHostFree(p);
+            }
             return;
         }
     }
