@@ -1181,6 +1181,24 @@ __device__ __forceinline__ bool slot_protocol(bool tracked, bool ok, uint32_t s,
 // window slots up to 126, the slot-127 marker of ops beyond the encodable
 // window exempt from the slot protocol (the search stops before it follows
 // one), and every :invoke's slot below the key's key_width.
+// One 64-event chunk of a key's validation (w: lane i holds event i of the
+// chunk, in: it is one): transition ids, window slots, the slot protocol.
+// Returns the LC_BATCH_E_* reasons found (0: none; pend is then advanced).
+template <bool GEN, int NW>
+__device__ __forceinline__ int32_t validate_chunk(uint32_t w, bool in, const uint32_t *trp, uint32_t ntr, uint32_t ns,
+                                                  uint32_t width, uint32_t (&pend)[NW]) {
+    int32_t why = 0;
+    const bool ok = (w & LC_EV_OK_BIT) != 0;
+    const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
+    const uint32_t d = (in && !ok && t < ntr) ? trp[t] : 0u;
+    if (__any(in && !ok && (t >= ntr || ((d & 3u) >= LC_T_WRITE && (d >> 17) >= ns)))) why |= LC_BATCH_E_TRANS;
+    const bool beyond = GEN && s == 127u;  // past the encodable window: no slot to track
+    if (__any(in && !beyond && (GEN ? (!ok && s >= width) : s >= 64u))) why |= LC_BATCH_E_FIT;
+    if (why) return why;
+    if (slot_protocol<NW>(in && !beyond, ok, s, pend)) why |= LC_BATCH_E_SLOTS;
+    return why;
+}
+
 template <bool GEN, bool E16 = false>
 __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
     const uint32_t lane = lane_id();
@@ -1202,14 +1220,7 @@ __device__ __forceinline__ void validate_key(const T0Args &a, int64_t k) {
         const uint32_t w = w_next;
         const uint64_t jn = j + 64;
         w_next = jn < ee ? (E16 ? LC_EV16_WIDE(a.events16[jn]) : a.events[jn]) : 0u;  // the next chunk, in flight
-        const bool ok = (w & LC_EV_OK_BIT) != 0;
-        const uint32_t s = LC_EV_SLOT(w), t = LC_EV_TRANS(w);
-        const uint32_t d = (in && !ok && t < ntr) ? a.trans[tb + t] : 0u;
-        if (__any(in && !ok && (t >= ntr || ((d & 3u) >= LC_T_WRITE && (d >> 17) >= ns)))) why |= LC_BATCH_E_TRANS;
-        const bool beyond = GEN && s == 127u;  // past the encodable window: no slot to track
-        if (__any(in && !beyond && (GEN ? (!ok && s >= width) : s >= 64u))) why |= LC_BATCH_E_FIT;
-        if (why) break;
-        if (slot_protocol<NW>(in && !beyond, ok, s, pend)) why |= LC_BATCH_E_SLOTS;
+        why = validate_chunk<GEN, NW>(w, in, a.trans + (ntr ? tb : 0u), ntr, ns, width, pend);
     }
     if (why && lane == 0) {
         atomicOr(&a.err[0], why);
@@ -1717,6 +1728,7 @@ hipError_t launch_segments(const SegArgs &a, int grid, hipStream_t s) {
 // assignments stay equal event by event.  Verdicts only.
 extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
 extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_xor_u32(uint32_t);
 
 constexpr uint32_t SPEC_NONE = 0xFFFFFFFFu;
 constexpr uint32_t SPEC_MIN_LEN = 128;  // events per segment at least
@@ -2264,6 +2276,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     __shared__ int32_t s_net[S];          // cut search: pending-count change over each part
     __shared__ int32_t s_cand[S], s_ncand[S];  // each target's cut (-1: none) and ops pending there
     __shared__ int32_t s_next[2];         // the block's queues: TOP walks, verifying runs
+    __shared__ uint32_t s_vx[W][2];       // self-validation: each wave's part, XOR of its slots' one-hots
     constexpr int NWS = spec_lds_ws<W>();
     __shared__ uint32_t s_ws[NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
     __shared__ int32_t s_ws_busy[NWS];
@@ -2276,7 +2289,12 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     const uint32_t blk = vfirst ? blockIdx.x - nb : blockIdx.x;  // the key block's LPT position
     if (vfirst ? blockIdx.x < nb : blockIdx.x >= (uint32_t)a.n_order) {
         const uint32_t vb = vfirst ? blockIdx.x : blockIdx.x - (uint32_t)a.n_order;
-        for (int64_t k = (int64_t)vb * W + wv; k < a.n_order; k += (int64_t)nb * W) validate_key<false, E16>(a, k);
+        for (int64_t k = (int64_t)vb * W + wv; k < a.n_order; k += (int64_t)nb * W) {
+            // (a key whose words its own block stages whole is validated
+            // there, from LDS: see below)
+            if (EVC > 0 && !(a.flags & T0_SPEC_NOSTAGE) && a.ev_off[k + 1] - a.ev_off[k] <= EVC) continue;
+            validate_key<false, E16>(a, k);
+        }
         return;  // the whole block: no barrier below is reached by half of it
     }
     const int32_t key = a.order[blk];
@@ -2324,6 +2342,34 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     if (threadIdx.x < NWS) s_ws_busy[threadIdx.x] = 0;
     if (threadIdx.x < 2) s_next[threadIdx.x] = 0;
     __syncthreads();
+    // T0_STRICT batches whose key the block staged whole: the key's
+    // validation here, from LDS, its 64-event chunks split over the W waves
+    // (the slot protocol's state at a wave's first chunk is the XOR of the
+    // earlier waves' slot parities, exchanged at the cut search's barrier),
+    // instead of a second HBM read of the words in the validation blocks.
+    bool self_val = false;
+    uint32_t vc0 = 0, vc1 = 0;
+    if constexpr (EVC > 0) {
+        self_val = (a.flags & T0_STRICT) && !(a.flags & T0_SPEC_NOSTAGE) && n_lds == nev &&
+                   !(a.key_error && a.key_error[key]);
+        const uint32_t nch = (nev + 63u) / 64u;
+        vc0 = nch * wv / W;
+        vc1 = nch * (wv + 1u) / W;
+        if (self_val) {
+            uint32_t x0 = 0, x1 = 0;
+            for (uint32_t ch = vc0; ch < vc1; ++ch) {
+                const uint32_t j = ch * 64u + lane;
+                if (j < nev) {
+                    const uint32_t sl = LC_EV_SLOT(LC_EV16_WIDE(s_ev[j]));
+                    x0 ^= sl < 32u ? 1u << sl : 0u;
+                    x1 ^= (sl >= 32u && sl < 64u) ? 1u << (sl - 32u) : 0u;
+                }
+            }
+            x0 = uni(__ockl_wfred_xor_u32(x0));
+            x1 = uni(__ockl_wfred_xor_u32(x1));
+            if (lane == 0) { s_vx[wv][0] = x0; s_vx[wv][1] = x1; }
+        }
+    }
     if (wv == 0) {
         for (uint32_t s = 0; s < (uint32_t)S; ++s) { SPEC_STAMP(s, 0, __builtin_amdgcn_s_memtime()) }
     }
@@ -2342,6 +2388,25 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
         }
     }
     __syncthreads();
+    if constexpr (EVC > 0) {
+        if (self_val) {
+            // (the states a transition may install: as validate_key reads them)
+            const uint32_t vns = a.trans_off ? (a.key_states ? a.key_states[key] : 0u) : a.shared_states;
+            uint32_t pend[2] = {0u, 0u};
+            for (uint32_t q = 0; q < wv; ++q) { pend[0] ^= uni(s_vx[q][0]); pend[1] ^= uni(s_vx[q][1]); }
+            int32_t why = 0;
+            for (uint32_t ch = vc0; ch < vc1 && !why; ++ch) {
+                const uint32_t j = ch * 64u + lane;
+                const bool in = j < nev;
+                const uint32_t w = in ? LC_EV16_WIDE(s_ev[j]) : 0u;
+                why = validate_chunk<false, 2>(w, in, trp, ntr, vns, 64u, pend);
+            }
+            if (why && lane == 0) {
+                atomicOr(&a.err[0], why);
+                atomicMax(&a.err[1], a.err_base + key + 1);
+            }
+        }
+    }
     if (!plain && !cost) {
         for (uint32_t s = wv; s < eff; s += W) {
             if (s == 0) continue;

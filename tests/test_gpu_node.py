@@ -234,6 +234,68 @@ def test_spec_validates_large_batch():
         np.testing.assert_array_equal(again, rec)
 
 
+def _ev16(w: int) -> int:
+    """include/lincheck.h LC_EV16_*: a 32-bit event word in 16 bits (slot <= 15,
+    transition id <= 2047)."""
+    return ((w >> 16) & 0x8000) | (((w >> 24) & 0x7F) << 11) | (w & 0x7FF)
+
+
+def test_spec_self_validates_staged_keys():
+    """k_spec validates a key whose 16-bit words its block stages whole in LDS
+    inside that block (its W waves, the slot protocol's state carried across
+    their parts), not by a second HBM read in the validation blocks.  Each
+    malformation the 16-bit words can carry, in keys early, in the middle and
+    at the end of the batch and at a wave's part boundary, is refused naming
+    its key; between refusals the same context gives the oracle's records."""
+    h = H.synth(n_keys=1000, ops_per_key=300, concurrency=6, anomaly_rate=0.05, seed=83)
+    pk = Packed(h)
+    K = pk.n_keys
+    assert pk.view.events16
+    dev = Device(0)
+    arrs, b = _batch_copy(pk)
+    n_ev = int(pk.ev_off[-1])
+    arrs["events16"] = np.ctypeslib.as_array(pk.view.events16, shape=(n_ev,)).copy()
+    b.events16 = N.ptr(arrs["events16"], C.c_uint16)
+    ev, e16 = arrs["events"], arrs["events16"]
+    _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
+
+    def node():
+        out = np.zeros(K, np.uint64)
+        st = N.LcStats()
+        N.check(N.lib().lc_check_node(dev.handle, C.byref(b), K, N.ptr(out, C.c_uint64), C.byref(st)))
+        return out, st
+
+    rec, st = node()
+    assert N.T0_PATH_NAMES.get(int(st.t0_path)) == "k_spec"
+    v, _, fe = _decode(rec, K)
+    np.testing.assert_array_equal(v, orc["valid"])
+    np.testing.assert_array_equal(fe, orc["fail_event"])
+
+    def at(key, pred, frac=0.0):
+        lo, hi = int(pk.ev_off[key]), int(pk.ev_off[key + 1])
+        start = lo + int((hi - lo) * frac)
+        return start + int(np.flatnonzero(pred(ev[start:hi]))[0])
+
+    is_ok = lambda e: (e & N.LC_EV_OK_BIT) != 0  # noqa: E731
+    is_inv = lambda e: (e & N.LC_EV_OK_BIT) == 0  # noqa: E731
+    cases = [
+        (3, at(3, lambda e: np.ones(len(e), bool)), lambda w: w | N.LC_EV_OK_BIT),   # :ok of a free slot
+        (500, at(500, is_ok, 0.5), lambda w: w & 0x7F000000),                        # :invoke into a busy slot
+        (501, at(501, is_ok, 0.26), lambda w: w & 0x7F000000),                       # near a wave's part boundary
+        (998, at(998, is_inv, 0.9), lambda w: (w & 0xFF000000) | 0x7FF),              # transition id past the table
+    ]
+    for key, j, mutate in cases:
+        saved, saved16 = int(ev[j]), int(e16[j])
+        ev[j] = mutate(saved)
+        e16[j] = _ev16(int(ev[j]))
+        with pytest.raises(N.LincheckError) as ei:
+            node()
+        assert ei.value.code == -1 and f"key {key}" in str(ei.value), str(ei.value)
+        ev[j], e16[j] = saved, saved16
+        again, _ = node()
+        np.testing.assert_array_equal(again, rec)
+
+
 def test_t0_refuses_understated_width():
     """key_width claims fewer ops pending at once than a key has: the batch is
     declared register-tier-only, T0 meets the 11th pending op, and the key is
