@@ -47,5 +47,5 @@ def test_wgl_work_loop_is_bounded():
     assert not re.search(r"for\s*\(\s*;\s*;\s*\)|while\s*\(\s*(true|1)\s*\)", body)
     assert re.search(r"for \(int32_t guard = 0; guard <= n_work; \+\+guard\)", body)
     assert "w = (int32_t)uni((uint32_t)w);" in body
-    key = _body(src, "__device__ void wgl_key(")
+    key = _body(src, "__device__ bool wgl_key(")
     assert re.search(r"for \(uint64_t it = 0; it < max_it; \+\+it\)", key), "the walk lost its step bound"
