@@ -120,6 +120,53 @@ void pinned_free(void *p) {
     std::free(p);
 }
 
+// (never destroyed: arrays in static objects of other files may be freed
+// after any destructor of this one would run; the cache holds each block by
+// the start of its allocation, so a leak checker finds them reachable)
+struct BigCache {
+    std::mutex mu;
+    std::multimap<size_t, char *> free;  // cached blocks by size -> their allocation
+    size_t cached = 0;
+};
+static BigCache &big_cache() {  // (made on first use: no static-initialisation order)
+    static BigCache *c = new BigCache;
+    return *c;
+}
+constexpr size_t BIG_CACHE_MAX = 1ull << 30;
+
+void *big_alloc(size_t bytes) {
+    BigCache &g_big = big_cache();
+    {
+        std::lock_guard<std::mutex> g(g_big.mu);
+        auto it = g_big.free.lower_bound(bytes);
+        if (it != g_big.free.end() && it->first <= 2 * bytes) {
+            char *raw = it->second;
+            g_big.cached -= it->first;
+            g_big.free.erase(it);
+            return raw + 64;
+        }
+    }
+    // the size in a 64-byte header, so a reused block goes back under its own size
+    char *raw = (char *)std::malloc(bytes + 64);
+    if (!raw) return nullptr;
+    *(size_t *)raw = bytes;
+    return raw + 64;
+}
+
+void big_free(void *p, size_t) {
+    if (!p) return;
+    char *raw = (char *)p - 64;
+    const size_t sz = *(size_t *)raw;
+    BigCache &g_big = big_cache();
+    std::lock_guard<std::mutex> g(g_big.mu);
+    if (g_big.cached + sz <= BIG_CACHE_MAX) {
+        g_big.free.emplace(sz, raw);
+        g_big.cached += sz;
+    } else {
+        std::free(raw);
+    }
+}
+
 }  // namespace lc
 
 extern "C" const char *lc_last_error(void) { return lc::g_last_error.c_str(); }

@@ -60,7 +60,16 @@ struct PinnedAlloc {
 template <class T>
 using pinned_vector = std::vector<T, PinnedAlloc<T>>;
 
-// std::allocator whose resize() default-initialises (no zero fill)
+// Blocks of 1 MB and more, kept when freed (up to 1 GB) and handed to the
+// next request they fit within 2x: a packed batch's arrays are the same
+// sizes from one check to the next, and fresh ones cost a page fault per
+// 4 KB on first touch.
+void *big_alloc(size_t bytes);
+void big_free(void *p, size_t bytes);
+constexpr size_t BIG_BLOCK = 1u << 20;
+
+// std::allocator whose resize() default-initialises (no zero fill), large
+// blocks through big_alloc
 template <class T>
 struct UninitAlloc : std::allocator<T> {
     using value_type = T;
@@ -69,6 +78,18 @@ struct UninitAlloc : std::allocator<T> {
     UninitAlloc(const UninitAlloc<U> &) {}
     template <class U>
     struct rebind { using other = UninitAlloc<U>; };
+    T *allocate(size_t n) {
+        if (n * sizeof(T) >= BIG_BLOCK) {
+            void *p = big_alloc(n * sizeof(T));
+            if (!p) throw std::bad_alloc();
+            return (T *)p;
+        }
+        return std::allocator<T>::allocate(n);
+    }
+    void deallocate(T *p, size_t n) {
+        if (n * sizeof(T) >= BIG_BLOCK) big_free(p, n * sizeof(T));
+        else std::allocator<T>::deallocate(p, n);
+    }
     template <class U>
     void construct(U *p) noexcept { ::new ((void *)p) U; }
     template <class U, class... A>

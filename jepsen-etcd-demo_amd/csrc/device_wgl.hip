@@ -398,6 +398,10 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     uint32_t deepest = WGL_NONE;  // the deepest return entry the walk got stuck on
     uint64_t steps = 0;
     bool fresh = true;       // the current node has not been probed yet
+    // the child the op of R leads to, as its probe round moved R there (valid
+    // for a step down in the same iteration as the probe)
+    bool have_child = false;
+    uint32_t ch_lm = 0, ch_occ0 = 0, ch_occ1 = 0, ch_dsc0 = 0, ch_dsc1 = 0, ch_R = 0, ch_z = 0;
     bool have_pos = false;   // ipos0/1 are insertion slots (nothing inserted since the probe)
     uint32_t ipos0 = 0, ipos1 = 0;
     // the last step down's pair, inserted during the next probe round (its
@@ -427,21 +431,39 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             // the ops returning in between leave X)
             uint32_t R2 = WGL_END, z2 = 0;
             uint64_t x2lo = 0, x2hi = 0;
+            have_child = false;
             if (r_ok) {
+                // the whole move of R (the advance a step down taking R's op
+                // makes), into the child's own lane state: the step down
+                // adopts it instead of scanning again (the :invokes' prev
+                // words written on the way are functions of the event alone)
                 WP_MARK(1);
-                uint32_t x2 = (lm & 3u) | lm_one(rs, LM_X);
+                uint32_t x2 = (lm & 0xFu) | lm_one(rs, LM_X);
+                uint32_t o0 = occ0, o1 = occ1, d0 = dsc0, d1 = dsc1;
                 z2 = zx ^ zob(rs);
-                EvWindow<LDS, false> win(io, n);
+                EvWindow<LDS, true> win(io, n);
                 for (uint32_t j = R; j < n; ++j) {
                     const uint32_t w = win.ev(j);
-                    if (!(w & LC_EV_OK_BIT)) continue;
                     const uint32_t sl = LC_EV_SLOT(w);
-                    if (lm_bit(x2, sl, LM_X)) { x2 &= ~lm_one(sl, LM_X); z2 ^= zob(sl); continue; }
-                    R2 = j;
-                    break;
+                    if (w & LC_EV_OK_BIT) {
+                        if (lm_bit(x2, sl, LM_X)) {
+                            x2 &= ~(lm_one(sl, LM_X) | lm_one(sl, LM_P));
+                            z2 ^= zob(sl);
+                            continue;
+                        }
+                        R2 = j;
+                        break;
+                    }
+                    const uint32_t d = win.dsc(j);
+                    const uint32_t l = sl & 63u;
+                    if (!WIDE || sl < 64) { io.set_prev(j, rdl(o0, l)); o0 = wsetl(o0, l, j); d0 = wsetl(d0, l, d); }
+                    else { io.set_prev(j, rdl(o1, l)); o1 = wsetl(o1, l, j); d1 = wsetl(d1, l, d); }
+                    x2 |= lm_one(sl, LM_P);
                 }
                 x2lo = ballot(x2 & 1u);
                 x2hi = WIDE ? ballot(x2 & 2u) : 0ull;
+                ch_lm = x2; ch_occ0 = o0; ch_occ1 = o1; ch_dsc0 = d0; ch_dsc1 = d1; ch_R = R2; ch_z = z2;
+                have_child = true;
                 WP_MARK(2);
             }
             // each candidate's child key
@@ -615,6 +637,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             }
             R = fR; s = fs; zx = fz; lm = mbyte;
             have_pos = false;
+            have_child = false;
             WP_MARK(3);
             continue;
         }
@@ -673,11 +696,21 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         // apply the step (taking R's op moves R: the child's R and X are then
         // what the probe round's tentative scan found)
         s = sc;
-        lm |= lm_one(c, LM_X);
-        zx ^= zob(c);
         WP_ADD(7, 1);
         WP_MARK(4);
-        if (c == rs) advance(R);
+        if (c == rs && have_child) {
+            // (C bits: set by the child's own probe round)
+            lm = ch_lm;
+            occ0 = ch_occ0; dsc0 = ch_dsc0;
+            if (WIDE) { occ1 = ch_occ1; dsc1 = ch_dsc1; }
+            R = ch_R;
+            zx = ch_z;
+        } else {
+            lm |= lm_one(c, LM_X);
+            zx ^= zob(c);
+            if (c == rs) advance(R);
+        }
+        have_child = false;
         WP_MARK(5);
         fresh = true;
     }
