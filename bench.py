@@ -665,7 +665,7 @@ def main():
                    "keys_spilled": int(wres.stats["wgl_spilled"]) if wres is not None else None,
                    "steps": wsteps, "cache_entries": cache_entries,
                    "steps_per_s": (wsteps / (avg_wgl * 1e-3)) if wsteps and avg_wgl > 0 else None}
-            if avg_wgl >= max(avg_t0, avg_t3):
+            if args.algorithm == "wgl" or avg_wgl >= max(avg_t0, avg_t3):
                 # Algorithmic bytes of a WGL launch: the event words (4 B),
                 # each cache entry written once (32 B), an 80-B frame written
                 # or read per step, the records -- the probes' reads come on

@@ -294,13 +294,27 @@ struct T0Args {
     uint32_t *spec_fin;          // exact segments: each run's saved set (2 per segment, SPEC_SAVE_WORDS each)
 };
 
-template <bool E16>
-__device__ __forceinline__ EvSrc<E16> ev_src(const T0Args &a) {
+// T0Args read through the kernarg segment where a field is used (k_spec,
+// LC_SPEC_KARG): a kernel that takes its arguments by value loads every field
+// it uses anywhere at its entry and holds it in a scalar register for its
+// whole life; with the walk's own scalars the file overflows into VGPR lanes
+// and uniform loop words are kept in VGPRs (copied at every event).  The empty
+// asm makes each use's pointer opaque, so no load is hoisted or shared.
+using KT0 = const __attribute__((address_space(4))) T0Args;
+__device__ __forceinline__ KT0 &t0k() {
+    KT0 *p = (KT0 *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
+template <bool E16, class A = T0Args>
+__device__ __forceinline__ EvSrc<E16> ev_src(const A &a) {
     if constexpr (E16) return {a.events16};
     else return {a.events};
 }
 
-__device__ __forceinline__ void t0_malformed(const T0Args &a, int32_t key, uint32_t why) {
+template <class A = T0Args>
+__device__ __forceinline__ void t0_malformed(const A &a, int32_t key, uint32_t why) {
     if (lane_id() == 0) {
         atomicOr(&a.err[0], (int32_t)why);
         atomicMax(&a.err[1], a.err_base + key + 1);
@@ -391,6 +405,15 @@ extern "C" int lc_debug_sweep_hist(unsigned long long *host) {
 // ds_bpermute, issued first so its latency hides under the mask setup.
 // lm[q] (0 / ~0) is lane bit q as a VGPR mask.  W = S on entry, S' on a
 // normal return.  Returns 0 normal, 1 invalid, 2 budget exceeded.
+// The closure sweeps run until one changes nothing, without a trip counter
+// (the sweeps only grow the set inside its closure, a finite lattice): the
+// loop is the sweep, one v_cmp and a vcc branch -- six scalar instructions
+// and a counter fewer per sweep than `for (s < nc) ... if (!__any) break`.
+// C2 k_spec 0.2786 -> 0.2754 ms, C5 0.2834 -> 0.2808 (A/B on one box,
+// tools/gpu_r4o.sh); LC_T0_SWEEP_DO=0 keeps the counted loop.
+#ifndef LC_T0_SWEEP_DO
+#define LC_T0_SWEEP_DO 1
+#endif
 template <int T>  // T = 1 + the highest live index (positions T.. are empty)
 __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, uint32_t k_v, uint32_t cap_v,
                                        uint32_t b_v, uint32_t pk, uint32_t pc, uint32_t pb, uint32_t lane,
@@ -415,6 +438,16 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
 #ifdef LC_T0_COUNT_SWEEPS
     uint32_t done_s = nc;
 #endif
+#if LC_T0_SWEEP_DO && !defined(LC_T0_COUNT_SWEEPS)
+    // until a sweep changes nothing (see ok_lane_closed)
+    (void)nc;
+    bool ch;
+    do {
+        const uint32_t nv = sweep_lanes<0, T>(I, m);
+        ch = nv != I;
+        I = nv;
+    } while (__any(ch));
+#else
 #pragma unroll 1
     for (uint32_t s = 0; s < nc; ++s) {
         const uint32_t nv = sweep_lanes<0, T>(I, m);
@@ -427,6 +460,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
             break;
         }
     }
+#endif
 #ifdef LC_T0_COUNT_SWEEPS
     if (lane == 0) atomicAdd(&lc_sweep_hist[nc * 8 + (done_s < 7 ? done_s : 7)], 1ull);
 #endif
@@ -473,6 +507,16 @@ __device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t 
             m.sb[q] = __builtin_amdgcn_readlane(b_v, q);
             if constexpr (TAG) m.sm[q] = __builtin_amdgcn_readlane(m_v, q);
         }
+#if LC_T0_SWEEP_DO
+        // until a sweep changes nothing: the sweeps only grow C inside the
+        // closure, a finite lattice, so the loop ends (no trip counter)
+        bool ch;
+        do {
+            const uint32_t nv = sweep_lanes<0, T, TAG>(C, m);
+            ch = nv != C;
+            C = nv;
+        } while (__any(ch));
+#else
         const uint32_t nc = (uint32_t)__popc(live);  // a path has at most nc steps
 #pragma unroll 1
         for (uint32_t s = 0; s < nc; ++s) {
@@ -481,6 +525,7 @@ __device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t 
             C = nv;
             if (!__any(ch)) break;
         }
+#endif
     }
     // (a DPP switch on p measured slower, in the compact T0 and in the
     // speculative segments' walk: 1,224 against 1,142 cycles per event)
@@ -1985,6 +2030,9 @@ constexpr uint32_t SPEC_SAVE_WORDS = (T0_RMEM + 2) * 64;
 // phase, for steps that report final configs; `save` (EX, may be null)
 // receives the run's set at its end or before its failing :ok, in the
 // LatMem row layout write_final_mem reads, with its slots and live indices.
+#ifndef LC_SPEC_CK_SPLIT
+#define LC_SPEC_CK_SPLIT 1
+#endif
 template <int MODE, int NWS, class EvT, bool EX = false>
 __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
                                          uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
@@ -2045,80 +2093,99 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
     uint32_t ck_at = MODE == 0 ? ck1 : (uni(ck_e[0]) >= 0 ? (uint32_t)uni(ck_e[0]) - b : ~0u);
     uint32_t W0 = st.W0;
     bool dirty = true;
-    for (uint32_t phase = 0; phase <= nev && e < lim; ++phase) {
-        while (e < lim) {  // lane phase: <= 6 pending
-            const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
-            const uint32_t slot = LC_EV_SLOT(evi);
-            if (!(evi & LC_EV_OK_BIT)) {
-                if (n == 6) break;
-                if (n >= T0_MAX_WIDTH || slot >= 64) {
-                    status = 3;
-                } else {
-                    const uint32_t idx = (uint32_t)__builtin_ctz(~live);
-                    slot_v = setl(slot_v, idx, slot);
-                    k_v = setl(k_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.k, i));
-                    cap_v = setl(cap_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.cap, i));
-                    b_v = setl(b_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.b, i));
-                    dense_v = setl(dense_v, slot, idx);
-                    live |= 1u << idx;
-                    ++n;
-                    dirty = true;
-                }
+    // One lane-phase event (<= 6 pending); true: an :invoke with 6 pending,
+    // for the dense phase.  CK: the event may be a checkpoint's :ok.  The
+    // events before the next checkpoint run the body without that test
+    // (LC_SPEC_CK_SPLIT), so the checkpoint words stay out of the hot loop.
+    auto lane_event = [&](auto ck_t) -> bool {
+        constexpr bool CK = decltype(ck_t)::value;
+        const uint32_t evi = __builtin_amdgcn_readlane(ev, i);
+        const uint32_t slot = LC_EV_SLOT(evi);
+        if (!(evi & LC_EV_OK_BIT)) {
+            if (n == 6) return true;
+            if (n >= T0_MAX_WIDTH || slot >= 64) {
+                status = 3;
             } else {
-                const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
-                int r;
-                // closed sets: exact ones (ok_lane, as the wide T0 keeps
-                // them) measured 10 % slower per event here
-                // sweeps specialised to the highest live index (one body for
-                // every live set measured 4 % slower per event here)
-                const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
-                if constexpr (EX) {
-                    // exact sets: p's transfer, then its lane cleared (as in lattice_key)
-                    const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
-                                   pb = __builtin_amdgcn_readlane(b_v, p);
-                    k_v = setl(k_v, p, 0u);
-                    uint32_t probes = 0, nSn = 0;
-                    if (top >= 6)
-                        r = ok_lane<6>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
-                                       false);
-                    else if (top == 5)
-                        r = ok_lane<5>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
-                                       false);
-                    else
-                        r = ok_lane<4>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
-                                       false);
+                const uint32_t idx = (uint32_t)__builtin_ctz(~live);
+                slot_v = setl(slot_v, idx, slot);
+                k_v = setl(k_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.k, i));
+                cap_v = setl(cap_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.cap, i));
+                b_v = setl(b_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.b, i));
+                dense_v = setl(dense_v, slot, idx);
+                live |= 1u << idx;
+                ++n;
+                dirty = true;
+            }
+        } else {
+            const uint32_t p = __builtin_amdgcn_readlane(dense_v, slot & 63u);
+            int r;
+            // closed sets: exact ones (ok_lane, as the wide T0 keeps
+            // them) measured 10 % slower per event here
+            // sweeps specialised to the highest live index (one body for
+            // every live set measured 4 % slower per event here)
+            const uint32_t top = 32u - (uint32_t)__builtin_clz(live);
+            if constexpr (EX) {
+                // exact sets: p's transfer, then its lane cleared (as in lattice_key)
+                const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
+                               pb = __builtin_amdgcn_readlane(b_v, p);
+                k_v = setl(k_v, p, 0u);
+                uint32_t probes = 0, nSn = 0;
+                if (top >= 6)
+                    r = ok_lane<6>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
+                                   false);
+                else if (top == 5)
+                    r = ok_lane<5>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
+                                   false);
+                else
+                    r = ok_lane<4>(W0, p, live, k_v, cap_v, b_v, pk, pc, pb, lane, lm, ~0ull, false, probes, nSn,
+                                   false);
+            } else {
+                if (top >= 6) r = ok_lane_closed<6>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
+                dirty = false;
+                k_v = setl(k_v, p, 0u);
+            }
+            live = r ? live : live & ~(1u << p);
+            n = r ? n : n - 1;
+            status = r;
+            fev = e;
+            if (CK && !r && e >= ck_at) {  // a checkpoint (a lane-phase :ok: the set is canonical)
+                if constexpr (MODE == 0) {
+                    ck_w[ck_i][lane] = W0;
+                    if (lane == 0) ck_e[ck_i] = (int32_t)(b + e);
+                    ++ck_i;
+                    ck_at = ck_i < 2 ? max(ck2, e + 1u) : ~0u;
                 } else {
-                    if (top >= 6) r = ok_lane_closed<6>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
-                    else if (top == 5) r = ok_lane_closed<5>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
-                    else r = ok_lane_closed<4>(W0, p, live, k_v, cap_v, b_v, lane, lm, dirty);
-                    dirty = false;
-                    k_v = setl(k_v, p, 0u);
-                }
-                live = r ? live : live & ~(1u << p);
-                n = r ? n : n - 1;
-                status = r;
-                fev = e;
-                if (!r && e >= ck_at) {  // a checkpoint (a lane-phase :ok: the set is canonical)
-                    if constexpr (MODE == 0) {
-                        ck_w[ck_i][lane] = W0;
-                        if (lane == 0) ck_e[ck_i] = (int32_t)(b + e);
-                        ++ck_i;
-                        ck_at = ck_i < 2 ? max(ck2, e + 1u) : ~0u;
+                    if (!__any(W0 != ck_w[ck_i][lane])) {
+                        status = 4;
                     } else {
-                        if (!__any(W0 != ck_w[ck_i][lane])) {
-                            status = 4;
-                        } else {
-                            ++ck_i;
-                            const int32_t nx = ck_i < 2 ? uni(ck_e[ck_i & 1]) : -1;
-                            ck_at = nx >= 0 ? (uint32_t)nx - b : ~0u;
-                            if (ck_i == 2) status = 5;
-                        }
+                        ++ck_i;
+                        const int32_t nx = ck_i < 2 ? uni(ck_e[ck_i & 1]) : -1;
+                        ck_at = nx >= 0 ? (uint32_t)nx - b : ~0u;
+                        if (ck_i == 2) status = 5;
                     }
                 }
             }
-            lim = status ? 0u : lim;
-            advance();
         }
+        lim = status ? 0u : lim;
+        advance();
+        return false;
+    };
+    for (uint32_t phase = 0; phase <= nev && e < lim; ++phase) {
+        bool dense = false;
+        while (e < lim) {  // lane phase: <= 6 pending
+#if LC_SPEC_CK_SPLIT
+            uint32_t stop = min(lim, ck_at);
+            while (e < stop) {
+                if (lane_event(std::false_type{})) { dense = true; break; }
+                stop = min(stop, lim);
+            }
+            if (dense || e >= lim) break;
+#endif
+            if (lane_event(std::true_type{})) { dense = true; break; }
+        }
+        (void)dense;
         if (e >= lim) break;
         W[0] = W0;
 #pragma unroll
@@ -2261,8 +2328,16 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 template <int S, bool E16>
 constexpr uint32_t spec_ev_lds() { return (E16 && S > 2) ? 4096u : 0u; }
 
+#ifndef LC_SPEC_KARG
+#define LC_SPEC_KARG 1
+#endif
 template <int S, int W, bool E16, bool EX = false>
 __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
+#if LC_SPEC_KARG
+#define KA t0k()
+#else
+#define KA a
+#endif
     constexpr uint32_t EVC = spec_ev_lds<S, E16>();
     __shared__ uint16_t s_ev[EVC ? EVC : 1];  // the key's event words (EvStaged)
     __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
@@ -2284,30 +2359,30 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     // T0_STRICT steps: the event-by-event validation, in nb blocks after the
     // keys' (no second stream, no cross-stream waits around the step), or
     // before them (T0_SPEC_VFIRST)
-    const uint32_t nb = gridDim.x - (uint32_t)a.n_order;
-    const bool vfirst = (a.flags & T0_SPEC_VFIRST) != 0;
+    const uint32_t nb = gridDim.x - (uint32_t)KA.n_order;
+    const bool vfirst = (KA.flags & T0_SPEC_VFIRST) != 0;
     const uint32_t blk = vfirst ? blockIdx.x - nb : blockIdx.x;  // the key block's LPT position
-    if (vfirst ? blockIdx.x < nb : blockIdx.x >= (uint32_t)a.n_order) {
-        const uint32_t vb = vfirst ? blockIdx.x : blockIdx.x - (uint32_t)a.n_order;
-        for (int64_t k = (int64_t)vb * W + wv; k < a.n_order; k += (int64_t)nb * W) {
+    if (vfirst ? blockIdx.x < nb : blockIdx.x >= (uint32_t)KA.n_order) {
+        const uint32_t vb = vfirst ? blockIdx.x : blockIdx.x - (uint32_t)KA.n_order;
+        for (int64_t k = (int64_t)vb * W + wv; k < KA.n_order; k += (int64_t)nb * W) {
             // (a key whose words its own block stages whole is validated
             // there, from LDS: see below)
-            if (EVC > 0 && !(a.flags & T0_SPEC_NOSTAGE) && a.ev_off[k + 1] - a.ev_off[k] <= EVC) continue;
+            if (EVC > 0 && !(KA.flags & T0_SPEC_NOSTAGE) && KA.ev_off[k + 1] - KA.ev_off[k] <= EVC) continue;
             validate_key<false, E16>(a, k);
         }
         return;  // the whole block: no barrier below is reached by half of it
     }
-    const int32_t key = a.order[blk];
-    uint32_t *ws = a.lat_ws + ((size_t)blk * W + wv) * (3 * T0_RMEM * 64);
-    const uint64_t eb = a.ev_off[key];
-    const uint32_t nev = (uint32_t)(a.ev_off[key + 1] - eb);
+    const int32_t key = KA.order[blk];
+    uint32_t *ws = KA.lat_ws + ((size_t)blk * W + wv) * (3 * T0_RMEM * 64);
+    const uint64_t eb = KA.ev_off[key];
+    const uint32_t nev = (uint32_t)(KA.ev_off[key + 1] - eb);
     // the key's words: staged in LDS (8 loads in flight per thread, then the
     // stores; made visible by the barrier below), else read from HBM
     uint32_t n_lds = 0;
     if constexpr (EVC > 0) {
-        if (!(a.flags & T0_SPEC_NOSTAGE)) {
+        if (!(KA.flags & T0_SPEC_NOSTAGE)) {
             n_lds = nev < EVC ? nev : EVC;
-            const uint16_t *g = a.events16 + eb;
+            const uint16_t *g = KA.events16 + eb;
             for (uint32_t base = 0; base < n_lds; base += 64u * W * 8u) {
                 uint16_t v[8];
 #pragma unroll
@@ -2325,17 +2400,17 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     }
     using EvK = typename std::conditional<(EVC > 0), EvStaged, EvSrc<E16>>::type;
     EvK evp;
-    if constexpr (EVC > 0) evp = EvStaged{s_ev, a.events16 + eb, n_lds};
-    else evp = ev_src<E16>(a) + eb;
-    const uint32_t tb = a.trans_off ? a.trans_off[key] : 0u;
-    const uint32_t ntr = a.n_trans > tb ? a.n_trans - tb : 0u;
-    const uint32_t *const trp = a.trans + (ntr ? tb : 0u);
-    const uint32_t nstates = a.trans_off ? (a.key_states ? a.key_states[key] : 0xFFFFu) : a.shared_states;
-    const uint32_t width = a.key_width ? a.key_width[key] : 0xFFu;
+    if constexpr (EVC > 0) evp = EvStaged{s_ev, KA.events16 + eb, n_lds};
+    else evp = ev_src<E16>(KA) + eb;
+    const uint32_t tb = KA.trans_off ? KA.trans_off[key] : 0u;
+    const uint32_t ntr = KA.n_trans > tb ? KA.n_trans - tb : 0u;
+    const uint32_t *const trp = KA.trans + (ntr ? tb : 0u);
+    const uint32_t nstates = KA.trans_off ? (KA.key_states ? KA.key_states[key] : 0xFFFFu) : KA.shared_states;
+    const uint32_t width = KA.key_width ? KA.key_width[key] : 0xFFu;
     // keys for the unsegmented search: errors, keys outside the tier (it
     // reports them), and keys too short to cut
-    const bool plain = (a.key_error && a.key_error[key]) || nstates > T0_MAX_STATES || nstates == 0 ||
-                       width > T0_MAX_WIDTH || a.init_state >= T0_MAX_STATES || nev < 2 * SPEC_MIN_LEN;
+    const bool plain = (KA.key_error && KA.key_error[key]) || nstates > T0_MAX_STATES || nstates == 0 ||
+                       width > T0_MAX_WIDTH || KA.init_state >= T0_MAX_STATES || nev < 2 * SPEC_MIN_LEN;
     const uint32_t eff = plain ? 1u : min((uint32_t)S, nev / SPEC_MIN_LEN);
     const uint32_t topmask = nstates >= 32 ? ~0u : (1u << nstates) - 1u;
 
@@ -2350,8 +2425,8 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     bool self_val = false;
     uint32_t vc0 = 0, vc1 = 0;
     if constexpr (EVC > 0) {
-        self_val = (a.flags & T0_STRICT) && !(a.flags & T0_SPEC_NOSTAGE) && n_lds == nev &&
-                   !(a.key_error && a.key_error[key]);
+        self_val = (KA.flags & T0_STRICT) && !(KA.flags & T0_SPEC_NOSTAGE) && n_lds == nev &&
+                   !(KA.key_error && KA.key_error[key]);
         const uint32_t nch = (nev + 63u) / 64u;
         vc0 = nch * wv / W;
         vc1 = nch * (wv + 1u) / W;
@@ -2379,7 +2454,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     // counts: the waves count the pending-count change over the parts
     // [t_p, t_p+1) (part p on wave p mod W), the parts' prefix gives the count
     // at each target, and the waves place the cuts likewise -- two barriers.
-    const bool cost = (a.flags & T0_SPEC_COST) != 0;
+    const bool cost = (KA.flags & T0_SPEC_COST) != 0;
     if (!plain && !cost) {
         for (uint32_t p = wv; p + 1 < eff; p += W) {
             const uint32_t t0 = (uint32_t)((uint64_t)nev * p / eff), t1 = (uint32_t)((uint64_t)nev * (p + 1) / eff);
@@ -2391,7 +2466,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     if constexpr (EVC > 0) {
         if (self_val) {
             // (the states a transition may install: as validate_key reads them)
-            const uint32_t vns = a.trans_off ? (a.key_states ? a.key_states[key] : 0u) : a.shared_states;
+            const uint32_t vns = KA.trans_off ? (KA.key_states ? KA.key_states[key] : 0u) : KA.shared_states;
             uint32_t pend[2] = {0u, 0u};
             for (uint32_t q = 0; q < wv; ++q) { pend[0] ^= uni(s_vx[q][0]); pend[1] ^= uni(s_vx[q][1]); }
             int32_t why = 0;
@@ -2402,8 +2477,8 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
                 why = validate_chunk<false, 2>(w, in, trp, ntr, vns, 64u, pend);
             }
             if (why && lane == 0) {
-                atomicOr(&a.err[0], why);
-                atomicMax(&a.err[1], a.err_base + key + 1);
+                atomicOr(&KA.err[0], why);
+                atomicMax(&KA.err[1], KA.err_base + key + 1);
             }
         }
     }
@@ -2487,7 +2562,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
             SpecState st{};
             uint32_t words = 0, np = 0;
             if (s == 0) {
-                st.W0 = lane == 0 ? 1u << a.init_state : 0u;
+                st.W0 = lane == 0 ? 1u << KA.init_state : 0u;
             } else {
                 words = spec_pending(evp, cut, n0, np);
                 spec_setup(st, words, np, trp, ntr);
@@ -2499,11 +2574,11 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
             // the ops found pending must be as many as the count says (else
             // the event stream is malformed): the key is searched unsegmented
             const bool lost = s != 0 && np != n0;
-            uint32_t *const sv = EX ? a.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS : nullptr;
+            uint32_t *const sv = EX ? KA.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS : nullptr;
             const int r = lost ? 6
                                : spec_walk<0, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
-                                                                   s_ck[s], s_ck_e[s], a.spec_ck1, a.spec_ck2, fev,
-                                                                   !(a.flags & T0_SPEC_NOPRIO), sv);
+                                                                   s_ck[s], s_ck_e[s], KA.spec_ck1, KA.spec_ck2, fev,
+                                                                   !(KA.flags & T0_SPEC_NOPRIO), sv);
             s_end[s][lane] = st.W0;
             uint64_t map = 0;
             for (uint32_t q = 0; q < 6; ++q) {
@@ -2551,7 +2626,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
                 st.W0 = lane < (1u << np) ? E : 0u;
                 uint32_t fev = 0;
                 uint32_t *const sv =
-                    EX ? a.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS + SPEC_SAVE_WORDS : nullptr;
+                    EX ? KA.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS + SPEC_SAVE_WORDS : nullptr;
                 const int r = spec_walk<1, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
                                                                 s_ck[s], s_ck_e[s], 0, 0, fev, false, sv);
                 bool last = true;
@@ -2574,7 +2649,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     }
     // 3. the key's verdict: the first segment whose real run dies
     if (wv == 0) {
-        const Args &f = *a.full;
+        const Args &f = *KA.full;
         bool rerun = plain, bad = false;
         int32_t fv = -1;
         // EX: the run whose set is the key's final one -- 2 x segment, + 1 for
@@ -2601,28 +2676,29 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
         // the unsegmented search runs in a launch of its own (k_spec_rerun):
         // inlined here it cost this kernel 27 VGPRs, 6 -> 4 waves per SIMD
         if (rerun) {
-            if (lane == 0) a.spec_rr[atomicAdd(a.spec_nrr, 1)] = key;
+            if (lane == 0) KA.spec_rr[atomicAdd(KA.spec_nrr, 1)] = key;
         } else if (bad) kr = K_SPILL;
         else if (fv >= 0) finish_key(f, key, LC_INVALID, LC_CAUSE_NONLIN, fv, 0, 0, (uint64_t)fv + 1u);
         else finish_key(f, key, LC_VALID, LC_CAUSE_NONE, -1, 0, 0, nev);
         if constexpr (EX) {
             if (!rerun && !bad) {
-                uint32_t *const sv = a.spec_fin + ((size_t)blk * S * 2 + fin_run) * SPEC_SAVE_WORDS;
+                uint32_t *const sv = KA.spec_fin + ((size_t)blk * S * 2 + fin_run) * SPEC_SAVE_WORDS;
                 const LatMem fm{sv, sv, sv};
                 write_final_mem(f, key, fm, lane, sv[T0_RMEM * 64 + lane], uni(sv[(T0_RMEM + 1) * 64]));
             }
         }
         if (kr == K_SPILL) {
-            if (a.flags & T0_STRICT) {
-                t0_malformed(a, key, LC_BATCH_E_FIT);
+            if (KA.flags & T0_STRICT) {
+                t0_malformed(KA, key, LC_BATCH_E_FIT);
                 finish_key(f, key, LC_UNKNOWN, LC_CAUSE_ERROR, -1, 0, 0, 0);
             } else {
-                const bool deep = f.deep && a.key_width && a.key_width[key] > LC_DIRECT_T3_WIDTH;
+                const bool deep = f.deep && KA.key_width && KA.key_width[key] > LC_DIRECT_T3_WIDTH;
                 push_list(deep ? f.deep : f.spill, deep ? f.n_deep : f.n_spill, key, f.list_cap);
             }
         }
     }
 }
+#undef KA
 
 // The keys k_spec left to the unsegmented search (compact T0, FAST).
 constexpr int SPEC_RERUN_WAVES = 4;

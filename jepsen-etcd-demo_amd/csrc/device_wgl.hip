@@ -126,6 +126,9 @@ extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
 // back through lc_debug_wgl_prof): [0] staging, [1] probe rounds, [2] child
 // scans inside them, [3] backtracks, [4] steps down before advance, [5]
 // advances, [6] probe-loop iterations, [7] steps.
+#ifndef LC_WGL_ADOPT
+#define LC_WGL_ADOPT 1
+#endif
 #ifdef LC_WGL_PROF
 __device__ unsigned long long lc_wgl_prof[8];
 #define WP_DECL uint64_t wp[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t wp_t = __builtin_amdgcn_s_memtime();
@@ -433,11 +436,18 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             uint64_t x2lo = 0, x2hi = 0;
             have_child = false;
             if (r_ok) {
-                // the whole move of R (the advance a step down taking R's op
-                // makes), into the child's own lane state: the step down
-                // adopts it instead of scanning again (the :invokes' prev
-                // words written on the way are functions of the event alone)
+                // narrow walks: the whole move of R (the advance a step down
+                // taking R's op makes), into the child's own lane state: the
+                // step down adopts it instead of scanning again (the
+                // :invokes' prev words written on the way are functions of the
+                // event alone).  Wide walks: only the child's key (the :oks)
+                // -- with many candidates R's op is seldom the one taken, and
+                // the whole scan is wasted (C2: 8.33 -> 8.07 ms with it, C4,
+                // mostly wide: 201 -> 220 ms; gating it on R's op having the
+                // earliest legal :invoke, two wave minima per round: 8.37 /
+                // 225 ms).  LC_WGL_ADOPT (A/B): 0 never, 2 every walk.
                 WP_MARK(1);
+                constexpr uint32_t whole = LC_WGL_ADOPT == 2 ? 1u : LC_WGL_ADOPT == 1 ? (WIDE ? 0u : 1u) : 0u;
                 uint32_t x2 = (lm & 0xFu) | lm_one(rs, LM_X);
                 uint32_t o0 = occ0, o1 = occ1, d0 = dsc0, d1 = dsc1;
                 z2 = zx ^ zob(rs);
@@ -454,6 +464,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                         R2 = j;
                         break;
                     }
+                    if (!whole) continue;
                     const uint32_t d = win.dsc(j);
                     const uint32_t l = sl & 63u;
                     if (!WIDE || sl < 64) { io.set_prev(j, rdl(o0, l)); o0 = wsetl(o0, l, j); d0 = wsetl(d0, l, d); }
@@ -463,7 +474,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                 x2lo = ballot(x2 & 1u);
                 x2hi = WIDE ? ballot(x2 & 2u) : 0ull;
                 ch_lm = x2; ch_occ0 = o0; ch_occ1 = o1; ch_dsc0 = d0; ch_dsc1 = d1; ch_R = R2; ch_z = z2;
-                have_child = true;
+                have_child = whole != 0;
                 WP_MARK(2);
             }
             // each candidate's child key
