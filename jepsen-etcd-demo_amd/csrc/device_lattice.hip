@@ -86,8 +86,13 @@ template <> struct EvSrc<true> {
 // A key's 16-bit event words staged in its workgroup's LDS (k_spec): the
 // first n_lds words from there, the rest from HBM.  The cut search, every
 // segment's TOP walk and its verifying run then read HBM once between them.
+// (The LDS copy is held as an LDS-typed pointer: a generic one made every
+// read a select between the two pointers and a flat load, waited on for both
+// counters at once -- C2 / C5 / C3-shard times equal either way, tools/
+// gpu_r4s.sh, but the window refill is a ds_read again.)
+using LdsU16 = __attribute__((address_space(3))) const uint16_t;
 struct EvStaged {
-    const uint16_t *l;  // the LDS copy
+    LdsU16 *l;          // the LDS copy
     const uint16_t *g;  // the words in HBM
     uint32_t n_lds;
     __device__ __forceinline__ uint32_t operator[](uint64_t j) const {
@@ -2400,7 +2405,7 @@ __global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
     }
     using EvK = typename std::conditional<(EVC > 0), EvStaged, EvSrc<E16>>::type;
     EvK evp;
-    if constexpr (EVC > 0) evp = EvStaged{s_ev, KA.events16 + eb, n_lds};
+    if constexpr (EVC > 0) evp = EvStaged{(LdsU16 *)s_ev, KA.events16 + eb, n_lds};
     else evp = ev_src<E16>(KA) + eb;
     const uint32_t tb = KA.trans_off ? KA.trans_off[key] : 0u;
     const uint32_t ntr = KA.n_trans > tb ? KA.n_trans - tb : 0u;
