@@ -150,6 +150,13 @@ __device__ __forceinline__ uint32_t setl(uint32_t v, uint32_t l, uint32_t x) {
     return (uint32_t)lc_writelane((int)x, (int)l, (int)v);
 }
 
+// x from lane (lane ^ 2^q), q < 6 uniform: one ds_bpermute on an address
+// (lane * 4) ^ (4 << q).  __shfl_xor adds a width check (a compare and a
+// select) and the shift of the lane index on every call.
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x, uint32_t q, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane << 2) ^ (4u << q)), (int)x);
+}
+
 // s & v as one v_and_b32 (kept opaque: the compiler would turn an AND with a
 // 0/~0 lane mask into a select through an SGPR pair)
 __device__ __forceinline__ uint32_t vand(uint32_t s, uint32_t v) {
@@ -425,7 +432,7 @@ __device__ __forceinline__ int ok_lane(uint32_t &W, uint32_t p, uint32_t live, u
                                        const uint32_t (&lm)[6], uint64_t budget, bool count, uint32_t &probes,
                                        uint32_t &nSn_out, bool want_size) {
     const uint32_t cand = live & ~(1u << p);
-    const uint32_t wup = (uint32_t)__shfl_xor((int)W, 1 << p);
+    const uint32_t wup = xor_lane(W, p, lane);
     // free indices and p hold zero accept masks in k_v (the caller cleared
     // lane p), so a position's masks need no gating by `cand`
     LaneMasks m;
@@ -534,8 +541,9 @@ __device__ __forceinline__ int ok_lane_closed(uint32_t &W, uint32_t p, uint32_t 
     }
     // (a DPP switch on p measured slower, in the compact T0 and in the
     // speculative segments' walk: 1,224 against 1,142 cycles per event)
-    const uint32_t up = (uint32_t)__shfl_xor((int)C, 1 << p);
-    const uint32_t Wn = ((lane >> p) & 1u) ? 0u : up;
+    const uint32_t up = xor_lane(C, p, lane);
+    // (lane bit p as a 0 / ~0 word: one v_bfe, and the select a v_bfi)
+    const uint32_t Wn = up & ~(uint32_t)__builtin_amdgcn_sbfe((int)lane, (int)p, 1);
     if (!__any(Wn != 0u)) return 1;
     W = Wn;
     return 0;
@@ -2108,14 +2116,20 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
         const uint32_t slot = LC_EV_SLOT(evi);
         if (!(evi & LC_EV_OK_BIT)) {
             if (n == 6) return true;
-            if (n >= T0_MAX_WIDTH || slot >= 64) {
+            // (n >= T0_MAX_WIDTH || slot >= 64 as one compare)
+            if ((n | (slot & ~63u)) >= T0_MAX_WIDTH) {
                 status = 3;
             } else {
                 const uint32_t idx = (uint32_t)__builtin_ctz(~live);
+                // the op's transfer read out first, then written: no wait
+                // states between a v_readlane and the v_writelane of its value
+                const uint32_t xk = (uint32_t)__builtin_amdgcn_readlane(xc.k, i),
+                               xcap = (uint32_t)__builtin_amdgcn_readlane(xc.cap, i),
+                               xb = (uint32_t)__builtin_amdgcn_readlane(xc.b, i);
                 slot_v = setl(slot_v, idx, slot);
-                k_v = setl(k_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.k, i));
-                cap_v = setl(cap_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.cap, i));
-                b_v = setl(b_v, idx, (uint32_t)__builtin_amdgcn_readlane(xc.b, i));
+                k_v = setl(k_v, idx, xk);
+                cap_v = setl(cap_v, idx, xcap);
+                b_v = setl(b_v, idx, xb);
                 dense_v = setl(dense_v, slot, idx);
                 live |= 1u << idx;
                 ++n;
