@@ -531,6 +531,11 @@ class Linearizable:
         ops_cache = None
         # the other checkers of a compose, and whether any reads a sub-history
         parts = [] if inner is self else list(inner.checkers.items())
+        # compose members whose answer is a constant (:timeline's stand-in):
+        # their map per key without the check-safe call and the per-key opts
+        const = {name for name, ch in parts if type(ch) is UnbridledOptimism}
+        only_const = all(ch is self or name in const for name, ch in parts)
+        draw = bool((test or {}).get("store-path"))
         valid = res.valid.tolist() if res is not None else []
         names = {code: name for code, name in N.ANALYZERS.items()}
         anl = res.analyzer.tolist() if res is not None and res.analyzer is not None else None
@@ -541,12 +546,18 @@ class Linearizable:
                 lin = {"analyzer": analyzer, "configs": [], "final-paths": [], "valid?": True}
             else:
                 lin = _render_key(packed, i, res, None, analyzer)
-            if lin.get("valid?") is False and (test or {}).get("store-path"):
+            if draw and lin.get("valid?") is False:
                 if ops_cache is None:
                     ops_cache = history if not isinstance(history, History) else history.to_ops()
                 _draw(test, subhistory(ops_cache, k), lin, ["independent", str(k)])
             if inner is self:
                 results[k] = lin
+                continue
+            if only_const:
+                # {:linear lin, :timeline {:valid? true}}: merge-valid is lin's
+                r = {name: (lin if ch is self else {"valid?": True}) for name, ch in parts}
+                r["valid?"] = merge_valid((lin.get("valid?"),))
+                results[k] = r
                 continue
             # compose: run the other checkers per key on the host (the
             # sub-history is built only for checkers that read one)
@@ -555,6 +566,9 @@ class Linearizable:
             for name, ch in parts:
                 if ch is self:
                     r[name] = lin
+                    continue
+                if name in const:
+                    r[name] = {"valid?": True}
                     continue
                 if sub is None and getattr(ch, "needs_history", True):
                     if ops_cache is None:
