@@ -1477,7 +1477,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         // the same launch (a second stream cost ~40 us of cross-stream waits)
         const int vblocks = a.strict ? (int)std::min<int64_t>(K, c->cu_count) : 0;
         HIPCHK(lcd::launch_spec(a0, dargs, segs, waves, c->spec_ws, c->spec_rr, c->spec_parity, ck1, ck2,
-                                c->cu_count * 4, vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
+                                // (rerun blocks: the launch usually finds no
+                                // key, so one block per CU keeps its dispatch
+                                // short; a longer rerun list walks the grid)
+                                c->cu_count, vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
                                 !(o.path_flags & LC_PATH_SPEC_NOPRIO),
                                 K * waves > (int64_t)c->cu_count * 16,  // more keys than one resident round
                                 exact_spec && !fast ? c->spec_fin : nullptr,

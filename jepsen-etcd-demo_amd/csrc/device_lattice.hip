@@ -2749,7 +2749,7 @@ __global__ __launch_bounds__(64 * SPEC_RERUN_WAVES) void k_spec_rerun(T0Args a) 
 size_t spec_ws_words(int64_t n_keys, int segs) { return (size_t)std::max<int64_t>(n_keys, 1) * segs * lat_ws_words(); }
 
 // Keys order[0 .. n_order) in workgroups of `segs` segments (2, 3, 4, 6 or
-// 8); ws: spec_ws_words(n_order, segs) words; rr: n_order + 2 ints (two
+// 8); rerun_grid: workgroups of the rerun launch at most; ws: spec_ws_words(n_order, segs) words; rr: n_order + 2 ints (two
 // rerun counts used in turn -- `parity` picks this launch's, which must be
 // zero, and k_spec_rerun zeroes the other -- then the rerun list).
 // validate: add the T0_STRICT validation blocks.
@@ -2775,7 +2775,7 @@ hipError_t launch_spec(const Args &a, const Args *a_dev, int segs, int waves, ui
     t.spec_rr = rr + 2;
     t.spec_fin = fin;
     const dim3 grid((unsigned)std::max(1, a.n_order + std::max(0, validate_blocks)));
-    const dim3 rgrid((unsigned)std::max(1, std::min(a.n_order, rerun_grid) / SPEC_RERUN_WAVES));
+    const dim3 rgrid((unsigned)std::max(1, std::min((a.n_order + SPEC_RERUN_WAVES - 1) / SPEC_RERUN_WAVES, rerun_grid)));
     // one wave per segment: more segments than waves (8, 12 or 16 on 4
     // waves, 4 or 8 on 2) measured slower (device_api.hip)
     (void)waves;
