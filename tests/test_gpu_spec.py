@@ -54,6 +54,21 @@ def test_spec_matches_oracle(shape):
         assert (orc["valid"] == 0).any()
 
 
+def test_spec_reruns_walk_the_rerun_grid():
+    """More keys left to the unsegmented search than the rerun launch has
+    waves (k_spec_rerun runs one 4-wave workgroup per CU, 1,024 waves on the
+    MI355X): checkpoints at the cut make runs miss each other, so most of the
+    3,000 keys go through the rerun kernel's grid-stride loop -- verdicts,
+    causes and failing events still the oracle's."""
+    h = H.synth(n_keys=3000, ops_per_key=300, concurrency=10, anomaly_rate=0.2, seed=102)
+    pk = Packed(h)
+    _, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)
+    for segs in (2, 4):
+        dev = Device(0, path_flags=N.LC_PATH_SPLIT_OFF, spec_segs=segs, spec_ck=(0, 0))
+        _check(dev, pk, orc, f"reruns, segs {segs}")
+    assert (orc["valid"] == 0).any()
+
+
 def test_spec_default_on_c2_shape():
     """The default choice for a C2-sized verdicts-only batch is the
     speculative path (checked through its result only: same as the oracle)."""
