@@ -353,7 +353,7 @@ struct Part {
 #define LC_T3L_TSA 4u
 #endif
 #ifndef LC_T3L_TSB
-#define LC_T3L_TSB 3u
+#define LC_T3L_TSB 2u  // C4 at 2^16: 14.09-14.12 ms against 14.28-14.32 (3) and 14.37 (5), tools/gpu_r4zb.sh, gpu_r4zc.sh
 #endif
 constexpr int UP = LC_T3L_UP;  // successor pairs per thread in flight (A/B: make variant VFLAGS=-DLC_T3L_UP=n)
 // The first two entries per thread of an S layer [sb, se), loaded ahead.
