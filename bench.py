@@ -64,7 +64,7 @@ for p in (os.path.join(ROOT, "jepsen-etcd-demo_amd"), os.path.join(ROOT, "oracle
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # profiles/*.json summaries (rocprofv3 --pmc / SQ) are used for `traffic` /
 # `issue` only when they were taken of this round's build
-PROFILE_ROUND = 4
+PROFILE_ROUND = 5
 ALGORITHMS = {"linear": 0, "wgl": 1, "competition": 2}
 SHADER_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 METRIC = "history ops linearizability-checked/sec (whole node)"
@@ -230,10 +230,20 @@ def bench_jepsen(args):
     n_bad = sum(r["valid?"] is False for r in res.values())
     parity = None
     if not args.no_cpu:
+        # each key against the oracle of the analysis that answered it
+        # (:analyzer -- competition answers :linear's budget keys with WGL)
         import cref
         keys, orc = cref.check_history(hist.as_c(), budget=args.budget, threads=16)
-        fails = sorted(int(k) for k, r in zip(keys, orc) if r["valid"] == 0)
-        parity = bool(sorted(out["failures"]) == fails)
+        worc = None
+        if args.algorithm != "linear":
+            _, worc, _, _ = cref.check_history_wgl(hist.as_c(), budget=args.budget, threads=16)
+        fails = []
+        for i, k in enumerate(keys):
+            anl = res[int(k)]["linear"].get("analyzer", "linear") if "linear" in res[int(k)] else "linear"
+            o = worc if anl == "wgl" else orc
+            if o[i]["valid"] == 0:
+                fails.append(int(k))
+        parity = bool(sorted(out["failures"]) == sorted(fails))
     line = {
         "metric": METRIC, "value": (n_valid + n_bad) * ops * args.steps / elapsed, "unit": "ops/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -336,6 +346,32 @@ def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quo
     if args.algorithm == "wgl":
         parity = bool(np.array_equal(worc["valid"], v_host[:kw]) and np.array_equal(worc["fail_event"], fe_host[:kw]))
     return cpu, parity
+
+
+def profile_mismatch(d, K, kname):
+    """Why a profiles/ summary does not describe the launch the line divides
+    by (None when it does): its key count, and whole launches only."""
+    if d.get("keys") != K:
+        return f"profile of {d.get('keys')} keys, launch of {K}"
+    if not d.get("whole_launch") or not d.get("grid_size"):
+        return "no whole-launch grid recorded (a median over dispatches of mixed size)"
+    if ("k_spec" in kname or "k_search_lattice" in kname) and d.get("workgroups", 0) < K:
+        # the register tier runs one workgroup per key (plus validation blocks)
+        return f"{d.get('workgroups')} workgroups < {K} keys: a chunk launch"
+    return None
+
+
+def probe_rates(probes, probes_t3, avg_t0, avg_t3, d1_t3, wgl):
+    """Probes per second of each tier's launch (None where not measured)."""
+    out = {}
+    if probes is not None and avg_t0 > 0:
+        t0p = probes - (probes_t3 or 0)
+        out["t0"] = t0p / (avg_t0 * 1e-3) if t0p > 0 else None
+    if probes_t3 and avg_t3 > 0:
+        out["t3"] = probes_t3 / (avg_t3 * 1e-3)
+    if wgl and wgl.get("probes") and wgl.get("ms_per_launch"):
+        out["wgl"] = wgl["probes"] / (wgl["ms_per_launch"] * 1e-3)
+    return out or None
 
 
 def bench_c3_strong(args, local):
@@ -680,6 +716,7 @@ def main():
         traffic = traffic_src = issue = None
         if "k_wgl" not in dominant:
             tags = (t0_name,) if "T0" in dominant else ("k_search_layers",)
+        refused = []
         for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*.json"))):
             try:
                 d = json.load(open(fpath))
@@ -692,6 +729,14 @@ def main():
                     or d.get("round") != PROFILE_ROUND or d.get("algorithm", "linear") != args.algorithm
                     or not any(t in kname for t in tags)):
                 continue
+            # counters of the launch this line divides by, and nothing else:
+            # the same key count, and whole launches only (tools/
+            # profile_summary.py keeps the dispatches of the largest grid; a
+            # chunk launch of a large shard's synchronous step is not one)
+            why = profile_mismatch(d, K, kname)
+            if why:
+                refused.append({"file": os.path.basename(fpath), "why": why})
+                continue
             if d.get("bytes_per_launch"):
                 traffic, traffic_src = d["bytes_per_launch"], os.path.basename(fpath)
             if d.get("sq_insts_valu_per_launch") and kt > 0:
@@ -702,7 +747,8 @@ def main():
                 cap = simds * SHADER_CLOCK_HZ / 2 * kt * 1e-3
                 issue = {"valu_per_launch": d["sq_insts_valu_per_launch"], "capacity": cap,
                          "frac": d["sq_insts_valu_per_launch"] / cap, "simds": simds,
-                         "clock_ghz": SHADER_CLOCK_HZ / 1e9, "source": os.path.basename(fpath)}
+                         "clock_ghz": SHADER_CLOCK_HZ / 1e9, "source": os.path.basename(fpath),
+                         "grid_size": d.get("grid_size"), "waves_per_launch": d.get("sq_waves_per_launch")}
         nproc, aff, quota = host_cores()
         cpu = parity = None
         if world == 1 and not args.no_cpu:
@@ -749,6 +795,10 @@ def main():
             "wgl": wgl,
             "probes": probes,
             "probes_t3": probes_t3,
+            # hash-probe throughput (north_star; SURVEY D-4): the oracle's
+            # probe count of the tier over that tier's launch time
+            "probes_per_s": probe_rates(probes, probes_t3, avg_t0, avg_t3, d1_t3, wgl),
+            "profiles_refused": refused or None,
             "ns_per_event_critical_path": avg_t0 * 1e6 / max(max_events, 1),
             "verdicts": {"valid": int((nv == 1).sum()), "invalid": int((nv == 0).sum()),
                          "unknown": int((nv == -1).sum())},
