@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 10
+#define LC_ABI_VERSION 11
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -220,7 +220,14 @@ typedef struct lc_pack_opts {
     int32_t model;     /* LC_MODEL_* (0 = cas-register) */
     int32_t n_init;    /* multi-register: initial registers, pairs        */
     const int64_t *init;  /* [2 * n_init] (register, value); others absent */
+    uint32_t flags;    /* LC_PACK_* (ABI 11); 0 = the library's choice     */
 } lc_pack_opts;
+
+/* lc_pack_opts.flags: path pins for A/B runs and tests; the packed batch is
+ * byte-identical whichever path builds it. */
+#define LC_PACK_GENERAL 0x1u  /* always the bucketing path (rows of a key
+                                 gathered through a row list), never the
+                                 key-major one (each key's rows one run)   */
 
 typedef struct lc_packed lc_packed;  /* library-owned */
 
@@ -246,6 +253,12 @@ int  lc_packed_view(const lc_packed *p, lc_batch *out);
 int64_t lc_packed_key(const lc_packed *p, int64_t i);
 /* History row (0-based position in the lc_history) of event j of key i. */
 int64_t lc_packed_event_row(const lc_packed *p, int64_t i, int64_t j);
+/* Which lc_pack path built p (diagnostics, ABI 11): 1 = key-major (every
+ * key's rows one run of the history), 0 = bucketing. */
+int lc_packed_path(const lc_packed *p);
+/* The history row of every event, in event order (ev_off's numbering);
+ * out may be NULL to query the count (ABI 11). */
+int64_t lc_packed_event_rows(const lc_packed *p, int64_t *out);
 /* Number of history rows in key i's sub-history (incl. nemesis rows) and the
  * rows themselves (out may be NULL to query the count). */
 int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows);
@@ -451,6 +464,10 @@ typedef struct lc_dev_batch lc_dev_batch;
 int         lc_abi_version(void);
 const char *lc_last_error(void);
 int         lc_device_count(void);
+/* Give back the host blocks the library keeps for reuse (page-locked and
+ * heap; up to 1 GB each, held after their arrays are freed).  Also done when
+ * the last context is destroyed.  Arrays still in use are not touched. */
+void        lc_trim(void);
 
 int  lc_create(const lc_opts *opts, lc_ctx **out);
 void lc_destroy(lc_ctx *ctx);

@@ -257,7 +257,7 @@
         _          (doseq [[j [r x]] (map-indexed vector init)]
                      (.setLong init-mem (* 16 j) (reg-id names r))
                      (.setLong init-mem (+ 8 (* 16 j)) (long-or-nil x)))
-        pack-opts  (doto (Memory. 16) (.clear)                 ; sizeof(lc_pack_opts), ABI 8
+        pack-opts  (doto (Memory. 24) (.clear)                 ; sizeof(lc_pack_opts), ABI 11 (flags 0)
                      (.setInt 0 (int (model-code model)))
                      (.setInt 4 (int (count init)))
                      (.setPointer 8 init-mem))

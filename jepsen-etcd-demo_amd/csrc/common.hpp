@@ -2,11 +2,17 @@
 // history storage.  Host code only (no device code in this header).
 #pragma once
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lincheck.h"
@@ -97,6 +103,129 @@ struct UninitAlloc : std::allocator<T> {
 };
 template <class T>
 using uninit_vector = std::vector<T, UninitAlloc<T>>;
+
+
+// Host memory of a size fixed at allocation, page-locked or not by a choice
+// made at run time (lc_pack decides after the pairing pass which event
+// array the device will read: the 16-bit words when every word fits, else
+// the 32-bit ones).  Not zero-filled.
+template <class T>
+class host_array {
+  public:
+    host_array() = default;
+    host_array(const host_array &) = delete;
+    host_array &operator=(const host_array &) = delete;
+    ~host_array() { release(); }
+    void alloc(size_t n, bool pinned) {
+        release();
+        if (n == 0) return;
+        const size_t bytes = n * sizeof(T);
+        void *p = pinned ? pinned_alloc(bytes) : (bytes >= BIG_BLOCK ? big_alloc(bytes) : std::malloc(bytes));
+        if (!p) throw std::bad_alloc();
+        p_ = (T *)p;
+        n_ = n;
+        pinned_ = pinned;
+    }
+    // Take another array's storage (and its pinning).
+    void adopt(host_array &o) {
+        release();
+        p_ = o.p_; n_ = o.n_; pinned_ = o.pinned_;
+        o.p_ = nullptr; o.n_ = 0;
+    }
+    void release() {
+        if (p_) {
+            const size_t bytes = n_ * sizeof(T);
+            if (pinned_) pinned_free(p_);
+            else if (bytes >= BIG_BLOCK) big_free(p_, bytes);
+            else std::free(p_);
+        }
+        p_ = nullptr;
+        n_ = 0;
+    }
+    T *data() { return p_; }
+    const T *data() const { return p_; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    bool pinned() const { return pinned_; }
+    T &operator[](size_t i) { return p_[i]; }
+    const T &operator[](size_t i) const { return p_[i]; }
+
+  private:
+    T *p_ = nullptr;
+    size_t n_ = 0;
+    bool pinned_ = false;
+};
+
+// Drop every cached host block (pinned and heap): lc_trim, and the last
+// lc_destroy.
+void trim_host_caches();
+
+// Host worker threads kept for the life of a context (per-event validation
+// and staging copies; one driver per extra device).  run(n, fn) calls
+// fn(0..n-1) on the workers and the caller, and returns when all have
+// finished.  Not reentrant: one run at a time.
+class HostPool {
+  public:
+    explicit HostPool(unsigned n) {
+        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+    void run(unsigned n, const std::function<void(unsigned)> &fn) {
+        n = std::min(n, size());
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &fn;
+            n_ = n;
+            pending_ = n > 1 ? n - 1 : 0;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)> *fn;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (id >= n_) continue;
+                fn = fn_;
+            }
+            (*fn)(id);
+            std::lock_guard<std::mutex> g(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)> *fn_ = nullptr;
+    unsigned n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// The process's host worker pool for lc_pack (created on first use, up to 16
+// threads with the caller).  run() is not reentrant: a caller that finds it
+// busy (another thread packing) gets nullptr and works without it.
+HostPool *pack_pool_acquire();
+void pack_pool_release();
 
 }  // namespace lc
 

@@ -140,66 +140,7 @@ __global__ void k_pack_records(const int8_t *valid, const uint8_t *cause, const 
 
 }  // namespace
 
-// Host worker threads kept for the life of a context (per-event validation
-// and staging copies; one driver per extra device).  run(n, fn) calls
-// fn(0..n-1) on the workers and the caller, and returns when all have
-// finished.  Not reentrant: one run at a time.
-class HostPool {
-  public:
-    explicit HostPool(unsigned n) {
-        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i + 1); });
-    }
-    ~HostPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
-    }
-    unsigned size() const { return (unsigned)th_.size() + 1; }
-    void run(unsigned n, const std::function<void(unsigned)> &fn) {
-        n = std::min(n, size());
-        {
-            std::lock_guard<std::mutex> g(m_);
-            fn_ = &fn;
-            n_ = n;
-            pending_ = n > 1 ? n - 1 : 0;
-            ++gen_;
-        }
-        cv_.notify_all();
-        fn(0);
-        std::unique_lock<std::mutex> g(m_);
-        done_.wait(g, [this] { return pending_ == 0; });
-        fn_ = nullptr;
-    }
-
-  private:
-    void loop(unsigned id) {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(unsigned)> *fn;
-            {
-                std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                if (id >= n_) continue;
-                fn = fn_;
-            }
-            (*fn)(id);
-            std::lock_guard<std::mutex> g(m_);
-            if (--pending_ == 0) done_.notify_one();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::function<void(unsigned)> *fn_ = nullptr;
-    unsigned n_ = 0, pending_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
+using lc::HostPool;
 
 // One device's part of a batch in HBM.
 struct DevBatch {
@@ -601,6 +542,8 @@ extern "C" int lc_comm_id(uint8_t *out) {
     return LC_OK;
 }
 
+static std::atomic<int> g_live_ctx{0};
+
 extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
     if (!out) return lc::fail(LC_E_INVALID, "lc_create: null out");
     lc_opts o{};
@@ -673,10 +616,19 @@ extern "C" int lc_create(const lc_opts *opts, lc_ctx **out) {
         c->size = o.comm_size;
     }
     *out = c;
+    g_live_ctx.fetch_add(1);
     return LC_OK;
 }
 
-extern "C" void lc_destroy(lc_ctx *c) { delete c; }
+// The last context's destruction also gives back the host blocks the
+// library keeps for reuse (page-locked memory is a limited resource; a JVM
+// that checked once should not hold it for its life).  lc_trim does it
+// at any time.
+extern "C" void lc_destroy(lc_ctx *c) {
+    if (!c) return;
+    delete c;
+    if (g_live_ctx.fetch_sub(1) == 1) lc::trim_host_caches();
+}
 
 // ---- validation -------------------------------------------------------------
 
@@ -689,6 +641,12 @@ extern "C" void lc_destroy(lc_ctx *c) { delete c; }
 // words; each thread copies the contiguous run of keys it validates, so the
 // events are read once, in cache, on their way to the DMA engine.
 // check = false: the copy alone (a batch T0 validates itself).
+// Event word j of b: the 32-bit words, or the 16-bit ones widened (lc_pack
+// gives only those when every word fits).
+static inline uint32_t ev_at(const lc_batch *b, uint64_t j) {
+    return b->events ? b->events[j] : LC_EV16_WIDE(b->events16[j]);
+}
+
 static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *stage, HostPool *hp, bool check = true) {
     const int64_t K = b->n_keys;
     unsigned nt = hp ? hp->size() : 1;
@@ -703,8 +661,12 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
         cut[t] = std::upper_bound(b->ev_off, b->ev_off + K, n_ev * t / nt) - b->ev_off - 1;
     auto work = [&](unsigned t) {
         const int64_t k0 = std::max<int64_t>(cut[t], 0), k1 = std::max<int64_t>(cut[t + 1], k0);
-        if (stage && k1 > k0)
-            std::memcpy(stage + b->ev_off[k0], b->events + b->ev_off[k0], (b->ev_off[k1] - b->ev_off[k0]) * 4);
+        if (stage && k1 > k0) {
+            if (b->events)
+                std::memcpy(stage + b->ev_off[k0], b->events + b->ev_off[k0], (b->ev_off[k1] - b->ev_off[k0]) * 4);
+            else
+                for (uint64_t j = b->ev_off[k0]; j < b->ev_off[k1]; ++j) stage[j] = LC_EV16_WIDE(b->events16[j]);
+        }
         if (!check) return;
         for (int64_t k = k0; k < k1 && !bad[t]; ++k) {
             if (b->key_error && b->key_error[k]) continue;  // not searched
@@ -717,7 +679,7 @@ static int validate_events(const lc_batch *b, int64_t *badkey_out, uint32_t *sta
             uint64_t pend[2] = {0, 0};
             uint32_t width = 0;
             for (uint64_t j = b->ev_off[k]; j < b->ev_off[k + 1]; ++j) {
-                const uint32_t ev = b->events[j];
+                const uint32_t ev = ev_at(b, j);
                 const uint32_t s = LC_EV_SLOT(ev);
                 // slot 127 marks ops beyond the encodable window: the search
                 // stops (LC_CAUSE_WINDOW) before it could follow one.
@@ -773,7 +735,7 @@ static int validate_batch(const lc_batch *b) {
         if (b->ev_off[k + 1] < b->ev_off[k]) return lc::fail(LC_E_INVALID, "batch: ev_off not monotone at key %lld", (long long)k);
         if (b->ev_off[k + 1] - b->ev_off[k] > 0x7FFFFFFFull) return lc::fail(LC_E_INVALID, "batch: key %lld has > 2^31 events", (long long)k);
     }
-    if (b->ev_off[b->n_keys] && !b->events) return lc::fail(LC_E_INVALID, "batch: events missing");
+    if (b->ev_off[b->n_keys] && !b->events && !b->events16) return lc::fail(LC_E_INVALID, "batch: events missing");
     if (b->init_state >= LC_STATE_NONE) return lc::fail(LC_E_INVALID, "batch: bad init_state");
     if (b->table) {
         // rows of a table model: trans[] are offsets into table[], checked per
@@ -810,7 +772,7 @@ struct Shape {
 // longest stretch is at most a quarter of their length.
 static bool segments_pay(const lc_batch *b) {
     const int64_t K = b->n_keys;
-    if (K <= 0 || !b->events) return false;
+    if (K <= 0 || (!b->events && !b->events16)) return false;
     uint64_t len = 0, gap = 0;
     for (int s = 0; s < 4; ++s) {
         const int64_t k = K * s / 4;
@@ -818,7 +780,7 @@ static bool segments_pay(const lc_batch *b) {
         int64_t pend = 0;
         uint64_t last = e0;
         for (uint64_t j = e0; j < e1; ++j) {
-            pend += (b->events[j] & LC_EV_OK_BIT) ? -1 : 1;
+            pend += (ev_at(b, j) & LC_EV_OK_BIT) ? -1 : 1;
             if (pend == 0) {
                 gap = std::max(gap, j + 1 - last);
                 last = j + 1;
@@ -933,8 +895,13 @@ static int upload_into(Dev *c, const lc_batch *b, DevBatch *d, const Shape &sh, 
     // page-locked 16-bit words crosses the host link at 2 bytes per event and
     // is widened on the device (the register tier validates what it reads).
     HIPCHK(grow(d->mem[1], d->events, (size_t)d->n_events));
-    const bool use16 = d->n_events && b->events16 && sh.t0_only && !(c->o->path_flags & LC_PATH_EV32) &&
-                       (!events_src || events_src == b->events) && pinned(b->events16);
+    // (a batch with no 32-bit words at all crosses as 16-bit words whatever
+    // its tiers: prepare_batch widened them into events_src where the host
+    // must, and the device widens them otherwise)
+    const bool use16 = d->n_events && b->events16 &&
+                       ((sh.t0_only && !(c->o->path_flags & LC_PATH_EV32) && (!events_src || events_src == b->events) &&
+                         pinned(b->events16)) ||
+                        (!b->events && !events_src));
     d->ev32_ready = !use16;
     if (use16) {
         // widened on the device only if a step's kernels need the 32-bit
@@ -1729,7 +1696,13 @@ static int prepare_batch(lc_ctx *c, const lc_batch *b, Shape *sh, const uint32_t
     const size_t n_ev = (size_t)b->ev_off[K];
     // Batches above 256 MB of events keep the pageable path (no pinned
     // allocation that large); page-locked caller memory is used as it is.
-    const bool stage = n_ev > 0 && n_ev <= (256u << 20) / 4 && !pinned(b->events);
+    // A batch given only as 16-bit words is widened here when its upload
+    // needs the 32-bit ones (keys beyond the register tier, or the A/B flag
+    // LC_PATH_EV32); a register-tier batch uploads the 16-bit words.
+    const bool up16 = b->events16 && sh->t0_only && !(c->o.path_flags & LC_PATH_EV32);
+    const bool widen = n_ev > 0 && !b->events && !up16;
+    const bool stage = widen || (n_ev > 0 && b->events && n_ev <= (256u << 20) / 4 && !pinned(b->events) &&
+                                 !(up16 && pinned(b->events16)));
     if (stage && n_ev > c->hstage_cap) {
         if (c->hstage) (void)hipHostFree(c->hstage);
         c->hstage = nullptr;

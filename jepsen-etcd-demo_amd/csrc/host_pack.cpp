@@ -401,7 +401,7 @@ void pack_multi_register(const lc_history &h, const int64_t *init, int32_t n_ini
     P->mr_reg_off.assign((size_t)K + 1, 0);
     P->mr_state_off.assign((size_t)K + 1, 0);
     for (int64_t k = 0; k < K; ++k) P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + ko[(size_t)k].ev.size();
-    P->events.resize((size_t)P->ev_off[(size_t)K]);
+    P->events.alloc((size_t)P->ev_off[(size_t)K], true);
     P->ev_row.resize((size_t)P->ev_off[(size_t)K]);
     for (int64_t k = 0; k < K; ++k) {
         MrKey &m = mr[(size_t)k];
@@ -435,6 +435,707 @@ void pack_multi_register(const lc_history &h, const int64_t *init, int32_t n_ini
     if (P->table.empty()) P->table.push_back(LC_TABLE_NONE);
 }
 
+
+// ---- register models: interning shared by both pack paths ----------------
+
+// Keys' surviving ops, interned, in arenas (no allocation per key): per key
+// the state values a write / cas can install and the distinct (f, a, b)
+// triples of its invokes, both in order of first appearance (invoke
+// order); number_and_describe then gives each triple its transition id.
+struct Arena {
+    std::vector<int64_t> vals;  // state values, key after key
+    std::vector<int64_t> trip;  // triples (3 words each), key after key
+    std::vector<uint32_t> tid;  // per triple: its transition id (number_and_describe)
+};
+struct KeySpan {                // one key's part of an arena
+    uint32_t arena = 0, nv = 0, nt = 0;  // values, triples
+    uint64_t v0 = 0, t0 = 0;    // first value, first triple (in triples)
+};
+
+// Per-thread interning tables, reset per key.  Small values (0 .. 14, and
+// nil) -- what Jepsen register tests write -- go through direct tables
+// stamped per key; others through a set / an open-addressing table of index
+// + 1 kept under half full.
+class Interner {
+  public:
+    void begin(Arena *A, int model) {
+        A_ = A;
+        model_ = model;
+        v0_ = A->vals.size();
+        t0_ = A->trip.size();
+        if (dstamp_.empty()) { dstamp_.assign(8 * 16 * 16, 0); dtrip_.assign(8 * 16 * 16, 0); }
+        if (++kstamp_ == 0) { std::fill(dstamp_.begin(), dstamp_.end(), 0u); kstamp_ = 1; }
+        vseen_ = 0;
+        seen_.clear();
+        tmask_ = 255;
+        tt_.assign(tmask_ + 1, 0);
+        if (model == LC_MODEL_MUTEX) A->vals.push_back(1);  // state 1 = locked (state 0, "nil", = unlocked)
+    }
+    // this key's span (call after its last op)
+    KeySpan end(uint32_t arena) const {
+        KeySpan sp;
+        sp.arena = arena;
+        sp.v0 = v0_;
+        sp.nv = (uint32_t)(A_->vals.size() - v0_);
+        sp.t0 = t0_ / 3;
+        sp.nt = (uint32_t)((A_->trip.size() - t0_) / 3);
+        return sp;
+    }
+    // A surviving op (its values after complete's fill): its state value,
+    // and the index of its (f, a, b) triple among the key's.
+    uint32_t op(int64_t f, int64_t v0, int64_t v1) {
+        if (model_ != LC_MODEL_MUTEX) {
+            if (f == LC_F_WRITE) add(v0);
+            if (f == LC_F_CAS) add(v1);
+        }
+        const int64_t a = (f == LC_F_ACQUIRE || f == LC_F_RELEASE) ? 0 : v0;
+        const int64_t b = f == LC_F_CAS ? v1 : 0;
+        const int64_t sa = small(a), sb = small(b);
+        if (sa >= 0 && sb >= 0 && f < 8) {
+            const size_t di = (size_t)f * 256 + (size_t)sa * 16 + (size_t)sb;
+            if (dstamp_[di] != kstamp_) {
+                dstamp_[di] = kstamp_;
+                dtrip_[di] = new_trip(f, a, b);
+            }
+            return dtrip_[di];
+        }
+        const int64_t *tr = A_->trip.data() + t0_;
+        size_t x = thash(f, a, b) & tmask_;
+        for (;; x = (x + 1) & tmask_) {
+            const uint64_t e = tt_[x];
+            if (!e) {
+                const uint32_t ti = new_trip(f, a, b);
+                tt_[x] = ti + 1;
+                if ((size_t)(ti + 1) * 2 > tmask_) {  // grow
+                    tmask_ = tmask_ * 2 + 1;
+                    tt_.assign(tmask_ + 1, 0);
+                    const int64_t *t2 = A_->trip.data() + t0_;
+                    for (uint32_t u = 0; u <= ti; ++u) {
+                        size_t y = thash(t2[3 * u], t2[3 * u + 1], t2[3 * u + 2]) & tmask_;
+                        while (tt_[y]) y = (y + 1) & tmask_;
+                        tt_[y] = u + 1;
+                    }
+                }
+                return ti;
+            }
+            const uint32_t u = (uint32_t)e - 1;
+            if (tr[3 * u] == f && tr[3 * u + 1] == a && tr[3 * u + 2] == b) return u;
+        }
+    }
+
+  private:
+    static constexpr int64_t SMALL = 15;  // values 0 .. 14, plus nil as 15
+    static int64_t small(int64_t v) { return v == LC_NIL ? SMALL : (v >= 0 && v < SMALL ? v : -1); }
+    static size_t thash(int64_t f, int64_t a, int64_t b) {
+        uint64_t x = (uint64_t)f * 0x9E3779B97F4A7C15ull ^ (uint64_t)a * 0xC2B2AE3D27D4EB4Full ^
+                     (uint64_t)b * 0x165667B19E3779F9ull;
+        return (size_t)(x ^ (x >> 29));
+    }
+    void add(int64_t v) {
+        if (v == LC_NIL) return;
+        std::vector<int64_t> &vals = A_->vals;
+        const int64_t sv = small(v);
+        if (sv >= 0) {
+            if (vseen_ >> sv & 1u) return;
+            vseen_ |= 1u << sv;
+            vals.push_back(v);
+            if (!seen_.empty()) seen_.emplace(v, 0);
+            return;
+        }
+        if (vals.size() - v0_ < 16) {
+            if (std::find(vals.begin() + (std::ptrdiff_t)v0_, vals.end(), v) == vals.end()) vals.push_back(v);
+            return;
+        }
+        if (seen_.empty())
+            for (size_t i = v0_; i < vals.size(); ++i) seen_.emplace(vals[i], 0);
+        if (seen_.emplace(v, 0).second) vals.push_back(v);
+    }
+    uint32_t new_trip(int64_t f, int64_t a, int64_t b) {
+        const uint32_t ti = (uint32_t)((A_->trip.size() - t0_) / 3);
+        A_->trip.push_back(f);
+        A_->trip.push_back(a);
+        A_->trip.push_back(b);
+        return ti;
+    }
+    Arena *A_ = nullptr;
+    size_t v0_ = 0, t0_ = 0;
+    int model_ = 0;
+    std::vector<uint32_t> dstamp_, dtrip_;  // (f, a, b) small -> stamp, index
+    uint32_t kstamp_ = 0;
+    uint32_t vseen_ = 0;  // small state values seen
+    std::unordered_map<int64_t, char> seen_;
+    std::vector<uint64_t> tt_;
+    size_t tmask_ = 255;
+};
+
+// Tasks over the pack pool (or threads of its own when another pack holds
+// the pool): fn(i) for every i in [0, n_tasks), claimed dynamically.
+struct Par {
+    lc::HostPool *pool = nullptr;
+    unsigned nt = 1;
+    template <class F>
+    void run(uint64_t n_tasks, const F &fn) const {
+        if (n_tasks == 0) return;
+        std::atomic<uint64_t> next{0};
+        auto body = [&](unsigned) {
+            for (uint64_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n_tasks;) fn(i);
+        };
+        const unsigned w = (unsigned)std::min<uint64_t>(nt, n_tasks);
+        if (w <= 1) { body(0); return; }
+        if (pool) {
+            const std::function<void(unsigned)> f = body;
+            pool->run(w, f);
+            return;
+        }
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < w; ++t) th.emplace_back(body, t);
+        body(0);
+        for (auto &x : th) x.join();
+    }
+};
+
+// Open-addressing map of 64-bit keys (stored + 1: 0 = empty) to u32, kept
+// under half full.  For the interning tables lc_pack builds per batch.
+class FlatMap {
+  public:
+    explicit FlatMap(size_t expect = 16) {
+        size_t c = 32;
+        while (c < 2 * expect) c <<= 1;
+        k_.assign(c, 0);
+        v_.resize(c);
+    }
+    // the value of key, or `none`
+    uint32_t get(uint64_t key, uint32_t none) const {
+        for (size_t x = hash(key) & (k_.size() - 1);; x = (x + 1) & (k_.size() - 1)) {
+            if (k_[x] == key + 1) return v_[x];
+            if (!k_[x]) return none;
+        }
+    }
+    // insert key -> val unless present; returns the value it maps to
+    uint32_t put(uint64_t key, uint32_t val) {
+        for (size_t x = hash(key) & (k_.size() - 1);; x = (x + 1) & (k_.size() - 1)) {
+            if (k_[x] == key + 1) return v_[x];
+            if (!k_[x]) {
+                k_[x] = key + 1;
+                v_[x] = val;
+                if (++n_ * 2 > k_.size()) grow();
+                return val;
+            }
+        }
+    }
+    size_t size() const { return n_; }
+
+  private:
+    static size_t hash(uint64_t x) {
+        x *= 0x9E3779B97F4A7C15ull;
+        return (size_t)(x ^ (x >> 31));
+    }
+    void grow() {
+        std::vector<uint64_t> ok;
+        std::vector<uint32_t> ov;
+        ok.swap(k_);
+        ov.swap(v_);
+        k_.assign(ok.size() * 2, 0);
+        v_.resize(ok.size() * 2);
+        for (size_t i = 0; i < ok.size(); ++i)
+            if (ok[i])
+                for (size_t x = hash(ok[i] - 1) & (k_.size() - 1);; x = (x + 1) & (k_.size() - 1))
+                    if (!k_[x]) { k_[x] = ok[i]; v_[x] = ov[i]; break; }
+    }
+    std::vector<uint64_t> k_;
+    std::vector<uint32_t> v_;
+    size_t n_ = 0;
+};
+
+// (2) the state numbering (one shared by every key while the batch has <
+// 255 values, else per key), (3) every triple's descriptor, and (4) the
+// descriptors' transition ids -- in order of first appearance over the keys
+// in order and each key's triples in order, the ids one serial pass over
+// keys and events would give -- into each arena's `tid`.  *max_tid = the
+// largest transition id a word carries.  false: more than 2^24 distinct
+// operations.
+bool number_and_describe(lc_packed *P, const std::vector<KeySpan> &ks, std::vector<Arena> &ar, const Par &par,
+                         uint32_t *max_tid) {
+    const int64_t K = (int64_t)ks.size();
+    for (Arena &A : ar) A.tid.resize(A.trip.size() / 3);
+    // (2) the shared numbering: values in order of first appearance over the
+    // keys (a few per key)
+    FlatMap gstate;
+    std::vector<int64_t> gvals;
+    bool shared = true;
+    for (int64_t k = 0; k < K && shared; ++k) {
+        const KeySpan &sp = ks[(size_t)k];
+        const int64_t *v = ar[sp.arena].vals.data() + sp.v0;
+        for (uint32_t i = 0; i < sp.nv; ++i) {
+            const uint32_t id = (uint32_t)gvals.size() + 1;
+            if (gstate.put((uint64_t)v[i], id) == id) {
+                if (gvals.size() >= LC_NARROW_MAX_STATES - 1) { shared = false; break; }
+                gvals.push_back(v[i]);
+            }
+        }
+    }
+    if (shared) {
+        P->state_vals.assign(gvals.size() + 1, LC_NIL);
+        for (size_t i = 0; i < gvals.size(); ++i) P->state_vals[i + 1] = gvals[i];
+    } else {
+        P->state_off.assign((size_t)K + 1, 0);
+    }
+    P->key_states.assign((size_t)K, 0);
+    // (3) per key (contiguous blocks in parallel): each triple's descriptor.
+    // Shared numbering: `tid` holds the descriptor for now, and each block
+    // lists the descriptors in order of their first appearance in it, so
+    // that (4) is a serial merge of short lists.  Per-key numbering: each
+    // key's distinct descriptors (its transition table) and local ids.
+    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)K, 64u * par.nt));
+    std::vector<std::vector<uint32_t>> bdesc(blocks);
+    std::vector<std::vector<uint32_t>> kud(shared ? 0 : (size_t)K);
+    std::vector<std::vector<int64_t>> ktab(shared ? 0 : (size_t)K);
+    par.run(blocks, [&](uint64_t bi) {
+        FlatMap bseen;
+        for (int64_t k = (int64_t)(bi * (uint64_t)K / blocks); k < (int64_t)((bi + 1) * (uint64_t)K / blocks); ++k) {
+            const KeySpan &sp = ks[(size_t)k];
+            Arena &A = ar[sp.arena];
+            const int64_t *vals = A.vals.data() + sp.v0;
+            std::unordered_map<int64_t, uint32_t> lstate;
+            if (!shared) {
+                for (uint32_t i = 0; i < sp.nv; ++i)
+                    lstate.emplace(vals[i], lstate.size() < LC_STATE_NONE - 1 ? (uint32_t)lstate.size() + 1 : LC_STATE_NONE);
+            }
+            auto sid = [&](int64_t v) -> uint32_t {
+                if (v == LC_NIL) return 0;
+                if (shared) return gstate.get((uint64_t)v, LC_STATE_NONE);
+                auto it = lstate.find(v);
+                return it == lstate.end() ? LC_STATE_NONE : it->second;
+            };
+            P->key_states[(size_t)k] = (uint16_t)std::min<size_t>((size_t)sp.nv + 1, 65535);
+            const int64_t *tr = A.trip.data() + 3 * sp.t0;
+            uint32_t *tid = A.tid.data() + sp.t0;
+            FlatMap local(shared ? 1 : sp.nt);
+            for (uint32_t u = 0; u < sp.nt; ++u) {
+                const int64_t f = tr[3 * u], a = tr[3 * u + 1], b = tr[3 * u + 2];
+                uint32_t d;
+                if (f == LC_F_ACQUIRE) d = LC_DESC(LC_T_CAS, 0, sid(1));  // unlocked -> locked
+                else if (f == LC_F_RELEASE) d = LC_DESC(LC_T_CAS, sid(1), 0);  // locked -> unlocked
+                else if (f == LC_F_READ) d = a == LC_NIL ? LC_DESC(LC_T_READ_ANY, 0, 0) : LC_DESC(LC_T_READ, sid(a), 0);
+                else if (f == LC_F_WRITE) d = LC_DESC(LC_T_WRITE, 0, sid(a));
+                else d = LC_DESC(LC_T_CAS, sid(a), sid(b));
+                if (shared) {
+                    tid[u] = d;
+                    const size_t before = bseen.size();
+                    bseen.put(d, 0);
+                    if (bseen.size() > before) bdesc[bi].push_back(d);
+                } else {
+                    std::vector<uint32_t> &ud = kud[(size_t)k];
+                    const uint32_t q = (uint32_t)ud.size();
+                    const uint32_t at = local.put(d, q);
+                    if (at == q) ud.push_back(d);
+                    tid[u] = at;  // the key's own id (< 2^24: its distinct descriptors are fewer)
+                }
+            }
+            if (!shared) {  // the key's state table, kept in lstate order as state ids
+                std::vector<int64_t> &tab = ktab[(size_t)k];
+                tab.assign(lstate.size() + 1, LC_NIL);
+                for (auto &kv : lstate)
+                    if (kv.second != LC_STATE_NONE) tab[kv.second] = kv.first;
+            }
+        }
+    });
+    // (4) transition ids, in key order
+    bool too_many = false;
+    uint32_t mt = 0;
+    if (!shared) {
+        P->trans_off.assign((size_t)K, 0);
+        for (int64_t k = 0; k < K && !too_many; ++k) {
+            const std::vector<uint32_t> &ud = kud[(size_t)k];
+            P->state_off[(size_t)k] = P->state_vals.size();
+            P->state_vals.insert(P->state_vals.end(), ktab[(size_t)k].begin(), ktab[(size_t)k].end());
+            P->trans_off[(size_t)k] = (uint32_t)P->trans.size();
+            P->trans.insert(P->trans.end(), ud.begin(), ud.end());
+            too_many = ud.size() > 0x1000000u;
+            if (!ud.empty()) mt = std::max<uint32_t>(mt, (uint32_t)ud.size() - 1);
+        }
+        P->state_off[(size_t)K] = P->state_vals.size();
+    } else {
+        // first appearance over the keys = over the blocks' own lists in block order
+        FlatMap gtrans;
+        for (const std::vector<uint32_t> &bd : bdesc)
+            for (uint32_t d : bd) {
+                const uint32_t id = (uint32_t)P->trans.size();
+                if (gtrans.put(d, id) == id) P->trans.push_back(d);
+            }
+        too_many = P->trans.size() > 0x1000000u;
+        if (!too_many)
+            par.run(blocks, [&](uint64_t bi) {
+                for (int64_t k = (int64_t)(bi * (uint64_t)K / blocks); k < (int64_t)((bi + 1) * (uint64_t)K / blocks); ++k) {
+                    const KeySpan &sp = ks[(size_t)k];
+                    uint32_t *tid = ar[sp.arena].tid.data() + sp.t0;
+                    for (uint32_t u = 0; u < sp.nt; ++u) tid[u] = gtrans.get(tid[u], 0);  // now: the global id
+                }
+            });
+        if (!P->trans.empty()) mt = (uint32_t)P->trans.size() - 1;
+    }
+    *max_tid = mt;
+    return !too_many;
+}
+
+inline uint16_t word16(uint32_t w) {
+    return (uint16_t)(((w >> 16) & 0x8000u) | (LC_EV_SLOT(w) << 11) | LC_EV_TRANS(w));
+}
+
+// ---- register models, key-major histories --------------------------------
+//
+// Every key's rows one run of the history and no row shared by every key:
+// what the demo writes (independent/concurrent-generator hands its 10
+// threads one key at a time, etcdemo.clj:120-125) and what the synthetic
+// C2-C5 generator writes.  No row list is built then.  One pass over the
+// history, in row ranges (one per thread; a run belongs to the range it
+// starts in), takes each key while its rows are in cache: (0) the run's end,
+// row-type counts and process span (validating :type / :f); (1) complete's
+// pairing, which records only each op's fate and completion row; (2) the
+// events in row order -- failed pairs dropped, lowest free slot at each
+// invoke, the op's values after complete's fill interned -- as words with
+// the key's own triple indices (16 bits while they fit, the common case,
+// else the pass restarts with 32-bit words), into the range's staging, and
+// a bit per row that emits no event (how each event's row is found again).
+// Then (2)-(4) as on the other path, and one pass writing each word with its
+// transition id into the arrays the device reads (page-locked): the 16-bit
+// words when every word fits, else the 32-bit ones.  The batch is
+// byte-identical to the bucketing path's (tests/test_pack_fast.py).
+//
+// *took = false (nothing kept) when the history is not key-major, or a key
+// needs complete's error or a sparse process map: the bucketing path then
+// packs it.
+struct KmRec {      // a key's run, as its range packed it
+    int64_t key, r0, n;
+    uint64_t w0, nw;  // its words in the range's staging
+    uint64_t b0;      // its skip bitmap in the range's (ceil(n / 64) words)
+    int width;
+    KeySpan sp;       // its values and triples in the range's arena
+};
+struct KmRange {
+    std::vector<KmRec> recs;
+    Arena A;
+    lc::uninit_vector<uint16_t> w16;
+    lc::uninit_vector<uint32_t> w32;
+    lc::uninit_vector<uint64_t> bits;
+};
+
+template <bool W16>
+bool km_ranges(const lc_history *h, int model, const Par &par, std::vector<KmRange> &rg, std::atomic<int> &stop) {
+    const int64_t n = h->n;
+    const unsigned nr = (unsigned)rg.size();
+    uint8_t client[256] = {0};  // :f codes the model steps
+    for (int f = 0; f <= LC_F_TXN; ++f) client[f] = is_client_f((uint8_t)f, model);
+    par.run(nr, [&](uint64_t t) {
+        static thread_local std::vector<uint8_t> fate, slot_of;
+        static thread_local std::vector<uint32_t> ret, inv_ev, inv_row, inv_id;
+        static thread_local std::vector<int32_t> dmap;
+        static thread_local Interner in;
+        KmRange &R = rg[t];
+        R.recs.clear();
+        R.A.vals.clear();
+        R.A.trip.clear();
+        const int64_t R0 = n * (int64_t)t / nr, R1 = n * (int64_t)(t + 1) / nr;
+        int64_t r = R0;
+        if (t > 0)
+            while (r < R1 && h->key[r] == h->key[R0 - 1]) ++r;  // the run of the range before
+        uint64_t nw = 0, nb = 0;
+        while (r < R1) {
+            if (stop.load(std::memory_order_relaxed)) return;
+            // (0) the run: its end, counts, process span
+            const int64_t k = h->key[r];
+            if (k == LC_NO_KEY) { stop = 1; return; }  // rows shared by every key: the other path
+            int64_t e = r;
+            int64_t pmin = h->process[r], pmax = pmin;
+            uint64_t ninv = 0;
+            for (; e < n && h->key[e] == k; ++e) {
+                const uint8_t ty = h->type[e];
+                if (ty > LC_INFO || h->f[e] > LC_F_TXN) { stop = 1; return; }
+                const int64_t p = h->process[e];
+                pmin = std::min(pmin, p);
+                pmax = std::max(pmax, p);
+                ninv += ty == LC_INVOKE;
+            }
+            const int64_t nrow = e - r;
+            if ((uint64_t)pmax - (uint64_t)pmin >= 4096 || nrow >= (1ll << 32)) { stop = 1; return; }
+            const uint64_t pm0 = (uint64_t)pmin;
+            dmap.assign((size_t)((uint64_t)pmax - pm0) + 1, -1);
+            if (fate.size() < ninv + 1) { fate.resize(ninv + 1); ret.resize(ninv + 1); slot_of.resize(ninv + 1); }
+            const uint8_t *ty = h->type + r, *fn = h->f + r;
+            const int64_t *pr = h->process + r, *v0 = h->v0 + r, *v1 = h->v1 + r;
+            // (1) pairing: each op's fate (0 pending forever, 1 ok, 2 failed)
+            // and completion row.  Branch-free (the row types come in no
+            // predictable order): a row that records nothing writes the
+            // scratch entry past the ops.
+            uint32_t q = 0;
+            {
+                const uint32_t scratch = (uint32_t)ninv;
+                uint32_t err = 0;
+                for (int64_t i = 0; i < nrow; ++i) {
+                    const size_t pi = (size_t)((uint64_t)pr[i] - pm0);
+                    const int32_t m = dmap[pi];
+                    const uint32_t t8 = ty[i];
+                    const uint32_t inv = t8 == LC_INVOKE, info = t8 == LC_INFO, comp = inv == 0 && info == 0;
+                    err |= (comp & (uint32_t)(m < 0)) | (inv & (uint32_t)!client[fn[i]]);
+                    const uint32_t idx = inv ? q : ((comp && m >= 0) ? (uint32_t)m : scratch);
+                    fate[idx] = (uint8_t)(inv ? 0 : (t8 == LC_OK_T ? 1 : 2));
+                    ret[idx] = (uint32_t)i;
+                    dmap[pi] = inv ? (int32_t)q : -1;
+                    q += inv;
+                }
+                // a completion without an invocation, or an op the model cannot
+                // step: complete's error (the other path reports it)
+                if (err) { stop = 1; return; }
+            }
+            // (2) the events, into the range's staging
+            const uint64_t cap = nw + (uint64_t)nrow;
+            if (W16) { if (R.w16.size() < cap) R.w16.resize(std::max<uint64_t>(cap, R.w16.size() * 2)); }
+            else if (R.w32.size() < cap) R.w32.resize(std::max<uint64_t>(cap, R.w32.size() * 2));
+            const uint64_t nbw = ((uint64_t)nrow + 63) / 64;
+            if (R.bits.size() < nb + nbw) R.bits.resize(std::max<uint64_t>(nb + nbw, R.bits.size() * 2));
+            uint16_t *o16 = W16 ? R.w16.data() + nw : nullptr;
+            uint32_t *o32 = W16 ? nullptr : R.w32.data() + nw;
+            uint64_t *ob = R.bits.data() + nb;
+            R.recs.emplace_back();
+            KmRec &rec = R.recs.back();
+            rec.key = k; rec.r0 = r; rec.n = nrow; rec.w0 = nw; rec.b0 = nb;
+            std::fill(dmap.begin(), dmap.end(), -1);
+            in.begin(&R.A, model);
+            int maxslot = -1;
+            uint64_t ne = 0, skipw = 0;
+            uint64_t freemask[2] = {~0ull, ~0ull};  // (32-bit words)
+            q = 0;
+            if (W16) {
+                // (2a) branch-free: slots, :ok words, skip bits, and the list
+                // of surviving invokes (event, row, op) ...
+                const uint32_t scratch = (uint32_t)ninv;
+                if (inv_ev.size() < ninv + 1) { inv_ev.resize(ninv + 1); inv_row.resize(ninv + 1); inv_id.resize(ninv + 1); }
+                uint64_t free64 = ~0ull;
+                uint32_t ni = 0, wide = 0;
+                for (int64_t i = 0; i < nrow; ++i) {
+                    if ((i & 63) == 0 && i) { ob[(i >> 6) - 1] = skipw; skipw = 0; }
+                    const size_t pi = (size_t)((uint64_t)pr[i] - pm0);
+                    const int32_t m = dmap[pi];
+                    const uint32_t t8 = ty[i];
+                    const uint32_t inv = t8 == LC_INVOKE, ok = t8 == LC_OK_T;
+                    const uint32_t id = inv ? q : (ok ? (uint32_t)m : scratch);
+                    const uint32_t ei = inv & (uint32_t)(fate[inv ? q : scratch] != 2);
+                    const uint32_t s_new = (uint32_t)__builtin_ctzll(free64);
+                    const uint32_t s_ok = slot_of[ok ? id : scratch];
+                    slot_of[ei ? id : scratch] = (uint8_t)s_new;
+                    free64 = (free64 & ~((uint64_t)ei << s_new)) | ((uint64_t)ok << (s_ok & 63));
+                    wide |= ei & (uint32_t)(s_new > LC_EV16_MAX_SLOT);
+                    maxslot = std::max(maxslot, ei ? (int)s_new : -1);
+                    o16[ne] = (uint16_t)(ok ? (0x8000u | s_ok << 11) : (s_new << 11));
+                    inv_ev[ni] = (uint32_t)ne;
+                    inv_row[ni] = (uint32_t)i;
+                    inv_id[ni] = id;
+                    ni += ei;
+                    ne += ei | ok;
+                    skipw |= (uint64_t)((ei | ok) ^ 1u) << (i & 63);
+                    dmap[pi] = inv ? (int32_t)q : -1;
+                    q += inv;
+                }
+                if (wide) { stop = 2; return; }  // a slot past 15: 32-bit words
+                // ... (2b) their values after complete's fill, interned in
+                // invoke order
+                for (uint32_t j = 0; j < ni; ++j) {
+                    const uint32_t i = inv_row[j], id = inv_id[j];
+                    const int64_t f = fn[i];
+                    int64_t a = v0[i], b = v1[i];
+                    if (fate[id] == 1) {  // (or (:value invocation) (:value completion))
+                        const uint32_t rr = ret[id];
+                        if (f == LC_F_CAS) {
+                            if (a == LC_NIL && b == LC_NIL) { a = v0[rr]; b = v1[rr]; }
+                        } else if (a == LC_NIL) {
+                            a = v0[rr];
+                        }
+                    }
+                    const uint32_t ti = in.op(f, a, b);
+                    if (ti > LC_EV16_MAX_TRANS) { stop = 2; return; }  // 32-bit words
+                    o16[inv_ev[j]] |= (uint16_t)ti;
+                }
+            } else
+            for (int64_t i = 0; i < nrow; ++i) {
+                if ((i & 63) == 0 && i) { ob[(i >> 6) - 1] = skipw; skipw = 0; }
+                int32_t &m = dmap[(size_t)((uint64_t)pr[i] - pm0)];
+                const uint8_t t8 = ty[i];
+                if (t8 == LC_INVOKE) {
+                    const uint32_t id = q++;
+                    m = (int32_t)id;
+                    const uint8_t fa = fate[id];
+                    if (fa == 2) { skipw |= 1ull << (i & 63); continue; }  // without-failures
+                    int s;
+                    if (freemask[0]) s = __builtin_ctzll(freemask[0]);
+                    else if (freemask[1]) s = 64 + __builtin_ctzll(freemask[1]);
+                    else s = 128;
+                    if (s < 127) freemask[s >> 6] &= ~(1ull << (s & 63));
+                    const int enc = s < 127 ? s : 127;  // >= 127 cannot be encoded; the search stops earlier
+                    slot_of[id] = (uint8_t)enc;
+                    maxslot = std::max(maxslot, s);
+                    // (or (:value invocation) (:value completion))
+                    const int64_t f = fn[i];
+                    int64_t a = v0[i], b = v1[i];
+                    if (fa == 1) {
+                        const uint32_t rr = ret[id];
+                        if (f == LC_F_CAS) {
+                            if (a == LC_NIL && b == LC_NIL) { a = v0[rr]; b = v1[rr]; }
+                        } else if (a == LC_NIL) {
+                            a = v0[rr];
+                        }
+                    }
+                    const uint32_t ti = in.op(f, a, b);
+                    if (W16) {
+                        if (s > (int)LC_EV16_MAX_SLOT || ti > LC_EV16_MAX_TRANS) { stop = 2; return; }  // 32-bit words
+                        o16[ne++] = (uint16_t)((uint32_t)s << 11 | ti);
+                    } else {
+                        o32[ne++] = ((uint32_t)enc << 24) | ti;
+                    }
+                } else if (t8 == LC_OK_T) {
+                    const uint32_t s = slot_of[(size_t)m];
+                    if (s < 127) freemask[s >> 6] |= 1ull << (s & 63);
+                    m = -1;
+                    if (W16) o16[ne++] = (uint16_t)(0x8000u | s << 11);
+                    else o32[ne++] = LC_EV_OK_BIT | (s << 24);
+                } else {
+                    m = -1;
+                    skipw |= 1ull << (i & 63);
+                }
+            }
+            ob[nbw - 1] = skipw;
+            rec.sp = in.end((uint32_t)t);
+            rec.nw = ne;
+            rec.width = std::min(maxslot + 1, 255);
+            nw += ne;
+            nb += nbw;
+            r = e;
+        }
+    });
+    return stop.load() == 0;
+}
+
+int pack_key_major(const lc_history *h, int model, lc_packed *P, const Par &par, bool *took) {
+    *took = false;
+    const int64_t n = h->n;
+    if (n == 0 || (h->mop_off && h->mop)) return LC_OK;  // (:txn rows: the other path)
+    static const bool timing = std::getenv("LC_TIMING") != nullptr;
+    auto tprev = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "lc_pack (key-major): %-22s %8.1f ms\n", what,
+                     std::chrono::duration<double, std::milli>(t - tprev).count());
+        tprev = t;
+    };
+    const unsigned nr = n >= (1 << 16) ? 4 * par.nt : 1u;
+    std::vector<KmRange> rg(nr);
+    std::atomic<int> stop{0};
+    bool w16 = true;
+    if (!km_ranges<true>(h, model, par, rg, stop)) {
+        if (stop.load() != 2) return LC_OK;  // not key-major (or complete's error): the other path
+        stop = 0;
+        w16 = false;
+        if (!km_ranges<false>(h, model, par, rg, stop)) return LC_OK;
+    }
+    lap(w16 ? "runs, pairing, events" : "runs, pairing, events (32-bit)");
+    // the keys in row order; each must be one run
+    int64_t K = 0;
+    for (const KmRange &R : rg) K += (int64_t)R.recs.size();
+    {
+        std::unordered_map<int64_t, char> seen;
+        seen.reserve((size_t)K * 2);
+        for (const KmRange &R : rg)
+            for (const KmRec &x : R.recs)
+                if (!seen.emplace(x.key, 0).second) return LC_OK;  // a key in two runs
+    }
+    P->keys.resize((size_t)K);
+    P->key_row0.resize((size_t)K);
+    P->krow_off.assign((size_t)K + 1, 0);
+    P->ev_off.resize((size_t)K + 1);
+    P->ev_off[0] = 0;
+    P->skip_off.assign((size_t)K + 1, 0);
+    P->key_width.assign((size_t)K, 0);
+    std::vector<KeySpan> ks((size_t)K);
+    std::vector<Arena> ar(nr);
+    std::vector<int64_t> rk(nr + 1, 0);  // first key of each range
+    {
+        int64_t k = 0;
+        for (unsigned t = 0; t < nr; ++t) {
+            rk[t] = k;
+            ar[t].vals.swap(rg[t].A.vals);
+            ar[t].trip.swap(rg[t].A.trip);
+            for (const KmRec &x : rg[t].recs) {
+                P->keys[(size_t)k] = x.key;
+                P->key_row0[(size_t)k] = x.r0;
+                P->krow_off[(size_t)k + 1] = P->krow_off[(size_t)k] + (uint64_t)x.n;
+                P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + x.nw;
+                P->skip_off[(size_t)k + 1] = P->skip_off[(size_t)k] + ((uint64_t)x.n + 63) / 64;
+                P->key_width[(size_t)k] = (uint8_t)x.width;
+                ks[(size_t)k] = x.sp;
+                ++k;
+            }
+        }
+        rk[nr] = k;
+    }
+    const uint64_t n_ev = P->ev_off[(size_t)K];
+    lap("keys, offsets");
+    uint32_t max_tid = 0;
+    if (!number_and_describe(P, ks, ar, par, &max_tid))
+        return lc::fail(LC_E_UNSUPPORTED, "lc_pack: more than 2^24 distinct operations");
+    lap("numbering, descriptors");
+    // (5) the words with their transition ids: 16-bit when every word fits
+    int maxw = 0;
+    for (int64_t k = 0; k < K; ++k) maxw = std::max(maxw, (int)P->key_width[(size_t)k]);
+    const bool fit16 = n_ev > 0 && maxw <= (int)LC_EV16_MAX_SLOT + 1 && max_tid <= LC_EV16_MAX_TRANS;
+    if (fit16) P->events16.alloc(n_ev, true);
+    else P->events.alloc(n_ev, true);
+    P->skip.alloc(std::max<uint64_t>(P->skip_off[(size_t)K], 1), false);
+    uint16_t *const E16 = P->events16.data();
+    uint32_t *const E32 = P->events.data();
+    par.run(nr, [&](uint64_t t) {
+        const KmRange &R = rg[t];
+        for (int64_t k = rk[t]; k < rk[t + 1]; ++k) {
+            const KmRec &x = R.recs[(size_t)(k - rk[t])];
+            const uint32_t *tid = ar[t].tid.data() + x.sp.t0;
+            const uint64_t e0 = P->ev_off[(size_t)k];
+            if (w16) {
+                // (an :ok word's id field is 0, and tid[0] exists: the key
+                // has an invoke; the select keeps the loop free of branches)
+                const uint16_t *src = R.w16.data() + x.w0;
+                if (E16) {
+                    uint16_t *dst = E16 + e0;
+                    for (uint64_t j = 0; j < x.nw; ++j) {
+                        const uint32_t w = src[j];
+                        const uint32_t id = tid[w & 0x7FFu];
+                        dst[j] = (uint16_t)((w & 0xF800u) | ((w & 0x8000u) ? 0u : id));
+                    }
+                } else {
+                    uint32_t *dst = E32 + e0;
+                    for (uint64_t j = 0; j < x.nw; ++j) {
+                        const uint32_t w = src[j];
+                        const uint32_t id = tid[w & 0x7FFu];
+                        dst[j] = ((w & 0x8000u) << 16) | ((w >> 11 & 0xFu) << 24) | ((w & 0x8000u) ? 0u : id);
+                    }
+                }
+            } else {
+                const uint32_t *src = R.w32.data() + x.w0;
+                for (uint64_t j = 0; j < x.nw; ++j) {
+                    const uint32_t w = src[j];
+                    const uint32_t v = (w & LC_EV_OK_BIT) ? w : (w & 0xFF000000u) | tid[w & 0xFFFFFFu];
+                    if (E16) E16[e0 + j] = word16(v);
+                    else E32[e0 + j] = v;
+                }
+            }
+            std::memcpy(P->skip.data() + P->skip_off[(size_t)k], R.bits.data() + x.b0,
+                        (P->skip_off[(size_t)k + 1] - P->skip_off[(size_t)k]) * 8);
+        }
+    });
+    if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
+    lap("transition ids");
+    P->key_major = true;
+    *took = true;
+    return LC_OK;
+}
 }  // namespace
 
 
@@ -443,6 +1144,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
     const int model = opts ? opts->model : LC_MODEL_CAS_REGISTER;
     if (model < LC_MODEL_CAS_REGISTER || model > LC_MODEL_MULTI_REGISTER)
         return lc::fail(LC_E_INVALID, "lc_pack: unknown model %d", model);
+    if (opts && (opts->flags & ~LC_PACK_GENERAL)) return lc::fail(LC_E_INVALID, "lc_pack: unknown flags 0x%x", opts->flags);
     const int32_t n_init = (opts && model == LC_MODEL_MULTI_REGISTER) ? opts->n_init : 0;
     if (n_init < 0 || (n_init > 0 && !opts->init)) return lc::fail(LC_E_INVALID, "lc_pack: bad initial registers");
     if (h->n < 0 || (h->n > 0 && (!h->type || !h->f || !h->process || !h->key || !h->v0 || !h->v1)))
@@ -460,6 +1162,20 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         tprev = t;
     };
     try {
+        if (model != LC_MODEL_MULTI_REGISTER && !(opts && (opts->flags & LC_PACK_GENERAL))) {
+            Par par;
+            par.pool = lc::pack_pool_acquire();
+            par.nt = par.pool ? par.pool->size() : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+            bool took = false;
+            int rc = pack_key_major(h, model, P, par, &took);
+            if (par.pool) lc::pack_pool_release();
+            if (rc) { delete P; return rc; }
+            if (took) {
+                lap("key-major pack");
+                *out = P;
+                return LC_OK;
+            }
+        }
         // ---- A2: key discovery + bucketing (stable) ----
         // Rows in contiguous ranges, one per thread: each range numbers its
         // keys in order of first appearance; the ranges' key lists are then
@@ -567,9 +1283,9 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         // ---- A3: per-key pairing, fail-drop, slots (parallel over keys) ----
         unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         if (K < 64) nt = 1;
-        auto par_keys = [&](const auto &fn) {
+        auto par_keys = [&](const auto &fn) {  // fn(key, thread)
             auto work = [&](unsigned t) {
-                for (int64_t k = t; k < K; k += nt) fn(k);
+                for (int64_t k = t; k < K; k += nt) fn(k, t);
             };
             std::vector<std::thread> pool;
             for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
@@ -600,7 +1316,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         };
         if (model == LC_MODEL_MULTI_REGISTER) {
             std::vector<KeyOut> ko((size_t)K);
-            par_keys([&](int64_t k) {
+            par_keys([&](int64_t k, unsigned) {
                 static thread_local std::vector<int64_t> merged;
                 const int64_t *rows;
                 int64_t nrows;
@@ -636,16 +1352,14 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         // descriptors each), their global transition ids; (5) per key, in
         // parallel, the event words.  The ids are those of one serial pass
         // over keys and events.  Per key only short lists outlive step (1).
-        struct KeyFlat {
-            std::vector<int64_t> vals;   // state values, order of first appearance
-            std::vector<int64_t> trip;   // distinct (f, v0, v1) of its invokes, order of first appearance
-            std::vector<uint32_t> ud;    // (3) its distinct descriptors; (4) their transition ids
-            std::vector<uint32_t> remap; // (3) triple -> index in ud
+        struct GenKey {
             int64_t n_ev = 0;
             int width = 0, err = 0;
             std::string msg;
         };
-        std::vector<KeyFlat> kf((size_t)K);
+        std::vector<GenKey> gk((size_t)K);
+        std::vector<KeySpan> ks((size_t)K);
+        std::vector<Arena> ar(nt);  // one per thread
         const uint64_t n_shared = P->shared_rows.size();
         auto stage_off = [&](int64_t k) { return P->krow_off[(size_t)k] + (uint64_t)k * n_shared; };
         // staging kept between calls (its pages stay mapped: no fresh page
@@ -657,224 +1371,73 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         stg.row.resize(std::max<uint64_t>(stage_off(K), 1));
         uint32_t *const st_ev = stg.ev.data();
         int64_t *const st_row = stg.row.data();
-        par_keys([&](int64_t k) {
+        par_keys([&](int64_t k, unsigned t) {
             static thread_local std::vector<int64_t> merged;
             static thread_local std::vector<KOp> ops;
             static thread_local std::vector<int32_t> row_op;
             static thread_local std::vector<uint32_t> tix;
-            static thread_local std::vector<uint64_t> tt;
-            KeyFlat &o = kf[(size_t)k];
-            if (model == LC_MODEL_MUTEX) o.vals.push_back(1);  // state 1 = locked (state 0, "nil", = unlocked)
+            GenKey &o = gk[(size_t)k];
             const int64_t *rows;
             int64_t nrows;
             key_rows(k, merged, rows, nrows);
-            if (!pair_rows(*h, rows, nrows, model, ops, row_op, o.err, o.msg)) return;
+            if (!pair_rows(*h, rows, nrows, model, ops, row_op, o.err, o.msg)) {
+                ks[(size_t)k] = KeySpan{t, 0, 0, ar[t].vals.size(), ar[t].trip.size() / 3};
+                if (model == LC_MODEL_MUTEX) {  // (the mutex's state value, as Interner.begin adds it)
+                    ks[(size_t)k].nv = 1;
+                    ar[t].vals.push_back(1);
+                }
+                return;
+            }
             uint32_t *ev = st_ev + stage_off(k);
             o.n_ev = emit_events(rows, nrows, ops, row_op, ev, st_row + stage_off(k), nullptr, o.width);
             // (1) distinct state values, and each surviving op's triple
             // index (the fields its descriptor reads), distinct triples in
-            // invoke order.  Small values (0 .. 14, and nil) -- what Jepsen
-            // register tests write -- go through direct tables stamped per
-            // key; others through a set / an open-addressing table of index +
-            // 1 kept under half full.
-            constexpr int64_t SMALL = 15;  // values 0 .. 14, plus nil as 15
-            auto small = [](int64_t v) -> int64_t { return v == LC_NIL ? SMALL : (v >= 0 && v < SMALL ? v : -1); };
-            static thread_local std::vector<uint32_t> dstamp, dtrip;  // (f, a, b) small -> stamp, index
-            static thread_local uint32_t kstamp = 0;
-            if (dstamp.empty()) { dstamp.assign(8 * 16 * 16, 0); dtrip.assign(8 * 16 * 16, 0); }
-            if (++kstamp == 0) { std::fill(dstamp.begin(), dstamp.end(), 0u); kstamp = 1; }
-            uint32_t vseen = 0;  // small state values seen
-            std::vector<int64_t> &vals = o.vals;
-            std::unordered_map<int64_t, char> seen;
-            auto add = [&](int64_t v) {
-                if (v == LC_NIL) return;
-                const int64_t sv = small(v);
-                if (sv >= 0) {
-                    if (vseen >> sv & 1u) return;
-                    vseen |= 1u << sv;
-                    vals.push_back(v);
-                    if (!seen.empty()) seen.emplace(v, 0);
-                    return;
-                }
-                if (vals.size() < 16) {
-                    if (std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
-                    return;
-                }
-                if (seen.empty())
-                    for (int64_t x : vals) seen.emplace(x, 0);
-                if (seen.emplace(v, 0).second) vals.push_back(v);
-            };
+            // invoke order (Interner)
+            static thread_local Interner in;
+            in.begin(&ar[t], model);
             tix.resize(ops.size());
-            size_t tmask = 255;
-            tt.assign(tmask + 1, 0);
-            auto thash = [](int64_t f, int64_t a, int64_t b) {
-                uint64_t x = (uint64_t)f * 0x9E3779B97F4A7C15ull ^ (uint64_t)a * 0xC2B2AE3D27D4EB4Full ^
-                             (uint64_t)b * 0x165667B19E3779F9ull;
-                return (size_t)(x ^ (x >> 29));
-            };
-            auto new_trip = [&](int64_t f, int64_t a, int64_t b) -> uint32_t {
-                const uint32_t ti = (uint32_t)(o.trip.size() / 3);
-                o.trip.push_back(f);
-                o.trip.push_back(a);
-                o.trip.push_back(b);
-                return ti;
-            };
             for (size_t q = 0; q < ops.size(); ++q) {
                 const KOp &op = ops[q];
                 if (op.fate == 2) continue;
-                if (model != LC_MODEL_MUTEX) {
-                    if (op.f == LC_F_WRITE) add(op.v0);
-                    if (op.f == LC_F_CAS) add(op.v1);
-                }
-                const int64_t f = op.f;
-                const int64_t a = (f == LC_F_ACQUIRE || f == LC_F_RELEASE) ? 0 : op.v0;
-                const int64_t b = f == LC_F_CAS ? op.v1 : 0;
-                const int64_t sa = small(a), sb = small(b);
-                if (sa >= 0 && sb >= 0 && f < 8) {
-                    const size_t di = (size_t)f * 256 + (size_t)sa * 16 + (size_t)sb;
-                    if (dstamp[di] != kstamp) {
-                        dstamp[di] = kstamp;
-                        dtrip[di] = new_trip(f, a, b);
-                    }
-                    tix[q] = dtrip[di];
-                    continue;
-                }
-                size_t x = thash(f, a, b) & tmask;
-                for (;; x = (x + 1) & tmask) {
-                    const uint64_t e = tt[x];
-                    if (!e) {
-                        const uint32_t ti = new_trip(f, a, b);
-                        tt[x] = ti + 1;
-                        tix[q] = ti;
-                        if ((size_t)(ti + 1) * 2 > tmask) {  // grow
-                            tmask = tmask * 2 + 1;
-                            tt.assign(tmask + 1, 0);
-                            for (uint32_t u = 0; u <= ti; ++u) {
-                                size_t y = thash(o.trip[3 * u], o.trip[3 * u + 1], o.trip[3 * u + 2]) & tmask;
-                                while (tt[y]) y = (y + 1) & tmask;
-                                tt[y] = u + 1;
-                            }
-                        }
-                        break;
-                    }
-                    const uint32_t u = (uint32_t)e - 1;
-                    if (o.trip[3 * u] == f && o.trip[3 * u + 1] == a && o.trip[3 * u + 2] == b) {
-                        tix[q] = u;
-                        break;
-                    }
-                }
+                tix[q] = in.op(op.f, op.v0, op.v1);
             }
+            ks[(size_t)k] = in.end(t);
             for (int64_t j = 0; j < o.n_ev; ++j)
                 if (!(ev[j] & LC_EV_OK_BIT)) ev[j] = (ev[j] & 0xFF000000u) | tix[ev[j] & 0xFFFFFFu];
         });
         lap("A3/A4 (1) pairing, values, triples");
         for (int64_t k = 0; k < K; ++k)
-            if (kf[(size_t)k].err) key_error(k, kf[(size_t)k].msg);
-        // (2) one numbering shared by every key while the batch has < 255 values
-        std::unordered_map<int64_t, uint32_t> gstate;
-        bool shared = true;
-        for (int64_t k = 0; k < K && shared; ++k)
-            for (int64_t v : kf[(size_t)k].vals) {
-                if (gstate.size() >= LC_NARROW_MAX_STATES - 1 && !gstate.count(v)) { shared = false; break; }
-                gstate.emplace(v, (uint32_t)gstate.size() + 1);
-            }
-        if (shared) {
-            P->state_vals.assign(gstate.size() + 1, LC_NIL);
-            for (auto &kv : gstate) P->state_vals[kv.second] = kv.first;
-        } else {
-            P->state_off.assign((size_t)K + 1, 0);
-        }
-        P->key_states.assign((size_t)K, 0);
+            if (gk[(size_t)k].err) key_error(k, gk[(size_t)k].msg);
         P->key_width.assign((size_t)K, 0);
         P->ev_off.assign((size_t)K + 1, 0);
-        for (int64_t k = 0; k < K; ++k) P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + (uint64_t)kf[(size_t)k].n_ev;
-        P->events.resize((size_t)P->ev_off[(size_t)K]);
+        for (int64_t k = 0; k < K; ++k) P->ev_off[(size_t)k + 1] = P->ev_off[(size_t)k] + (uint64_t)gk[(size_t)k].n_ev;
+        P->events.alloc((size_t)P->ev_off[(size_t)K], true);
         P->ev_row.resize((size_t)P->ev_off[(size_t)K]);
-        lap("A4 (2) numbering, arrays");
-        auto sid = [](const std::unordered_map<int64_t, uint32_t> &m, int64_t v) -> uint32_t {
-            if (v == LC_NIL) return 0;
-            auto it = m.find(v);
-            return it == m.end() ? LC_STATE_NONE : it->second;
-        };
-        // (3) per key: its state table (unshared), each triple's descriptor
-        // and the distinct descriptors in order of first appearance
-        par_keys([&](int64_t k) {
-            KeyFlat &o = kf[(size_t)k];
-            const std::vector<int64_t> &vals = o.vals;
-            std::unordered_map<int64_t, uint32_t> lstate;
-            if (!shared) {
-                for (int64_t v : vals) lstate.emplace(v, lstate.size() < LC_STATE_NONE - 1 ? (uint32_t)lstate.size() + 1
-                                                                                            : LC_STATE_NONE);
-            }
-            const std::unordered_map<int64_t, uint32_t> &sm = shared ? gstate : lstate;
-            P->key_states[(size_t)k] = (uint16_t)std::min<size_t>(vals.size() + 1, 65535);
-            const size_t nt3 = o.trip.size() / 3;
-            o.remap.resize(nt3);
-            std::unordered_map<uint32_t, uint32_t> local;
-            for (size_t u = 0; u < nt3; ++u) {
-                const int64_t f = o.trip[3 * u], a = o.trip[3 * u + 1], b = o.trip[3 * u + 2];
-                uint32_t d;
-                if (f == LC_F_ACQUIRE) d = LC_DESC(LC_T_CAS, 0, sid(sm, 1));  // unlocked -> locked
-                else if (f == LC_F_RELEASE) d = LC_DESC(LC_T_CAS, sid(sm, 1), 0);  // locked -> unlocked
-                else if (f == LC_F_READ) d = a == LC_NIL ? LC_DESC(LC_T_READ_ANY, 0, 0) : LC_DESC(LC_T_READ, sid(sm, a), 0);
-                else if (f == LC_F_WRITE) d = LC_DESC(LC_T_WRITE, 0, sid(sm, a));
-                else d = LC_DESC(LC_T_CAS, sid(sm, a), sid(sm, b));
-                auto it = local.emplace(d, (uint32_t)o.ud.size());
-                if (it.second) o.ud.push_back(d);
-                o.remap[u] = it.first->second;  // (< 2^24: the key's distinct descriptors are fewer)
-            }
-            std::vector<int64_t>().swap(o.trip);
-            if (!shared) {  // the key's state table, kept in lstate order as state ids
-                std::vector<int64_t> tab(lstate.size() + 1, LC_NIL);
-                for (auto &kv : lstate)
-                    if (kv.second != LC_STATE_NONE) tab[kv.second] = kv.first;
-                o.vals.swap(tab);
-            }
-        });
-        lap("A5 (3) descriptors");
-        // (4) global transition ids, in key order
-        std::unordered_map<uint32_t, uint32_t> gtrans;
-        if (!shared) P->trans_off.assign((size_t)K, 0);
-        bool too_many = false;
-        for (int64_t k = 0; k < K && !too_many; ++k) {
-            std::vector<uint32_t> &ud = kf[(size_t)k].ud;
-            if (!shared) {
-                P->state_off[(size_t)k] = P->state_vals.size();
-                P->state_vals.insert(P->state_vals.end(), kf[(size_t)k].vals.begin(), kf[(size_t)k].vals.end());
-                P->trans_off[(size_t)k] = (uint32_t)P->trans.size();
-                P->trans.insert(P->trans.end(), ud.begin(), ud.end());
-                too_many = ud.size() > 0x1000000u;
-                for (uint32_t q = 0; q < ud.size(); ++q) ud[q] = q;  // local ids are the key's own
-            } else {
-                for (uint32_t &d : ud) {
-                    auto it = gtrans.emplace(d, (uint32_t)P->trans.size());
-                    if (it.second) P->trans.push_back(d);
-                    d = it.first->second;  // now: the global id
-                }
-                too_many = P->trans.size() > 0x1000000u;
+        lap("A4 (2) arrays");
+        {
+            Par par;
+            par.nt = nt;
+            uint32_t max_tid = 0;
+            if (!number_and_describe(P, ks, ar, par, &max_tid)) {
+                delete P;
+                return lc::fail(LC_E_UNSUPPORTED, "lc_pack: more than 2^24 distinct operations");
             }
         }
-        if (too_many) {
-            delete P;
-            return lc::fail(LC_E_UNSUPPORTED, "lc_pack: more than 2^24 distinct operations");
-        }
-        lap("A5 (4) transition ids");
+        lap("A5 (2)-(4) numbering, descriptors, transition ids");
         // (5) event words with transition ids, rows, widths
-        par_keys([&](int64_t k) {
-            KeyFlat &o = kf[(size_t)k];
+        par_keys([&](int64_t k, unsigned) {
+            const GenKey &o = gk[(size_t)k];
+            const uint32_t *tid = ar[ks[(size_t)k].arena].tid.data() + ks[(size_t)k].t0;
             const uint32_t *src = st_ev + stage_off(k);
             const int64_t *srow = st_row + stage_off(k);
             const uint64_t base = P->ev_off[(size_t)k];
             for (int64_t j = 0; j < o.n_ev; ++j) {
                 const uint32_t w = src[j];
-                P->events[base + (uint64_t)j] =
-                    (w & LC_EV_OK_BIT) ? w : (w & 0xFF000000u) | o.ud[o.remap[w & 0xFFFFFFu]];
+                P->events[base + (uint64_t)j] = (w & LC_EV_OK_BIT) ? w : (w & 0xFF000000u) | tid[w & 0xFFFFFFu];
                 P->ev_row[base + (uint64_t)j] = srow[j];
             }
             P->key_width[(size_t)k] = (uint8_t)o.width;
-            o = KeyFlat{};
         });
-        if (!shared) P->state_off[(size_t)K] = P->state_vals.size();
         if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
         lap("A5 (5) event words");
         // 16-bit event words (lc_batch.events16) when every word fits: half
@@ -897,13 +1460,11 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         });
         const bool fit16 = n_ev > 0 && std::all_of(fits.begin(), fits.end(), [](char c) { return c != 0; });
         if (fit16) {
-            P->events16.resize(n_ev);
+            P->events16.alloc(n_ev, true);
             range_pass([&](unsigned, size_t j0, size_t j1) {
-                for (size_t j = j0; j < j1; ++j) {
-                    const uint32_t w = P->events[j];
-                    P->events16[j] = (uint16_t)(((w >> 16) & 0x8000u) | (LC_EV_SLOT(w) << 11) | LC_EV_TRANS(w));
-                }
+                for (size_t j = j0; j < j1; ++j) P->events16[j] = word16(P->events[j]);
             });
+            P->events.release();  // the 16-bit words are the batch's (the device widens them)
         }
         lap("16-bit words");
     } catch (const std::bad_alloc &) {
@@ -971,13 +1532,30 @@ extern "C" int64_t lc_packed_event_row(const lc_packed *p, int64_t i, int64_t j)
     if (!p || i < 0 || i >= (int64_t)p->keys.size()) return lc::fail(LC_E_INVALID, "lc_packed_event_row: bad key");
     uint64_t b = p->ev_off[(size_t)i], e = p->ev_off[(size_t)i + 1];
     if (j < 0 || (uint64_t)j >= e - b) return lc::fail(LC_E_INVALID, "lc_packed_event_row: bad event");
-    return p->ev_row[b + (uint64_t)j];
+    return p->event_row((size_t)i, b + (uint64_t)j);
+}
+
+extern "C" int lc_packed_path(const lc_packed *p) { return p && p->key_major ? 1 : 0; }
+
+extern "C" int64_t lc_packed_event_rows(const lc_packed *p, int64_t *out) {
+    if (!p) return lc::fail(LC_E_INVALID, "lc_packed_event_rows: null packed batch");
+    const size_t K = p->keys.size();
+    const int64_t n = K ? (int64_t)p->ev_off[K] : 0;
+    if (out)
+        for (size_t k = 0; k < K; ++k)
+            for (uint64_t e = p->ev_off[k]; e < p->ev_off[k + 1]; ++e) out[e] = p->event_row(k, e);
+    return n;
 }
 
 extern "C" int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows) {
     if (!p || i < 0 || i >= (int64_t)p->keys.size()) return lc::fail(LC_E_INVALID, "lc_packed_subhistory: bad key");
-    const int64_t *a = p->krows.data() + p->krow_off[(size_t)i];
     int64_t na = (int64_t)(p->krow_off[(size_t)i + 1] - p->krow_off[(size_t)i]);
+    if (p->key_major) {  // the key's rows are one run (no shared rows)
+        if (out_rows)
+            for (int64_t j = 0; j < na; ++j) out_rows[j] = p->key_row0[(size_t)i] + j;
+        return na;
+    }
+    const int64_t *a = p->krows.data() + p->krow_off[(size_t)i];
     const int64_t *s = p->shared_rows.data();
     int64_t ns = (int64_t)p->shared_rows.size();
     if (out_rows) std::merge(a, a + na, s, s + ns, out_rows);

@@ -55,7 +55,7 @@ struct KeyView {
         n = p->ev_off[(size_t)k + 1] - eb;
         upto = std::min<uint64_t>(upto, n);
         for (uint64_t j = 0; j < upto; ++j) {
-            const uint32_t w = p->events[eb + j];
+            const uint32_t w = p->word(eb + j);
             const uint32_t s = LC_EV_SLOT(w);
             if (w & LC_EV_OK_BIT) {
                 held.erase(s);
@@ -65,19 +65,19 @@ struct KeyView {
             }
         }
     }
-    int64_t row(uint64_t j) const { return p->ev_row[eb + j]; }
+    int64_t row(uint64_t j) const { return p->event_row((size_t)key, eb + j); }
     // the row completing invoke event j (its slot's next event, when an :ok)
     int64_t done_row(uint64_t j) const {
-        const uint32_t s = LC_EV_SLOT(p->events[eb + j]);
+        const uint32_t s = LC_EV_SLOT(p->word(eb + j));
         for (uint64_t i = j + 1; i < n; ++i) {
-            const uint32_t w = p->events[eb + i];
+            const uint32_t w = p->word(eb + i);
             if (LC_EV_SLOT(w) == s) return (w & LC_EV_OK_BIT) ? row(i) : -1;
         }
         return -1;
     }
     uint32_t desc(uint64_t j) const {
         const uint64_t tb = p->trans_off.empty() ? 0 : p->trans_off[(size_t)key];
-        return p->trans[tb + LC_EV_TRANS(p->events[eb + j])];
+        return p->trans[tb + LC_EV_TRANS(p->word(eb + j))];
     }
     // the op of invoke event j from state st: next state or LC_STATE_NONE
     uint32_t step(uint64_t j, uint32_t st) const {
@@ -125,7 +125,7 @@ static int64_t report(const lc_packed *p, int64_t key, int32_t valid, int32_t fa
         auto in_mask = [](const std::pair<uint64_t, uint64_t> &m, uint32_t s) {
             return s < 64 ? ((m.first >> s) & 1) != 0 : ((m.second >> (s - 64)) & 1) != 0;
         };
-        const uint32_t p_slot = fail_event >= 0 ? LC_EV_SLOT(p->events[kv.eb + (uint64_t)fail_event]) : 0xFFFFFFFFu;
+        const uint32_t p_slot = fail_event >= 0 ? LC_EV_SLOT(p->word(kv.eb + (uint64_t)fail_event)) : 0xFFFFFFFFu;
         const size_t want = (size_t)std::max(max_paths, 0);
         std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> shown(
             finals.begin(), finals.begin() + (ptrdiff_t)std::min(finals.size(), want));

@@ -12,14 +12,42 @@
 struct lc_packed {
     std::vector<int64_t> keys;
     lc::pinned_vector<uint64_t> ev_off;  // page-locked on a GPU host: lc_check_* DMA it directly
-    lc::pinned_vector<uint32_t> events;
-    lc::pinned_vector<uint16_t> events16;  // the same words in 16 bits when all fit (empty otherwise)
+    // the event words, page-locked for the device; left out (empty) when
+    // the 16-bit form below is given (the device widens it; word() here)
+    lc::host_array<uint32_t> events;
+    // the same words in 16 bits when all fit (empty otherwise), page-locked
+    lc::host_array<uint16_t> events16;
+    uint32_t word(uint64_t e) const { return events.empty() ? LC_EV16_WIDE(events16[e]) : events[e]; }
+    // history row of each event: ev_row (the bucketing path), or, when every
+    // key's rows are one run of the history (key_major), a bitmap of the
+    // key's rows that emit no event (skip, from word skip_off[key]): event j
+    // of key k is the j-th row of its run without a skip bit
     lc::uninit_vector<int64_t> ev_row;
+    lc::host_array<uint64_t> skip;
+    std::vector<uint64_t> skip_off;
+    std::vector<int64_t> key_row0;
+    bool key_major = false;
+    int64_t event_row(size_t key, uint64_t e) const {  // e: index into the event words
+        if (!key_major) return ev_row[e];
+        uint64_t j = e - ev_off[key];
+        const uint64_t *w = skip.data() + skip_off[key];
+        for (int64_t base = 0;; base += 64, ++w) {
+            const uint64_t keep = ~*w;
+            const uint64_t c = (uint64_t)__builtin_popcountll(keep);
+            if (j < c) {
+                uint64_t x = keep;
+                for (uint64_t i = 0; i < j; ++i) x &= x - 1;  // drop the j lowest kept rows
+                return key_row0[key] + base + __builtin_ctzll(x);
+            }
+            j -= c;
+        }
+    }
     std::vector<uint32_t> trans;
     std::vector<uint32_t> trans_off;  // empty = shared table
     std::vector<uint8_t> key_width;
     std::vector<uint16_t> key_states;
-    // sub-history rows: per-key rows + rows shared by every key
+    // sub-history rows: per-key rows + rows shared by every key (key_major:
+    // krows empty, key k's rows are key_row0[k] + [0, krow_off[k+1] - krow_off[k]))
     std::vector<uint64_t> krow_off;
     lc::uninit_vector<int64_t> krows;
     std::vector<int64_t> shared_rows;

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 10
+LC_ABI_VERSION = 11
 LC_MAX_DEVICES = 8
 LC_COMM_ID_BYTES = 128
 LC_OPT_COUNT_PROBES = 0x1
@@ -68,7 +68,10 @@ class LcBatch(C.Structure):
 
 
 class LcPackOpts(C.Structure):
-    _fields_ = [("model", C.c_int32), ("n_init", C.c_int32), ("init", P(C.c_int64))]
+    _fields_ = [("model", C.c_int32), ("n_init", C.c_int32), ("init", P(C.c_int64)), ("flags", C.c_uint32)]
+
+
+LC_PACK_GENERAL = 0x1  # lc_pack_opts.flags (ABI 11): always the bucketing path
 
 
 class LcOpts(C.Structure):
@@ -109,6 +112,7 @@ class LcSynthOpts(C.Structure):
 # this table against include/lincheck.h.
 SIGNATURES = {
     "lc_abi_version": (C.c_int, []),
+    "lc_trim": (None, []),
     "lc_last_error": (C.c_char_p, []),
     "lc_device_count": (C.c_int, []),
     "lc_create": (C.c_int, [P(LcOpts), P(C.c_void_p)]),
@@ -131,6 +135,8 @@ SIGNATURES = {
     "lc_packed_view": (C.c_int, [C.c_void_p, P(LcBatch)]),
     "lc_packed_key": (C.c_int64, [C.c_void_p, C.c_int64]),
     "lc_packed_event_row": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int64]),
+    "lc_packed_path": (C.c_int, [C.c_void_p]),
+    "lc_packed_event_rows": (C.c_int64, [C.c_void_p, P(C.c_int64)]),
     "lc_packed_subhistory": (C.c_int64, [C.c_void_p, C.c_int64, P(C.c_int64)]),
     "lc_packed_key_error": (C.c_char_p, [C.c_void_p, C.c_int64]),
     "lc_packed_state_value": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint32, P(C.c_int64), P(C.c_int)]),

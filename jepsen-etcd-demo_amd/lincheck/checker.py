@@ -18,6 +18,7 @@ Jepsen's check-safe would.
 from __future__ import annotations
 
 import ctypes as C
+import gc
 import os
 import threading
 import time
@@ -80,11 +81,25 @@ class Packed:
     def n_events(self, i: int) -> int:
         return int(self.ev_off[i + 1] - self.ev_off[i])
 
+    def all_events(self) -> np.ndarray:
+        """Every event word (u32), widened from the 16-bit form when lc_pack
+        gave only that (lc_batch.events NULL, ABI 11)."""
+        n = int(self.ev_off[-1]) if self.n_keys else 0
+        if n == 0:
+            return np.zeros(0, np.uint32)
+        if self.view.events:
+            return np.ctypeslib.as_array(self.view.events, shape=(n,)).copy()
+        e = np.ctypeslib.as_array(self.view.events16, shape=(n,)).astype(np.uint32)
+        return ((e & 0x8000) << 16) | (((e >> 11) & 0xF) << 24) | (e & 0x7FF)
+
     def events(self, i: int) -> np.ndarray:
         b, e = int(self.ev_off[i]), int(self.ev_off[i + 1])
         if e == b:
             return np.zeros(0, np.uint32)
-        return np.ctypeslib.as_array(self.view.events, shape=(int(self.ev_off[-1]) or 1,))[b:e].copy()
+        if self.view.events:
+            return np.ctypeslib.as_array(self.view.events, shape=(int(self.ev_off[-1]) or 1,))[b:e].copy()
+        e16 = np.ctypeslib.as_array(self.view.events16, shape=(int(self.ev_off[-1]) or 1,))[b:e].astype(np.uint32)
+        return ((e16 & 0x8000) << 16) | (((e16 >> 11) & 0xF) << 24) | (e16 & 0x7FF)
 
     def event_row(self, i: int, j: int) -> int:
         return int(N.check(N.lib().lc_packed_event_row(self.handle, i, j)))
@@ -527,6 +542,19 @@ class Linearizable:
         t1 = time.perf_counter()
         res = self._dev().check(packed, peaks=False) if packed.n_keys else None
         t2 = time.perf_counter()
+        # the result maps are thousands of small dicts, none cyclic: the
+        # collector's passes over the process's objects while they are made
+        # cost more than making them (3x on the box, bench --jepsen)
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            return self._shape(test, history, opts, inner, hist, packed, res, t0, t1, t2)
+        finally:
+            if gc_was:
+                gc.enable()
+
+    def _shape(self, test, history, opts, inner, hist, packed, res, t0, t1, t2) -> Dict:
+        from .independent import merge_results, subhistory
         results = {}
         ops_cache = None
         # the other checkers of a compose, and whether any reads a sub-history

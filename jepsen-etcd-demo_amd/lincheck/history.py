@@ -50,7 +50,7 @@ class _HistOwner:
         self.handle = handle
 
     def __del__(self):
-        if self.handle:
+        if self.handle and N is not None:  # (at interpreter exit the module may be gone)
             N.lib().lc_hist_free(self.handle)
             self.handle = None
 

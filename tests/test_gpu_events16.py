@@ -2,10 +2,13 @@
 batch uploaded at 2 bytes per event and widened on the GPU gives the same
 records as the 32-bit upload, in every path that takes it (lc_check_node,
 lc_check_batch, lc_upload + resident steps), and the oracle's verdicts."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
 import cref
+from lincheck import _native as N
 from lincheck import history as H
 from lincheck import parallel as P
 from lincheck.checker import Device, Packed
@@ -27,11 +30,14 @@ def test_events16_same_records(keys, ops, anom):
     dev.wait()
     res16 = dev.node_records(keys)
     del db
-    e16 = pk.view.events16
-    pk.view.events16 = None  # the 32-bit upload
+    # the 32-bit upload: the same words widened on the host (lc_pack gives
+    # only the 16-bit ones when every word fits, ABI 11)
+    e32 = pk.all_events()
+    saved = (pk.view.events, pk.view.events16)
+    pk.view.events, pk.view.events16 = N.ptr(e32, C.c_uint32), None
     rec32, _ = dev.check_node(pk, keys)
     r32 = dev.check(pk, verdicts_only=True)
-    pk.view.events16 = e16
+    pk.view.events, pk.view.events16 = saved
     np.testing.assert_array_equal(rec16, rec32)
     np.testing.assert_array_equal(res16, rec32)
     np.testing.assert_array_equal(r16.valid, r32.valid)

@@ -111,7 +111,7 @@ def _batch_copy(pk):
     K = pk.n_keys
     n_ev = int(pk.ev_off[-1])
     arrs = dict(ev_off=pk.ev_off.copy(),
-                events=np.ctypeslib.as_array(pk.view.events, shape=(n_ev,)).copy(),
+                events=pk.all_events(),
                 trans=np.ctypeslib.as_array(pk.view.trans, shape=(int(pk.view.n_trans),)).copy(),
                 width=np.ctypeslib.as_array(pk.view.key_width, shape=(K,)).copy(),
                 states=np.ctypeslib.as_array(pk.view.key_states, shape=(K,)).copy())

@@ -182,10 +182,12 @@ def test_events16_widen_to_events():
     from lincheck.checker import Packed
     pk = Packed(H.synth(n_keys=50, ops_per_key=200, concurrency=10, anomaly_rate=0.2, seed=9))
     n = int(pk.ev_off[-1])
-    e32 = np.ctypeslib.as_array(pk.view.events, shape=(n,)).astype(np.uint32)
+    # the 16-bit words are the batch's (ABI 11: no 32-bit copy beside them;
+    # tests/test_pack_fast.py holds them to the bucketing path's)
+    assert not pk.view.events
     e16 = np.ctypeslib.as_array(pk.view.events16, shape=(n,)).astype(np.uint32)
     wide = ((e16 & 0x8000) << 16) | (((e16 >> 11) & 0xF) << 24) | (e16 & 0x7FF)
-    np.testing.assert_array_equal(wide, e32)
+    np.testing.assert_array_equal(pk.all_events(), wide)
     # > 16 ops pending at once: slots past 15, no 16-bit form
     pk = Packed(H.synth(n_keys=4, ops_per_key=300, concurrency=40, mean_think=0.1, seed=9))
     assert not pk.view.events16
