@@ -261,22 +261,12 @@ def bench_jepsen(args):
     print(json.dumps(line, default=str), flush=True)
 
 
-def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quota):
-    """oracle/linear_ref.c with a pthread pool over keys (independent/
-    checker's pmap) on this host: all usable cores, then one core, each on a
-    bounded sample of the same batch (~10-20 s of CPU work in all)."""
+def cpu_linear(args, K, hist, ops, threads, first_keys, v_host, fe_host, nproc, aff, quota):
+    """oracle/linear_ref.c on all usable cores, then one core (cpu_baseline's
+    :linear part)."""
     import numpy as np
 
     import cref
-    from lincheck import history as H
-    threads = max(1, min(aff, quota or aff))
-
-    def first_keys(k):  # the batch's first k keys (per-key seeded generator)
-        if k == K:
-            return hist
-        return H.synth(n_keys=k, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
-                       anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"], key_base=key0)
-
     kp = min(K, threads)
     tc = time.perf_counter()
     keys, orc = cref.check_history(first_keys(kp).as_c(), budget=args.budget, threads=threads)
@@ -317,6 +307,34 @@ def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quo
         parity = None
     if ks < K:
         cpu["parity_sample_keys"] = ks
+    return cpu, parity
+
+
+def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quota):
+    """oracle/linear_ref.c with a pthread pool over keys (independent/
+    checker's pmap) on this host: all usable cores, then one core, each on a
+    bounded sample of the same batch (~10-20 s of CPU work in all)."""
+    import numpy as np
+
+    import cref
+    from lincheck import history as H
+    threads = max(1, min(aff, quota or aff))
+
+    def first_keys(k):  # the batch's first k keys (per-key seeded generator)
+        if k == K:
+            return hist
+        return H.synth(n_keys=k, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
+                       anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"], key_base=key0)
+
+    cpu, parity = None, None
+    # :linear at a large budget on C4-shaped keys takes minutes per key sample
+    # (54 s for 16 keys at 2^22, profiles/r05_c4_budget_sweep.json): a --algorithm
+    # wgl line at such a budget times the restatement of knossos.wgl alone
+    if not (args.algorithm == "wgl" and args.budget > (1 << 20)):
+        cpu, parity = cpu_linear(args, K, hist, ops, threads, first_keys, v_host, fe_host, nproc, aff, quota)
+    else:
+        cpu = {"linear": "not timed: the budget is beyond a bounded sample of :linear on this workload",
+               "cores": threads, "host": {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota}}
     # knossos.wgl's search (the other analysis jepsen.checker/linearizable
     # offers, north_star's "CPU :linear/:wgl"): oracle/wgl_ref.c on the same
     # cores, on as many of the batch's first keys as ~8 s allow
@@ -345,6 +363,8 @@ def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quo
                   "keys_decided": int((worc["valid"] != -1).sum()), "keys": kw}
     if args.algorithm == "wgl":
         parity = bool(np.array_equal(worc["valid"], v_host[:kw]) and np.array_equal(worc["fail_event"], fe_host[:kw]))
+    if "value" not in cpu:  # (the --algorithm wgl line at a large budget: knossos.wgl's restatement)
+        cpu.update({k: cpu["wgl"][k] for k in ("value", "unit", "kind", "sample")})
     return cpu, parity
 
 
@@ -700,6 +720,7 @@ def main():
                    "keys_decided": int(((wres.valid != -1) & wsel).sum()) if wsel is not None else None,
                    "keys_spilled": int(wres.stats["wgl_spilled"]) if wres is not None else None,
                    "steps": wsteps, "cache_entries": cache_entries,
+                   "probes": int(wres.stats["probes"]) if wres is not None else None,
                    "steps_per_s": (wsteps / (avg_wgl * 1e-3)) if wsteps and avg_wgl > 0 else None}
             if args.algorithm == "wgl" or avg_wgl >= max(avg_t0, avg_t3):
                 # Algorithmic bytes of a WGL launch: the event words (4 B),

@@ -390,7 +390,9 @@ typedef struct lc_opts {
                                       table the budget fits)                        */
 #define LC_PATH_SPEC_NOSTAGE 0x1000 /* speculative segments: event words read from HBM
                                       by every run, not staged in LDS once per key  */
-#define LC_PATH_ALL          0x1FFF
+#define LC_PATH_WGL_EV_HBM   0x2000 /* WGL: every key's events read from HBM, none
+                                       staged in LDS (tests of that walk; ABI 11)   */
+#define LC_PATH_ALL          0x3FFF
 
 /* lc_opts.flags */
 #define LC_OPT_COUNT_PROBES 0x1  /* count successor-config probes (lc_stats.probes,

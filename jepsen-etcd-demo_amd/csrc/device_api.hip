@@ -328,12 +328,12 @@ struct Dev {
         lcd::LayWs w{};
     } lws;
     // knossos.wgl workspaces (device_wgl.hip): [0] tables sized to share at
-    // most WGL_SMALL_BYTES among the resident waves, [1] tables the budget
+    // most a share of the free HBM (WGL_SHARE_MAX), [1] tables the budget
     // fits, for the keys that outgrow [0]; zeroed once (entries are stamped)
     struct WWs {
         char *base = nullptr;
         size_t bytes = 0;
-        size_t slot_bytes = 0;
+        lcd::WglWs layout{};  // the layout its contents were written under
         int slots = 0;
     } wws[2];
     uint32_t wgl_seq = 0;     // launches so far (the high half of every cache stamp)
@@ -1034,13 +1034,19 @@ static int ensure_segments(Dev *c, int64_t n_keys) {
 
 // ---- knossos.wgl (device_wgl.hip) ---------------------------------------------
 
-// Lowe's caches of the resident waves share at most this many bytes; a key
-// whose cache outgrows its share is searched again with a table the budget
-// fits (fewer waves at once).
-constexpr size_t WGL_SMALL_BYTES = 4ull << 30;
+// Lowe's caches of the resident waves share at most this much of the free
+// HBM (a third, and at most 96 GB); a key whose cache outgrows its share is
+// searched again with a table the budget fits (fewer waves at once).  C4 at
+// a budget of 2^22 (256 keys x a 2^23-entry table, 64 GB) then searches
+// every key once; with a 4 GB share, 253 of its 256 keys outgrew their
+// 2^19-entry tables and were searched twice (profiles/r05_c4_budget_sweep.json).
+constexpr size_t WGL_SHARE_MAX = 96ull << 30;
+constexpr uint64_t WGL_SPILL_ENTRIES = 1ull << 19;  // first tables when the budget's do not fit the share
 constexpr uint32_t WGL_LDS_EVENTS = 8192;  // events (+ slot history) per key held in LDS
 
 // Allocate (or reuse) WGL workspace `which` for `slots` waves of layout w.
+// Contents written under another layout are cleared (a table entry is the
+// key's by its stamp only where every earlier write was a table entry too).
 static int ensure_wgl_ws(Dev *c, int which, const lcd::WglWs &w, int want, int *slots_out) {
     Dev::WWs &W = c->wws[which];
     size_t free_b = 0, total_b = 0;
@@ -1051,16 +1057,19 @@ static int ensure_wgl_ws(Dev *c, int which, const lcd::WglWs &w, int want, int *
     if ((size_t)slots * w.slot_bytes > limit)
         return lc::fail(LC_E_NOMEM, "WGL workspace: one wave needs %zu bytes (budget %llu)", w.slot_bytes,
                         (unsigned long long)c->o->max_configs);
-    if (!W.base || W.slot_bytes != w.slot_bytes || W.slots < slots) {
+    const size_t need = (size_t)slots * w.slot_bytes;
+    if (!W.base || W.bytes < need) {
         if (W.base) HIPCHK(hipStreamSynchronize(c->stream));
         dfree(W.base);
-        W.bytes = 0; W.slots = 0; W.slot_bytes = 0;
-        HIPCHK(hipMalloc((void **)&W.base, (size_t)slots * w.slot_bytes));
-        HIPCHK(hipMemsetAsync(W.base, 0, (size_t)slots * w.slot_bytes, c->stream));  // stamp 0: never a key's
-        W.bytes = (size_t)slots * w.slot_bytes;
-        W.slots = slots;
-        W.slot_bytes = w.slot_bytes;
+        W.bytes = 0; W.slots = 0; W.layout = lcd::WglWs{};
+        HIPCHK(hipMalloc((void **)&W.base, need));
+        HIPCHK(hipMemsetAsync(W.base, 0, need, c->stream));  // stamp 0: never a key's
+        W.bytes = need;
+    } else if (!W.layout.same_layout(w)) {
+        HIPCHK(hipMemsetAsync(W.base, 0, W.bytes, c->stream));
     }
+    W.layout = w;
+    W.slots = (int)std::min<size_t>(W.bytes / w.slot_bytes, (size_t)INT32_MAX);
     *slots_out = std::min(slots, W.slots);
     return LC_OK;
 }
@@ -1081,10 +1090,20 @@ static int run_wgl(Dev *c, const DevBatch *d, const lcd::Args &a, const int32_t 
     if (max_ev > 0x7FFFFFFFull) return lc::fail(LC_E_INVALID, "WGL: a key with more than 2^31 events");
     const uint64_t need = lcd::wgl_table_entries(o.max_configs);
     const int slots_a = (int)std::min<int64_t>(n_hint, (int64_t)c->cu_count * 4);
-    uint64_t t_a = 1ull << 14;
-    while (t_a * 2 <= need && t_a * 2 * 32 * (uint64_t)slots_a <= WGL_SMALL_BYTES) t_a *= 2;
+    // Lowe's tables of the first launch: the budget's table for every resident
+    // wave -- twice that (a quarter full at the budget) when the share holds
+    // it -- if a third of the free HBM holds them (C4 at 2^22: 64 GB); else
+    // 2^19 entries, and the keys that pass half of that are searched again
+    // with the budget's table (early, so the walk repeated is short).  Both
+    // measured in round 5 against tables that grow into a pool.
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t share = std::min<uint64_t>((c->wws[0].bytes + free_b) / 3, WGL_SHARE_MAX);
+    const uint64_t per = 32ull * (uint64_t)slots_a;
+    uint64_t t_a = need * per <= share ? need : std::min<uint64_t>(need, WGL_SPILL_ENTRIES);
+    if (t_a == need && 2 * need * per <= share) t_a = 2 * need;
     if (o.path_flags & LC_PATH_WGL_SMALL) t_a = 1ull << 14;
-    t_a = std::min(t_a, need);
+    t_a = std::min(t_a, 2 * need);
     const lcd::WglWs wa = lcd::wgl_layout(o.max_configs, (uint32_t)max_ev, (uint32_t)t_a);
     int slots = 0;
     int rc = ensure_wgl_ws(c, 0, wa, slots_a, &slots);
@@ -1108,6 +1127,7 @@ static int run_wgl(Dev *c, const DevBatch *d, const lcd::Args &a, const int32_t 
     if (!lcd::wgl_allow_lds(lds_cap)) lds_cap = std::min<size_t>(lds_cap, 64u << 10);
     w.lds_events = (uint32_t)std::min<uint64_t>(max_ev, WGL_LDS_EVENTS);
     if (d->narrow_keys == 0) w.lds_events = (uint32_t)std::min<uint64_t>(max_ev, 3 * WGL_LDS_EVENTS / 2);
+    if (o.path_flags & LC_PATH_WGL_EV_HBM) w.lds_events = 0;  // every key's events from HBM (tests)
     w.lds_tab = d->narrow_keys > 0 ? 4096u : 0u;
     w.lds_events = (w.lds_events + 1u) & ~1u;  // even: the cache tier after it is 8-byte aligned
     while (lcd::wgl_lds_bytes(w.lds_events, w.lds_tab) > lds_cap) {
@@ -1126,6 +1146,7 @@ static int run_wgl(Dev *c, const DevBatch *d, const lcd::Args &a, const int32_t 
     w.valid = a.valid; w.fail_event = a.fail_event; w.cause = a.cause; w.peak = a.peak;
     w.final_cfg = a.final_cfg; w.n_final = a.n_final; w.analyzer = analyzer; w.rec = a.rec;
     w.ev_count = a.ev_count; w.keys_done = a.keys_done;
+    w.probes = o.algorithm == LC_ALGO_WGL ? a.probes : nullptr;  // (competition: :linear's probe count)
     HIPCHK(hipEventRecord(c->et3a, c->stream));
     HIPCHK(lcd::launch_wgl(w, slots, c->stream));
     int32_t n_spill = 0;
@@ -1256,6 +1277,7 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             st->wgl_keys = c->hctl[2];
             st->wgl_steps = c->hctl[1];
             st->events = c->hctl[1];
+            st->probes = c->hctl[0];  // Lowe's cache lookups
             st->wgl_spilled = ws.wgl_spilled;
         }
         return LC_OK;

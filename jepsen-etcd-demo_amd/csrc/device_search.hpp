@@ -166,6 +166,9 @@ struct WglWs {
     size_t slot_bytes;
     uint32_t tab_mask;
     size_t off_frames, off_prev;
+    bool same_layout(const WglWs &o) const {
+        return slot_bytes == o.slot_bytes && tab_mask == o.tab_mask && off_frames == o.off_frames && off_prev == o.off_prev;
+    }
 };
 struct WglArgs {
     const uint64_t *ev_off;
@@ -202,6 +205,7 @@ struct WglArgs {
     uint64_t *rec;               // may be null: LC_REC_* records
     unsigned long long *ev_count;   // search steps
     unsigned long long *keys_done;
+    unsigned long long *probes;     // may be null: cache lookups (one per legal candidate of a probe round)
 };
 WglWs wgl_layout(uint64_t budget, uint32_t max_events, uint32_t table_entries);
 size_t wgl_table_entries(uint64_t budget);

@@ -239,9 +239,10 @@ __device__ __forceinline__ KargWgl &cold_args() {
 }
 
 __device__ __forceinline__ void wgl_finish(const WglArgs &, int32_t key, int verdict, int cause, int32_t fev,
-                                           uint32_t cache_n, uint32_t n_front, uint64_t steps) {
+                                           uint32_t cache_n, uint32_t n_front, uint64_t steps, uint64_t lookups = 0) {
     KargWgl &a = cold_args();
     if (__lane_id() == 0) {
+        if (a.probes) atomicAdd(a.probes, (unsigned long long)lookups);
         a.valid[key] = (int8_t)verdict;
         a.cause[key] = (uint8_t)cause;
         a.fail_event[key] = fev;
@@ -400,6 +401,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
     uint32_t ring_lo = 0;  // frames [ring_lo, depth) are in the LDS ring too
     uint32_t deepest = WGL_NONE;  // the deepest return entry the walk got stuck on
     uint64_t steps = 0;
+    uint64_t lookups = 0;    // cache lookups: one per legal candidate of a probe round
     bool fresh = true;       // the current node has not been probed yet
     // the child the op of R leads to, as its probe round moved R there (valid
     // for a step down in the same iteration as the probe)
@@ -430,6 +432,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             const bool ok0 = (lm & 4u) && !(lm & 1u) && step(a.table, s, dsc0, s20);
             const bool ok1 = WIDE && (lm & 8u) && !(lm & 2u) && step(a.table, s, dsc1, s21);
             const bool r_ok = has_R && ((ballot(rs < 64 ? ok0 : ok1) >> (rs & 63)) & 1ull);
+            lookups += (uint64_t)__builtin_popcountll(ballot(ok0)) + (WIDE ? (uint64_t)__builtin_popcountll(ballot(ok1)) : 0ull);
             // the child reached by taking the op of R: R moves on (tentatively;
             // the ops returning in between leave X)
             uint32_t R2 = WGL_END, z2 = 0;
@@ -520,11 +523,12 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     const uint4 pe = tab[2 * (size_t)((ph + lane) & mask) + 1];
                     pfree = ((uint64_t)pe.z | (uint64_t)pe.w << 32) != gen;
                 }
+                // (one entry per round trip: reading two, p and p + 1, was
+                // measured in round 5 -- C2 8.21 -> 8.54 ms, C4 at 2^16 204 ->
+                // 208 ms, at 2^20 3,255 -> 3,187 ms; not kept)
                 for (uint32_t probe = 0; probe <= mask; ++probe) {
                     if (!ballot((act0 | act1) != 0u)) break;
                     WP_ADD(6, 1);
-                    // (the loads only where a probe is active: an HBM entry is
-                    // 32 bytes; the updates branch-free)
                     uint4 e00 = {}, e01 = {}, e10 = {}, e11 = {};
                     if (act0) { e00 = tab[2 * (size_t)p0]; e01 = tab[2 * (size_t)p0 + 1]; }
                     if (act1) { e10 = tab[2 * (size_t)p1]; e11 = tab[2 * (size_t)p1 + 1]; }
@@ -543,6 +547,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     p0 = (p0 + act0) & mask;
                     p1 = (p1 + act1) & mask;
                 }
+
             }
             lm = (lm & 0xFu) | (ok0 && !hit0 ? 1u << LM_C : 0u) | (ok1 && !hit1 ? 2u << LM_C : 0u);
             (void)act0;
@@ -594,7 +599,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             // ---- no candidate left ----
             if (!has_R) {  // the walk runs off the end of the list: linearizable
                 WP_DUMP();
-                wgl_finish(a, key, LC_VALID, LC_CAUSE_NONE, -1, cache_n, 0, steps);
+                wgl_finish(a, key, LC_VALID, LC_CAUSE_NONE, -1, cache_n, 0, steps, lookups);
                 return true;
             }
             // stuck on the return entry R: the deepest such entries' nodes
@@ -614,7 +619,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             }
             if (depth == 0) {
                 WP_DUMP();
-                wgl_finish(a, key, LC_INVALID, LC_CAUSE_NONLIN, (int32_t)deepest, cache_n, n_front, steps);
+                wgl_finish(a, key, LC_INVALID, LC_CAUSE_NONLIN, (int32_t)deepest, cache_n, n_front, steps, lookups);
                 return true;
             }
             // backtrack: the frame of the node above (the LDS ring holds the
@@ -665,7 +670,11 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         sc = uni(sc);
         if (a.spill_at && cache_n + 1 > a.spill_at) {
             // the table would pass half full: the key is searched again with
-            // a table the budget fits (no result written here)
+            // a table the budget fits (no result written here).  Growing the
+            // table in place instead (a rehash into a 4x table from a pool)
+            // was built and measured in round 5: the rehash code alone, never
+            // run, made every walk ~15 % slower (C2 8.6 -> 9.9 ms, C4 at 2^16
+            // 216 -> 250 ms).
             if (lane == 0) {
                 KargWgl &ca = cold_args();
                 const int32_t i = atomicAdd(ca.n_spill, 1);
@@ -678,7 +687,7 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
         ++steps;
         if ((uint64_t)cache_n > a.budget) {
             WP_DUMP();
-            wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_BUDGET, -1, cache_n, 0, steps);
+            wgl_finish(a, key, LC_UNKNOWN, LC_CAUSE_BUDGET, -1, cache_n, 0, steps, lookups);
             return true;
         }
         // the pair joins the cache in the next probe round; at the slot this
@@ -793,9 +802,12 @@ WglWs wgl_layout(uint64_t budget, uint32_t max_events, uint32_t table_entries) {
     return w;
 }
 
+// Lowe's cache holds at most budget + 1 pairs (the one past the budget ends
+// the walk :unknown): a table of twice the budget keeps linear probing at
+// most half full.
 size_t wgl_table_entries(uint64_t budget) {
-    uint64_t T = 1;
-    while (T < 2 * (budget + 2)) T <<= 1;
+    uint64_t T = 64;
+    while (T < 2 * budget || T < budget + 64) T <<= 1;
     return (size_t)T;
 }
 

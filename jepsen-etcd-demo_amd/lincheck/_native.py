@@ -25,6 +25,7 @@ LC_OPT_COUNT_PROBES = 0x1
 LC_PATH_SPLIT_ON, LC_PATH_SPLIT_OFF, LC_PATH_SPEC_OFF, LC_PATH_LAYERS_OFF = 0x01, 0x02, 0x04, 0x08
 LC_PATH_NODE_SYNC, LC_PATH_NODE_STAGED, LC_PATH_CHUNKS_ON, LC_PATH_CHUNKS_OFF = 0x10, 0x20, 0x40, 0x80
 LC_PATH_SPEC_COST, LC_PATH_EV32, LC_PATH_SPEC_NOPRIO, LC_PATH_WGL_SMALL = 0x100, 0x200, 0x400, 0x800
+LC_PATH_WGL_EV_HBM = 0x2000  # ABI 11
 LC_PATH_SPEC_NOSTAGE = 0x1000
 LC_T0_PATH_NONE, LC_T0_PATH_LATTICE, LC_T0_PATH_SPEC, LC_T0_PATH_SEGMENTS = 0, 1, 2, 3
 T0_PATH_NAMES = {0: "none", 1: "k_search_lattice", 2: "k_spec", 3: "k_search_segments"}

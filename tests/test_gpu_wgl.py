@@ -140,3 +140,32 @@ def test_competition_answers_budget_keys_with_wgl():
         else:
             assert r["analyzer"] == "linear" and r["valid?"] == a.valid, k
     assert any(r["analyzer"] == "wgl" and r["valid?"] is True for r in out["results"].values())
+
+
+@pytest.mark.parametrize("name,kw,budget", [
+    ("c2", dict(n_keys=60, ops_per_key=1000, concurrency=10, seed=2), 1 << 20),
+    ("c5", dict(n_keys=120, ops_per_key=1000, concurrency=10, anomaly_rate=0.2, seed=5), 1 << 20),
+    ("c4", dict(n_keys=8, ops_per_key=1200, concurrency=30, info_rate=0.02, seed=4), 1 << 16),
+])
+def test_wgl_events_from_hbm(name, kw, budget):
+    """the walk that reads a key's events, slot history and
+    descriptors from HBM (wgl_key<false, *>: keys longer than the LDS
+    staging) -- every key forced onto it (LC_PATH_WGL_EV_HBM), narrow and
+    wide windows, valid, invalid and budget keys -- gives the restatement's
+    records."""
+    _, res, orc = wgl_vs_oracle(H.synth(**kw), budget, path_flags=N.LC_PATH_WGL_EV_HBM)
+    if name == "c5":
+        assert (orc["valid"] == 0).sum() > 5
+    # Lowe's cache lookups (one per legal candidate of a probe round): every
+    # pair the cache holds was a lookup's miss first
+    assert res.stats["probes"] >= int(res.peak.astype(np.int64).sum())
+
+
+def test_wgl_decides_c4_keys_at_a_larger_budget():
+    """BASELINE C4's first 16 keys at full size (5,000 ops, 30 clients, 2 %
+    crashed) at a cache budget of 2^20: :linear gives up on all of them at
+    any budget measured (profiles/r05_c4_budget_sweep.json); the walk
+    decides most, with the restatement's records, cache sizes included."""
+    h = H.synth(n_keys=16, ops_per_key=5000, concurrency=30, info_rate=0.02, seed=4)
+    _, res, orc = wgl_vs_oracle(h, 1 << 20)
+    assert int((res.valid == 1).sum()) >= 8
