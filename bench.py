@@ -598,8 +598,12 @@ def main():
         del d1_t0[:], d1_t3[:], d1_t3b[:], d1_wgl[:]
         n_enq[0] = 0
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for i in range(args.steps):
+            ts = time.perf_counter()
             rec = step()
+            if time.perf_counter() - ts > 10.0:  # (long steps: a sign of life for the job's watchdog)
+                print(f"[rank {rank}] step {i + 1}/{args.steps}: {time.perf_counter() - ts:.1f} s", file=sys.stderr,
+                      flush=True)
         sync(); barrier(); sync()
         el = time.perf_counter() - t0
         if world > 1:

@@ -28,7 +28,7 @@ pmc c3s "k_spec<2, 2, true, false>" C3 12500 1048576 linear
 pmc c4 "k_search_layers" C4 256 65536 linear
 pmc c4wgl "k_wgl" C4 256 65536 wgl
 pmc c2wgl "k_wgl" C2 1000 1048576 wgl
-for b in c2 c5 c3s c4 c4_wgl c4_comp c2_wgl c5_jepsen; do
+for b in c2 c5 c3s c4 c4_wgl c4_comp c2_wgl c5_jepsen c4_wgl24; do
   [ -f "$O/bench_$b.json" ] && tail -1 "$O/bench_$b.json" > $P/${T}_${b}_bench.json
 done
 [ -f "$O/tests.log" ] && { grep -E "passed|failed" "$O/tests.log" | tail -1 > $P/${T}_gpu_tests_summary.txt; }

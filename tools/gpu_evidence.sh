@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 R=${R:-5}
 O=gpurun_out/r$R
 mkdir -p $O/prof
-PARTS=${PARTS:-"tests c2 c5 c3s c4 c4wgl c2wgl c4comp c5jepsen"}
+PARTS=${PARTS:-"tests c2 c5 c3s c4 c4wgl c2wgl c4comp c5jepsen c4wgl24"}
 step() { echo "== $1 $(date +%T)"; }
 PROF="--no-cpu --no-resident --no-probes --no-c3"
 SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
@@ -69,6 +69,10 @@ for part in $PARTS; do
     bench c4_comp 400 --config C4 --budget 65536 --algorithm competition --steps 3 --warmup 1 --no-resident --no-cpu ;;
   c5jepsen)
     bench c5_jepsen 400 --config C5 --jepsen --steps 10 --warmup 2 ;;
+  c4wgl24)
+    # BASELINE C4 decided: knossos.wgl's walk at a 2^24 cache budget
+    # (profiles/r05_c4_budget_sweep.json: every key valid there)
+    bench c4_wgl24 600 --config C4 --budget 16777216 --algorithm wgl --d1-sync --steps 1 --warmup 1 --no-resident ;;
   *) echo "unknown part $part"; exit 2 ;;
   esac
 done
