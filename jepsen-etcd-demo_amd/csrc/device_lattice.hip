@@ -2350,8 +2350,17 @@ constexpr uint32_t spec_ev_lds() { return (E16 && S > 2) ? 4096u : 0u; }
 #ifndef LC_SPEC_KARG
 #define LC_SPEC_KARG 1
 #endif
+// The 2-wave build (the many-key batches: C3's shards, throughput-bound) is
+// held to 6 waves per SIMD: 79 VGPRs instead of 84, no spill, 5.5 waves per
+// SIMD where its 14 KB of LDS per block allows (11 blocks per CU).  A/B on
+// one box, the C3 shard (12,500 x 2,000): 4.04 -> 3.89 ms per step, kernel
+// 3.85 -> 3.72 ms, records identical (round 5).  7 is beyond the walk's
+// registers (the attribute is not met).
+#ifndef LC_SPEC2_WAVES
+#define LC_SPEC2_WAVES 6
+#endif
 template <int S, int W, bool E16, bool EX = false>
-__global__ __launch_bounds__(64 * W) void k_spec(T0Args a) {
+__global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : 1)) void k_spec(T0Args a) {
 #if LC_SPEC_KARG
 #define KA t0k()
 #else
