@@ -1103,12 +1103,23 @@ int pack_key_major(const lc_history *h, int model, lc_packed *P, const Par &par,
                 // has an invoke; the select keeps the loop free of branches)
                 const uint16_t *src = R.w16.data() + x.w0;
                 if (E16) {
+                    // (four words per 8-byte non-temporal store: the array is
+                    // read next by the DMA engine, not by this core, so its
+                    // lines need not be fetched first)
                     uint16_t *dst = E16 + e0;
-                    for (uint64_t j = 0; j < x.nw; ++j) {
+                    auto word = [&](uint64_t j) -> uint16_t {
                         const uint32_t w = src[j];
                         const uint32_t id = tid[w & 0x7FFu];
-                        dst[j] = (uint16_t)((w & 0xF800u) | ((w & 0x8000u) ? 0u : id));
+                        return (uint16_t)((w & 0xF800u) | ((w & 0x8000u) ? 0u : id));
+                    };
+                    uint64_t j = 0;
+                    for (; j < x.nw && ((uintptr_t)(dst + j) & 7u); ++j) dst[j] = word(j);
+                    for (; j + 4 <= x.nw; j += 4) {
+                        const uint64_t q = (uint64_t)word(j) | (uint64_t)word(j + 1) << 16 |
+                                           (uint64_t)word(j + 2) << 32 | (uint64_t)word(j + 3) << 48;
+                        __builtin_nontemporal_store(q, (uint64_t *)(dst + j));
                     }
+                    for (; j < x.nw; ++j) dst[j] = word(j);
                 } else {
                     uint32_t *dst = E32 + e0;
                     for (uint64_t j = 0; j < x.nw; ++j) {
@@ -1131,6 +1142,7 @@ int pack_key_major(const lc_history *h, int model, lc_packed *P, const Par &par,
         }
     });
     if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
+    std::atomic_thread_fence(std::memory_order_seq_cst);  // (the non-temporal stores drained: sfence)
     lap("transition ids");
     P->key_major = true;
     *took = true;

@@ -23,6 +23,17 @@ pmc() {  # name kernel workload keys budget algorithm
       --budget $b --round $R --algorithm $alg --cmd "$cmd" --out $P/${T}_${n}_sq.json "$s1" "$s2"
   return 0
 }
+# whole-launch kernel times from the traces (the stats CSV mixes launch sizes)
+tr() {  # name kernel workload keys budget algorithm
+  local t=$(csv kt_$1 '*kernel_trace.csv')
+  [ -n "$t" ] && python3 tools/profile_summary.py trace --kernel "$2" --workload $3 --keys $4 --budget $5 --round $R \
+      --algorithm $6 --cmd "rocprofv3 --kernel-trace --stats -- python3 bench.py (tools/gpu_evidence.sh part $1)" \
+      --out $P/${T}_$1_trace.json "$t"
+  return 0
+}
+tr c3s "k_spec<2, 2, true, false>" C3 12500 1048576 linear
+tr c4wgl "k_wgl" C4 256 65536 wgl
+tr c2wgl "k_wgl" C2 1000 1048576 wgl
 pmc c2 "k_spec<4, 4, true, false>" C2 1000 1048576 linear
 pmc c3s "k_spec<2, 2, true, false>" C3 12500 1048576 linear
 pmc c4 "k_search_layers" C4 256 65536 linear

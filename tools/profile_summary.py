@@ -67,7 +67,7 @@ def whole(ds):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=("bytes", "sq"))
+    ap.add_argument("mode", choices=("bytes", "sq", "trace"))
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--workload", required=True)
     ap.add_argument("--keys", type=int, required=True, help="keys of the launch the bench divides by")
@@ -80,7 +80,25 @@ def main():
     a = ap.parse_args()
     base = {"workload": a.workload, "keys": a.keys, "budget": a.budget, "round": a.round,
             "algorithm": a.algorithm, "command": a.cmd, "passes": a.csvs}
-    if a.mode == "bytes":
+    if a.mode == "trace":
+        # rocprofv3 --kernel-trace: the average duration of the kernel's whole
+        # launches (the stats CSV averages every launch of the command,
+        # chunk launches of a synchronous large-shard step included)
+        rows = [r for r in csv.DictReader(open(a.csvs[0])) if a.kernel in r["Kernel_Name"]]
+        if not rows:
+            raise SystemExit("no dispatch of the kernel in the trace")
+        gx = lambda r: int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) * int(r.get("Grid_Size_Z", 1) or 1)
+        g = max(gx(r) for r in rows)
+        kept = [r for r in rows if gx(r) == g]
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in kept]
+        d = dict(base, kernel=kept[0]["Kernel_Name"], grid_size=g,
+                 workgroup_size=int(kept[0]["Workgroup_Size_X"]),
+                 workgroups=g // max(int(kept[0]["Workgroup_Size_X"]), 1), whole_launch=True,
+                 dispatches_kept=len(kept), dispatches_total=len(rows),
+                 avg_ms_whole_launch=statistics.mean(durs), min_ms=min(durs), max_ms=max(durs),
+                 avg_ms_all_launches=statistics.mean((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                                                     for r in rows))
+    elif a.mode == "bytes":
         if len(a.csvs) != 2:
             raise SystemExit("bytes: FETCH_CSV WRITE_CSV")
         f, sf = whole(dispatches([a.csvs[0]], a.kernel))
@@ -119,6 +137,7 @@ def main():
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     json.dump(d, open(a.out, "w"), indent=1)
     print(json.dumps({k: d[k] for k in ("kernel", "grid_size", "dispatches_kept", "dispatches_total")}))
+    return 0
 
 
 if __name__ == "__main__":
