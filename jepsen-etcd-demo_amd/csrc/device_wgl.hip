@@ -52,6 +52,7 @@ namespace {
 constexpr uint32_t WGL_END = 0xFFFFFFFFu;  // R past the last return: every :ok passed
 constexpr uint32_t WGL_NONE = 0xFFFFFFFFu; // no :invoke (prev of a slot's first op)
 constexpr uint32_t WGL_RING = 32;          // frames of the walk's top levels kept in LDS
+constexpr uint32_t WGL_PEND_LANES = 8;     // HBM tier: entries read for the pending pair's slot with the probes
 
 extern "C" __device__ int lc_wgl_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ uint32_t wsetl(uint32_t v, uint32_t l, uint32_t x) {
@@ -519,9 +520,13 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             } else {
                 p0 = h0 & mask;
                 p1 = h1 & mask;
-                if (pend && !pend_known) {
-                    const uint4 pe = tab[2 * (size_t)((ph + lane) & mask) + 1];
-                    pfree = ((uint64_t)pe.z | (uint64_t)pe.w << 32) != gen;
+                if (pend && !pend_known && lane < WGL_PEND_LANES) {
+                    // (the stamp words of the first WGL_PEND_LANES entries
+                    // from its home: all 64 read 2 KB of lines per probe
+                    // round, 5x the walk's algorithmic bytes, for a slot that
+                    // is nearly always among the first few)
+                    const uint2 ps = *((const uint2 *)(tab + 2 * (size_t)((ph + lane) & mask) + 1) + 1);
+                    pfree = ((uint64_t)ps.x | (uint64_t)ps.y << 32) != gen;
                 }
                 // (one entry per round trip: reading two, p and p + 1, was
                 // measured in round 5 -- C2 8.21 -> 8.54 ms, C4 at 2^16 204 ->
@@ -563,9 +568,9 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
                     const uint64_t fm = ballot(pfree);
                     if (fm) {
                         pend_pos = (ph + (uint32_t)__builtin_ctzll(fm)) & tm;
-                    } else {  // 64 taken in a row (a table at most half full: rare)
+                    } else {  // the first ones all taken (a table at most half full: rare)
                         pend_pos = ph & tm;
-                        for (uint32_t probe = 64; probe <= tm; probe += 64) {
+                        for (uint32_t probe = in_lds ? 64u : WGL_PEND_LANES; probe <= tm; probe += 64) {
                             const uint32_t q = (ph + probe + lane) & tm;
                             bool fr;
                             if (in_lds) fr = ltab[q] == ~0ull;
