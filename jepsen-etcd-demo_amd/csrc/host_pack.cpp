@@ -840,6 +840,15 @@ bool km_ranges(const lc_history *h, int model, const Par &par, std::vector<KmRan
         if (t > 0)
             while (r < R1 && h->key[r] == h->key[R0 - 1]) ++r;  // the run of the range before
         uint64_t nw = 0, nb = 0;
+        {
+            // the staging sized once for the range's rows (its last run may
+            // pass R1: the resizes below still grow it), not grown by
+            // doubling -- each doubling copied the words written so far
+            const uint64_t guess = (uint64_t)(R1 - r) + 8192;
+            if (W16) { if (R.w16.size() < guess) R.w16.resize(guess); }
+            else if (R.w32.size() < guess) R.w32.resize(guess);
+            if (R.bits.size() < guess / 64 + 256) R.bits.resize(guess / 64 + 256);
+        }
         while (r < R1) {
             if (stop.load(std::memory_order_relaxed)) return;
             // (0) the run: its end, counts, process span

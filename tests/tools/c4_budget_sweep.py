@@ -6,9 +6,11 @@ and budget, one full-C4 lc_check_batch on the device: verdict counts, the
 event each :unknown key gave up at (:linear: the `:ok` whose set passed the
 budget -> "events reached"), time per launch, WGL steps and cache sizes; and
 the C restatements (oracle/linear_ref.c, oracle/wgl_ref.c) on the batch's
-first `--sample` keys at the same budget, records compared.
+first `--sample` keys at the same budget, records compared.  Test
+infrastructure (under tests/ because it runs the oracle as the checker); the
+product path it measures is liblincheck.so.
 
-    python tools/c4_budget_sweep.py --budgets 16,18,20,22 --algos linear,wgl \
+    python tests/tools/c4_budget_sweep.py --budgets 16,18,20,22 --algos linear,wgl \
         --sample 16 --out gpurun_out/c4sweep.json
 
 Writes the JSON after every point (a long sweep that is cut off keeps what it
@@ -21,7 +23,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for p in (os.path.join(ROOT, "jepsen-etcd-demo_amd"), os.path.join(ROOT, "oracle")):
     sys.path.insert(0, p)
 
