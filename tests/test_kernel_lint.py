@@ -31,7 +31,9 @@ def _code(text: str) -> str:
 
 def test_spec_queue_loops_keep_fixed_trip_counts():
     src = open(os.path.join(CSRC, "device_lattice.hip")).read()
-    body = _code(_body(src, "__global__ __launch_bounds__(64 * W) void k_spec("))
+    head = re.search(r"__global__ __launch_bounds__\(64 \* W[^)]*\)\) void k_spec\(", src)
+    assert head, "k_spec's definition not found"
+    body = _code(_body(src, head.group(0)))
     assert not re.search(r"for\s*\(\s*;\s*;\s*\)|while\s*\(\s*(true|1)\s*\)", body), "an open loop in k_spec"
     for start, queue in (("0", "s_next[0]"), ("1", "s_next[1]")):
         m = re.search(r"for \(uint32_t k = %s; k < \(uint32_t\)S; \+\+k\) \{(.{0,400})" % start, body, re.S)
