@@ -252,6 +252,7 @@ struct Dev {
     hipEvent_t e0 = nullptr, e1 = nullptr, et0 = nullptr, et3a = nullptr, et3b = nullptr;
     hipEvent_t ea0 = nullptr, ea1 = nullptr;  // span of the LC_DEV_ASYNC steps since lc_wait
     uint32_t n_async = 0;
+    bool ea1_pending = false;  // asynchronous steps enqueued since ea1 was last recorded
     hipEvent_t ring[4] = {};  // end of each of the last 4 LC_DEV_ASYNC steps (lc_wait_step)
     uint64_t async_seq = 0;
     // scratch, grown on demand
@@ -308,10 +309,13 @@ struct Dev {
     int64_t hnode_cap = 0;
     // lc_check_node_async: two staging batches used in turn, so a step's
     // upload (on cstream) runs while the step before it searches; pipe_ready
-    // = a slot's upload is done, pipe_free = the step that read it is done
+    // = a slot's upload is done; the step that read a slot is done when its
+    // ring event (async_seq pipe_seq[s]) is
     static constexpr int PIPE = 2;
     DevBatch *pipe[PIPE] = {};
-    hipEvent_t pipe_ready[PIPE] = {}, pipe_free[PIPE] = {};
+    hipEvent_t pipe_ready[PIPE] = {};
+    uint64_t pipe_seq[PIPE] = {};
+    bool pipe_busy[PIPE] = {};
     uint64_t pipe_next = 0;
     // T3 (HBM tier) workspaces: narrow / wide configs
     struct Ws {
@@ -355,7 +359,7 @@ struct Dev {
         delete staged;
         for (int i = 0; i < PIPE; ++i) {
             delete pipe[i];
-            for (hipEvent_t e : {pipe_ready[i], pipe_free[i]})
+            for (hipEvent_t e : {pipe_ready[i]})
                 if (e) (void)hipEventDestroy(e);
         }
         for (int i = 0; i < NODE_CHUNKS; ++i) {
@@ -1179,6 +1183,12 @@ enum ResMode { RES_HOST = 0, RES_DEV = 1, RES_CTX = 2 };
 // results; RES_DEV: r's arrays are device memory on c; RES_CTX: results stay
 // in c's own device arrays (r unused).  allow_async: a step that is T0 alone
 // is only enqueued (*enqueued = true; errors surface at the next wait).
+// k_spec_rerun's workgroups at most (0: one per CU; A/B: make variant
+// VFLAGS=-DLC_SPEC_RERUN_BLOCKS=n -- 16 and 64 measured the same as 256 on
+// C2 in round 5, 0.2552-0.2556 ms per step)
+#ifndef LC_SPEC_RERUN_BLOCKS
+#define LC_SPEC_RERUN_BLOCKS 0
+#endif
 static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mode, bool allow_async, int64_t key0,
                       lc_stats *st, bool *enqueued = nullptr, int64_t res_off = 0) {
     lc::Range range("lincheck: search");
@@ -1294,6 +1304,10 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // result download when the results go to host memory).
     const bool t0_step = K > 0 && d->t0_only && !(o.flags & LC_OPT_COUNT_PROBES);
     const bool async = t0_step && allow_async && mode != RES_HOST;
+    if (!async && c->ea1_pending) {  // the asynchronous steps' span ends before this one
+        HIPCHK(hipEventRecord(c->ea1, c->stream));
+        c->ea1_pending = false;
+    }
     // an enqueued step reports a malformed batch through its own error words
     if (async) a.err = c->counters + ERR_RING + 2 * (int)(c->async_seq % 4);
     // Key segments (device_lattice.hip): verdicts only, a batch of about one
@@ -1469,7 +1483,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
                                 // (rerun blocks: the launch usually finds no
                                 // key, so one block per CU keeps its dispatch
                                 // short; a longer rerun list walks the grid)
-                                c->cu_count, vblocks, ev16, (o.path_flags & LC_PATH_SPEC_COST) != 0,
+                                LC_SPEC_RERUN_BLOCKS > 0 ? LC_SPEC_RERUN_BLOCKS : c->cu_count, vblocks, ev16,
+                                (o.path_flags & LC_PATH_SPEC_COST) != 0,
                                 !(o.path_flags & LC_PATH_SPEC_NOPRIO),
                                 K * waves > (int64_t)c->cu_count * 16,  // more keys than one resident round
                                 exact_spec && !fast ? c->spec_fin : nullptr,
@@ -1484,8 +1499,11 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     }
     if (side_validate) HIPCHK(hipStreamWaitEvent(c->stream, c->vdone, 0));
     if (async) {
-        HIPCHK(hipEventRecord(c->ea1, c->stream));
+        // (the span's end, ea1, is recorded by dev_wait after the last
+        // enqueued step: one timing event per step cost the stream a few
+        // microseconds between searches)
         HIPCHK(hipEventRecord(c->ring[c->async_seq % 4], c->stream));
+        c->ea1_pending = true;
         ++c->async_seq;
         ++c->n_async;
         c->ticket_next = (split || spec) ? ticket_base : ticket_base + (uint32_t)K + (uint32_t)g0;
@@ -1660,6 +1678,8 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
 static int dev_wait(Dev *c, int *n_async, float *span_ms) {
     lc::Range range("lincheck: wait");
     HIPCHK(hipSetDevice(c->device));
+    if (c->ea1_pending) HIPCHK(hipEventRecord(c->ea1, c->stream));
+    c->ea1_pending = false;
     HIPCHK(hipMemcpyAsync(c->hctl + 6, c->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     *n_async = (int)c->n_async;
@@ -2118,14 +2138,22 @@ extern "C" int lc_check_node_async(lc_ctx *c, const lc_batch *b, int64_t block, 
                 if (!d->pipe[s]) {
                     d->pipe[s] = new (std::nothrow) DevBatch();
                     if (!d->pipe[s]) return lc::fail(LC_E_NOMEM, "lc_check_node_async: out of memory");
-                    HIPCHK(hipEventCreateWithFlags(&d->pipe_ready[s], hipEventDisableTiming));
-                    HIPCHK(hipEventCreateWithFlags(&d->pipe_free[s], hipEventDisableTiming));
-                    HIPCHK(hipEventRecord(d->pipe_free[s], d->stream));
+                    // (a device-scope release: the host only learns from it
+                    // that the upload's device writes are done)
+                    if (hipEventCreateWithFlags(&d->pipe_ready[s], hipEventDisableTiming | hipEventReleaseToDevice) !=
+                        hipSuccess) {
+                        (void)hipGetLastError();
+                        HIPCHK(hipEventCreateWithFlags(&d->pipe_ready[s], hipEventDisableTiming));
+                    }
                 }
                 // the step that last read this slot has finished (at most one
                 // other step stays in flight), so its buffers may be rewritten
-                // or regrown
-                HIPCHK(hipEventSynchronize(d->pipe_free[s]));
+                // or regrown.  Its end is the ring event its search recorded:
+                // a marker of its own after every step cost the stream ~5 us
+                // between consecutive searches (a system-scope fence each).
+                // (A ring slot re-recorded since by a later step only makes
+                // this wait for that later step.)
+                if (d->pipe_busy[s]) HIPCHK(hipEventSynchronize(d->ring[d->pipe_seq[s] % 4]));
                 // One rank: the search writes the records straight into the
                 // caller's page-locked buffer (device-mapped), so no download
                 // follows it; with a communicator they go through HBM for the
@@ -2171,7 +2199,8 @@ extern "C" int lc_check_node_async(lc_ctx *c, const lc_batch *b, int64_t block, 
                                                     d->stream) != hipSuccess)
                         return drained(lc::fail(LC_E_DEVICE, "lc_check_node_async: record download failed"));
                 }
-                HIPCHK(hipEventRecord(d->pipe_free[s], d->stream));
+                d->pipe_busy[s] = enq;
+                d->pipe_seq[s] = d->async_seq - 1;
                 ++d->pipe_next;
                 if (enq) return 1;
                 HIPCHK(hipStreamSynchronize(d->stream));  // not reached for a register-tier batch
