@@ -1339,6 +1339,9 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // 4.75 ms, 8 on 2 5.30, against 4.40 for 2 on 2.
     int segs = K > 0 ? (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1)) : 0;
     segs = segs >= 8 ? 8 : segs >= 4 ? 4 : K > 0 ? 2 : 0;
+    // (8 per key while 8 x keys waves are resident at the 8-wave build's 8
+    // per SIMD: device_search.hpp LC_SPEC8_WAVES)
+    if (LC_SPEC8_WAVES >= 8 && K > 0 && K * 8 <= (int64_t)c->cu_count * 4 * 8) segs = 8;
     if (o.spec_segs) segs = o.spec_segs;
     // Final configs wanted and no set sizes (the Jepsen-shaped checkers):
     // the segments with exact sets (Knossos's S, not its closure), each run

@@ -2018,10 +2018,21 @@ __device__ __forceinline__ void spec_setup(SpecState &st, uint32_t words, uint32
 // 4 (MODE 1) met the TOP run, 5 (MODE 1) passed both checkpoints unmet.
 // The 9-10-pending workspace: one of the workgroup's NWS LDS slots while one
 // is free (busy flags in LDS), else the wave's global slot (an :ok there costs
-// ~40k cycles against ~2k in LDS).  NWS = 1, 2, 4 slots for 2, 4, 8 waves
-// keep 4 waves per SIMD within the CU's LDS.
+// ~40k cycles against ~2k in LDS).  NWS = 1, 2, 3 slots for 2, 4, 8 waves
+// keep 4 waves per SIMD within the CU's LDS; the 8-wave build held to 8
+// waves per SIMD (LC_SPEC8_WAVES) has 2, so that 4 of its workgroups fit.
+#ifndef LC_SPEC8_NWS
+#define LC_SPEC8_NWS (LC_SPEC8_WAVES >= 8 ? 2 : 3)
+#endif
+// The 2-wave build keeps no LDS workspace (its 9-10-pending :oks use the
+// waves' global ones): 12 KB of LDS per workgroup held it to 5.5 waves per
+// SIMD, and the occupancy is worth more to the many-key batches it runs
+// than the rare 9-10-pending :ok (LC_SPEC2_WAVES below).
+#ifndef LC_SPEC2_NWS
+#define LC_SPEC2_NWS 0
+#endif
 template <int S>
-constexpr int spec_lds_ws() { return S <= 3 ? 1 : S <= 6 ? 2 : 3; }
+constexpr int spec_lds_ws() { return S <= 2 ? LC_SPEC2_NWS : S <= 3 ? 1 : S <= 6 ? 2 : LC_SPEC8_NWS; }
 // Issue priority of a TOP walk by progress (MODE 0, prio): the SIMD's
 // arbiter favours the higher s_setprio, then the older wave, so with age
 // alone the last-dispatched blocks' walks trail by up to a quarter of a walk
@@ -2046,6 +2057,18 @@ constexpr uint32_t SPEC_SAVE_WORDS = (T0_RMEM + 2) * 64;
 #ifndef LC_SPEC_CK_SPLIT
 #define LC_SPEC_CK_SPLIT 1
 #endif
+// Checkpoints of a TOP run: at ck1, ck2 and evenly between (a verifying run
+// compares its set at each and stops at the first match; one that passes
+// them all unmet sends the key to the unsegmented search).  A run that
+// misses the first one no longer walks on to ck2 at the 8-wave build's
+// per-event cost (A/B: make variant VFLAGS=-DLC_SPEC_NCK=n).
+#ifndef LC_SPEC_NCK
+#define LC_SPEC_NCK 3
+#endif
+constexpr uint32_t SPEC_NCK = LC_SPEC_NCK;
+__device__ __forceinline__ uint32_t spec_ck_target(uint32_t i, uint32_t ck1, uint32_t ck2) {
+    return i == 0 ? ck1 : i + 1 >= SPEC_NCK ? ck2 : ck1 + (ck2 - ck1) * i / (SPEC_NCK - 1);
+}
 template <int MODE, int NWS, class EvT, bool EX = false>
 __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
                                          uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
@@ -2174,15 +2197,15 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                     ck_w[ck_i][lane] = W0;
                     if (lane == 0) ck_e[ck_i] = (int32_t)(b + e);
                     ++ck_i;
-                    ck_at = ck_i < 2 ? max(ck2, e + 1u) : ~0u;
+                    ck_at = ck_i < SPEC_NCK ? max(spec_ck_target(ck_i, ck1, ck2), e + 1u) : ~0u;
                 } else {
                     if (!__any(W0 != ck_w[ck_i][lane])) {
                         status = 4;
                     } else {
                         ++ck_i;
-                        const int32_t nx = ck_i < 2 ? uni(ck_e[ck_i & 1]) : -1;
+                        const int32_t nx = ck_i < SPEC_NCK ? uni(ck_e[ck_i]) : -1;
                         ck_at = nx >= 0 ? (uint32_t)nx - b : ~0u;
-                        if (ck_i == 2) status = 5;
+                        if (ck_i == SPEC_NCK) status = 5;
                     }
                 }
             }
@@ -2343,24 +2366,27 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 // memory: the workgroup's LDS workspaces are shared, NWS of them).
 // 16-bit event words of a key k_spec stages in LDS: none for 2-segment
 // workgroups (the many-key batches, where 6 KB more per block would cost
-// occupancy), 4,096 (8 KB) otherwise -- C2's keys have ~1,470.
+// occupancy), 4,096 (8 KB) otherwise -- C2's keys have ~1,470 -- and 3,072
+// for the 8-wave build, whose 4 workgroups per CU (8 waves per SIMD) must
+// fit the CU's 160 KB with their 3 checkpoint sets per segment.
 template <int S, bool E16>
-constexpr uint32_t spec_ev_lds() { return (E16 && S > 2) ? 4096u : 0u; }
+constexpr uint32_t spec_ev_lds() { return (E16 && S > 2) ? (S >= 8 ? 3072u : 4096u) : 0u; }
 
 #ifndef LC_SPEC_KARG
 #define LC_SPEC_KARG 1
 #endif
 // The 2-wave build (the many-key batches: C3's shards, throughput-bound) is
-// held to 6 waves per SIMD: 79 VGPRs instead of 84, no spill, 5.5 waves per
-// SIMD where its 14 KB of LDS per block allows (11 blocks per CU).  A/B on
-// one box, the C3 shard (12,500 x 2,000): 4.04 -> 3.89 ms per step, kernel
-// 3.85 -> 3.72 ms, records identical (round 5).  7 is beyond the walk's
-// registers (the attribute is not met).
+// held to 8 waves per SIMD: 64 VGPRs, 140 B per lane spilled to scratch, and
+// no LDS workspace (LC_SPEC2_NWS) so that 8 fit.  A/B on one box, the C3
+// shard (12,500 x 2,000), two rounds each (round 5): 6 waves per SIMD with
+// the LDS workspace (5.5 resident) 3.881 ms per step, kernel 3.694; 6
+// without it 3.814 / 3.650; 7 3.607 / 3.421; 8 3.601 / 3.427.  Records
+// identical.  (Before: 84 VGPRs, 4 waves, 4.04 ms per step.)
 #ifndef LC_SPEC2_WAVES
-#define LC_SPEC2_WAVES 6
+#define LC_SPEC2_WAVES 8
 #endif
 template <int S, int W, bool E16, bool EX = false>
-__global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : 1)) void k_spec(T0Args a) {
+__global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC8_WAVES : 1)) void k_spec(T0Args a) {
 #if LC_SPEC_KARG
 #define KA t0k()
 #else
@@ -2369,10 +2395,10 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : 1)) void k_spec(
     constexpr uint32_t EVC = spec_ev_lds<S, E16>();
     __shared__ uint16_t s_ev[EVC ? EVC : 1];  // the key's event words (EvStaged)
     __shared__ uint32_t s_end[S][64];     // TOP run's set at the segment's end
-    __shared__ uint32_t s_ck[S][2][64];   // TOP run's checkpoint sets
+    __shared__ uint32_t s_ck[S][SPEC_NCK][64];  // TOP run's checkpoint sets
     __shared__ uint32_t s_pend[S][8];     // ops pending at the cut ([0..5] words, [6] count)
     __shared__ uint64_t s_map[S];         // end: byte i = 0x80 | slot of live op index i
-    __shared__ int32_t s_ck_e[S][2];      // checkpoint events (-1: none)
+    __shared__ int32_t s_ck_e[S][SPEC_NCK];  // checkpoint events (-1: none)
     __shared__ int32_t s_cut[S], s_segend[S];  // segment [cut, end); cut -1: no segment
     __shared__ int32_t s_top[S];          // TOP run: -1 alive, -2 does not fit, -3 lost, else its failing event
     __shared__ int32_t s_ver[S], s_vfev[S];
@@ -2381,8 +2407,8 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : 1)) void k_spec(
     __shared__ int32_t s_next[2];         // the block's queues: TOP walks, verifying runs
     __shared__ uint32_t s_vx[W][2];       // self-validation: each wave's part, XOR of its slots' one-hots
     constexpr int NWS = spec_lds_ws<W>();
-    __shared__ uint32_t s_ws[NWS * 3 * T0_RMEM * 64];  // 9-10-pending workspaces (12 KB each)
-    __shared__ int32_t s_ws_busy[NWS];
+    __shared__ uint32_t s_ws[NWS ? NWS * 3 * T0_RMEM * 64 : 1];  // 9-10-pending workspaces (12 KB each)
+    __shared__ int32_t s_ws_busy[NWS ? NWS : 1];
     const uint32_t lane = lane_id(), wv = uni((uint32_t)threadIdx.x >> 6);  // uniform per wave
     // T0_STRICT steps: the event-by-event validation, in nb blocks after the
     // keys' (no second stream, no cross-stream waits around the step), or
@@ -2557,7 +2583,7 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : 1)) void k_spec(
         for (uint32_t s = eff; s-- > 0;) {
             s_segend[s] = end;
             if (s_cut[s] >= 0) end = s_cut[s];
-            s_ck_e[s][0] = s_ck_e[s][1] = -1;
+            for (uint32_t q = 0; q < SPEC_NCK; ++q) s_ck_e[s][q] = -1;
             s_top[s] = -1;
         }
     }

@@ -70,6 +70,16 @@ constexpr int32_t LC_BATCH_E_FIT = 4;    // a key declared to fit T0 (width, sta
 // Ops pending at once above which a key leaving T0 goes straight to T3.
 constexpr uint32_t LC_DIRECT_T3_WIDTH = 28;
 
+// The speculative segments' 8-wave build (k_spec<8, 8>, device_lattice.hip)
+// held to 8 waves per SIMD -- 64 VGPRs, the rest spilled -- so a batch of up
+// to 1,024 keys (C2, C5) has all 8 walks of every key resident at once: the
+// launch chooses 8 segments per key there instead of 4 (round 5, C2
+// 0.2488 -> 0.2415 ms per resident step).  1 = no bound (then 8 segments
+// only for batches of <= 512 keys, where 8 x keys waves fit at 4 per SIMD).
+#ifndef LC_SPEC8_WAVES
+#define LC_SPEC8_WAVES 8
+#endif
+
 // Per-block HBM workspace of the T3 tier (one slot per resident block).
 struct HbmWs {
     char *base;
