@@ -2681,6 +2681,9 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
                 uint32_t fev = 0;
                 uint32_t *const sv =
                     EX ? KA.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS + SPEC_SAVE_WORDS : nullptr;
+                // (the verifying runs at a TOP walk's highest issue priority,
+                // against the other blocks' TOP walks on the SIMD, measured
+                // slower in round 5: C2 0.2484 -> 0.2501, C5 0.2997 -> 0.3068)
                 const int r = spec_walk<1, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
                                                                 s_ck[s], s_ck_e[s], 0, 0, fev, false, sv);
                 bool last = true;
