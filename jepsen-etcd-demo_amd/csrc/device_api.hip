@@ -1339,15 +1339,16 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // 4.75 ms, 8 on 2 5.30, against 4.40 for 2 on 2.
     int segs = K > 0 ? (int)std::min<int64_t>(8, (int64_t)c->cu_count * 4 * 4 / std::max<int64_t>(K, 1)) : 0;
     segs = segs >= 8 ? 8 : segs >= 4 ? 4 : K > 0 ? 2 : 0;
-    // (8 per key while 8 x keys waves are resident at the 8-wave build's 8
-    // per SIMD: device_search.hpp LC_SPEC8_WAVES)
-    if (LC_SPEC8_WAVES >= 8 && K > 0 && K * 8 <= (int64_t)c->cu_count * 4 * 8) segs = 8;
-    if (o.spec_segs) segs = o.spec_segs;
     // Final configs wanted and no set sizes (the Jepsen-shaped checkers):
     // the segments with exact sets (Knossos's S, not its closure), each run
     // saving its set at its end or death, the true run's written as the
     // key's final configs (k_spec<.., EX>).
     const bool exact_spec = !a.peak && a.final_cfg && a.n_final && o.max_configs >= 16ull * 64 * 32;
+    // Verdicts only: 8 per key while 8 x keys waves are resident at the
+    // 8-wave build's 8 per SIMD (device_search.hpp LC_SPEC8_WAVES).  Not for
+    // the exact segments: on C5 their launch went 0.289 -> 0.352 ms with it.
+    if (LC_SPEC8_WAVES >= 8 && fast && K > 0 && K * 8 <= (int64_t)c->cu_count * 4 * 8) segs = 8;
+    if (o.spec_segs) segs = o.spec_segs;
     if (exact_spec && !fast) segs = segs >= 8 ? 8 : segs >= 4 ? 4 : 2;  // the exact builds
     const int waves = segs;
     bool spec = !split && t0_step && (fast || exact_spec) && segs >= 2 && !(o.path_flags & LC_PATH_SPEC_OFF);

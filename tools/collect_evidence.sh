@@ -31,11 +31,11 @@ tr() {  # name kernel workload keys budget algorithm
       --out $P/${T}_$1_trace.json "$t"
   return 0
 }
-tr c3s "k_spec<2, 2, true, false>" C3 12500 1048576 linear
+tr c3s "k_spec<" C3 12500 1048576 linear
 tr c4wgl "k_wgl" C4 256 65536 wgl
 tr c2wgl "k_wgl" C2 1000 1048576 wgl
-pmc c2 "k_spec<4, 4, true, false>" C2 1000 1048576 linear
-pmc c3s "k_spec<2, 2, true, false>" C3 12500 1048576 linear
+pmc c2 "k_spec<" C2 1000 1048576 linear
+pmc c3s "k_spec<" C3 12500 1048576 linear
 pmc c4 "k_search_layers" C4 256 65536 linear
 pmc c4wgl "k_wgl" C4 256 65536 wgl
 pmc c2wgl "k_wgl" C2 1000 1048576 wgl
