@@ -1004,17 +1004,28 @@ static int take_error(Dev *c) {
 
 // The error words of the LC_DEV_ASYNC steps in ring slots `mask` (first
 // `first`, when it is one of them), read and cleared on stream s.
-static int take_ring(Dev *c, uint32_t mask, int first, hipStream_t s) {
+// (enqueue, then ring_taken after the stream has passed it: dev_wait does
+// both around its one synchronisation)
+static int take_ring_enqueue(Dev *c, uint32_t mask, hipStream_t s) {
     hipLaunchKernelGGL(k_take_err, dim3(1), dim3(64), 0, s, c->counters + ERR_RING, mask, c->counters + ERR_TAKEN);
     HIPCHK(hipGetLastError());
-    int32_t *h = (int32_t *)(c->hctl + 16);
-    HIPCHK(hipMemcpyAsync(h, c->counters + ERR_TAKEN, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpyAsync((int32_t *)(c->hctl + 16), c->counters + ERR_TAKEN, 8 * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, s));
+    return LC_OK;
+}
+static int ring_taken(Dev *c, int first) {
+    const int32_t *h = (const int32_t *)(c->hctl + 16);
     int q = first >= 0 && h[2 * first] ? first : -1;
     for (int i = 0; i < 4 && q < 0; ++i)
         if (h[2 * i]) q = i;
     if (q < 0) return LC_OK;
     return batch_error(h[2 * q], (int64_t)h[2 * q + 1] - 1);
+}
+static int take_ring(Dev *c, uint32_t mask, int first, hipStream_t s) {
+    const int rc = take_ring_enqueue(c, mask, s);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return ring_taken(c, first);
 }
 
 // Segment arrays for n_keys keys (grown on demand).
@@ -1685,13 +1696,17 @@ static int dev_wait(Dev *c, int *n_async, float *span_ms) {
     if (c->ea1_pending) HIPCHK(hipEventRecord(c->ea1, c->stream));
     c->ea1_pending = false;
     HIPCHK(hipMemcpyAsync(c->hctl + 6, c->counters + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    // every step's ring slot read and cleared behind them: one
+    // synchronisation for the wait and both error reads
+    const int re = take_ring_enqueue(c, 0xFu, c->stream);
+    if (re) return re;
     HIPCHK(hipStreamSynchronize(c->stream));
     *n_async = (int)c->n_async;
     *span_ms = 0;
     if (c->n_async) HIPCHK(hipEventElapsedTime(span_ms, c->ea0, c->ea1));
     c->n_async = 0;
+    const int rr = ring_taken(c, -1);
     const int rs = take_error(c);
-    const int rr = take_ring(c, 0xFu, -1, c->stream);  // every step has finished: all slots
     return rs ? rs : rr;
 }
 
