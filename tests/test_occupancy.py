@@ -1,0 +1,70 @@
+"""The register tier's occupancy, read from the built library's gfx950 code
+object (no GPU needed).
+
+Round 4 asked the compiler for 8 waves per SIMD on the 8-wave k_spec build
+and silently did not get it: a waves-per-SIMD bound that the workgroup's LDS
+makes unreachable is dropped, and the build kept 85 VGPRs.  Round 5's 8-wave
+and 2-wave builds reach 8 waves per SIMD only while their VGPRs stay at 64
+and their LDS lets 4 (8-wave) or 16 (2-wave) workgroups share a CU's 160 KB;
+an edit that grows either would lose the occupancy without any test on the
+GPU failing (only the time).  So the limits are checked here, in the kernel
+descriptors' metadata (llvm-readelf --notes of the offload bundle)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "jepsen-etcd-demo_amd", "lincheck", "liblincheck.so")
+LLVM = "/opt/rocm/llvm/bin"
+LDS_PER_CU = 160 * 1024
+
+
+def _kernels(tmp_path):
+    for tool in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf"):
+        if not os.path.exists(os.path.join(LLVM, tool)):
+            pytest.skip(f"{tool} not in {LLVM}")
+    if not os.path.exists(SO):
+        pytest.skip("liblincheck.so not built")
+    fat, co = str(tmp_path / "fat.bin"), str(tmp_path / "k.co")
+    subprocess.run([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", SO, str(tmp_path / "x")],
+                   check=True, capture_output=True)
+    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+    notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True, capture_output=True,
+                           text=True).stdout
+    out = {}
+    for block in re.split(r"\n  - \.agpr_count:", notes):
+        m = re.search(r"\.name:\s+(\S+)", block)
+        if not m:
+            continue
+        f = {k: int(v) for k, v in re.findall(r"\.(vgpr_count|group_segment_fixed_size|private_segment_fixed_size"
+                                               r"|max_flat_workgroup_size):\s+(\d+)", block)}
+        out[m.group(1)] = f
+    return out
+
+
+def _waves_per_simd(k):
+    """Resident waves per SIMD: registers (512 per lane, granule 8) and LDS."""
+    vg = max(8, -(-k["vgpr_count"] // 8) * 8)
+    by_regs = min(8, 512 // vg)
+    waves_per_wg = k["max_flat_workgroup_size"] // 64
+    lds = k["group_segment_fixed_size"]
+    wg_per_cu = LDS_PER_CU // lds if lds else 32
+    by_lds = wg_per_cu * waves_per_wg / 4.0
+    return min(by_regs, by_lds)
+
+
+@pytest.mark.parametrize("name,want", [
+    ("_ZN3lcd6k_specILi8ELi8ELb1ELb0EEEvNS_6T0ArgsE", 8),  # C2/C5-sized batches: 8 segments, all resident
+    ("_ZN3lcd6k_specILi2ELi2ELb1ELb0EEEvNS_6T0ArgsE", 8),  # the many-key batches (C3 shards)
+    ("_ZN3lcd6k_specILi4ELi4ELb1ELb0EEEvNS_6T0ArgsE", 4),
+])
+def test_spec_builds_keep_their_occupancy(tmp_path, name, want):
+    ks = _kernels(tmp_path)
+    assert name in ks, f"{name} not in the code object"
+    k = ks[name]
+    got = _waves_per_simd(k)
+    assert got >= want, f"{name}: {got} waves per SIMD ({k}), want {want}"
