@@ -2059,11 +2059,11 @@ constexpr uint32_t SPEC_SAVE_WORDS = (T0_RMEM + 2) * 64;
 #endif
 // Checkpoints of a TOP run: at ck1, ck2 and evenly between (a verifying run
 // compares its set at each and stops at the first match; one that passes
-// them all unmet sends the key to the unsegmented search).  A run that
-// misses the first one no longer walks on to ck2 at the 8-wave build's
-// per-event cost (A/B: make variant VFLAGS=-DLC_SPEC_NCK=n).
+// them all unmet sends the key to the unsegmented search).  A third one
+// between measured no faster in round 5 (C2 0.2472 ms with two, 0.2492
+// with three; A/B: make variant VFLAGS=-DLC_SPEC_NCK=n).
 #ifndef LC_SPEC_NCK
-#define LC_SPEC_NCK 3
+#define LC_SPEC_NCK 2
 #endif
 constexpr uint32_t SPEC_NCK = LC_SPEC_NCK;
 __device__ __forceinline__ uint32_t spec_ck_target(uint32_t i, uint32_t ck1, uint32_t ck2) {
@@ -2366,11 +2366,11 @@ extern "C" int lc_debug_spec_stamps(unsigned long long *host, int n) {
 // memory: the workgroup's LDS workspaces are shared, NWS of them).
 // 16-bit event words of a key k_spec stages in LDS: none for 2-segment
 // workgroups (the many-key batches, where 6 KB more per block would cost
-// occupancy), 4,096 (8 KB) otherwise -- C2's keys have ~1,470 -- and 3,072
-// for the 8-wave build, whose 4 workgroups per CU (8 waves per SIMD) must
-// fit the CU's 160 KB with their 3 checkpoint sets per segment.
+// occupancy), 4,096 (8 KB) otherwise -- C2's keys have ~1,470.  (The 8-wave
+// build's 4 workgroups per CU, 8 waves per SIMD, fit the CU's 160 KB with
+// these and 2 checkpoint sets per segment; a third set needs 3,072 here.)
 template <int S, bool E16>
-constexpr uint32_t spec_ev_lds() { return (E16 && S > 2) ? (S >= 8 ? 3072u : 4096u) : 0u; }
+constexpr uint32_t spec_ev_lds() { return (E16 && S > 2) ? (S >= 8 && SPEC_NCK > 2 ? 3072u : 4096u) : 0u; }
 
 #ifndef LC_SPEC_KARG
 #define LC_SPEC_KARG 1
