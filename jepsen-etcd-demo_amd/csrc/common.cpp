@@ -200,10 +200,13 @@ void *big_alloc(size_t bytes) {
         // 2 MB-aligned and marked for transparent huge pages: first touch
         // then faults a 2 MB page at a time (a C3-sized pack writes GBs of
         // fresh arrays; 4 KB faults cost more than the writes)
+        // (the whole rounded length is allocated, so the advice covers only
+        // this block's own pages)
         void *q = nullptr;
-        if (posix_memalign(&q, 2u << 20, bytes + 64) == 0) {
+        const size_t len = (bytes + 64 + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+        if (posix_memalign(&q, 2u << 20, len) == 0) {
             raw = (char *)q;
-            (void)madvise(raw, (bytes + 64 + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1), MADV_HUGEPAGE);
+            (void)madvise(raw, len, MADV_HUGEPAGE);
         }
     } else {
         raw = (char *)std::malloc(bytes + 64);

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <functional>
 #include <memory>
+#include <exception>
 #include <mutex>
 #include <new>
 #include <string>
@@ -188,10 +189,21 @@ class HostPool {
             ++gen_;
         }
         cv_.notify_all();
-        fn(0);
+        // The workers hold references to fn: wait for them whatever fn(0)
+        // does, then hand the first exception (caller's or a worker's) on.
+        std::exception_ptr ex;
+        try {
+            fn(0);
+        } catch (...) {
+            ex = std::current_exception();
+        }
         std::unique_lock<std::mutex> g(m_);
         done_.wait(g, [this] { return pending_ == 0; });
         fn_ = nullptr;
+        if (!ex) ex = ex_;
+        ex_ = nullptr;
+        g.unlock();
+        if (ex) std::rethrow_exception(ex);
     }
 
   private:
@@ -207,8 +219,14 @@ class HostPool {
                 if (id >= n_) continue;
                 fn = fn_;
             }
-            (*fn)(id);
+            std::exception_ptr ex;
+            try {
+                (*fn)(id);
+            } catch (...) {  // never out of a worker thread (std::terminate)
+                ex = std::current_exception();
+            }
             std::lock_guard<std::mutex> g(m_);
+            if (ex && !ex_) ex_ = ex;
             if (--pending_ == 0) done_.notify_one();
         }
     }
@@ -216,6 +234,7 @@ class HostPool {
     std::mutex m_;
     std::condition_variable cv_, done_;
     const std::function<void(unsigned)> *fn_ = nullptr;
+    std::exception_ptr ex_;  // a worker's first exception in this run
     unsigned n_ = 0, pending_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
@@ -226,6 +245,38 @@ class HostPool {
 // busy (another thread packing) gets nullptr and works without it.
 HostPool *pack_pool_acquire();
 void pack_pool_release();
+
+// work(0..n-1) on n-1 fresh threads and the caller; joins them all, then
+// rethrows the first exception any of them raised (none escapes a thread).
+template <class F>
+void run_threads(unsigned n, const F &work) {
+    std::mutex em;
+    std::exception_ptr ex;
+    auto guarded = [&](unsigned t) {
+        try {
+            work(t);
+        } catch (...) {
+            std::lock_guard<std::mutex> g(em);
+            if (!ex) ex = std::current_exception();
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < n; ++t) th.emplace_back(guarded, t);
+    guarded(0);
+    for (auto &x : th) x.join();
+    if (ex) std::rethrow_exception(ex);
+}
+
+// Holds the pack pool for a scope (released on every exit, exceptions too).
+struct PackPoolGuard {
+    HostPool *pool = pack_pool_acquire();
+    PackPoolGuard() = default;
+    PackPoolGuard(const PackPoolGuard &) = delete;
+    PackPoolGuard &operator=(const PackPoolGuard &) = delete;
+    ~PackPoolGuard() {
+        if (pool) pack_pool_release();
+    }
+};
 
 }  // namespace lc
 

@@ -371,10 +371,7 @@ void pack_multi_register(const lc_history &h, const int64_t *init, int32_t n_ini
             for (int64_t k = t; k < K; k += nt)
                 if (!ko[(size_t)k].err) memo_multi_register(h, ko[(size_t)k], init, n_init, mr[(size_t)k]);
         };
-        std::vector<std::thread> pool;
-        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
-        work(0);
-        for (auto &th : pool) th.join();
+        lc::run_threads(nt, work);
     }
     for (int64_t k = 0; k < K; ++k) {
         MrKey &m = mr[(size_t)k];
@@ -577,50 +574,67 @@ struct Par {
     void run(uint64_t n_tasks, const F &fn) const {
         if (n_tasks == 0) return;
         std::atomic<uint64_t> next{0};
+        // A task that throws (std::bad_alloc in a task's allocations) stops
+        // the claiming of tasks; every thread is joined and the first
+        // exception is rethrown here, on the caller.
+        std::mutex em;
+        std::exception_ptr ex;
         auto body = [&](unsigned) {
-            for (uint64_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n_tasks;) fn(i);
+            try {
+                for (uint64_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n_tasks;) fn(i);
+            } catch (...) {
+                next.store(n_tasks, std::memory_order_relaxed);
+                std::lock_guard<std::mutex> g(em);
+                if (!ex) ex = std::current_exception();
+            }
         };
         const unsigned w = (unsigned)std::min<uint64_t>(nt, n_tasks);
-        if (w <= 1) { body(0); return; }
-        if (pool) {
+        if (w <= 1) {
+            body(0);
+        } else if (pool) {
             const std::function<void(unsigned)> f = body;
             pool->run(w, f);
-            return;
+        } else {
+            std::vector<std::thread> th;
+            for (unsigned t = 1; t < w; ++t) th.emplace_back(body, t);
+            body(0);
+            for (auto &x : th) x.join();
         }
-        std::vector<std::thread> th;
-        for (unsigned t = 1; t < w; ++t) th.emplace_back(body, t);
-        body(0);
-        for (auto &x : th) x.join();
+        if (ex) std::rethrow_exception(ex);
     }
 };
 
-// Open-addressing map of 64-bit keys (stored + 1: 0 = empty) to u32, kept
-// under half full.  For the interning tables lc_pack builds per batch.
+// Open-addressing map of 64-bit keys to u32, kept under half full.  Slot
+// occupancy is its own byte array, so every 64-bit key -- -1 and INT64_MAX
+// included -- is a key like any other (no key value doubles as "empty").
+// For the interning tables lc_pack builds per batch.
 class FlatMap {
   public:
     explicit FlatMap(size_t expect = 16) {
         size_t c = 32;
         while (c < 2 * expect) c <<= 1;
-        k_.assign(c, 0);
+        k_.resize(c);
         v_.resize(c);
+        used_.assign(c, 0);
     }
     // the value of key, or `none`
     uint32_t get(uint64_t key, uint32_t none) const {
         for (size_t x = hash(key) & (k_.size() - 1);; x = (x + 1) & (k_.size() - 1)) {
-            if (k_[x] == key + 1) return v_[x];
-            if (!k_[x]) return none;
+            if (!used_[x]) return none;
+            if (k_[x] == key) return v_[x];
         }
     }
     // insert key -> val unless present; returns the value it maps to
     uint32_t put(uint64_t key, uint32_t val) {
         for (size_t x = hash(key) & (k_.size() - 1);; x = (x + 1) & (k_.size() - 1)) {
-            if (k_[x] == key + 1) return v_[x];
-            if (!k_[x]) {
-                k_[x] = key + 1;
+            if (!used_[x]) {
+                used_[x] = 1;
+                k_[x] = key;
                 v_[x] = val;
                 if (++n_ * 2 > k_.size()) grow();
                 return val;
             }
+            if (k_[x] == key) return v_[x];
         }
     }
     size_t size() const { return n_; }
@@ -633,17 +647,21 @@ class FlatMap {
     void grow() {
         std::vector<uint64_t> ok;
         std::vector<uint32_t> ov;
+        std::vector<uint8_t> ou;
         ok.swap(k_);
         ov.swap(v_);
-        k_.assign(ok.size() * 2, 0);
+        ou.swap(used_);
+        k_.resize(ok.size() * 2);
         v_.resize(ok.size() * 2);
+        used_.assign(ok.size() * 2, 0);
         for (size_t i = 0; i < ok.size(); ++i)
-            if (ok[i])
-                for (size_t x = hash(ok[i] - 1) & (k_.size() - 1);; x = (x + 1) & (k_.size() - 1))
-                    if (!k_[x]) { k_[x] = ok[i]; v_[x] = ov[i]; break; }
+            if (ou[i])
+                for (size_t x = hash(ok[i]) & (k_.size() - 1);; x = (x + 1) & (k_.size() - 1))
+                    if (!used_[x]) { used_[x] = 1; k_[x] = ok[i]; v_[x] = ov[i]; break; }
     }
     std::vector<uint64_t> k_;
     std::vector<uint32_t> v_;
+    std::vector<uint8_t> used_;
     size_t n_ = 0;
 };
 
@@ -1099,6 +1117,7 @@ int pack_key_major(const lc_history *h, int model, lc_packed *P, const Par &par,
     if (fit16) P->events16.alloc(n_ev, true);
     else P->events.alloc(n_ev, true);
     P->skip.alloc(std::max<uint64_t>(P->skip_off[(size_t)K], 1), false);
+    P->skip_pre.resize(std::max<uint64_t>(P->skip_off[(size_t)K], 1));
     uint16_t *const E16 = P->events16.data();
     uint32_t *const E32 = P->events.data();
     par.run(nr, [&](uint64_t t) {
@@ -1146,8 +1165,13 @@ int pack_key_major(const lc_history *h, int model, lc_packed *P, const Par &par,
                     else E32[e0 + j] = v;
                 }
             }
-            std::memcpy(P->skip.data() + P->skip_off[(size_t)k], R.bits.data() + x.b0,
-                        (P->skip_off[(size_t)k + 1] - P->skip_off[(size_t)k]) * 8);
+            const uint64_t s0 = P->skip_off[(size_t)k], s1 = P->skip_off[(size_t)k + 1];
+            std::memcpy(P->skip.data() + s0, R.bits.data() + x.b0, (s1 - s0) * 8);
+            uint32_t kept = 0;
+            for (uint64_t w = s0; w < s1; ++w) {
+                P->skip_pre[w] = kept;
+                kept += (uint32_t)__builtin_popcountll(~P->skip[w]);
+            }
         }
     });
     if (P->trans.empty()) P->trans.push_back(LC_DESC(LC_T_READ_ANY, 0, 0));
@@ -1184,12 +1208,15 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
     };
     try {
         if (model != LC_MODEL_MULTI_REGISTER && !(opts && (opts->flags & LC_PACK_GENERAL))) {
-            Par par;
-            par.pool = lc::pack_pool_acquire();
-            par.nt = par.pool ? par.pool->size() : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
             bool took = false;
-            int rc = pack_key_major(h, model, P, par, &took);
-            if (par.pool) lc::pack_pool_release();
+            int rc;
+            {
+                const lc::PackPoolGuard hold;  // released on every exit
+                Par par;
+                par.pool = hold.pool;
+                par.nt = par.pool ? par.pool->size() : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+                rc = pack_key_major(h, model, P, par, &took);
+            }
             if (rc) { delete P; return rc; }
             if (took) {
                 lap("key-major pack");
@@ -1206,10 +1233,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         const unsigned nr = n >= (1 << 20) ? hw : 1u;
         auto range_rows = [&](const auto &fn) {
             auto work = [&](unsigned t) { fn(t, n * (int64_t)t / nr, n * (int64_t)(t + 1) / nr); };
-            std::vector<std::thread> pool;
-            for (unsigned t = 1; t < nr; ++t) pool.emplace_back(work, t);
-            work(0);
-            for (auto &th : pool) th.join();
+            lc::run_threads(nr, work);
         };
         lc::uninit_vector<int32_t> row_key((size_t)n);  // every row written below
         std::vector<std::vector<int64_t>> rkeys(nr), rshared(nr);
@@ -1308,10 +1332,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
             auto work = [&](unsigned t) {
                 for (int64_t k = t; k < K; k += nt) fn(k, t);
             };
-            std::vector<std::thread> pool;
-            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
-            work(0);
-            for (auto &th : pool) th.join();
+            lc::run_threads(nt, work);
         };
         // key k's rows plus the shared rows, in history order
         auto key_rows = [&](int64_t k, std::vector<int64_t> &merged, const int64_t *&rows, int64_t &nrows) {
@@ -1468,10 +1489,7 @@ extern "C" int lc_pack(const lc_history *h, const lc_pack_opts *opts, lc_packed 
         std::vector<char> fits(nt, 1);
         auto range_pass = [&](const auto &fn) {
             auto work = [&](unsigned t) { fn(t, n_ev * t / nt, n_ev * (t + 1) / nt); };
-            std::vector<std::thread> pool;
-            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
-            work(0);
-            for (auto &th : pool) th.join();
+            lc::run_threads(nt, work);
         };
         range_pass([&](unsigned t, size_t j0, size_t j1) {
             for (size_t j = j0; j < j1 && fits[t]; ++j) {
@@ -1562,10 +1580,22 @@ extern "C" int64_t lc_packed_event_rows(const lc_packed *p, int64_t *out) {
     if (!p) return lc::fail(LC_E_INVALID, "lc_packed_event_rows: null packed batch");
     const size_t K = p->keys.size();
     const int64_t n = K ? (int64_t)p->ev_off[K] : 0;
-    if (out)
-        for (size_t k = 0; k < K; ++k)
-            for (uint64_t e = p->ev_off[k]; e < p->ev_off[k + 1]; ++e) out[e] = p->event_row(k, e);
+    if (out) p->event_rows(out);
     return n;
+}
+
+void lc_packed::event_rows(int64_t *out) const {
+    const size_t K = keys.size();
+    for (size_t k = 0; k < K; ++k) {
+        if (!key_major) {
+            for (uint64_t e = ev_off[k]; e < ev_off[k + 1]; ++e) out[e] = ev_row[e];
+            continue;
+        }
+        uint64_t e = ev_off[k];
+        for (uint64_t w = skip_off[k]; w < skip_off[k + 1] && e < ev_off[k + 1]; ++w)
+            for (uint64_t x = ~skip[w]; x && e < ev_off[k + 1]; x &= x - 1)
+                out[e++] = key_row0[k] + (int64_t)(64 * (w - skip_off[k])) + __builtin_ctzll(x);
+    }
 }
 
 extern "C" int64_t lc_packed_subhistory(const lc_packed *p, int64_t i, int64_t *out_rows) {

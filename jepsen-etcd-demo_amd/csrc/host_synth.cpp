@@ -185,10 +185,7 @@ extern "C" int lc_synth_generate(const lc_synth_opts *o, lc_hist **out) {
                     anom[(size_t)k] = a;
                 }
             };
-            std::vector<std::thread> pool;
-            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
-            work(0);
-            for (auto &th : pool) th.join();
+            lc::run_threads(nt, work);
             // concatenation: every key's rows at its offset, in parallel
             std::vector<int64_t> off((size_t)K + 1, 0);
             for (int64_t k = 0; k < K; ++k) off[(size_t)k + 1] = off[(size_t)k] + (int64_t)per[(size_t)k].size();
@@ -206,10 +203,7 @@ extern "C" int lc_synth_generate(const lc_synth_opts *o, lc_hist **out) {
                     std::vector<Row>().swap(per[(size_t)k]);
                 }
             };
-            pool.clear();
-            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(fill, t);
-            fill(0);
-            for (auto &th : pool) th.join();
+            lc::run_threads(nt, fill);
             for (int64_t k = 0; k < K; ++k)
                 if (anom[(size_t)k]) h->anomalous_keys.push_back(o->key_base + k);
         } else {

@@ -3,6 +3,7 @@
 // result shaping (host_report.cpp) needs.  Host code only.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -27,21 +28,21 @@ struct lc_packed {
     std::vector<uint64_t> skip_off;
     std::vector<int64_t> key_row0;
     bool key_major = false;
+    // skip_pre[w]: rows kept before skip word w within its key, so a lookup
+    // is a binary search over the key's words (not a walk from its start)
+    lc::uninit_vector<uint32_t> skip_pre;
     int64_t event_row(size_t key, uint64_t e) const {  // e: index into the event words
         if (!key_major) return ev_row[e];
-        uint64_t j = e - ev_off[key];
-        const uint64_t *w = skip.data() + skip_off[key];
-        for (int64_t base = 0;; base += 64, ++w) {
-            const uint64_t keep = ~*w;
-            const uint64_t c = (uint64_t)__builtin_popcountll(keep);
-            if (j < c) {
-                uint64_t x = keep;
-                for (uint64_t i = 0; i < j; ++i) x &= x - 1;  // drop the j lowest kept rows
-                return key_row0[key] + base + __builtin_ctzll(x);
-            }
-            j -= c;
-        }
+        const uint64_t j = e - ev_off[key];
+        const uint32_t *p0 = skip_pre.data() + skip_off[key], *p1 = skip_pre.data() + skip_off[key + 1];
+        const uint32_t *at = std::upper_bound(p0, p1, (uint32_t)j) - 1;  // the last word starting at or before j
+        const uint64_t w = (uint64_t)(at - p0);
+        uint64_t x = ~skip[skip_off[key] + w];
+        for (uint64_t i = *at; i < j; ++i) x &= x - 1;  // drop the kept rows before event j
+        return key_row0[key] + (int64_t)(64 * w) + __builtin_ctzll(x);
     }
+    // every event's row, key by key (one forward scan of each key's words)
+    void event_rows(int64_t *out) const;
     std::vector<uint32_t> trans;
     std::vector<uint32_t> trans_off;  // empty = shared table
     std::vector<uint8_t> key_width;

@@ -219,3 +219,15 @@ def test_c4_full_size_bench_budget():
     _, res, orc = device_vs_oracle(h, Device(0, budget=budget), budget=budget)
     assert res.stats["deep_keys"] > 0 and res.stats["tier3_ms"] > 0  # the HBM tier ran
 
+
+
+@pytest.mark.parametrize("x", [-1, 2**63 - 1])
+def test_extreme_register_values_on_device(device, x):
+    """a read of -1 on a never-written register is not a
+    read of nil; writes of -1 / INT64_MAX are writes of that value.  Device
+    verdicts and failing events equal the C restatement's, which reads the
+    history itself (tests/test_pack_fast.py has the pack-level check)."""
+    from test_pack_fast import _extreme_value_ops
+    h = H.History.from_ops(_extreme_value_ops(x))
+    _, res, orc = device_vs_oracle(h, device)
+    assert list(res.valid) == [0, 1, 0, 1]
