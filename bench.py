@@ -1,17 +1,17 @@
 """Benchmark: history ops linearizability-checked per second (BASELINE.json metric).
 
-`value` is the node's check rate with each rank's shard already resident in
-HBM when the timed region starts: one step is one lc_check_node_device call
-per rank (asynchronous: search -> verdict records -> all-gather of every
-rank's records over RCCL on the library's stream; one rank: none), K steps
-between barriers, the slowest rank's time.  SURVEY.md 8(d) D-1's
-host-link-inclusive rate is reported beside it, never as `value`:
-`d1_pipelined` (lc_check_node_async, two steps in flight: this rank's shard
-of packed struct-of-arrays in host memory -> H2D -> search -> records in
-page-locked host memory, each step's upload overlapping the search before
-it) and `d1_sync` (lc_check_node, one step at a time; the roofline's
-per-launch times of the set tiers come from those synchronous steps).
-`resident` holds the resident steps' own record (HIP-event span per launch).
+`value` is SURVEY.md 8(d) D-1's rate: timed end to end from each rank's
+shard of packed struct-of-arrays in host memory to the node's verdict
+records -- lc_check_node_async, two steps in flight (H2D -> search -> verdict
+records -> all-gather of every rank's records over RCCL -> records in
+page-locked host memory; each step's upload overlaps the search before it),
+K steps between barriers, the slowest rank's time.  Reported beside it:
+`resident` (the same step with the shard already resident in HBM when the
+timed region starts: lc_check_node_device, asynchronous, HIP-event span per
+launch -- the kernel-side rate, never `value`), `d1_pipelined` (the same
+numbers as `value`, kept under their round-5 name) and `d1_sync`
+(lc_check_node, one step at a time; the roofline's per-launch times of the
+set tiers come from those synchronous steps).
 
 Workloads (BASELINE.json configs; synthetic, liblincheck's seeded generator):
   N = 1 (default): C2, 1,000 keys x 1,000 client ops, concurrency 10,
@@ -430,8 +430,8 @@ def bench_c3_strong(args, local):
     torch.cuda.synchronize()
     el = time.perf_counter() - t
     v, c, fe = P.unpack_records(np.asarray(buf)[:K].astype(np.int64))
-    # the same steps with the key space resident in HBM (how the N > 1 lines'
-    # `value` is timed): the headline form of this point
+    # the same steps with the key space resident in HBM (reported beside
+    # the D-1 rate, never as it)
     db = dev.upload(packed)
     db.check_node(K, asynchronous=True)
     dev.wait()
@@ -456,11 +456,12 @@ def bench_c3_strong(args, local):
     packed = Packed(hist)
     pack_warm_s = time.perf_counter() - t
     out = {"workload": cfg["desc"] + " -- all on one GPU", "keys": K, "ops_per_key": cfg["ops"],
-           "ops_per_s": ops_total * steps / el_r, "ms_per_step": el_r / steps * 1e3, "steps": steps,
-           "step": "lc_check_node_device (asynchronous), the key space resident in HBM, as the N > 1 lines",
-           "pipelined": {"ops_per_s": ops_total * steps / el, "ms_per_step": el / steps * 1e3,
-                         "step": "lc_check_node_async (two steps in flight): host SoA -> H2D -> search -> records",
-                         "same_records_as_resident": same_r},
+           "ops_per_s": ops_total * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
+           "step": "lc_check_node_async (two steps in flight): host SoA -> H2D -> search -> records "
+                   "(SURVEY D-1, as the N > 1 lines' value)",
+           "resident": {"ops_per_s": ops_total * steps / el_r, "ms_per_step": el_r / steps * 1e3,
+                        "step": "lc_check_node_device (asynchronous), the key space resident in HBM",
+                        "same_records_as_pipelined": same_r},
            "t0_kernel": NN.T0_PATH_NAMES.get(int(st.t0_path)), "t0_ms_sync_step": float(st.tier0_ms),
            "t0_achieved_gbs": alg / (st.tier0_ms * 1e-3) / 1e9 if st.tier0_ms > 0 else None,
            "events": n_ev, "synth_s": round(synth_s, 2), "pack_ms": pack_s * 1e3,
@@ -515,13 +516,28 @@ def main():
     K, ops = cfg["keys"], cfg["ops"]
     strong = bool(cfg.get("strong"))
     key0 = rank * K
-    if strong:  # C3: a fixed key space split over the ranks (contiguous, balanced shards)
-        key0, k1 = P.shard_range(cfg["keys"], world, rank)
-        K = k1 - key0
-    block = -(-cfg["keys"] // world) if strong else K  # equal all-gather blocks
+    shards = None
+    if strong:
+        # C3: a fixed key space split over the ranks by estimated cost (SURVEY
+        # E-1, parallel.cost_shards: ops x concurrency x 2^crashed, heavy keys
+        # by LPT).  Every key of a synthetic config has the same estimate, so
+        # the shards come out as contiguous balanced ranges; a rank
+        # synthesises its own keys only, run by run.
+        crashed = min(20, int(round(cfg["info_rate"] * ops * 2 / 3)))
+        est = np.full(cfg["keys"], float(ops * cfg["concurrency"]) * 2.0 ** crashed)
+        shards = P.cost_shards(est, world)
+        K = len(shards[rank])
+        key0 = int(shards[rank][0]) if K else 0
+    block = max(len(x) for x in shards) if strong else K  # equal all-gather blocks
     t_gen = time.perf_counter()
-    hist = H.synth(n_keys=K, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
-                   anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"], key_base=key0)
+    runs = [(key0, K)]
+    if strong and not P.contiguous(shards[rank]):
+        cut = np.flatnonzero(np.diff(shards[rank]) != 1) + 1
+        runs = [(int(r[0]), len(r)) for r in np.split(shards[rank], cut)]
+    parts = [H.synth(n_keys=n, ops_per_key=ops, concurrency=cfg["concurrency"], info_rate=cfg["info_rate"],
+                     anomaly_rate=cfg["anomaly_rate"], seed=cfg["seed"], key_base=b) for b, n in runs]
+    hist = parts[0] if len(parts) == 1 else H.History.concat(parts)
+    del parts
     synth_s = time.perf_counter() - t_gen
     t_pack = time.perf_counter()
     packed = Packed(hist)
@@ -686,26 +702,26 @@ def main():
         del dev_c
 
     if rank == 0:
-        shard_keys = [P.shard_range(cfg["keys"], world, r) for r in range(world)] if strong else \
-            [(r * K, (r + 1) * K) for r in range(world)]
-        # the node's verdicts from its gathered blocks (rank order, padding 0)
-        nv, _, nfe = P.node_verdicts(node, [hi - lo for lo, hi in shard_keys], block)
-        v_host, fe_host = nv[:K], nfe[:K]  # rank 0's own shard
+        if not strong:
+            shards = [np.arange(r * K, (r + 1) * K) for r in range(world)]
+        # the node's verdicts from its gathered blocks (rank order, padding 0),
+        # back in the key space's order
+        nv, _, nfe = P.node_key_order(node, shards, block)
+        v_host, fe_host = nv[shards[0]], nfe[shards[0]]  # rank 0's own shard
         n_keys_total = int(nv.size)
         decided = int(((nv == 1) | (nv == 0)).sum())
         # ops checked: every op of a key that reached a verdict (valid or
         # invalid); a key that ends :unknown (budget) was not checked
         ops_total = (cfg["keys"] if strong else K * world) * ops
         ops_checked = decided * ops
-        # `value`: the step with the shard already resident in HBM when the
-        # timed region starts (the resident loop: search -> verdict records
-        # -> all-gather, K steps between barriers, max over ranks); the
-        # host-SoA steps, whose every step crosses the host link, are
-        # reported beside it (d1_pipelined, d1_sync) and are never `value`
+        # `value`: SURVEY D-1's host-link-inclusive step (packed host SoA ->
+        # verdict records in host memory, pipelined), K steps between
+        # barriers, max over ranks.  The resident step (the shard already in
+        # HBM) is reported beside it in `resident` and is never `value`.
         el_pipe = elapsed
-        if resident:
-            elapsed = resident["ms_per_step"] * args.steps * 1e-3
         value = ops_checked * args.steps / elapsed
+        if resident:
+            resident["ops_checked_per_s"] = ops_checked * args.steps / (resident["ms_per_step"] * args.steps * 1e-3)
         d1_pipelined = None
         if pipelined:
             d1_pipelined = {"ms_per_step": el_pipe / args.steps * 1e3, "ops_per_s": ops_checked * args.steps / el_pipe,
@@ -843,10 +859,8 @@ def main():
                        "concurrency": cfg["concurrency"], "budget": args.budget, "algorithm": args.algorithm,
                        "parallelism": f"keys sharded over {world} GPU(s), records all-gathered "
                                       f"({('host/gloo, RCCL unavailable: ' + rccl_error) if rccl_error else 'host/gloo rehearsal' if host_gather else 'RCCL' if world > 1 else 'one rank'})"},
-            "step": ("lc_check_node_device (asynchronous): the shard resident in HBM -> search -> verdict records "
-                     "-> all-gather" if resident else
-                     ("lc_check_node_async (two steps in flight)" if pipelined else "lc_check_node") +
-                     ": packed host SoA -> H2D -> search -> verdict records -> all-gather -> host"),
+            "step": (("lc_check_node_async (two steps in flight)" if pipelined else "lc_check_node") +
+                     ": packed host SoA -> H2D -> search -> verdict records -> all-gather -> host (SURVEY D-1)"),
             "d1_pipelined": d1_pipelined,
             "d1_sync": d1_sync,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -191,6 +191,36 @@ class History:
             h.anomalous_keys = buf.tolist()
         return h
 
+    # -- key subsets (a rank's shard) ---------------------
+    def select_keys(self, keys) -> "History":
+        """The rows of the given keys plus every row without a key (those
+        belong to every key's sub-history, independent/subhistory), in
+        history order; :index kept, so results name the original ops."""
+        if self.mop is not None:
+            raise NotImplementedError("select_keys: :txn histories")
+        keep = np.isin(self.key, np.asarray(keys, np.int64)) | (self.key == N.LC_NO_KEY)
+        rows = np.flatnonzero(keep)
+        h = History(self.type[rows], self.f[rows], self.process[rows], self.key[rows], self.v0[rows],
+                    self.v1[rows], self.index[rows], reg_names=self.reg_names)
+        h.other_f = {int(j): self.other_f[int(r)] for j, r in enumerate(rows) if int(r) in self.other_f}
+        return h
+
+    @classmethod
+    def concat(cls, parts: Sequence["History"]) -> "History":
+        """One history of the parts' rows in order (keys must not overlap);
+        :index renumbered to the row position, as a single run's history."""
+        if any(p.mop is not None for p in parts):
+            raise NotImplementedError("concat: :txn histories")
+        cat = lambda a: np.concatenate([getattr(p, a) for p in parts])
+        n = sum(len(p) for p in parts)
+        h = cls(cat("type"), cat("f"), cat("process"), cat("key"), cat("v0"), cat("v1"), np.arange(n, dtype=np.int64))
+        base = 0
+        for p in parts:
+            h.other_f.update({base + r: f for r, f in p.other_f.items()})
+            h.anomalous_keys += p.anomalous_keys
+            base += len(p)
+        return h
+
     # -- views --------------------------------------------------------------
     def as_c(self) -> N.LcHistory:
         h = N.LcHistory()

@@ -39,6 +39,100 @@ def lpt_shards(costs: Sequence[float], world: int) -> List[np.ndarray]:
     return [np.array(sorted(x), dtype=np.int64) for x in out]
 
 
+def key_costs(hist, budget: int = 1 << 20) -> Tuple[np.ndarray, np.ndarray]:
+    """SURVEY.md 8(e) E-1's cost estimate per key, from the history's columns
+    alone (before anything is packed): ops x concurrency x 2^crashed, with
+    2^crashed capped at the search budget (a key's config sets never exceed
+    it).  ops = the key's rows / 2, concurrency = its distinct processes,
+    crashed = its :info completions (ops callable forever: each can double the
+    frontier).  Returns (keys in order of first appearance -- the packed
+    batch's key order -- and their costs)."""
+    from . import _native as N
+    key = np.asarray(hist.key, np.int64)
+    has = key != N.LC_NO_KEY
+    rows = np.flatnonzero(has)
+    keys, first, inv, n_rows = np.unique(key[rows], return_index=True, return_inverse=True, return_counts=True)
+    order = np.argsort(first, kind="stable")          # first appearance
+    info = np.bincount(inv, weights=(np.asarray(hist.type)[rows] == N.LC_INFO), minlength=keys.size)
+    kp = np.unique(np.stack([inv, np.asarray(hist.process, np.int64)[rows]]), axis=1)
+    procs = np.bincount(kp[0], minlength=keys.size)
+    cap = max(0, int(budget).bit_length() - 1)
+    cost = (n_rows / 2.0) * np.maximum(procs, 1) * np.exp2(np.minimum(info, cap))
+    return keys[order], cost[order]
+
+
+def cost_shards(costs: Sequence[float], world: int, heavy: float = 1.0 / 32) -> List[np.ndarray]:
+    """Key indices of each rank (sorted), balanced by estimated cost (E-1).
+
+    Keys costing more than `heavy` of one rank's fair share go first, by LPT
+    (longest first, each to the least-loaded rank): those are the keys that
+    would otherwise leave one rank holding the walk that decides the node's
+    time.  The rest, in key order, are then cut into one contiguous run per
+    rank, sized by water-filling so every rank ends as near the common level
+    as whole keys allow (each rank's load is within one light key -- at most
+    `heavy` of a share -- of it, unless its heavy keys alone exceed it).
+    With equal costs there are no heavy keys and the shards are contiguous
+    balanced ranges, as shard_range's (the bench synthesises a rank's range
+    directly)."""
+    costs = np.asarray(costs, dtype=np.float64)
+    n = costs.size
+    if world <= 1 or n == 0:
+        return [np.arange(n, dtype=np.int64)] + [np.zeros(0, np.int64) for _ in range(max(world, 1) - 1)]
+    total = float(costs.sum())
+    thr = heavy * total / world
+    is_heavy = costs > thr
+    load = np.zeros(world)
+    parts: List[List[int]] = [[] for _ in range(world)]
+    hv = np.flatnonzero(is_heavy)
+    for k in hv[np.argsort(-costs[hv], kind="stable")]:
+        r = int(np.argmin(load))
+        parts[r].append(int(k))
+        load[r] += costs[k]
+    light = np.flatnonzero(~is_heavy)
+    lt = float(costs[light].sum())
+    # water level lam: sum over ranks of max(0, lam - load) = lt
+    srt = np.sort(load)
+    lam = srt[-1]
+    for i in range(world):
+        # level between srt[i] and srt[i+1] fills the i+1 lowest ranks
+        nxt = srt[i + 1] if i + 1 < world else np.inf
+        need = (i + 1) * nxt - srt[:i + 1].sum()
+        if need >= lt:
+            lam = (lt + srt[:i + 1].sum()) / (i + 1)
+            break
+    quota = np.maximum(0.0, lam - load)
+    bounds = np.cumsum(quota)
+    cum = np.cumsum(costs[light])
+    mid = cum - costs[light] / 2.0
+    owner = np.minimum(np.searchsorted(bounds, mid, side="left"), world - 1)
+    return [np.sort(np.concatenate([np.asarray(parts[r], np.int64), light[owner == r]])) for r in range(world)]
+
+
+def shard_costs(costs: Sequence[float], shards: Sequence[np.ndarray]) -> np.ndarray:
+    """Each rank's estimated cost under a sharding."""
+    costs = np.asarray(costs, dtype=np.float64)
+    return np.array([costs[s].sum() for s in shards])
+
+
+def contiguous(shard: np.ndarray) -> bool:
+    """Whether a shard is one run of consecutive key indices."""
+    return shard.size == 0 or int(shard[-1]) - int(shard[0]) + 1 == shard.size
+
+
+def node_key_order(node, shards: Sequence[np.ndarray], block: int):
+    """(valid, cause, fail_event) of every key in the caller's key order from
+    the gathered node records (rank r's records are the first len(shards[r])
+    of block r, in the order of shards[r]; the padding must be 0)."""
+    v, c, fe = node_verdicts(node, [len(s) for s in shards], block)
+    n = sum(len(s) for s in shards)
+    at = np.concatenate([np.asarray(s, np.int64) for s in shards]) if shards else np.zeros(0, np.int64)
+    if n and not np.array_equal(np.sort(at), np.arange(n)):
+        raise ValueError("shards do not partition the keys")
+    vo, co, fo = np.empty_like(v), np.empty_like(c), np.empty_like(fe)
+    vo[at], co[at], fo[at] = v, c, fe
+    return vo, co, fo
+
+
 def pack_records(valid, cause, fail_event):
     """Verdict records, numpy or torch (same arithmetic)."""
     try:

@@ -1,6 +1,7 @@
 """One rank of tests/test_gpu_node.py::test_two_rank_node_step (run as a
 fresh process per rank, before any GPU call in it): the library's node step
-(lc_check_node, one rank's context) on this rank's shard of the key space,
+(lc_check_node, one rank's context) on this rank's cost-balanced shard of a
+mixed key space (parallel.key_costs / cost_shards, SURVEY E-1),
 its block of LC_REC_* records all-gathered over gloo (the bench's host-gather
 path: RCCL refuses two ranks on one GPU), rank 0 saving the node's records.
 usage: node_rank_main.py RANK WORLD PORT N_KEYS OPS OUT"""
@@ -14,6 +15,19 @@ import numpy as np  # noqa: E402
 import torch.distributed as dist  # noqa: E402  (torch first: the library binds its HIP runtime)
 
 
+BUDGET = 1 << 16
+
+
+def mixed_history(n_keys, ops):
+    """n_keys C2/C5-shaped keys (concurrency 10, 2 % anomalous) followed by 6
+    C4-shaped ones (concurrency 30, 2 % crashed write/cas): the batch whose
+    contiguous split leaves every C4-shaped key on the last rank."""
+    from lincheck import history as H
+    return H.History.concat([
+        H.synth(n_keys=n_keys, ops_per_key=ops, concurrency=10, anomaly_rate=0.02, seed=9),
+        H.synth(n_keys=6, ops_per_key=400, concurrency=30, info_rate=0.02, seed=4, key_base=n_keys)])
+
+
 def main():
     rank, world, port, n_keys, ops = (int(x) for x in sys.argv[1:6])
     out = sys.argv[6]
@@ -21,10 +35,11 @@ def main():
     from lincheck import history as H
     from lincheck import parallel as P
     from lincheck.checker import Device, Packed
-    lo, hi = P.shard_range(n_keys, world, rank)
-    block = -(-n_keys // world)
-    h = H.synth(n_keys=hi - lo, ops_per_key=ops, concurrency=10, anomaly_rate=0.02, seed=9, key_base=lo)
-    rec, st = Device(0).check_node(Packed(h), block)
+    h = mixed_history(n_keys, ops)
+    keys, costs = P.key_costs(h, BUDGET)
+    shards = P.cost_shards(costs, world)
+    block = max(len(s) for s in shards)
+    rec, st = Device(0, budget=BUDGET).check_node(Packed(h.select_keys(keys[shards[rank]])), block)
     node = P.gather_blocks(np.asarray(rec, np.int64))
     if rank == 0:
         np.save(out, node)

@@ -121,3 +121,80 @@ def test_record_round_trip():
     v = np.array([1, 0, -1], np.int8); c = np.array([0, 1, 2], np.uint8); fe = np.array([-1, 17, 2**30], np.int32)
     vv, cc, ff = parallel.unpack_records(parallel.pack_records(v, c, fe))
     assert (vv == v).all() and (cc == c).all() and (ff == fe).all()
+
+
+def _mixed():
+    from lincheck import history as H
+    return H.History.concat([
+        H.synth(n_keys=300, ops_per_key=300, concurrency=10, anomaly_rate=0.05, seed=7),
+        H.synth(n_keys=100, ops_per_key=150, concurrency=6, anomaly_rate=0.1, seed=8, key_base=300),
+        H.synth(n_keys=4, ops_per_key=200, concurrency=30, info_rate=0.02, seed=4, key_base=400)])
+
+
+def _rank_cost(rank, world, port, out_path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "jepsen-etcd-demo_amd"), os.path.join(root, "oracle")]
+    import torch.distributed as dist
+    import cref
+    from lincheck import parallel as P
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    h = _mixed()
+    keys, costs = P.key_costs(h, 1 << 16)
+    shards = P.cost_shards(costs, world)
+    block = max(len(s) for s in shards)
+    sub = h.select_keys(keys[shards[rank]])
+    k, r = cref.check_history(sub.as_c(), budget=1 << 16)
+    assert list(k) == list(keys[shards[rank]])  # the shard's keys, in the caller's order
+    node = P.gather_blocks(P.node_block(r["valid"], r["cause"], r["fail_event"], block))
+    if rank == 0:
+        np.save(out_path, node)
+    dist.destroy_process_group()
+
+
+def test_cost_sharded_mixed_batch(tmp_path):
+    """VERDICT r5 next #5 / SURVEY E-1: a batch mixing C4-shaped keys
+    (concurrency 30, crashed ops) into C5/C2-shaped ones, sharded by
+    estimated cost (ops x concurrency x 2^crashed: parallel.key_costs,
+    cost_shards) over a gloo world of 2; the node's records put back in the
+    caller's key order equal one rank's check of the whole batch, and the
+    ranks' estimated costs are within 10 % -- where the contiguous split
+    leaves every C4-shaped key on one rank."""
+    import cref
+    h = _mixed()
+    keys, costs = parallel.key_costs(h, 1 << 16)
+    shards = parallel.cost_shards(costs, 2)
+    loads = parallel.shard_costs(costs, shards)
+    assert loads.max() <= 1.1 * loads.min()
+    heavy = np.flatnonzero(costs > 10 * np.median(costs))
+    assert len(heavy) >= 2 and set(heavy) <= {400, 401, 402, 403}  # C4-shaped keys are the heavy ones
+    contig = [np.arange(*parallel.shard_range(len(costs), 2, r)) for r in range(2)]
+    cl = parallel.shard_costs(costs, contig)
+    assert cl.max() > 1.1 * cl.min()  # what cost sharding fixes
+    out = str(tmp_path / "gathered.npy")
+    mp.spawn(_rank_cost, args=(2, free_port(), out), nprocs=2, join=True)
+    node = np.load(out)
+    v, c, fe = parallel.node_key_order(node, shards, max(len(s) for s in shards))
+    k, r = cref.check_history(h.as_c(), budget=1 << 16)
+    assert list(k) == list(keys)
+    np.testing.assert_array_equal(v, r["valid"])
+    np.testing.assert_array_equal(c, r["cause"])
+    np.testing.assert_array_equal(fe, r["fail_event"])
+    assert (v == 0).any()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_cost_shards_properties(world):
+    rng = np.random.default_rng(world)
+    for trial in range(20):
+        costs = rng.pareto(1.5, size=int(rng.integers(1, 400))) + 0.01
+        sh = parallel.cost_shards(costs, world)
+        assert len(sh) == world
+        allk = np.concatenate(sh)
+        assert np.array_equal(np.sort(allk), np.arange(len(costs)))
+        for s in sh:
+            assert np.array_equal(s, np.sort(s))
+        # no rank above the LPT bound: the fair share plus the largest key
+        assert parallel.shard_costs(costs, sh).max() <= costs.sum() / world + costs.max() + 1e-9
+    eq = parallel.cost_shards(np.ones(1001), world)
+    assert all(parallel.contiguous(s) for s in eq) and max(map(len, eq)) - min(map(len, eq)) <= 1

@@ -417,15 +417,19 @@ def test_many_keys_take_the_unsegmented_tier():
 def test_two_rank_node_step(tmp_path):
     """E-1 (independent/checker's pmap, etcdemo.clj:115) with two ranks: two
     fresh processes on the one GPU, each running the library's node step
-    (lc_check_node) on its contiguous shard of 4,001 keys, their blocks of
-    LC_REC_* records all-gathered over gloo in rank order.  The node's
-    records, decoded (parallel.node_verdicts: the padding of the odd shard
-    must be 0), equal the oracle's for every key and a single-process check
-    of the same key space split over two shards (devices=[0, 0])."""
+    (lc_check_node) on its shard of a mixed batch -- 4,001 C5-shaped keys and
+    6 C4-shaped ones -- split by estimated cost (parallel.key_costs /
+    cost_shards: the C4-shaped keys by LPT, the rest in contiguous runs),
+    their blocks of LC_REC_* records all-gathered over gloo in rank order.
+    The node's records, put back in the caller's key order
+    (parallel.node_key_order; the padding of the shorter shard must be 0),
+    equal the oracle's for every key and a single-process check of the same
+    batch (devices=[0, 0]); the ranks' estimated costs are within 10 %."""
     import socket
     import subprocess
     import sys
     from lincheck import parallel as P
+    from node_rank_main import BUDGET, mixed_history
     n_keys, ops, world = 4001, 300, 2
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -444,17 +448,20 @@ def test_two_rank_node_step(tmp_path):
                 p.kill()
                 p.wait()
     node = np.load(out)
-    block = -(-n_keys // world)
-    sizes = [hi - lo for lo, hi in (P.shard_range(n_keys, world, r) for r in range(world))]
-    assert node.size == block * world and sizes == [2001, 2000]
-    v, c, fe = P.node_verdicts(node, sizes, block)
-    h = H.synth(n_keys=n_keys, ops_per_key=ops, concurrency=10, anomaly_rate=0.02, seed=9)
-    _, orc = cref.check_history(h.as_c(), budget=1 << 20, threads=8)
+    h = mixed_history(n_keys, ops)
+    keys, costs = P.key_costs(h, BUDGET)
+    shards = P.cost_shards(costs, world)
+    block = max(len(s) for s in shards)
+    loads = P.shard_costs(costs, shards)
+    assert loads.max() <= 1.1 * loads.min()
+    assert node.size == block * world
+    v, c, fe = P.node_key_order(node, shards, block)
+    _, orc = cref.check_history(h.as_c(), budget=BUDGET, threads=8)
     np.testing.assert_array_equal(v, orc["valid"])
     np.testing.assert_array_equal(c, orc["cause"])
     np.testing.assert_array_equal(fe, orc["fail_event"])
     assert (v == 0).sum() > 10
-    one = Device(0, devices=[0, 0]).check(Packed(h), verdicts_only=True)
+    one = Device(0, devices=[0, 0], budget=BUDGET).check(Packed(h), verdicts_only=True)
     np.testing.assert_array_equal(one.valid, v)
     np.testing.assert_array_equal(one.fail_event, fe)
 

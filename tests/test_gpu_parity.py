@@ -507,3 +507,113 @@ def test_concurrent_calls_on_one_context():
         _, orc = cref.check_history(h.as_c(), budget=dev.budget, threads=8)
         np.testing.assert_array_equal(res.valid, orc["valid"])
         np.testing.assert_array_equal(res.fail_event, orc["fail_event"])
+
+
+def _c5_bench_history():
+    """bench.py --config C5: 1,000 keys x 1,000 ops, concurrency 10, 5 %
+    anomalous keys, seed 5 (BASELINE configs[4])."""
+    return H.synth(n_keys=1000, ops_per_key=1000, concurrency=10, anomaly_rate=0.05, seed=5)
+
+
+def _c5_subhistories(h, keys):
+    """Each key's sub-history (independent/subhistory: the key's rows, tuple
+    values unwrapped), built from the history's own key column -- not from
+    the packed batch, so the split is checked too."""
+    kk = np.asarray(h.key)
+    out = {}
+    for k in keys:
+        sub = []
+        for r in np.flatnonzero(kk == k):
+            o = h.op(int(r))
+            v = o.get("value")
+            if getattr(v, "_lc_tuple", False):
+                o["value"] = v[1]
+            sub.append(o)
+        out[k] = sub
+    return out
+
+
+def test_c5_full_size_counterexamples_linear():
+    """BASELINE config 5's "verdict plus counterexample
+    parity" at its own size, through the Jepsen-shaped path at
+    etcdemo.clj:115-119 (independent/checker over compose {:linear
+    (linearizable {:model cas-register :algorithm :linear}), :timeline}) --
+    the exact speculative segments (k_spec<..., EX>, final configs, no
+    peaks).  Every key's :valid? equals the C restatement's; for every
+    invalid key, :op / :previous-ok / :last-op :index, the :configs set and
+    the :final-paths set equal oracle/linear_ref.py's analysis of the key's
+    sub-history (subsets when the restatement has more than 10, jepsen's
+    truncation)."""
+    import linear_ref as LR
+    from helpers import config_tuple, path_tuple
+    from lincheck import checker as ck
+    from lincheck import independent, model
+    h = _c5_bench_history()
+    lin = ck.linearizable({"model": model.cas_register(), "algorithm": "linear"})
+    out = independent.checker(ck.compose({"linear": lin, "timeline": ck.unbridled_optimism()})).check({}, h, {})
+    keys, orc = cref.check_history(h.as_c(), threads=8)
+    exp_valid = {int(k): {1: True, 0: False, -1: "unknown"}[int(r["valid"])] for k, r in zip(keys, orc)}
+    assert {k: r["linear"]["valid?"] for k, r in out["results"].items()} == exp_valid
+    bad = sorted(k for k, v in exp_valid.items() if v is False)
+    assert sorted(out["failures"]) == bad and out["valid?"] is False
+    subs = _c5_subhistories(h, bad)
+    n_cfg = n_paths = 0
+    for k in bad:
+        sub, m = subs[k], out["results"][k]["linear"]
+        a = LR.analysis(sub)
+        assert a.valid is False
+        assert m["op"]["index"] == sub[a.fail_pos]["index"] and m["op"]["type"] == "ok", k
+        prev = sub[a.previous_ok_pos]["index"] if a.previous_ok_pos is not None else None
+        assert (m["previous-ok"] or {}).get("index") == prev, k
+        assert (m["last-op"] or {}).get("index") == prev, k
+        exp_cfgs = {(st, frozenset(sub[a.ops[q].invoke_pos]["index"] for q in L)) for st, L in a.final_configs}
+        got_cfgs = [config_tuple(c, "cas-register") for c in m["configs"]]
+        assert len(set(got_cfgs)) == len(got_cfgs) == min(10, len(exp_cfgs)), k
+        assert set(got_cfgs) <= exp_cfgs, k
+        if len(exp_cfgs) <= 10:
+            assert set(got_cfgs) == exp_cfgs, k
+        exp_paths = LR.final_paths(a, sub)
+        got_paths = {path_tuple(p, "cas-register") for p in m["final-paths"]}
+        assert len(got_paths) == len(m["final-paths"]) > 0, k
+        assert exp_paths is not None and got_paths <= exp_paths, k
+        if len(exp_cfgs) <= 10 and len(exp_paths) <= 10:
+            assert got_paths == exp_paths, k
+        n_cfg += len(got_cfgs)
+        n_paths += len(got_paths)
+    assert len(bad) > 20 and n_cfg >= len(bad) and n_paths >= len(bad)
+
+
+def test_c5_full_size_counterexamples_wgl():
+    """The same history through (linearizable {:algorithm :wgl}): every key's
+    :valid? equals oracle/wgl_ref.c's; for every invalid key, :op and
+    :previous-ok :index and the :configs frontier equal oracle/wgl_ref.py's
+    walk on the key's sub-history (a subset when its frontier has more than
+    10 configs)."""
+    import wgl_ref as W
+    from lincheck import checker as ck
+    from lincheck import independent, model
+    h = _c5_bench_history()
+    lin = ck.linearizable({"model": model.cas_register(), "algorithm": "wgl"})
+    out = independent.checker(lin).check({}, h, {})
+    keys, orc, _, _ = cref.check_history_wgl(h.as_c(), threads=8)
+    exp_valid = {int(k): {1: True, 0: False, -1: "unknown"}[int(r["valid"])] for k, r in zip(keys, orc)}
+    assert {k: r["valid?"] for k, r in out["results"].items()} == exp_valid
+    bad = sorted(k for k, v in exp_valid.items() if v is False)
+    assert sorted(out["failures"]) == bad
+    subs = _c5_subhistories(h, bad)
+    n_cfg = 0
+    for k in bad:
+        sub, g = subs[k], out["results"][k]
+        w = W.analysis(sub)
+        assert w.valid is False and g["analyzer"] == "wgl"
+        assert g["op"]["index"] == sub[w.fail_pos]["index"], k
+        prev = sub[w.previous_ok_pos]["index"] if w.previous_ok_pos is not None else None
+        assert (g["previous-ok"] or {}).get("index") == prev, k
+        idx = lambda oid: sub[w.ops[oid].invoke_pos]["index"]
+        want = {(st, frozenset(idx(q) for q in L)) for st, L in w.frontier}
+        got = {(c["model"]["value"], frozenset(o["index"] for o in c["linearized"])) for c in g["configs"]}
+        assert got and got <= want, k
+        if len(want) <= 10:
+            assert got == want, k
+        n_cfg += len(got)
+    assert len(bad) > 20 and n_cfg >= len(bad)
