@@ -93,6 +93,8 @@ def parse():
                     help="default: C2 at one GPU, C3 (strong scaling) at more")
     ap.add_argument("--budget", type=int, default=1 << 20)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="time the CPU :wgl restatement on the whole batch, not a bounded sample")
     ap.add_argument("--no-resident", action="store_true", help="skip the resident-shard steps")
     ap.add_argument("--d1-sync", action="store_true",
                     help="time the synchronous lc_check_node step instead of the pipelined one")
@@ -338,7 +340,7 @@ def cpu_baseline(args, cfg, K, key0, hist, ops, v_host, fe_host, nproc, aff, quo
     # knossos.wgl's search (the other analysis jepsen.checker/linearizable
     # offers, north_star's "CPU :linear/:wgl"): oracle/wgl_ref.c on the same
     # cores, on as many of the batch's first keys as ~8 s allow
-    kw = min(K, threads)
+    kw = K if args.cpu_full else min(K, threads)
     tw = time.perf_counter()
     _, worc, _, _ = cref.check_history_wgl(first_keys(kw).as_c(), budget=args.budget, threads=threads)
     twc = time.perf_counter() - tw

@@ -669,6 +669,18 @@ struct LatMem {
     uint32_t *W, *R, *I;
 };
 
+// The lane's column of a workspace row array, its address formed where it is
+// used: with a plain m.W[k * 64 + lane] the compiler hoisted the 16 rows'
+// 64-bit addresses out of the walk's event loop and kept them for its whole
+// life -- 16 VGPR pairs, spilled to scratch in the 64-VGPR k_spec builds and
+// rewritten there at every walk's start (round 5's 29.8x traffic).  The empty
+// asm makes the lane index opaque, so each use site rebuilds one address and
+// the rows are immediate offsets from it.
+__device__ __forceinline__ uint32_t opq_lane(uint32_t lane) {
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+
 template <int RL, bool TAG = false>
 __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_t n, uint32_t k_v,
                                             uint32_t cap_v, uint32_t b_v, uint32_t lane, uint64_t budget,
@@ -777,26 +789,28 @@ __device__ __forceinline__ int ok_event_mem_gs(const LatMem &m, uint32_t p, uint
     const uint32_t pk = __builtin_amdgcn_readlane(k_v, p), pc = __builtin_amdgcn_readlane(cap_v, p),
                    pb = __builtin_amdgcn_readlane(b_v, p);
     const uint32_t plm = p < 6 ? 1u << p : 0u, prm = p >= 6 ? 1u << (p - 6) : 0u;
+    const uint32_t ol = opq_lane(lane);
+    uint32_t *const mW = m.W + ol, *const mR = m.R + ol, *const mI = m.I + ol;
 #pragma unroll 1
     for (int k = 0; k < RL; ++k) {
-        const uint32_t w = m.W[k * 64 + lane];
-        const uint32_t src = (uint32_t)__shfl_xor((int)m.W[(k ^ prm) * 64 + lane], (int)plm);
+        const uint32_t w = mW[k * 64];
+        const uint32_t src = (uint32_t)__shfl_xor((int)mW[(k ^ prm) * 64], (int)plm);
         const bool hp = (lane & plm) || ((uint32_t)k & prm);
-        m.R[k * 64 + lane] = hp ? 0u : src;
-        m.I[k * 64 + lane] = hp ? 0u : w;
+        mR[k * 64] = hp ? 0u : src;
+        mI[k * 64] = hp ? 0u : w;
     }
 #pragma unroll 1
     for (int s = 0; s < NB; ++s) {
         bool ch = false;
 #pragma unroll 1
         for (int k = 0; k < RL; ++k) {
-            const uint32_t x = m.I[k * 64 + lane];
+            const uint32_t x = mI[k * 64];
             uint32_t nv = sweep_lanes<0, 6>(x, lmk);
 #pragma unroll
             for (int r = 0; r < NR; ++r)
-                if ((k >> r) & 1) nv = xacc(nv, m.I[(k ^ (1 << r)) * 64 + lane], rk[r], lmk.sc[6 + r], lmk.sb[6 + r]);
+                if ((k >> r) & 1) nv = xacc(nv, mI[(k ^ (1 << r)) * 64], rk[r], lmk.sc[6 + r], lmk.sb[6 + r]);
             if (nv != x) {
-                m.I[k * 64 + lane] = nv;
+                mI[k * 64] = nv;
                 ch = true;
             }
         }
@@ -805,8 +819,8 @@ __device__ __forceinline__ int ok_event_mem_gs(const LatMem &m, uint32_t p, uint
     uint32_t cS = 0;
 #pragma unroll 1
     for (int k = 0; k < RL; ++k) {
-        const uint32_t r = m.R[k * 64 + lane] | xapply(m.I[k * 64 + lane], pk, pc, pb);
-        m.R[k * 64 + lane] = r;
+        const uint32_t r = mR[k * 64] | xapply(mI[k * 64], pk, pc, pb);
+        mR[k * 64] = r;
         cS |= r;
     }
     if (!__any(cS != 0u)) return 1;
@@ -814,11 +828,11 @@ __device__ __forceinline__ int ok_event_mem_gs(const LatMem &m, uint32_t p, uint
     const uint32_t llm = last < 6 ? 1u << last : 0u, lrm = last >= 6 ? 1u << (last - 6) : 0u;
 #pragma unroll 1
     for (int k = 0; k < RL; ++k) {
-        const uint32_t r = m.R[k * 64 + lane];
-        const uint32_t src = (uint32_t)__shfl_xor((int)m.R[(k ^ (prm | lrm)) * 64 + lane], (int)(plm | llm));
+        const uint32_t r = mR[k * 64];
+        const uint32_t src = (uint32_t)__shfl_xor((int)mR[(k ^ (prm | lrm)) * 64], (int)(plm | llm));
         const bool hp = (lane & plm) || ((uint32_t)k & prm);
         const bool hl = (lane & llm) || ((uint32_t)k & lrm);
-        m.W[k * 64 + lane] = p == last ? r : (hl ? 0u : (hp ? src : r));
+        mW[k * 64] = p == last ? r : (hl ? 0u : (hp ? src : r));
     }
     return 0;
 }
@@ -2248,8 +2262,9 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                         held = uni(got);
                         uint32_t *const mb = held >= 0 ? lds_ws + (size_t)held * (3 * T0_RMEM * 64) : ws;
                         m = LatMem{mb, mb + T0_RMEM * 64, mb + 2 * T0_RMEM * 64};
+                        uint32_t *const mW = m.W + opq_lane(lane);
 #pragma unroll
-                        for (int k = 0; k < T0_RMEM; ++k) m.W[k * 64 + lane] = k < RM ? W[k < RM ? k : 0] : 0u;
+                        for (int k = 0; k < T0_RMEM; ++k) mW[k * 64] = k < RM ? W[k < RM ? k : 0] : 0u;
                         in_mem = true;
                     }
                     const uint32_t idx = n;
@@ -2283,8 +2298,9 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                 }
                 live = r ? live : (1u << last) - 1u;
                 if (in_mem && n == 9 && !r) {
+                    const uint32_t *const mW = m.W + opq_lane(lane);
 #pragma unroll
-                    for (int k = 0; k < RM; ++k) W[k] = m.W[k * 64 + lane];
+                    for (int k = 0; k < RM; ++k) W[k] = mW[k * 64];
                     in_mem = false;
                     if (held >= 0 && lane == 0) atomicExch(&lds_busy[held], 0);
                     held = -1;
@@ -2308,7 +2324,7 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
 #pragma unroll 1
                 for (int k = 0; k < T0_RMEM; ++k) {
                     uint32_t x = 0;
-                    if (in_mem) x = m.W[k * 64 + lane];
+                    if (in_mem) x = m.W[k * 64 + opq_lane(lane)];
                     else {
 #pragma unroll
                         for (int q = 0; q < RM; ++q)
@@ -2426,7 +2442,8 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
         }
         return;  // the whole block: no barrier below is reached by half of it
     }
-    const int32_t key = KA.order[blk];
+    // (scalar: as a VGPR it was the 64-VGPR builds' last spill to scratch)
+    const int32_t key = (int32_t)uni((uint32_t)KA.order[blk]);
     uint32_t *ws = KA.lat_ws + ((size_t)blk * W + wv) * (3 * T0_RMEM * 64);
     const uint64_t eb = KA.ev_off[key];
     const uint32_t nev = (uint32_t)(KA.ev_off[key + 1] - eb);

@@ -564,6 +564,8 @@ class Linearizable:
         const = {name for name, ch in parts if type(ch) is UnbridledOptimism}
         only_const = all(ch is self or name in const for name, ch in parts)
         draw = bool((test or {}).get("store-path"))
+        if not draw and (inner is self or only_const) and res is not None and SHARED_VALID_MAPS:
+            return self._shape_fast(parts, inner, packed, res, t0, t1, t2)
         valid = res.valid.tolist() if res is not None else []
         names = {code: name for code, name in N.ANALYZERS.items()}
         anl = res.analyzer.tolist() if res is not None and res.analyzer is not None else None
@@ -613,6 +615,61 @@ class Linearizable:
         self.last_timing = {"pack_ms": (t1 - t0) * 1e3, "search_ms": (t2 - t1) * 1e3,
                             "shape_ms": (time.perf_counter() - t2) * 1e3}
         return out
+
+
+    def _shape_fast(self, parts, inner, packed, res, t0, t1, t2) -> Dict:
+        """_shape for the drop-in's own expression (etcdemo.clj:115-119:
+        linearizable alone, or composed with constant checkers such as
+        :timeline's stand-in) when nothing is drawn.  The valid keys -- nearly
+        all of them -- carry one shared result map per analyzer, placed by
+        dict.fromkeys, the key-order failure list and merge-valid come from
+        the verdict array, and only the other keys are rendered one by one.
+        The maps are values, as Clojure's persistent maps are (do not mutate
+        them: a valid key's map is shared with the other valid keys of the
+        same check).  VERDICT r5 next #7: C5's 1,000-key result shaping."""
+        keys = packed.keys
+        valid = np.asarray(res.valid)
+        names = N.ANALYZERS
+        anl = np.asarray(res.analyzer) if res.analyzer is not None else None
+        base_code = N.LC_ALGO_WGL if self.analyzer == "wgl" else N.LC_ALGO_LINEAR
+
+        def wrap(lin):
+            if inner is self:
+                return lin
+            r = {name: (lin if ch is self else {"valid?": True}) for name, ch in parts}
+            r["valid?"] = merge_valid((lin.get("valid?"),))
+            return r
+
+        shared = {}
+
+        def valid_map(code):
+            m = shared.get(code)
+            if m is None:
+                m = shared[code] = wrap({"analyzer": names.get(code, "linear"), "configs": [], "final-paths": [],
+                                         "valid?": True})
+            return m
+        results = dict.fromkeys(keys, valid_map(base_code))
+        odd = valid != N.LC_VALID
+        if anl is not None:
+            odd |= anl != base_code
+        for i in np.flatnonzero(odd).tolist():
+            code = int(anl[i]) if anl is not None else base_code
+            analyzer = names.get(code, "linear")
+            results[keys[i]] = valid_map(code) if valid[i] == N.LC_VALID else wrap(_render_key(packed, i, res, None,
+                                                                                               analyzer))
+        bad = np.flatnonzero(valid == N.LC_INVALID)
+        # merge-valid over the keys: false > :unknown > true
+        out = {"valid?": False if bad.size else ("unknown" if (valid != N.LC_VALID).any() else True),
+               "results": results, "failures": [keys[i] for i in bad.tolist()]}
+        out["stats"] = res.stats
+        self.last_timing = {"pack_ms": (t1 - t0) * 1e3, "search_ms": (t2 - t1) * 1e3,
+                            "shape_ms": (time.perf_counter() - t2) * 1e3}
+        return out
+
+
+# The fast result shaping (Linearizable._shape_fast); False takes the general
+# per-key path (tests compare the two).
+SHARED_VALID_MAPS = True
 
 
 class Compose:

@@ -201,3 +201,45 @@ def test_final_paths_random(model_name):
         ops = random_history(seed, n_keys=2, max_ops=8, procs=4, model=model_name)
         checked += _final_paths_case(ops, model_name)
     assert checked > 20
+
+
+@pytest.mark.parametrize("inner_kind", ["linearizable", "compose"])
+def test_fast_result_shaping_equals_general(inner_kind):
+    """Linearizable._shape_fast (shared maps for the valid keys, merge-valid
+    from the verdict array) returns what the general per-key shaping does,
+    on a C5-shaped batch whose device results are stood in by the C
+    restatement's (no GPU here: verdicts, causes, failing events; one key
+    made :unknown at the budget)."""
+    import cref
+    from lincheck import _native as N
+    h = H.synth(n_keys=300, ops_per_key=200, concurrency=8, anomaly_rate=0.1, seed=12)
+    keys, orc = cref.check_history(h.as_c(), threads=4)
+    K = len(keys)
+    valid = orc["valid"].astype(np.int8).copy()
+    cause = orc["cause"].astype(np.uint8).copy()
+    valid[5], cause[5] = -1, 2  # :unknown at the budget
+    res = KeyResults(valid=valid, fail_event=orc["fail_event"].astype(np.int32), cause=cause,
+                     peak=np.zeros(K, np.uint32), final=np.zeros((K, 10, 2), np.uint64),
+                     n_final=np.zeros(K, np.uint32), stats={"kernel_ms": 0.0})
+
+    class FakeDev:
+        def check(self, packed, peaks=True, verdicts_only=False):
+            return res
+
+    outs = []
+    for fast in (True, False):
+        lin = ck.linearizable({"model": model.cas_register(), "algorithm": "linear"})
+        lin._dev = lambda: FakeDev()
+        inner = lin if inner_kind == "linearizable" else ck.compose({"linear": lin,
+                                                                     "timeline": ck.unbridled_optimism()})
+        old = ck.SHARED_VALID_MAPS
+        ck.SHARED_VALID_MAPS = fast
+        try:
+            outs.append(independent.checker(inner).check({}, h, {}))
+        finally:
+            ck.SHARED_VALID_MAPS = old
+    a, b = outs
+    assert list(a["results"]) == list(b["results"]) == [int(k) for k in keys]
+    assert a["results"] == b["results"]
+    assert a["failures"] == b["failures"] and a["failures"]
+    assert a["valid?"] == b["valid?"] is False

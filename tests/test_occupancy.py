@@ -68,3 +68,17 @@ def test_spec_builds_keep_their_occupancy(tmp_path, name, want):
     k = ks[name]
     got = _waves_per_simd(k)
     assert got >= want, f"{name}: {got} waves per SIMD ({k}), want {want}"
+
+
+@pytest.mark.parametrize("name", [
+    "_ZN3lcd6k_specILi8ELi8ELb1ELb0EEEvNS_6T0ArgsE",  # C2 / C5 (verdict records)
+    "_ZN3lcd6k_specILi2ELi2ELb1ELb0EEEvNS_6T0ArgsE",  # the C3 shards
+    "_ZN3lcd6k_specILi4ELi4ELb1ELb0EEEvNS_6T0ArgsE",
+])
+def test_spec_builds_do_not_spill(tmp_path, name):
+    """the 64-VGPR builds held their occupancy by spilling
+    to scratch (84 and 148 B per lane; 29.8x and 14.4x the algorithmic HBM
+    bytes).  With the workspace rows addressed where used (opq_lane) and the
+    key index scalar, no build of the verdict path keeps a private segment."""
+    k = _kernels(tmp_path)[name]
+    assert k["private_segment_fixed_size"] == 0, f"{name}: {k}"

@@ -72,7 +72,8 @@ for part in $PARTS; do
   c4wgl24)
     # BASELINE C4 decided: knossos.wgl's walk at a 2^24 cache budget
     # (profiles/r05_c4_budget_sweep.json: every key valid there)
-    bench c4_wgl24 600 --config C4 --budget 16777216 --algorithm wgl --d1-sync --steps 1 --warmup 1 --no-resident ;;
+    # (--cpu-full: oracle/wgl_ref.c on all 256 keys beside it)
+    bench c4_wgl24 900 --config C4 --budget 16777216 --algorithm wgl --d1-sync --steps 1 --warmup 1 --no-resident --cpu-full ;;
   *) echo "unknown part $part"; exit 2 ;;
   esac
 done
