@@ -64,7 +64,7 @@ for p in (os.path.join(ROOT, "jepsen-etcd-demo_amd"), os.path.join(ROOT, "oracle
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # profiles/*.json summaries (rocprofv3 --pmc / SQ) are used for `traffic` /
 # `issue` only when they were taken of this round's build
-PROFILE_ROUND = 5
+PROFILE_ROUND = 6
 ALGORITHMS = {"linear": 0, "wgl": 1, "competition": 2}
 SHADER_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 METRIC = "history ops linearizability-checked/sec (whole node)"

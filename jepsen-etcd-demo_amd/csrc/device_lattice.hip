@@ -333,6 +333,19 @@ __device__ __forceinline__ void t0_malformed(const A &a, int32_t key, uint32_t w
     }
 }
 
+// The lane index made opaque where it is used (workspace rows, lane masks).
+// For the workspace: a row array's lane column, its address formed where
+// used: with a plain m.W[k * 64 + lane] the compiler hoisted the 16 rows'
+// 64-bit addresses out of the walk's event loop and kept them for its whole
+// life -- 16 VGPR pairs, spilled to scratch in the 64-VGPR k_spec builds and
+// rewritten there at every walk's start (round 5's 29.8x traffic).  The empty
+// asm makes the lane index opaque, so each use site rebuilds one address and
+// the rows are immediate offsets from it.
+__device__ __forceinline__ uint32_t opq_lane(uint32_t lane) {
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+
 // Transfer masks of one event: vk[q] = op q's accept mask on lanes with bit
 // q (0 elsewhere and for q = p); sc[q] / sb[q] = op q's cap / shift.
 struct LaneMasks {
@@ -346,11 +359,16 @@ __device__ __forceinline__ void lane_masks(LaneMasks &m, uint32_t p, uint32_t k_
     for (int q = 0; q < 6; ++q) m.vk[q] = 0u;
 #pragma unroll
     for (int q = 0; q < 10; ++q) { m.sc[q] = 0u; m.sb[q] = 0u; }
+    // (lane bit q as a 0 / ~0 word from an opaque lane index, p's mask
+    // cleared in the scalar: written as `lane bit q && q != p ? sk : 0`, the
+    // six lane conditions became loop-invariant 64-bit scalar masks, hoisted
+    // out of the walk and spilled into VGPR lanes -- 12 v_readlane and 12
+    // scalar selects at every 7-10-pending :ok of the 64-VGPR k_spec builds)
+    const uint32_t ol = opq_lane(lane);
 #pragma unroll
     for (int q = 0; q < (N < 6 ? N : 6); ++q) {
-        const bool on = ((lane >> q) & 1u) && (uint32_t)q != p;
-        const uint32_t sk = __builtin_amdgcn_readlane(k_v, q);
-        m.vk[q] = on ? sk : 0u;
+        const uint32_t sk = (uint32_t)q != p ? (uint32_t)__builtin_amdgcn_readlane(k_v, q) : 0u;
+        m.vk[q] = sk & (uint32_t)__builtin_amdgcn_sbfe((int)ol, q, 1);
     }
 #pragma unroll
     for (int q = 0; q < (N < 10 ? N : 10); ++q) {
@@ -669,17 +687,6 @@ struct LatMem {
     uint32_t *W, *R, *I;
 };
 
-// The lane's column of a workspace row array, its address formed where it is
-// used: with a plain m.W[k * 64 + lane] the compiler hoisted the 16 rows'
-// 64-bit addresses out of the walk's event loop and kept them for its whole
-// life -- 16 VGPR pairs, spilled to scratch in the 64-VGPR k_spec builds and
-// rewritten there at every walk's start (round 5's 29.8x traffic).  The empty
-// asm makes the lane index opaque, so each use site rebuilds one address and
-// the rows are immediate offsets from it.
-__device__ __forceinline__ uint32_t opq_lane(uint32_t lane) {
-    asm volatile("" : "+v"(lane));
-    return lane;
-}
 
 template <int RL, bool TAG = false>
 __device__ __forceinline__ int ok_event_mem(const LatMem &m, uint32_t p, uint32_t n, uint32_t k_v,

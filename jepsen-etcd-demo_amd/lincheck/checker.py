@@ -430,30 +430,44 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
             ops[(inv, done)] = o
         return ops[(inv, done)]
 
+    states: Dict[int, Any] = {}  # state id -> (model state, its rendered map): a key has a few
+
+    def state_of(x: int):
+        x = int(x)
+        got = states.get(x)
+        if got is None:
+            if isinstance(packed.model, MultiRegister):
+                st = packed.model.of_map(packed.state_map(i, x))
+            else:
+                st = packed.model.of_state(None if x == N.LC_NIL else x)
+            got = states[x] = (st, st.render())
+        return got
+
     def state(x: int):
-        if isinstance(packed.model, MultiRegister):
-            return packed.model.of_map(packed.state_map(i, int(x)))
-        return packed.model.of_state(None if x == N.LC_NIL else int(x))
+        return state_of(x)[0]
+
+    def rendered(x: int) -> Dict:
+        return state_of(x)[1]
 
     op_row, prev_row, n_cfg, n_paths = (int(x) for x in w[:4])
     prev = _sub_op(packed, prev_row) if prev_row >= 0 else None
     at = 4
     configs = []
     for _ in range(n_cfg):
-        st = state(w[at]); at += 1
+        st = rendered(w[at]); at += 1
         lists = []
         for _ in range(2):
             n = int(w[at]); at += 1
             lists.append([op(int(w[at + 2 * j]), int(w[at + 2 * j + 1])) for j in range(n)])
             at += 2 * n
-        configs.append({"model": st.render(), "last-op": prev, "pending": lists[0], "linearized": lists[1]})
+        configs.append({"model": st, "last-op": prev, "pending": lists[0], "linearized": lists[1]})
     paths = []
     fail_op = _sub_op(packed, op_row) if op_row >= 0 else None
     for _ in range(n_paths):
-        path = [{"op": prev, "model": state(w[at]).render()}]
+        path = [{"op": prev, "model": rendered(w[at])}]
         n = int(w[at + 1]); at += 2
         for j in range(n):
-            path.append({"op": op(int(w[at]), int(w[at + 1])), "model": state(w[at + 2]).render()})
+            path.append({"op": op(int(w[at]), int(w[at + 1])), "model": rendered(w[at + 2])})
             at += 3
         f, val = fail_op["f"], fail_op.get("value")
         bad = state(w[at]).step(f, val); at += 1

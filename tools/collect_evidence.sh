@@ -9,7 +9,7 @@ O=${O:-gpurun_out/r$R}
 P=profiles
 T=$(printf "r%02d" $R)
 csv() { find "$O/prof/$1" -name "$2" 2>/dev/null | head -1; }
-for n in c2 c3s c4 c4wgl c2wgl; do
+for n in c2 c5 c3s c4 c4wgl c2wgl; do
   f=$(csv kt_$n '*kernel_stats.csv'); [ -n "$f" ] && cp "$f" $P/${T}_${n}_kernel_stats.csv
 done
 pmc() {  # name kernel workload keys budget algorithm

@@ -48,7 +48,8 @@ for part in $PARTS; do
     prof c2 400 --steps 50 --warmup 5 $PROF
     pmc c2 --steps 5 --warmup 1 $PROF ;;
   c5)
-    bench c5 300 --config C5 --steps 20 --warmup 3 ;;
+    bench c5 300 --config C5 --steps 20 --warmup 3
+    prof c5 300 --config C5 --steps 20 --warmup 3 $PROF ;;
   c3s)
     bench c3s 300 --config C3 --keys 12500 --steps 10 --warmup 2 --no-cpu
     prof c3s 300 --config C3 --keys 12500 --steps 10 --warmup 2 $PROF

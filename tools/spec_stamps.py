@@ -16,7 +16,8 @@ from lincheck.checker import Device, Packed  # noqa: E402
 keys = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 4         # segments per key (lc_opts.spec_segs)
 flags = int(sys.argv[3], 0) if len(sys.argv) > 3 else 0  # lc_opts.path_flags (e.g. 0x100: even cuts)
-h = H.synth(n_keys=keys, ops_per_key=1000, concurrency=10, seed=2)
+# SPEC_CFG=C5: the C5 shape (5 % anomalous keys, seed 5); default C2
+h = H.synth(**dict(H.CONFIGS[os.environ.get("SPEC_CFG", "C2")], n_keys=keys))
 pk = Packed(h)
 dev = Device(0, spec_segs=S, path_flags=flags)
 for _ in range(10):
@@ -105,3 +106,15 @@ for x in sorted(set(xr.tolist())):
     m = xr == x
     print("xcc %d: TOP cycles/event median %.0f p90 %.0f" % (x, np.median((tw / np.maximum(seg_len.ravel(), 1))[m]),
                                                             np.percentile((tw / np.maximum(seg_len.ravel(), 1))[m], 90)))
+
+# the launch's tail: the slowest blocks, segment by segment (C5: the invalid
+# keys' verifying runs)
+ends = end.max(1)
+print("slowest blocks: key, block end; per segment: TOP cycles / events, verify cycles / events / outcome")
+for bi in np.argsort(-ends)[:6]:
+    segs = []
+    for w in range(S):
+        vv = int(b[bi, w, 7]) if w else 0
+        segs.append("%d/%d v%d/%d/%d" % (top[bi, w], seg_len[bi, w], ver[bi, w] if w else 0, vv & 0xFFFFFFFF,
+                                          vv >> 32))
+    print("  key %6d end %8d  %s" % (keyid[bi], ends[bi], "  ".join(segs)))
