@@ -2087,7 +2087,16 @@ constexpr uint32_t SPEC_SAVE_WORDS = (T0_RMEM + 2) * 64;
 #define LC_SPEC_NCK 2
 #endif
 constexpr uint32_t SPEC_NCK = LC_SPEC_NCK;
+// With three (a diagnostic build): an early one at ck1 / 4 before them
+// (LC_SPEC_CK_EARLY), where most pairs of runs have already met; one that
+// has not goes on to ck1 and ck2 as with two.  Measured in round 6
+// (profiles/r06_segments_seeds.txt): (8, 32, 120) no faster than (32, 120) on
+// C2 or C5.
+#ifndef LC_SPEC_CK_EARLY
+#define LC_SPEC_CK_EARLY 1
+#endif
 __device__ __forceinline__ uint32_t spec_ck_target(uint32_t i, uint32_t ck1, uint32_t ck2) {
+    if (LC_SPEC_CK_EARLY && SPEC_NCK == 3) return i == 0 ? max(ck1 / 4u, 4u) : i == 1 ? ck1 : ck2;
     return i == 0 ? ck1 : i + 1 >= SPEC_NCK ? ck2 : ck1 + (ck2 - ck1) * i / (SPEC_NCK - 1);
 }
 template <int MODE, int NWS, class EvT, bool EX = false>

@@ -18,6 +18,8 @@ from lincheck.checker import Device, Packed, PinnedRecords  # noqa: E402
 cfg, keys, ops = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 shape = dict(C2=dict(concurrency=10, seed=2), C5=dict(concurrency=10, anomaly_rate=0.05, seed=5),
              C3=dict(concurrency=10, seed=3))[cfg]
+if os.environ.get("SEED"):  # another instance of the same shape
+    shape = dict(shape, seed=int(os.environ["SEED"]))
 pk = Packed(H.synth(n_keys=keys, ops_per_key=ops, **shape))
 K = pk.n_keys
 ref = None
