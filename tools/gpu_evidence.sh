@@ -68,6 +68,8 @@ for part in $PARTS; do
     pmc c2wgl --config C2 --algorithm wgl --steps 3 --warmup 1 $PROF ;;
   c4comp)
     bench c4_comp 400 --config C4 --budget 65536 --algorithm competition --steps 3 --warmup 1 --no-resident --no-cpu ;;
+  c1)
+    bench c1 200 --config C1 --steps 20 --warmup 3 ;;
   c5jepsen)
     bench c5_jepsen 400 --config C5 --jepsen --steps 10 --warmup 2 ;;
   c4wgl24)
