@@ -520,39 +520,57 @@ __device__ bool wgl_key(const WglArgs &a, int32_t key, uint32_t ticket, char *sl
             } else {
                 p0 = h0 & mask;
                 p1 = h1 & mask;
-                if (pend && !pend_known && lane < WGL_PEND_LANES) {
-                    // (the stamp words of the first WGL_PEND_LANES entries
-                    // from its home: all 64 read 2 KB of lines per probe
-                    // round, 5x the walk's algorithmic bytes, for a slot that
-                    // is nearly always among the first few)
-                    const uint2 ps = *((const uint2 *)(tab + 2 * (size_t)((ph + lane) & mask) + 1) + 1);
-                    pfree = ((uint64_t)ps.x | (uint64_t)ps.y << 32) != gen;
-                }
+                // (the stamp words of the first WGL_PEND_LANES entries from
+                // its home: all 64 read 2 KB of lines per probe round, 5x the
+                // walk's algorithmic bytes, for a slot that is nearly always
+                // among the first few).  Loaded here and compared after the
+                // probe loop, so the load shares the probes' wait: compared
+                // at once, the compiler waited for it before the first probe
+                // -- a serial round trip of its own at every probe round
+                // after a backtrack (round 6).
+                // (every lane loads, with no branch around it: a slot when the
+                // pair's slot is wanted, else entry 0's stamp, a line that
+                // stays cached -- a load under a lane condition drew the
+                // compiler's copies, and their wait, into the branch)
+                const bool want_ps = pend && !pend_known && lane < WGL_PEND_LANES;
+                const size_t ps_at = pend && !pend_known ? (size_t)((ph + (lane & (WGL_PEND_LANES - 1u))) & mask) : 0u;
+                const uint2 ps = *((const uint2 *)(tab + 2 * ps_at + 1) + 1);
                 // (one entry per round trip: reading two, p and p + 1, was
                 // measured in round 5 -- C2 8.21 -> 8.54 ms, C4 at 2^16 204 ->
                 // 208 ms, at 2^20 3,255 -> 3,187 ms; not kept)
                 for (uint32_t probe = 0; probe <= mask; ++probe) {
                     if (!ballot((act0 | act1) != 0u)) break;
                     WP_ADD(6, 1);
-                    uint4 e00 = {}, e01 = {}, e10 = {}, e11 = {};
-                    if (act0) { e00 = tab[2 * (size_t)p0]; e01 = tab[2 * (size_t)p0 + 1]; }
-                    if (act1) { e10 = tab[2 * (size_t)p1]; e11 = tab[2 * (size_t)p1 + 1]; }
-                    const bool own0 = ((uint64_t)e01.z | (uint64_t)e01.w << 32) == gen;
-                    const bool own1 = ((uint64_t)e11.z | (uint64_t)e11.w << 32) == gen;
-                    const bool eq0 = own0 && e01.x == kR0 && e01.y == s20 &&
-                                     ((uint64_t)e00.x | (uint64_t)e00.y << 32) == k0lo &&
-                                     ((uint64_t)e00.z | (uint64_t)e00.w << 32) == k0hi;
-                    const bool eq1 = own1 && e11.x == kR1 && e11.y == s21 &&
-                                     ((uint64_t)e10.x | (uint64_t)e10.y << 32) == k1lo &&
-                                     ((uint64_t)e10.z | (uint64_t)e10.w << 32) == k1hi;
-                    hit0 |= act0 & (eq0 ? 1u : 0u);
-                    hit1 |= act1 & (eq1 ? 1u : 0u);
-                    act0 &= (own0 && !eq0) ? 1u : 0u;
-                    act1 &= (own1 && !eq1) ? 1u : 0u;
+                    // Both candidates' entries loaded without a branch and
+                    // every field of both compared with bitwise ANDs, so the
+                    // loads go out together and share one wait.  Loaded under
+                    // `if (act0)` / `if (act1)`, or compared with a
+                    // short-circuit &&, the compiler waited for the first
+                    // entry (or for its stamp word alone) before issuing the
+                    // rest -- dependent HBM round trips within one probe
+                    // iteration on the wide walks (round 6).  A lane whose
+                    // probe is done reads entry 0 (one line for all such
+                    // lanes of a load, instead of one line each).
+                    const size_t q0 = act0 ? (size_t)p0 : 0u, q1 = act1 ? (size_t)p1 : 0u;
+                    const uint4 e00 = tab[2 * q0], e01 = tab[2 * q0 + 1];
+                    uint4 e10 = {}, e11 = {};
+                    if constexpr (WIDE) { e10 = tab[2 * q1]; e11 = tab[2 * q1 + 1]; }
+                    const uint32_t own0 = (uint32_t)(e01.z == (uint32_t)gen) & (uint32_t)(e01.w == (uint32_t)(gen >> 32));
+                    const uint32_t own1 = (uint32_t)(e11.z == (uint32_t)gen) & (uint32_t)(e11.w == (uint32_t)(gen >> 32));
+                    const uint32_t eq0 = own0 & (uint32_t)(e01.x == kR0) & (uint32_t)(e01.y == s20) &
+                                         (uint32_t)(e00.x == (uint32_t)k0lo) & (uint32_t)(e00.y == (uint32_t)(k0lo >> 32)) &
+                                         (uint32_t)(e00.z == (uint32_t)k0hi) & (uint32_t)(e00.w == (uint32_t)(k0hi >> 32));
+                    const uint32_t eq1 = own1 & (uint32_t)(e11.x == kR1) & (uint32_t)(e11.y == s21) &
+                                         (uint32_t)(e10.x == (uint32_t)k1lo) & (uint32_t)(e10.y == (uint32_t)(k1lo >> 32)) &
+                                         (uint32_t)(e10.z == (uint32_t)k1hi) & (uint32_t)(e10.w == (uint32_t)(k1hi >> 32));
+                    hit0 |= act0 & eq0;
+                    hit1 |= act1 & eq1;
+                    act0 &= own0 & (eq0 ^ 1u);
+                    act1 &= own1 & (eq1 ^ 1u);
                     p0 = (p0 + act0) & mask;
                     p1 = (p1 + act1) & mask;
                 }
-
+                pfree = want_ps && ((uint64_t)ps.x | (uint64_t)ps.y << 32) != gen;
             }
             lm = (lm & 0xFu) | (ok0 && !hit0 ? 1u << LM_C : 0u) | (ok1 && !hit1 ? 2u << LM_C : 0u);
             (void)act0;
