@@ -2099,12 +2099,50 @@ __device__ __forceinline__ uint32_t spec_ck_target(uint32_t i, uint32_t ck1, uin
     if (LC_SPEC_CK_EARLY && SPEC_NCK == 3) return i == 0 ? max(ck1 / 4u, 4u) : i == 1 ? ck1 : ck2;
     return i == 0 ? ck1 : i + 1 >= SPEC_NCK ? ck2 : ck1 + (ck2 - ck1) * i / (SPEC_NCK - 1);
 }
+// Flags between the waves of one k_spec workgroup (LDS, workgroup scope).  A
+// wave publishes after its stores (a release fence for the whole wave, then
+// lane 0's store); a waiter polls with an acquire load and sleeps between
+// polls, a fixed trip count over a uniform value (the queue loops' rule
+// below).  The wait is bounded: a waiter that gives up takes the exact path
+// (the key is searched unsegmented), so a timeout costs time, never a result.
+constexpr uint32_t SPEC_WAIT_MAX = 1u << 22;
+__device__ __forceinline__ void spec_publish(int32_t *f, int32_t v = 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane_id() == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int32_t spec_load(const int32_t *f) {
+    return uni(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ bool spec_wait(const int32_t *f) {
+#pragma unroll 1
+    for (uint32_t it = 0; it < SPEC_WAIT_MAX; ++it) {
+        if (spec_load(f) != 0) return true;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+// A verifying run's checkpoint event i (relative to nothing: the event
+// index), read while the TOP run it compares with may still be walking
+// (LC_SPEC_OVERLAP): waits until that run has recorded it or has ended
+// without it (-1: no such checkpoint); -1 on a timeout too.
+__device__ __forceinline__ int32_t spec_ck_event(const int32_t *ck_e, uint32_t i, const int32_t *top_done) {
+    if (!top_done) return uni(ck_e[i]);
+#pragma unroll 1
+    for (uint32_t it = 0; it < SPEC_WAIT_MAX; ++it) {
+        const int32_t e = spec_load(ck_e + i);
+        if (e >= 0) return e;
+        if (spec_load(top_done) != 0) return spec_load(ck_e + i);
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return -1;
+}
+
 template <int MODE, int NWS, class EvT, bool EX = false>
 __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t ntr, uint32_t b,
                                          uint32_t e_end, SpecState &st, uint32_t *ws, uint32_t *lds_ws,
                                          int32_t *lds_busy, uint32_t (*ck_w)[64], int32_t *ck_e, uint32_t ck1,
                                          uint32_t ck2, uint32_t &fev_out, bool prio = false,
-                                         uint32_t *save = nullptr) {
+                                         uint32_t *save = nullptr, const int32_t *top_done = nullptr) {
     constexpr int RM = T0_RSMALL;
     const uint32_t lane = lane_id();
     LatMem m{ws, ws + T0_RMEM * 64, ws + 2 * T0_RMEM * 64};
@@ -2156,7 +2194,11 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
     };
     // next checkpoint (relative event; ~0u: none)
     uint32_t ck_i = 0;
-    uint32_t ck_at = MODE == 0 ? ck1 : (uni(ck_e[0]) >= 0 ? (uint32_t)uni(ck_e[0]) - b : ~0u);
+    uint32_t ck_at = ck1;
+    if constexpr (MODE != 0) {
+        const int32_t e0 = spec_ck_event(ck_e, 0, top_done);
+        ck_at = e0 >= 0 ? (uint32_t)e0 - b : ~0u;
+    }
     uint32_t W0 = st.W0;
     bool dirty = true;
     // One lane-phase event (<= 6 pending); true: an :invoke with 6 pending,
@@ -2225,7 +2267,7 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
             if (CK && !r && e >= ck_at) {  // a checkpoint (a lane-phase :ok: the set is canonical)
                 if constexpr (MODE == 0) {
                     ck_w[ck_i][lane] = W0;
-                    if (lane == 0) ck_e[ck_i] = (int32_t)(b + e);
+                    spec_publish(&ck_e[ck_i], (int32_t)(b + e));  // (after the set: a verifier may be waiting)
                     ++ck_i;
                     ck_at = ck_i < SPEC_NCK ? max(spec_ck_target(ck_i, ck1, ck2), e + 1u) : ~0u;
                 } else {
@@ -2233,7 +2275,7 @@ __device__ __forceinline__ int spec_walk(EvT evp, const uint32_t *trp, uint32_t 
                         status = 4;
                     } else {
                         ++ck_i;
-                        const int32_t nx = ck_i < SPEC_NCK ? uni(ck_e[ck_i]) : -1;
+                        const int32_t nx = ck_i < SPEC_NCK ? spec_ck_event(ck_e, ck_i, top_done) : -1;
                         ck_at = nx >= 0 ? (uint32_t)nx - b : ~0u;
                         if (ck_i == SPEC_NCK) status = 5;
                     }
@@ -2437,6 +2479,7 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
     __shared__ int32_t s_net[S];          // cut search: pending-count change over each part
     __shared__ int32_t s_cand[S], s_ncand[S];  // each target's cut (-1: none) and ops pending there
     __shared__ int32_t s_next[2];         // the block's queues: TOP walks, verifying runs
+    __shared__ int32_t s_prdy[S], s_done[S];  // LC_SPEC_OVERLAP: s_pend / s_top -3 of s out; TOP run of s ended
     __shared__ uint32_t s_vx[W][2];       // self-validation: each wave's part, XOR of its slots' one-hots
     constexpr int NWS = spec_lds_ws<W>();
     __shared__ uint32_t s_ws[NWS ? NWS * 3 * T0_RMEM * 64 : 1];  // 9-10-pending workspaces (12 KB each)
@@ -2619,8 +2662,120 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
             for (uint32_t q = 0; q < SPEC_NCK; ++q) s_ck_e[s][q] = -1;
             s_top[s] = -1;
         }
+        for (uint32_t s = 0; s < (uint32_t)S; ++s) {
+            s_prdy[s] = 0;
+            s_done[s] = 0;
+            s_ver[s] = 0;
+            s_vfev[s] = -1;
+        }
     }
     __syncthreads();
+#ifndef LC_SPEC_OVERLAP
+#define LC_SPEC_OVERLAP 1
+#endif
+    if constexpr (LC_SPEC_OVERLAP && S == W) {
+        // 1 + 2, overlapped (LC_SPEC_OVERLAP): wave w walks segment w from
+        // TOP, then at once verifies the next kept segment from the set its
+        // own walk ended with -- without waiting at a barrier for every TOP
+        // walk of the block.  The verifying run compares with that segment's
+        // TOP run at its checkpoints, which that run publishes as it passes
+        // them (spec_ck_event waits for one not reached yet), and with its end
+        // set once it has ended.  A block then takes about its slowest TOP
+        // walk, not its slowest TOP walk plus its slowest verifying run.
+        if (!plain) {
+            const uint32_t s = wv;
+            const bool kept = s < eff && uni(s_cut[s]) >= 0;
+            int32_t top_s = -1;
+            if (kept) {
+                const int32_t cut_i = uni(s_cut[s]);
+                const uint32_t cut = (uint32_t)cut_i, end = (uint32_t)uni(s_segend[s]);
+                const uint32_t n0 = s == 0 ? 0u : (uint32_t)uni(s_ncand[s]);
+                SPEC_STAMP(s, 1, __builtin_amdgcn_s_memtime())
+                SPEC_STAMP(s, 6, ((unsigned long long)end << 32) | cut)
+                SPEC_STAMP(s, 8, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                     ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32))
+                SPEC_STAMP(s, 9, (unsigned long long)key)
+                SpecState st{};
+                uint32_t words = 0, np = 0;
+                if (s == 0) {
+                    st.W0 = lane == 0 ? 1u << KA.init_state : 0u;
+                } else {
+                    words = spec_pending(evp, cut, n0, np);
+                    spec_setup(st, words, np, trp, ntr);
+                    st.W0 = lane < (1u << np) ? topmask : 0u;
+                }
+                if (lane < 6) s_pend[s][lane] = words;
+                if (lane == 6) s_pend[s][6] = np;
+                const bool lost = s != 0 && np != n0;
+                if (lost && lane == 0) s_top[s] = -3;
+                spec_publish(&s_prdy[s]);
+                uint32_t fev = 0;
+                uint32_t *const sv = EX ? KA.spec_fin + ((size_t)blk * S + s) * 2 * SPEC_SAVE_WORDS : nullptr;
+                const int r = lost ? 6
+                                   : spec_walk<0, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
+                                                                       s_ck[s], s_ck_e[s], KA.spec_ck1, KA.spec_ck2,
+                                                                       fev, !(KA.flags & T0_SPEC_NOPRIO), sv);
+                s_end[s][lane] = st.W0;
+                uint64_t map = 0;
+                for (uint32_t q = 0; q < 6; ++q) {
+                    const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, q);
+                    if ((st.live >> q) & 1u) map |= (uint64_t)(0x80u | sl) << (8 * q);
+                }
+                SPEC_STAMP(s, 2, __builtin_amdgcn_s_memtime())
+                top_s = r == 1 ? (int32_t)fev : r == 3 ? -2 : r == 6 ? -3 : -1;
+                if (lane == 0) {
+                    s_map[s] = map;
+                    s_top[s] = top_s;
+                }
+                spec_publish(&s_done[s]);
+            }
+            // the next kept segment (its predecessor is this one)
+            uint32_t v = s + 1;
+            while (v < eff && uni(s_cut[v]) < 0) ++v;
+            if (kept && top_s == -1 && v < eff) {
+                SPEC_STAMP(v, 3, __builtin_amdgcn_s_memtime())
+                int32_t ver = 3, vfev = -1;  // (a wait that gives up: the key goes unsegmented)
+                uint32_t fev = 0;
+                if (spec_wait(&s_prdy[v]) && spec_load(&s_top[v]) != -3) {
+                    const uint32_t cut = (uint32_t)uni(s_cut[v]), end = (uint32_t)uni(s_segend[v]);
+                    const uint32_t np = uni(s_pend[v][6]);
+                    SpecState st{};
+                    spec_setup(st, lane < 6 ? s_pend[v][lane] : 0u, np, trp, ntr);
+                    // this walk's end set, relabelled from its op indices to v's
+                    const uint64_t map = uni(s_map[s]);
+                    uint32_t src = 0;
+                    for (uint32_t j = 0; j < np; ++j) {
+                        const uint32_t sl = __builtin_amdgcn_readlane(st.slot_v, j);
+                        uint32_t at = 31;
+                        for (uint32_t q = 0; q < 6; ++q)
+                            if (((map >> (8 * q)) & 0xFFu) == (0x80u | sl)) at = q;
+                        src |= ((lane >> j) & 1u) << at;
+                    }
+                    const uint32_t E = (uint32_t)__shfl((int)s_end[s][lane], (int)(src & 63u));
+                    st.W0 = lane < (1u << np) ? E : 0u;
+                    uint32_t *const sv =
+                        EX ? KA.spec_fin + ((size_t)blk * S + v) * 2 * SPEC_SAVE_WORDS + SPEC_SAVE_WORDS : nullptr;
+                    const int r = spec_walk<1, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
+                                                                    s_ck[v], s_ck_e[v], 0, 0, fev, false, sv,
+                                                                    &s_done[v]);
+                    bool last = true;
+                    for (uint32_t q = v + 1; q < eff; ++q) last = last && uni(s_cut[q]) < 0;
+                    if (r == 4) ver = 1;                        // met the TOP run
+                    else if (r == 1) { ver = 2; vfev = (int32_t)fev; }  // died before meeting it
+                    else if (r == 3) ver = 6;                   // does not fit
+                    else if (r == 5) ver = 3;                   // never met
+                    else if (last) ver = 5;                     // the last segment, searched exactly to its end
+                    else if (spec_wait(&s_done[v])) ver = (st.n <= 6 && !__any(st.W0 != s_end[v][lane])) ? 1 : 3;
+                }
+                SPEC_STAMP(v, 7, ((unsigned long long)ver << 32) | (fev - (uint32_t)uni(s_cut[v])))
+                SPEC_STAMP(v, 4, __builtin_amdgcn_s_memtime())
+                if (lane == 0) {
+                    s_ver[v] = ver;
+                    s_vfev[v] = vfev;
+                }
+            }
+        }
+    } else {
     // 1. every segment from TOP (segment 0 exactly), from the block's queue.
     // INVARIANT (both queue loops below): a fixed trip count (S, S - 1) and a
     // queue index made wave-uniform by uni() before any branch on it.  With
@@ -2733,6 +2888,7 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
             if (lane == 0) { s_ver[s] = ver; s_vfev[s] = vfev; }
         }
     }
+    }  // LC_SPEC_OVERLAP
     __syncthreads();
     if (wv == 0) {
         for (uint32_t s = 0; s < (uint32_t)S; ++s) { SPEC_STAMP(s, 5, __builtin_amdgcn_s_memtime()) }
