@@ -2501,6 +2501,14 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
         }
         return;  // the whole block: no barrier below is reached by half of it
     }
+    // The block's set-up -- staging, validation, the cuts -- at a TOP walk's
+    // first-quarter issue priority (LC_SPEC_CUT_PRIO=1, A/B): measured in
+    // round 6 at -0.3 % on C2 / C5 and other seeds (tools/gpu_r6n.sh,
+    // profiles/r06_segments_seeds.txt), within noise; not the default.
+#ifndef LC_SPEC_CUT_PRIO
+#define LC_SPEC_CUT_PRIO 0
+#endif
+    if (LC_SPEC_CUT_PRIO && !(KA.flags & T0_SPEC_NOPRIO)) __builtin_amdgcn_s_setprio(3);
     // (scalar: as a VGPR it was the 64-VGPR builds' last spill to scratch)
     const int32_t key = (int32_t)uni((uint32_t)KA.order[blk]);
     uint32_t *ws = KA.lat_ws + ((size_t)blk * W + wv) * (3 * T0_RMEM * 64);
@@ -2889,6 +2897,7 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
         }
     }
     }  // LC_SPEC_OVERLAP
+    if (LC_SPEC_CUT_PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     if (wv == 0) {
         for (uint32_t s = 0; s < (uint32_t)S; ++s) { SPEC_STAMP(s, 5, __builtin_amdgcn_s_memtime()) }
