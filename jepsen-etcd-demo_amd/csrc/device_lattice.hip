@@ -2763,9 +2763,16 @@ __global__ __launch_bounds__(64 * W, (W == 2 ? LC_SPEC2_WAVES : W == 8 ? LC_SPEC
                     st.W0 = lane < (1u << np) ? E : 0u;
                     uint32_t *const sv =
                         EX ? KA.spec_fin + ((size_t)blk * S + v) * 2 * SPEC_SAVE_WORDS + SPEC_SAVE_WORDS : nullptr;
+// (issue priority of the verifying runs: 0; 2 and 3 measured slower on
+// C2 and most seeds in round 6, profiles/r06_segments_seeds.txt)
+#ifndef LC_SPEC_VER_PRIO
+#define LC_SPEC_VER_PRIO 0
+#endif
+                    if (LC_SPEC_VER_PRIO) __builtin_amdgcn_s_setprio(LC_SPEC_VER_PRIO);
                     const int r = spec_walk<1, NWS, EvK, EX>(evp, trp, ntr, cut, end, st, ws, s_ws, s_ws_busy,
                                                                     s_ck[v], s_ck_e[v], 0, 0, fev, false, sv,
                                                                     &s_done[v]);
+                    if (LC_SPEC_VER_PRIO) __builtin_amdgcn_s_setprio(0);
                     bool last = true;
                     for (uint32_t q = v + 1; q < eff; ++q) last = last && uni(s_cut[q]) < 0;
                     if (r == 4) ver = 1;                        // met the TOP run
