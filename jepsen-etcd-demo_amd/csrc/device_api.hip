@@ -1355,10 +1355,13 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     // saving its set at its end or death, the true run's written as the
     // key's final configs (k_spec<.., EX>).
     const bool exact_spec = !a.peak && a.final_cfg && a.n_final && o.max_configs >= 16ull * 64 * 32;
-    // Verdicts only: 8 per key while 8 x keys waves are resident at the
-    // 8-wave build's 8 per SIMD (device_search.hpp LC_SPEC8_WAVES).  Not for
-    // the exact segments: on C5 their launch went 0.289 -> 0.352 ms with it.
-    if (LC_SPEC8_WAVES >= 8 && fast && K > 0 && K * 8 <= (int64_t)c->cu_count * 4 * 8) segs = 8;
+    // 8 per key while 8 x keys waves are resident at the 8-wave build's 8
+    // per SIMD (device_search.hpp LC_SPEC8_WAVES).  The exact segments too
+    // since round 6 (spill-free builds, overlapped verifying runs;
+    // tools/ex_segs_ab.py, records equal): C2 0.2843 -> 0.2530 ms, a C5-shaped
+    // batch of another seed 0.2822 -> 0.2627, BASELINE's C5 0.2717 -> 0.2755.
+    // (Round 5, before both: C5 0.289 -> 0.352 ms with 8.)
+    if (LC_SPEC8_WAVES >= 8 && (fast || exact_spec) && K > 0 && K * 8 <= (int64_t)c->cu_count * 4 * 8) segs = 8;
     if (o.spec_segs) segs = o.spec_segs;
     if (exact_spec && !fast) segs = segs >= 8 ? 8 : segs >= 4 ? 4 : 2;  // the exact builds
     const int waves = segs;
