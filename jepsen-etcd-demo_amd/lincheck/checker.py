@@ -376,11 +376,7 @@ def merge_valid(vals: Sequence[Any]) -> Any:
 def _sub_op(packed: Packed, row: int) -> Dict:
     """Row as it appears in the key's sub-history (independent/subhistory
     unwraps the tuple value)."""
-    op = packed.hist.op(row)
-    v = op.get("value")
-    if getattr(v, "_lc_tuple", False):
-        op["value"] = v[1]
-    return op
+    return packed.hist.sub_op(row)
 
 
 def _report(packed: Packed, i: int, res: "KeyResults", analyzer: str = "linear") -> np.ndarray:

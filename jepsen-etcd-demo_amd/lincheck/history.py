@@ -257,6 +257,27 @@ class History:
         op["index"] = int(self.index[i]) if self.index[i] >= 0 else i
         return op
 
+    def sub_op(self, i: int) -> dict:
+        """Row i as it appears in its key's sub-history (independent/subhistory
+        unwraps the tuple value): op() without building the tuple."""
+        i = int(i)
+        f = int(self.f[i])
+        fn = F_NAMES.get(f, self.other_f.get(i, "nemesis" if f == N.LC_F_OTHER else f))
+        if f == N.LC_F_CAS:
+            a, b = int(self.v0[i]), int(self.v1[i])
+            val = [None if a == NIL else a, None if b == NIL else b]
+        elif f in (N.LC_F_OTHER, N.LC_F_ACQUIRE, N.LC_F_RELEASE):
+            val = None
+        elif f == N.LC_F_TXN:
+            val = self.txn(i)
+        else:
+            a = int(self.v0[i])
+            val = None if a == NIL else a
+        proc = int(self.process[i])
+        ix = int(self.index[i])
+        return {"type": TYPE_NAMES[int(self.type[i])], "f": fn, "value": val,
+                "process": "nemesis" if proc == N.LC_NO_PROCESS else proc, "index": ix if ix >= 0 else i}
+
     def txn(self, i: int):
         """Row i's :txn micro-ops as [f, register, value] lists (None: nil)."""
         if self.mop_off is None or self.mop_off[i + 1] == self.mop_off[i]:
