@@ -2060,10 +2060,14 @@ constexpr int spec_lds_ws() { return S <= 2 ? LC_SPEC2_NWS : S <= 3 ? 1 : S <= 6
 // and end running alone on their SIMDs.  A walk in its first quarter runs at
 // priority 3, its last quarter at 0: the four walks a SIMD holds advance
 // together and keep it busy to the end.
+#ifndef LC_SPEC_PRIO_TOP
+#define LC_SPEC_PRIO_TOP 3
+#endif
 __device__ __forceinline__ void spec_prio(uint32_t quarter) {
-    if (quarter == 0) __builtin_amdgcn_s_setprio(3);
-    else if (quarter == 1) __builtin_amdgcn_s_setprio(2);
-    else if (quarter == 2) __builtin_amdgcn_s_setprio(1);
+    const int lv = LC_SPEC_PRIO_TOP - (int)quarter;
+    if (lv >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (lv == 2) __builtin_amdgcn_s_setprio(2);
+    else if (lv == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 }
 
