@@ -386,9 +386,9 @@ def _report(packed: Packed, i: int, res: "KeyResults", analyzer: str = "linear")
     fin = np.ascontiguousarray(res.final[i], dtype=np.uint64) if len(res.final) else np.zeros((1, 2), np.uint64)
     nf = int(res.n_final[i]) if len(res.n_final) else 0
     fn = N.lib().lc_report_wgl if analyzer == "wgl" else N.lib().lc_report
-    cap = 256
+    cap = 4096  # (C5's counterexamples: a few hundred words; a second call only past this)
     while True:
-        buf = np.zeros(cap, np.int64)
+        buf = np.empty(cap, np.int64)
         n = N.check(fn(packed.handle, i, int(res.valid[i]), int(res.fail_event[i]),
                        N.ptr(fin, C.c_uint64), nf, TRUNCATE, N.ptr(buf, C.c_int64), cap))
         if n <= cap:
@@ -410,7 +410,7 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
         # nothing to render: the device keeps final configs of invalid keys
         # only (as gpu_checker.clj, which skips lc_report here too)
         return {"analyzer": analyzer, "configs": [], "final-paths": [], "valid?": True}
-    w = _report(packed, i, res, analyzer)
+    w = _report(packed, i, res, analyzer).tolist()  # Python ints: no numpy scalar per word
     ops: Dict[tuple, Dict] = {}
 
     def op(inv: int, done: int) -> Dict:
@@ -429,7 +429,6 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
     states: Dict[int, Any] = {}  # state id -> (model state, its rendered map): a key has a few
 
     def state_of(x: int):
-        x = int(x)
         got = states.get(x)
         if got is None:
             if isinstance(packed.model, MultiRegister):
@@ -445,7 +444,7 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
     def rendered(x: int) -> Dict:
         return state_of(x)[1]
 
-    op_row, prev_row, n_cfg, n_paths = (int(x) for x in w[:4])
+    op_row, prev_row, n_cfg, n_paths = w[:4]
     prev = _sub_op(packed, prev_row) if prev_row >= 0 else None
     at = 4
     configs = []
@@ -453,17 +452,17 @@ def _render_key(packed: Packed, i: int, res: KeyResults, sub_rows: Optional[np.n
         st = rendered(w[at]); at += 1
         lists = []
         for _ in range(2):
-            n = int(w[at]); at += 1
-            lists.append([op(int(w[at + 2 * j]), int(w[at + 2 * j + 1])) for j in range(n)])
+            n = w[at]; at += 1
+            lists.append([op(w[at + 2 * j], w[at + 2 * j + 1]) for j in range(n)])
             at += 2 * n
         configs.append({"model": st, "last-op": prev, "pending": lists[0], "linearized": lists[1]})
     paths = []
     fail_op = _sub_op(packed, op_row) if op_row >= 0 else None
     for _ in range(n_paths):
         path = [{"op": prev, "model": rendered(w[at])}]
-        n = int(w[at + 1]); at += 2
+        n = w[at + 1]; at += 2
         for j in range(n):
-            path.append({"op": op(int(w[at]), int(w[at + 1])), "model": rendered(w[at + 2])})
+            path.append({"op": op(w[at], w[at + 1]), "model": rendered(w[at + 2])})
             at += 3
         f, val = fail_op["f"], fail_op.get("value")
         bad = state(w[at]).step(f, val); at += 1
