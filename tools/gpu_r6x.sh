@@ -1,0 +1,12 @@
+# Round 6: T3L cooperation -- handoff variants on the layered tests and C4 at
+# 2^16: cf3 (same XCD, device-scope invalidate, no L2 write-back), the
+# default (same XCD, agent fences), and no cooperation.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r6x; mkdir -p $O
+L=$PWD/jepsen-etcd-demo_amd/lincheck
+LINCHECK_LIB_OVERRIDE=$L/liblincheck_cf3.so timeout -k 10 300 python -u -m pytest tests/test_gpu_layers.py -v --timeout 120 --timeout-method thread > $O/layers_cf3.log 2>&1; echo "cf3: $(tail -1 $O/layers_cf3.log)"
+for v in cf3 nocoop cf3; do
+  LINCHECK_LIB_OVERRIDE=$L/liblincheck_$v.so timeout -k 10 200 python -u bench.py --config C4 --budget 65536 --steps 3 --warmup 1 --no-cpu --no-resident --no-probes --no-c3 > $O/c4_$v.json 2> $O/c4_$v.err || { tail -5 $O/c4_$v.err; exit 1; }
+  python -c "import json,sys; d=json.loads(open('$O/c4_$v.json').read().strip().splitlines()[-1]); print('$v', 'ms', round(d['ms_per_step'],3), 't3', d.get('tier3_ms'), d['verdicts'])"
+done

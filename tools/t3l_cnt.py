@@ -15,7 +15,10 @@ dev = Device(0, budget=budget)
 for it in range(2):
     r = dev.check(p)
     print(f"iter {it}: kernel {r.stats['kernel_ms']:.2f} ms t3 {r.stats['tier3_ms']:.2f} ms", flush=True)
-q = r.final.reshape(len(p.keys), -1)[:, :10].astype(np.int64)
+qa = r.final.reshape(len(p.keys), -1).astype(np.int64)
+q = qa[:, :10]
+# whole-table steps: insert cycles, scan cycles, I passes, S' passes, pairs + S entries per I pass (thread 0)
+ws = qa[:, 10:16]
 names = ["between", "okhead", "inserts", "scans", "fast", "slowcyc", "oks", "entries", "redo|slow<<20", "total"]
 order = np.argsort(-q[:, 9])
 for i in order[:6]:
@@ -23,5 +26,9 @@ for i in order[:6]:
     d["slow"] = d["redo|slow<<20"] >> 20
     d["redo"] = d["redo|slow<<20"] & 0xFFFFF
     print(i, d, "cyc/step", d["total"] // max(1, d["fast"] + d["slow"]))
+    w = ws[i]
+    print("   whole-table: inserts %d cyc, scans %d cyc (%.1f%% / %.1f%% of the key), I passes %d, S' passes %d, "
+          "inputs per I pass %.0f" % (w[0], w[1], 100 * w[0] / d["total"], 100 * w[1] / d["total"], w[2], w[3],
+                                      w[5] / max(1, w[2])))
 tot = q.sum(0)
 print("sums", dict(zip(names, tot.tolist())))
