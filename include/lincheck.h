@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 12
+#define LC_ABI_VERSION 11
 
 /* ---- error codes --------------------------------------------------------- */
 #define LC_OK            0
@@ -452,8 +452,6 @@ typedef struct lc_stats {
     uint64_t wgl_spilled;     /* of those, keys searched again with a table the
                                  budget fits (they outgrew the shared tables)   */
     uint64_t wgl_steps;       /* WGL walk steps (linearizations + backtracks)   */
-    uint64_t t3_coop_passes;  /* layered HBM tier: whole-table passes run by a
-                                 cooperating (helping) workgroup (ABI 12)       */
 } lc_stats;
 
 /* lc_stats.t0_path */

@@ -330,8 +330,6 @@ struct Dev {
         size_t bytes = 0;
         int slots = 0;
         lcd::LayWs w{};
-        char *coop = nullptr;  // the cooperating blocks' board
-        size_t coop_bytes = 0;
     } lws;
     // knossos.wgl workspaces (device_wgl.hip): [0] tables sized to share at
     // most a share of the free HBM (WGL_SHARE_MAX), [1] tables the budget
@@ -350,7 +348,7 @@ struct Dev {
         dfree(lists); dfree(ctl); dfree(valid); dfree(fail_event);
         if (hctl) (void)hipHostFree(hctl);
         dfree(cause); dfree(peak); dfree(final_cfg); dfree(n_final);
-        dfree(ws[0].base); dfree(ws[1].base); dfree(lws.base); dfree(lws.coop); dfree(dargs); dfree(send); dfree(node);
+        dfree(ws[0].base); dfree(ws[1].base); dfree(lws.base); dfree(dargs); dfree(send); dfree(node);
         dfree(wws[0].base); dfree(wws[1].base); dfree(analyzer);
         dfree(seg_cnt); dfree(seg_end); dfree(seg_out); dfree(seg_work); dfree(seg_rerun); dfree(seg_rerun_init);
         dfree(seg0_fev); dfree(seg_ctl); dfree(spec_ws); dfree(spec_rr); dfree(spec_fin);
@@ -455,18 +453,8 @@ static int ensure_lay_ws(Dev *c, int want, int *slots_out) {
         W.slots = slots;
     }
     w.base = W.base;
-    const int used = std::min(slots, W.slots);
-    const size_t cb = lcd::t3l_coop_bytes(used);
-    if (cb > W.coop_bytes) {
-        dfree(W.coop);
-        W.coop_bytes = 0;
-        HIPCHK(hipMalloc((void **)&W.coop, cb));
-        W.coop_bytes = cb;
-    }
-    w.coop = W.coop;
-    w.coop_slots = (uint32_t)used;
     W.w = w;
-    *slots_out = used;
+    *slots_out = std::min(slots, W.slots);
     return LC_OK;
 }
 
@@ -1605,7 +1593,6 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
     }
     bool t3 = false;
     const unsigned long long probes_pre_t3 = acc[0];
-    uint64_t coop_passes = 0;  // T3L whole-table passes run by helping workgroups
     const int32_t n_deep = cnt[2], n_widek = cnt[3];
     if (K > 0 && (n_deep > 0 || n_widek > 0)) {
         // T3 (HBM tier): keys beyond T2, then keys needing wide configs
@@ -1626,16 +1613,9 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
             if (rc) return rc;
             a3.order = spill2; a3.n_order = 0; a3.n_in = n_spill2; a3.ticket = c->counters + 11;
             a3.spill = old_narrow; a3.n_spill = c->counters + 6;
-            // (the board's open jobs and counters start at zero every launch)
-            HIPCHK(hipMemsetAsync(c->lws.w.coop, 0, lcd::t3l_coop_bytes(slots), c->stream));
             HIPCHK(lcd::launch_t3_layers(a3, c->lws.w, slots, c->stream));
             HIPCHK(hipMemcpyAsync(c->hctl, c->ctl, CTL_BYTES, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
-            {
-                uint32_t passes = 0;
-                HIPCHK(hipMemcpy(&passes, c->lws.w.coop + lcd::t3l_coop_passes_offset(), 4, hipMemcpyDeviceToHost));
-                coop_passes = passes;
-            }
             narrow_list = old_narrow; narrow_n = c->counters + 6;
             n_narrow = cnt[6];
         }
@@ -1696,7 +1676,6 @@ static int dev_search(Dev *c, const DevBatch *d, const lc_result *r, ResMode mod
         st->tier3_ms = ms3;
         st->probes_t3 = t3 ? acc[0] - probes_pre_t3 : 0;
         st->t3_bytes = t3 ? acc[3] : 0;
-        st->t3_coop_passes = coop_passes;
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         st->probes = acc[0];
         st->events = acc[1];
@@ -1750,7 +1729,6 @@ static void merge_stats(lc_stats &t, const lc_stats &s) {
     t.wgl_keys += s.wgl_keys;
     t.wgl_spilled += s.wgl_spilled;
     t.wgl_steps += s.wgl_steps;
-    t.t3_coop_passes += s.t3_coop_passes;
 }
 
 // Run fn(g) for every device g of c at once (one driver thread per device

@@ -41,7 +41,6 @@
 
 #include <hip/hip_runtime.h>
 
-#include <cstddef>
 #include <cstdint>
 
 #include "../../include/lincheck.h"
@@ -83,11 +82,8 @@ struct LayShared {
     StepCtr ct[2];
     uint32_t n_sn, err;
     int32_t work;
-    int32_t coop_part;  // a cooperative pass claimed (-1: none left), broadcast by thread 0
-    int32_t coop_slot;  // a helper's job slot
-    uint32_t coop_res;  // a cooperative step: 1 a pass overflowed, 2 the wait timed out
 #ifdef LC_T3L_CNT
-    unsigned long long sc[6];  // whole-table steps (thread 0): insert / scan cycles (I, S'), passes (I, S'), entries in
+    unsigned long long sc[6];  // whole-table steps (thread 0): insert / scan cycles (I, S'), passes (I, S'), -, inputs
 #endif
 };
 
@@ -498,357 +494,18 @@ __device__ __forceinline__ void zero_ctr(StepCtr *c) {
     c->cfg = 0; c->cfg2 = 0; c->probes = 0;
 }
 
-// ---- cooperating blocks (the slowest key's whole-table steps)
-//
-// A block whose key queue is empty does not exit: it helps the blocks still
-// searching with their whole-table steps.  Such a step is P independent
-// passes, one per hash partition of its entries (pass j merges the entries
-// whose hash has top bits j into an LDS table of its own and appends them to
-// the step's output array); a block that reaches one with helpers idle posts
-// it on the launch's board (one job slot per block), split into at least as
-// many partitions as there are idle helpers (2 .. LC_T3L_COOP_MAX), and waits
-// while they run them.  Output positions come from one counter in HBM, the
-// sums (configs, overflow, errors) from atomics on the job.  Helpers leave
-// only when no block searches a key, so a posted job always has one.  The output is the same set of entries as the block's own passes
-// produce (its order within a layer is a scan order either way), so records
-// are unchanged.  Not used while counting probes (a pass's early exit at the
-// budget is the sequential step's).
-#ifndef LC_T3L_COOP
-#define LC_T3L_COOP 1
-#endif
-#ifndef LC_T3L_COOP_MAX
-#define LC_T3L_COOP_MAX 8u
-#endif
-struct CoopHead {
-    uint32_t active;   // blocks searching a key
-    uint32_t broken;   // a wait timed out: no more posting in this launch
-    uint32_t passes;   // passes run by helpers (lc_stats.t3_coop_passes; offset 8)
-    uint32_t pad0;
-    uint32_t idle[8];  // per XCD: blocks helping (their queue is empty)
-    uint32_t busy[8];  // per XCD: blocks searching a key
-    uint32_t open[8];  // per XCD: jobs open -- what the helpers poll (scanning every slot at each
-                       // poll took the fabric's request rate from the searches)
-    uint32_t pad1[36];
-};
-// One block's job: word = seq << 32 | passes claimed (seq odd: open).  The
-// fields are stored before the word; a claim is a CAS on the word, so it
-// belongs to the job the fields describe.
-struct CoopJob {
-    unsigned long long word;
-    uint32_t P, kind, done, emit, ovf, err, xcc, pad1;
-    unsigned long long cfg;
-    const uint64_t *S, *Ik;
-    uint64_t *out;
-    uint64_t cand;
-    uint32_t sb, se, nk, cap, p, xp, nc, pad0;
-    uint32_t cq[64], cx[64];
-};
-constexpr size_t COOP_HEAD = 256, COOP_STRIDE = 1024;
-static_assert(sizeof(CoopHead) <= COOP_HEAD && sizeof(CoopJob) <= COOP_STRIDE, "board layout");
-__device__ __forceinline__ CoopHead *coop_head(const LayWs &w) { return (CoopHead *)w.coop; }
-__device__ __forceinline__ CoopJob *coop_job(const LayWs &w, uint32_t slot) {
-    return (CoopJob *)(w.coop + COOP_HEAD + (size_t)slot * COOP_STRIDE);
-}
-// A job is helped only by blocks of the poster's XCD: they share its L2, so
-// the passes' output, the job's fields and the poster's arrays meet there
-// and the handoff needs no more than the CU's L1 invalidated (agent-scope
-// fences write back and invalidate whole L2s: posting through them made
-// every search of the launch 2-6x slower, its set arrays evicted).
-#ifndef LC_T3L_COOP_FENCE  // 2: the poster's XCD, agent-scope fences; 1: any XCD; 0: the same XCD, L1 only
-#define LC_T3L_COOP_FENCE 2
-#endif
-#if LC_T3L_COOP_FENCE == 3  // the poster's XCD; device-scope invalidate, no L2 write-back
-__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u; }
-__device__ __forceinline__ void l1_inv() { asm volatile("buffer_inv sc1" ::: "memory"); }
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-#elif LC_T3L_COOP_FENCE
-#if LC_T3L_COOP_FENCE == 2  // ... helpers of the poster's XCD only
-__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u; }
-#else
-__device__ __forceinline__ uint32_t xcc_id() { return 0u; }
-#endif
-__device__ __forceinline__ void l1_inv() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
-__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
-#else
-__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u; }
-__device__ __forceinline__ void l1_inv() { asm volatile("buffer_inv sc0" ::: "memory"); }
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-#endif
-__device__ __forceinline__ uint32_t ld_rlx(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_rlx64(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_rlx(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_rlx64(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Thread 0: claim a pass of the job open in j (its index), or -1.  After a
-// claim the CU's L1 is invalidated: the job's fields and arrays are read
-// fresh from the XCD's L2.
-__device__ int coop_claim(CoopJob *j) {
-    unsigned long long w = __hip_atomic_load(&j->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int t = 0; t < 64; ++t) {
-        if (!((w >> 32) & 1ull)) return -1;
-        // (P is the open job's once the CAS below succeeds on this word)
-        const uint32_t P = ld_rlx(&j->P);
-        if ((uint32_t)w >= P) return -1;
-        if (__hip_atomic_compare_exchange_strong(&j->word, &w, w + 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-            l1_inv();
-            return (int)(uint32_t)w;
-        }
-    }
-    return -1;
-}
-
-// One pass (partition `part` of P) of job j, by the whole block: kind 0
-// merges I_{k+1}, kind 1 S'_k, into sh.tab, and appends the partition to
-// j->out from j->emit.  Counts itself done in j.  Leaves the table clear and
-// ct[0] dirty.
-__device__ void coop_pass(LayShared &sh, const OkCtx &o, uint32_t sb, uint32_t se, const uint64_t *Ik, uint32_t nk,
-                          uint32_t kind, uint32_t P, uint32_t part, uint64_t *out, uint32_t cap, CoopJob *j) {
-    const uint32_t tid = threadIdx.x;
-    StepCtr *c = &sh.ct[0];
-    const Part pt{32u - (uint32_t)__builtin_ctz(P), part, P > 1};
-    __syncthreads();
-    if (tid == 0) { zero_ctr(c); sh.err = 0; }
-    __syncthreads();
-    if (kind == 0)
-        step_inserts(sh, o, sb, se, Ik, nk, sh.tab, TS - 1, nullptr, 0, pt, c, s_prefetch(o, sb, se));
-    else
-        step_inserts(sh, o, sb, se, Ik, nk, nullptr, 0, sh.tab, TS - 1, pt, c, s_prefetch(o, sb, se));
-    __syncthreads();
-    const bool bad = c->ovf || (kind == 0 && c->claims > CLAIM_MAX);
-    if (bad) {
-        clear_slots(sh.tab, TS);
-    } else {
-        uint32_t ca = 0, pa = 0, cs = 0;
-        if (kind == 0) scan_emit(sh, sh.tab, TS - 1, out, cap, &j->emit, IVisit{sh, o, ca, pa});
-        else scan_emit(sh, sh.tab, TS - 1, out, cap, &j->emit, SVisit{cs});
-        add_sums(c, ca, cs, 0);
-    }
-    vm_drain();  // this thread's output stores in the XCD's L2
-    __syncthreads();
-    if (tid == 0) {
-        if (bad) atomicOr(&j->ovf, 1u);
-        else atomicAdd(&j->cfg, kind == 0 ? c->cfg : c->cfg2);
-        if (sh.err) atomicOr(&j->err, 1u);
-        sh.err = 0;
-        vm_drain();
-        __hip_atomic_fetch_add(&j->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Partitions for a cooperative step now: the idle helpers as a power of two,
-// at least 2 (1: no cooperation).
-__device__ __forceinline__ uint32_t coop_parts(const LayWs &w) {
-    if (!LC_T3L_COOP || !w.coop) return 1u;
-    CoopHead *hd = coop_head(w);
-    if (ld_rlx(&hd->broken)) return 1u;
-    // helpers per searching block of the XCD: posting with fewer swamps the
-    // helpers (every pass generates all the step's pairs) while the posters
-    // wait -- C4 at 2^16 measured 2x slower posting whenever 2 helpers were idle
-    const uint32_t x = xcc_id();
-    const uint32_t n = min(ld_rlx(&hd->idle[x]) / max(ld_rlx(&hd->busy[x]), 1u), (uint32_t)LC_T3L_COOP_MAX);
-    return n < 2u ? 1u : 1u << (31 - __builtin_clz(n));
-}
-
-// A whole-table step's passes (kind, P) through this block's job slot: the
-// helpers run them, the block waits (its own registers stay the search's:
-// the passes' code lives in coop_help only).  Output from `base` in out.  Returns in sh.coop_res
-// (after a barrier) 0, 1 (a pass overflowed: redo with more passes) or 2
-// (the wait timed out); the job's output count and configs in ct[0].emit /
-// ct[0].cfg.
-__device__ void coop_step(LayShared &sh, const LayWs &w, const OkCtx &o, uint32_t sb, uint32_t se,
-                          const uint64_t *Ik, uint32_t nk, uint32_t kind, uint32_t P, uint64_t *out, uint32_t base) {
-    const uint32_t tid = threadIdx.x;
-    CoopJob *j = coop_job(w, blockIdx.x);
-    // (the board is read and written with agent-scope atomics only: a plain
-    // store waits dirty in the poster's L2 where the helpers' atomic loads
-    // do not look -- they read an earlier job's fields)
-    if (tid < 64) { st_rlx(&j->cq[tid], sh.cq[tid]); st_rlx(&j->cx[tid], sh.cx[tid]); }
-    const uint32_t xcc = xcc_id();
-    if (tid == 0) {
-        st_rlx(&j->P, P); st_rlx(&j->kind, kind); st_rlx(&j->done, 0); st_rlx(&j->emit, base); st_rlx(&j->ovf, 0);
-        st_rlx(&j->err, 0); st_rlx64((uint64_t *)&j->cfg, 0); st_rlx(&j->xcc, xcc);
-        st_rlx64((uint64_t *)&j->S, (uint64_t)o.S); st_rlx64((uint64_t *)&j->Ik, (uint64_t)Ik);
-        st_rlx64((uint64_t *)&j->out, (uint64_t)out); st_rlx64(&j->cand, o.cand);
-        st_rlx(&j->sb, sb); st_rlx(&j->se, se); st_rlx(&j->nk, nk); st_rlx(&j->cap, o.cap); st_rlx(&j->p, o.p);
-        st_rlx(&j->xp, o.xp); st_rlx(&j->nc, o.nc);
-    }
-    vm_drain();  // the fields, and the I_k copy in `spare`, in the XCD's L2
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned long long seq = (__hip_atomic_load(&j->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) + 1ull;
-        __hip_atomic_store(&j->word, seq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // open
-        atomicAdd(&coop_head(w)->open[xcc], 1u);
-    }
-    if (tid == 0) {
-        uint32_t res = 0;
-        for (uint32_t spins = 0; ld_rlx(&j->done) < P; ++spins) {
-            if (spins > (1u << 24)) {  // ~seconds: a helper cannot take that long; never hang the launch
-                res = 2;
-                __hip_atomic_store(&coop_head(w)->broken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8);
-        }
-        l1_inv();  // the passes' output, fresh from the XCD's L2 for every thread of the CU
-        if (res == 0 && ld_rlx(&j->ovf)) res = 1;
-        if (ld_rlx(&j->err)) sh.err = 1u;
-        sh.ct[0].emit = ld_rlx(&j->emit);
-        sh.ct[0].cfg = __hip_atomic_load(&j->cfg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long wd = __hip_atomic_load(&j->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&j->word, ((wd >> 32) + 1ull) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // close
-        atomicSub(&coop_head(w)->open[xcc], 1u);
-        sh.coop_res = res;
-    }
-    __syncthreads();  // (thread 0's acquire invalidated the CU's and the XCD's caches for every thread)
-}
-
-// A helper: runs other blocks' passes until no block searches a key.
-__device__ void coop_help(LayShared &sh, const LayWs &w) {
-    const uint32_t tid = threadIdx.x, lane = lane_id();
-    CoopHead *hd = coop_head(w);
-    const uint32_t ns = w.coop_slots, xcc = xcc_id();
-    if (tid == 0) atomicAdd(&hd->idle[xcc], 1u);
-    for (;;) {
-        if (tid < 64) {  // wave 0 looks for an open job with passes left, from a slot of its own
-            int got = -1, slot = -1;
-            const bool any = ld_rlx(&hd->open[xcc]) != 0;
-            for (uint32_t b0 = 0; any && b0 < ns && got < 0; b0 += 64) {
-                const uint32_t s = (b0 + lane + blockIdx.x) % ns;
-                bool open = false;
-                if (b0 + lane < ns) {
-                    CoopJob *j = coop_job(w, s);
-                    const unsigned long long wd = __hip_atomic_load(&j->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    open = ((wd >> 32) & 1ull) && (uint32_t)wd < ld_rlx(&j->P) && ld_rlx(&j->xcc) == xcc;
-                }
-                uint64_t bm = __ballot(open);
-                while (bm && got < 0) {
-                    const uint32_t l = (uint32_t)__builtin_ctzll(bm);
-                    bm &= bm - 1ull;
-                    const uint32_t s2 = (b0 + l + blockIdx.x) % ns;
-                    int g = -1;
-                    if (lane == 0) g = coop_claim(coop_job(w, s2));
-                    g = __builtin_amdgcn_readfirstlane(g);
-                    if (g >= 0) { got = g; slot = (int)s2; }
-                }
-            }
-            if (lane == 0) {
-                sh.coop_part = got;
-                sh.coop_slot = slot;
-                // done: nothing open and no block searching (it could post)
-                if (got < 0) sh.coop_res = ld_rlx(&hd->active) == 0 ? 1u : 0u;
-            }
-        }
-        __syncthreads();
-        const int part = sh.coop_part;
-        if (part < 0) {
-            const bool done = sh.coop_res != 0;
-            __syncthreads();
-            if (done) break;
-            __builtin_amdgcn_s_sleep(64);  // ~4k cycles between polls
-            continue;
-        }
-        // the job's fields (stable: our pass is claimed and not done), read
-        // with vector loads: a uniform field read through the scalar cache,
-        // which no L1 invalidation reaches, returned an earlier job's
-        CoopJob *j = coop_job(w, (uint32_t)sh.coop_slot);
-        if (tid < 64) { sh.cq[tid] = ld_rlx(&j->cq[tid]); sh.cx[tid] = ld_rlx(&j->cx[tid]); }
-        OkCtx o;
-        o.S = (const uint64_t *)ld_rlx64((const uint64_t *)&j->S);
-        o.so = nullptr;
-        uint64_t *out = (uint64_t *)ld_rlx64((const uint64_t *)&j->out);
-        o.Sn = out;
-        o.cand = ld_rlx64(&j->cand);
-        o.p = ld_rlx(&j->p); o.xp = ld_rlx(&j->xp); o.nc = ld_rlx(&j->nc); o.cap = ld_rlx(&j->cap); o.probes = false;
-        const uint32_t sb = ld_rlx(&j->sb), se = ld_rlx(&j->se), nk = ld_rlx(&j->nk), kind = ld_rlx(&j->kind),
-                       P = ld_rlx(&j->P);
-        const uint64_t *Ik = (const uint64_t *)ld_rlx64((const uint64_t *)&j->Ik);
-        __syncthreads();  // cq / cx
-        coop_pass(sh, o, sb, se, Ik, nk, kind, P, (uint32_t)part, out, o.cap, j);
-        if (tid == 0) atomicAdd(&hd->passes, 1u);
-        __syncthreads();
-    }
-}
-
 // The whole-table form of one step (a layer too large for the fused step, or
 // one whose fused merge overflowed): I_{k+1} (if want_i) in P passes into
 // `iout` (HBM), doubling P while a pass overflows; then S'_k (if want_s),
 // likewise.  Adds the configs to cfg_i / cfg_s and thread 0's probes.
 // Returns false when the budget was exceeded (or err).  Uses ct[0]; leaves
 // both counter sets zeroed.
-// Cooperative (coop: helpers idle, no probe counting): each pass list goes
-// through coop_step instead, at least as many passes as helpers plus one;
-// an I_k held in LDS is first copied to `spare` (an HBM array no step output
-// uses), where the helpers can read it.
 __device__ bool step_slow(LayShared &sh, const OkCtx &o, uint32_t sb, uint32_t se, const uint64_t *Ik, uint32_t nk,
                           bool want_i, bool want_s, uint64_t *iout, uint32_t &n_out, uint32_t &pc, uint64_t &cfg_i,
-                          uint64_t &cfg_s, uint64_t &probes, uint64_t budget, const LayWs &w, uint64_t *spare,
-                          bool coop) {
+                          uint64_t &cfg_s, uint64_t &probes, uint64_t budget) {
     const uint32_t tid = threadIdx.x;
     StepCtr *c = &sh.ct[0];
     bool ok = true;
-    // (one thread reads the board: the block must agree on the branch)
-    if (coop) {
-        __syncthreads();
-        if (tid == 0) sh.coop_part = (int32_t)coop_parts(w);
-        __syncthreads();
-    }
-    const uint32_t cp = coop ? (uint32_t)sh.coop_part : 1u;
-    if (cp > 1u) {
-        const uint64_t *src = Ik;
-        if (Ik == sh.icmp && nk) {
-            for (uint32_t q = tid; q < nk; q += LWG) spare[q] = sh.icmp[q];
-            src = spare;  // (made visible to the helpers by coop_step's fence before it posts)
-        }
-        if (want_i) {
-            uint32_t P = max(pc, cp);
-            for (;;) {
-                coop_step(sh, w, o, sb, se, src, nk, 0u, P, iout, 0u);
-                const uint32_t res = sh.coop_res;
-                if (res == 2u) { if (tid == 0) sh.err = 1u; break; }
-                if (res == 0u) break;
-                P *= 2u;
-                if (P > 65536u) { if (tid == 0) sh.err = 1u; break; }
-            }
-            n_out = c->emit;
-            cfg_i += c->cfg;
-            const uint32_t want = (uint32_t)((2ull * n_out + CLAIM_MAX - 1) / CLAIM_MAX);
-            pc = pow2_at_least(want > 0 ? want : 1u);
-            __syncthreads();  // ct[0] read
-            if (cfg_i > budget || sh.err) ok = false;
-        }
-        if (ok && want_s) {
-            const uint64_t bound = (uint64_t)nk + (se - sb);
-            uint32_t P2 = max(cp, pow2_at_least((uint32_t)((2 * bound + CLAIM_MAX - 1) / CLAIM_MAX)));
-            __syncthreads();
-            const uint32_t n0 = sh.n_sn;
-            for (;;) {
-                coop_step(sh, w, o, sb, se, src, nk, 1u, P2, o.Sn, n0);
-                const uint32_t res = sh.coop_res;
-                if (res == 2u) { if (tid == 0) sh.err = 1u; break; }
-                if (res == 0u) break;
-                P2 *= 2u;
-                if (P2 > 65536u) { if (tid == 0) sh.err = 1u; break; }
-            }
-            cfg_s += c->cfg;
-            const uint32_t n1 = c->emit;
-            __syncthreads();  // ct[0] read
-            if (tid == 0) sh.n_sn = n1;
-            if (cfg_s > budget || sh.err) ok = false;
-        }
-        __syncthreads();
-        if (tid == 0) { zero_ctr(&sh.ct[0]); zero_ctr(&sh.ct[1]); }
-        __syncthreads();
-        return ok;
-    }
     if (want_i) {
         uint32_t P = pc;
         uint64_t cfg = 0, pr = 0;
@@ -1125,7 +782,7 @@ __device__ int search_key_layers(const Args &a, const LayWs &w, int32_t key, Lay
                     // not touch; I_{k+1} goes to HBM
                     inext = ib ? I1 : I0;
                     if (!step_slow(sh, o, sb, se, Ik, nk, want_i, want_s, inext, n_next, pc, nIcfg, nSncfg, probes,
-                                   budget, w, ib ? I0 : I1, !a.count_probes)) { over = true; break; }
+                                   budget)) { over = true; break; }
                     ib ^= 1;
                     par = 0;
                     sbytes += want_i ? 16ull * n_next : 0ull;
@@ -1188,29 +845,14 @@ __global__ __launch_bounds__(LWG) void k_search_layers(Args a, LayWs w) {
         if (n == 0 || batch_refused(ka)) return;  // empty work list / malformed batch
     }
     clear_slots(sh.tab, TS);
-    // cooperating blocks: the board is this launch's (one job slot per block)
-    const bool coop = LC_T3L_COOP && w.coop && w.coop_slots >= gridDim.x;
-    LayWs wl = w;
-    if (!coop) wl.coop = nullptr;
     for (;;) {
-        if (threadIdx.x == 0) {
-            // counted as searching before the ticket: a helper stops only
-            // when no block searches, or is about to
-            if (coop) atomicAdd(&coop_head(wl)->active, 1u);
-            sh.work = atomicAdd(kargs().ticket, 1);
-            if (coop && sh.work >= n) atomicSub(&coop_head(wl)->active, 1u);
-            if (coop && sh.work < n) atomicAdd(&coop_head(wl)->busy[xcc_id()], 1u);
-        }
+        if (threadIdx.x == 0) sh.work = atomicAdd(kargs().ticket, 1);
         __syncthreads();
         const int32_t wi = sh.work;
         __syncthreads();
         if (wi >= n) break;
         const int32_t key = kargs().order[wi];
-        const int r = search_key_layers(a, wl, key, sh);
-        if (threadIdx.x == 0 && coop) {
-            atomicSub(&coop_head(wl)->busy[xcc_id()], 1u);
-            atomicSub(&coop_head(wl)->active, 1u);
-        }
+        const int r = search_key_layers(a, w, key, sh);
         if (threadIdx.x == 0 && (r == K_WIDE || r == K_OLD)) {
             KArgs &ka = kargs();
             int32_t *list = r == K_WIDE ? ka.wide : ka.spill, *count = r == K_WIDE ? ka.n_wide : ka.n_spill;
@@ -1219,7 +861,6 @@ __global__ __launch_bounds__(LWG) void k_search_layers(Args a, LayWs w) {
         }
         __syncthreads();
     }
-    if (coop) coop_help(sh, wl);
 }
 
 }  // namespace
@@ -1230,7 +871,5 @@ hipError_t launch_t3_layers(const Args &a, const LayWs &w, int grid, hipStream_t
 }
 // Entries a set array can hold past the budget before the block sees it.
 int t3l_slack() { return (int)TS; }
-size_t t3l_coop_bytes(int slots) { return COOP_HEAD + (size_t)(slots > 0 ? slots : 1) * COOP_STRIDE; }
-size_t t3l_coop_passes_offset() { return offsetof(CoopHead, passes); }
 
 }  // namespace lcd

@@ -158,13 +158,9 @@ struct LayWs {
     size_t slot_bytes;
     uint32_t cap;    // entries per array (budget + t3l_slack() + margin)
     size_t off_S0, off_S1, off_I0, off_I1;
-    char *coop;      // the cooperating blocks' board (t3l_coop_bytes, zeroed before each launch), or null
-    uint32_t coop_slots;
 };
 hipError_t launch_t3_layers(const Args &a, const LayWs &w, int grid, hipStream_t s);
 int t3l_slack();
-size_t t3l_coop_bytes(int slots);  // the board of a T3L launch of `slots` blocks
-size_t t3l_coop_passes_offset();   // where the board counts the helpers' passes (u32)
 hipError_t launch_t3_narrow(const Args &a, const HbmWs &w, int grid, hipStream_t s);
 hipError_t launch_t3_wide(const Args &a, const HbmWs &w, int grid, hipStream_t s);
 int t3_block();

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LINCHECK_LIB_OVERRIDE") or os.path.join(HERE, "liblincheck.so")  # override: diagnostics only
 
 # ---- constants (mirror include/lincheck.h) ---------------------------------
-LC_ABI_VERSION = 12
+LC_ABI_VERSION = 11
 LC_MAX_DEVICES = 8
 LC_COMM_ID_BYTES = 128
 LC_OPT_COUNT_PROBES = 0x1
@@ -98,7 +98,7 @@ class LcStats(C.Structure):
                 ("probes_t3", C.c_uint64), ("t3_bytes", C.c_uint64),
                 ("t0_path", C.c_uint32), ("ev_word_bytes", C.c_uint32),
                 ("wgl_ms", C.c_double), ("wgl_keys", C.c_uint64), ("wgl_spilled", C.c_uint64),
-                ("wgl_steps", C.c_uint64), ("t3_coop_passes", C.c_uint64)]
+                ("wgl_steps", C.c_uint64)]
 
 
 class LcSynthOpts(C.Structure):

@@ -241,7 +241,7 @@ class Device:
                                keys_done=st.lds_keys, deep_keys=st.deep_keys, events=st.events,
                                t0_path=N.T0_PATH_NAMES.get(st.t0_path, st.t0_path), ev_word_bytes=st.ev_word_bytes,
                                wgl_ms=st.wgl_ms, wgl_keys=st.wgl_keys, wgl_spilled=st.wgl_spilled,
-                               wgl_steps=st.wgl_steps, t3_coop_passes=st.t3_coop_passes),
+                               wgl_steps=st.wgl_steps),
                           arrs["analyzer"][:K])
 
     def check(self, packed: Packed, verdicts_only: bool = False, peaks: bool = True) -> KeyResults:

@@ -88,22 +88,3 @@ def test_layers_final_configs(device):
         fb = {tuple(r) for r in b.final[i][:nb].tolist()}
         if na < 10:  # the whole set: equal
             assert fa == fb
-
-
-def test_layers_cooperating_blocks():
-    """Cooperating blocks (device_layers.hip, LC_T3L_COOP): four long C4-shaped
-    keys among many short ones, so the blocks whose queue empties early help
-    the long keys' whole-table steps (the passes of a hash-partitioned
-    merge); records bit-exact with the oracle, and equal to the config-keyed
-    tier's.  No probe counting: that keeps each step on its own block."""
-    budget = 1 << 16
-    long_ = H.synth(n_keys=4, ops_per_key=5000, concurrency=30, info_rate=0.02, seed=46)
-    # short keys of the same shape: they reach the layered tier too (its
-    # launch has a block per key), and end early, leaving helpers
-    short = H.synth(n_keys=60, ops_per_key=700, concurrency=30, info_rate=0.02, seed=47, key_base=4)
-    h = H.History.concat([long_, short])
-    _, res, orc = device_vs_oracle(h, Device(0, budget=budget), budget=budget)
-    assert res.stats["deep_keys"] > 0
-    assert res.stats["t3_coop_passes"] > 0, "no pass was helped"
-    a, b = _same_records(h, budget)
-    assert a.stats["t3_coop_passes"] > 0

@@ -1,3 +1,4 @@
+# (Record of round 6's cooperative-T3L runs, commit 141027e; that build was reverted after them: profiles/r06_t3l_coop.txt.)
 # Round 6: T3L cooperating blocks (LC_T3L_COOP) -- the layered tier's GPU
 # tests, then C4 at 2^16 with and without cooperation (T3L kernel time).
 set -o pipefail

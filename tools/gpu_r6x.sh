@@ -1,3 +1,4 @@
+# (Record of round 6's cooperative-T3L runs, commit 141027e; that build was reverted after them: profiles/r06_t3l_coop.txt.)
 # Round 6: T3L cooperation -- handoff variants on the layered tests and C4 at
 # 2^16: cf3 (same XCD, device-scope invalidate, no L2 write-back), the
 # default (same XCD, agent fences), and no cooperation.

@@ -1,3 +1,4 @@
+# (Record of round 6's cooperative-T3L runs, commit 141027e; that build was reverted after them: profiles/r06_t3l_coop.txt.)
 # Round 6: T3L cooperation -- is the slowdown the helpers' polling?  Helpers
 # poll but no block posts (LC_T3L_COOP_MAX=1) against no cooperation.
 set -o pipefail
