@@ -24,7 +24,6 @@
 // :last-op and :final-paths are shaped as for :linear.
 
 #include <algorithm>
-#include <map>
 #include <set>
 #include <vector>
 
@@ -47,23 +46,37 @@ struct KeyView {
     const lc_packed *p;
     int64_t key;
     uint64_t eb, n;             // the key's events: [eb, eb + n)
-    std::map<uint32_t, uint64_t> held;  // slot -> invoke event (ordinal) holding it at `upto`
+    // (slot, invoke event (ordinal)) holding it at `upto`, in slot order.
+    // Built from a per-slot array in one pass: a std::map updated at every
+    // event was most of a C5 counterexample's rendering (~70 us per key).
+    std::vector<std::pair<uint32_t, uint64_t>> held;
     int64_t last_ok = -1;       // last :ok event before `upto`
 
     KeyView(const lc_packed *pk, int64_t k, uint64_t upto) : p(pk), key(k) {
         eb = p->ev_off[(size_t)k];
         n = p->ev_off[(size_t)k + 1] - eb;
         upto = std::min<uint64_t>(upto, n);
+        constexpr uint32_t NS = 128;  // LC_EV_SLOT's range
+        uint64_t at[NS];
+        bool on[NS] = {};
         for (uint64_t j = 0; j < upto; ++j) {
             const uint32_t w = p->word(eb + j);
             const uint32_t s = LC_EV_SLOT(w);
             if (w & LC_EV_OK_BIT) {
-                held.erase(s);
+                on[s] = false;
                 last_ok = (int64_t)j;
             } else {
-                held[s] = j;
+                on[s] = true;
+                at[s] = j;
             }
         }
+        for (uint32_t s = 0; s < NS; ++s)
+            if (on[s]) held.push_back({s, at[s]});
+    }
+    const std::pair<uint32_t, uint64_t> *find(uint32_t s) const {
+        for (const auto &h : held)
+            if (h.first == s) return &h;
+        return nullptr;
     }
     int64_t row(uint64_t j) const { return p->event_row((size_t)key, eb + j); }
     // the row completing invoke event j (its slot's next event, when an :ok)
@@ -167,8 +180,8 @@ static int64_t report(const lc_packed *p, int64_t key, int32_t valid, int32_t fa
         }
         o[2] = (int64_t)n_cfg;
         if (valid == LC_INVALID && fail_event >= 0 && max_paths > 0) {
-            auto ph = kv.held.find(p_slot);
-            if (ph != kv.held.end()) {
+            const auto *ph = kv.find(p_slot);
+            if (ph) {
                 const uint64_t p_inv = ph->second;
                 std::vector<std::pair<uint32_t, uint64_t>> others;  // (slot, invoke event)
                 for (auto &h : kv.held)
